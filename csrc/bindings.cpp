@@ -1,0 +1,407 @@
+// TORCH_LIBRARY registration of every scaletorch_amd HIP kernel as a
+// `torch.ops.st_amd.*` custom op (CUDA dispatch key == HIP on ROCm).
+//
+// The kernels themselves live in csrc/*.hip behind plain `extern "C"`
+// launchers (no torch headers in device code, so they compile in seconds);
+// this file only validates shapes/dtypes, allocates outputs through the
+// PyTorch caching allocator and launches on the current HIP stream.  Shape
+// checks here are the host-side guard required before any hand-written kernel
+// touches memory: a kernel is never launched on a shape its grid does not
+// cover.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+int st_rmsnorm_fwd(const void* x, const void* res, const void* w, void* y, void* sum_out,
+                   float* rstd, int rows, int h, float eps, hipStream_t st);
+int st_rmsnorm_bwd(const void* dy, const void* s, const void* w, const float* rstd,
+                   const void* dres, void* ds, float* partial, float* dw_out, int rows, int h,
+                   hipStream_t st);
+int st_rmsnorm_bwd_nwaves(int rows);
+int st_rope_inplace(void* x, const float* cos_t, const float* sin_t, const int64_t* pos, int B,
+                    int S, int NH, int D, int64_t sB, int64_t sS, int64_t sH, int pos_offset,
+                    int backward, hipStream_t st);
+int st_swiglu_fwd(const void* gu, void* out, int64_t N, int64_t I, hipStream_t st);
+int st_swiglu_bwd(const void* dout, const void* gu, void* dgu, int64_t N, int64_t I,
+                  hipStream_t st);
+int st_adamw_step(float* master, float* m, float* v, const void* g, int g_is_bf16, void* p,
+                  const float* clip, int64_t n, float lr, float b1, float b2, float eps, float wd,
+                  float bc1, float bc2_sqrt, hipStream_t st);
+int st_sumsq_partials();
+int st_sumsq(const void* g, int g_is_bf16, int64_t n, float* partial, float* out, hipStream_t st);
+int st_xent_fwd(const void* logits, int64_t ld, const int64_t* tgt, int64_t N, int V,
+                int64_t vocab_start, float* lse, float* tlogit, hipStream_t st);
+int st_xent_bwd(const void* logits, int64_t ld, const int64_t* tgt, int64_t N, int V,
+                int64_t vocab_start, const float* lse, const float* dloss, void* dlogits,
+                int64_t ldd, hipStream_t st);
+int st_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int Sq,
+                 int Sk, int H, int Hkv, int D, int64_t sqb, int64_t sqs, int64_t sqh,
+                 int64_t skb, int64_t sks, int64_t skh, int64_t svb, int64_t svs, int64_t svh,
+                 int64_t sob, int64_t sos, int64_t soh, float scale, int causal, int64_t q_offset,
+                 int64_t k_offset, hipStream_t st);
+int st_flash_bwd_preprocess(const void* o, const void* dout, float* delta, int B, int S, int H,
+                            int D, int64_t sob, int64_t sos, int64_t soh, int64_t sdb, int64_t sds,
+                            int64_t sdh, hipStream_t st);
+int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse,
+                 const float* delta, void* dq, void* dk, void* dv, float* work, int B, int Sq, int Sk,
+                 int H, int Hkv, int D, int64_t sqb, int64_t sqs, int64_t sqh, int64_t skb,
+                 int64_t sks, int64_t skh, int64_t svb, int64_t svs, int64_t svh, int64_t sdb,
+                 int64_t sds, int64_t sdh, int64_t sdqb, int64_t sdqs, int64_t sdqh, int64_t sdkb,
+                 int64_t sdks, int64_t sdkh, float scale, int causal, int64_t q_offset,
+                 int64_t k_offset, hipStream_t st);
+int st_lse_merge(float* out, float* lse, const void* bout, const float* blse, int B, int S, int H,
+                 int D, int64_t sbb, int64_t sbs, int64_t sbh, hipStream_t st);
+}
+
+namespace {
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define ST_CHECK_RC(rc, name) \
+  TORCH_CHECK((rc) == 0, "st_amd::" name " launch failed with code ", (rc))
+
+void check_bf16_cuda(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16, got ", t.scalar_type());
+}
+
+// ---------------------------------------------------------------- RMSNorm
+std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& res,
+                                    const at::Tensor& w, double eps) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "weight");
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous(), "rmsnorm: x and weight must be contiguous");
+  const int64_t h = x.size(-1);
+  TORCH_CHECK(w.numel() == h, "rmsnorm: weight size ", w.numel(), " != hidden ", h);
+  TORCH_CHECK(h % 8 == 0 && h <= 8192, "rmsnorm: hidden must be a multiple of 8 and <= 8192");
+  const int64_t rows = x.numel() / h;
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto y = at::empty_like(x);
+  auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  at::Tensor s;
+  const void* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_bf16_cuda(*res, "residual");
+    TORCH_CHECK(res->is_contiguous() && res->sizes() == x.sizes(), "rmsnorm: residual shape");
+    s = at::empty_like(x);
+    rp = res->data_ptr();
+  } else {
+    s = at::empty({0}, x.options());
+  }
+  int rc = st_rmsnorm_fwd(x.data_ptr(), rp, w.data_ptr(), y.data_ptr(),
+                          rp ? s.data_ptr() : nullptr, rstd.data_ptr<float>(), (int)rows, (int)h,
+                          (float)eps, cur_stream());
+  ST_CHECK_RC(rc, "rmsnorm_fwd");
+  return {y, rstd, s};
+}
+
+at::Tensor rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& s, const at::Tensor& w,
+                       const at::Tensor& rstd, const c10::optional<at::Tensor>& dres,
+                       at::Tensor dw_accum) {
+  check_bf16_cuda(dy, "dy");
+  check_bf16_cuda(s, "s");
+  check_bf16_cuda(w, "weight");
+  TORCH_CHECK(dy.is_contiguous() && s.is_contiguous() && dy.sizes() == s.sizes(), "rmsnorm_bwd: shapes");
+  const int64_t h = s.size(-1);
+  const int64_t rows = s.numel() / h;
+  TORCH_CHECK(rstd.numel() == rows && rstd.scalar_type() == at::kFloat, "rmsnorm_bwd: rstd");
+  TORCH_CHECK(dw_accum.numel() == h && dw_accum.scalar_type() == at::kFloat &&
+                  dw_accum.is_contiguous(), "rmsnorm_bwd: dw_accum must be fp32 [h]");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(s.device());
+  const void* dp = nullptr;
+  if (dres.has_value() && dres->defined()) {
+    check_bf16_cuda(*dres, "dres");
+    TORCH_CHECK(dres->is_contiguous() && dres->sizes() == s.sizes(), "rmsnorm_bwd: dres shape");
+    dp = dres->data_ptr();
+  }
+  auto ds = at::empty_like(s);
+  const int nw = st_rmsnorm_bwd_nwaves((int)rows);
+  auto partial = at::empty({(int64_t)nw * h}, s.options().dtype(at::kFloat));
+  int rc = st_rmsnorm_bwd(dy.data_ptr(), s.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), dp,
+                          ds.data_ptr(), partial.data_ptr<float>(), dw_accum.data_ptr<float>(),
+                          (int)rows, (int)h, cur_stream());
+  ST_CHECK_RC(rc, "rmsnorm_bwd");
+  return ds;
+}
+
+// ---------------------------------------------------------------- RoPE
+void rope_(at::Tensor x, const at::Tensor& cos_t, const at::Tensor& sin_t,
+           const c10::optional<at::Tensor>& pos, int64_t pos_offset, bool backward) {
+  check_bf16_cuda(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.stride(3) == 1, "rope: x must be [B,S,NH,D] with contiguous D");
+  const int64_t B = x.size(0), S = x.size(1), NH = x.size(2), D = x.size(3);
+  TORCH_CHECK(D % 16 == 0, "rope: head_dim must be a multiple of 16");
+  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat &&
+                  cos_t.is_contiguous() && sin_t.is_contiguous() && cos_t.size(-1) == D / 2,
+              "rope: tables must be fp32 contiguous [max_pos, D/2]");
+  const int64_t maxpos = cos_t.size(0);
+  const int64_t* pp = nullptr;
+  if (pos.has_value() && pos->defined()) {
+    TORCH_CHECK(pos->scalar_type() == at::kLong && pos->is_contiguous() && pos->numel() == B * S,
+                "rope: position_ids must be int64 [B,S]");
+    pp = pos->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(S + pos_offset <= maxpos && pos_offset >= 0, "rope: positions exceed table");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  int rc = st_rope_inplace(x.data_ptr(), cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), pp,
+                           (int)B, (int)S, (int)NH, (int)D, x.stride(0), x.stride(1), x.stride(2),
+                           (int)pos_offset, backward ? 1 : 0, cur_stream());
+  ST_CHECK_RC(rc, "rope_");
+}
+
+// ---------------------------------------------------------------- SwiGLU
+at::Tensor swiglu_fwd(const at::Tensor& gu) {
+  check_bf16_cuda(gu, "gate_up");
+  TORCH_CHECK(gu.is_contiguous() && gu.size(-1) % 16 == 0, "swiglu: [.., 2I] contiguous, I%8==0");
+  const int64_t I = gu.size(-1) / 2, N = gu.numel() / gu.size(-1);
+  auto sizes = gu.sizes().vec();
+  sizes.back() = I;
+  c10::hip::HIPGuardMasqueradingAsCUDA g(gu.device());
+  auto out = at::empty(sizes, gu.options());
+  int rc = st_swiglu_fwd(gu.data_ptr(), out.data_ptr(), N, I, cur_stream());
+  ST_CHECK_RC(rc, "swiglu_fwd");
+  return out;
+}
+
+at::Tensor swiglu_bwd(const at::Tensor& dout, const at::Tensor& gu) {
+  check_bf16_cuda(dout, "dout");
+  check_bf16_cuda(gu, "gate_up");
+  TORCH_CHECK(gu.is_contiguous() && dout.is_contiguous(), "swiglu_bwd: contiguous inputs");
+  const int64_t I = gu.size(-1) / 2, N = gu.numel() / gu.size(-1);
+  TORCH_CHECK(dout.numel() == N * I, "swiglu_bwd: dout shape");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(gu.device());
+  auto dgu = at::empty_like(gu);
+  int rc = st_swiglu_bwd(dout.data_ptr(), gu.data_ptr(), dgu.data_ptr(), N, I, cur_stream());
+  ST_CHECK_RC(rc, "swiglu_bwd");
+  return dgu;
+}
+
+// ---------------------------------------------------------------- AdamW / norms
+void adamw_step_(at::Tensor master, at::Tensor exp_avg, at::Tensor exp_avg_sq,
+                 const at::Tensor& grad, const c10::optional<at::Tensor>& param,
+                 const c10::optional<at::Tensor>& clip_coef, double lr, double beta1, double beta2,
+                 double eps, double weight_decay, int64_t step) {
+  TORCH_CHECK(master.is_cuda() && master.scalar_type() == at::kFloat && master.is_contiguous(),
+              "adamw: master must be contiguous fp32 on GPU");
+  const int64_t n = master.numel();
+  TORCH_CHECK(exp_avg.numel() == n && exp_avg_sq.numel() == n && grad.numel() == n,
+              "adamw: arena sizes differ");
+  TORCH_CHECK(exp_avg.scalar_type() == at::kFloat && exp_avg_sq.scalar_type() == at::kFloat &&
+                  exp_avg.is_contiguous() && exp_avg_sq.is_contiguous() && grad.is_contiguous(),
+              "adamw: states must be contiguous fp32");
+  TORCH_CHECK(grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16,
+              "adamw: grad must be fp32 or bf16");
+  TORCH_CHECK(n % 4 == 0, "adamw: arena length must be a multiple of 4");
+  void* pp = nullptr;
+  if (param.has_value() && param->defined()) {
+    check_bf16_cuda(*param, "param");
+    TORCH_CHECK(param->numel() == n && param->is_contiguous(), "adamw: param arena");
+    pp = param->data_ptr();
+  }
+  const float* cp = nullptr;
+  if (clip_coef.has_value() && clip_coef->defined()) {
+    TORCH_CHECK(clip_coef->scalar_type() == at::kFloat && clip_coef->numel() == 1, "adamw: clip");
+    cp = clip_coef->data_ptr<float>();
+  }
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(master.device());
+  int rc = st_adamw_step(master.data_ptr<float>(), exp_avg.data_ptr<float>(),
+                         exp_avg_sq.data_ptr<float>(), grad.data_ptr(),
+                         grad.scalar_type() == at::kBFloat16 ? 1 : 0, pp, cp, n, (float)lr,
+                         (float)beta1, (float)beta2, (float)eps, (float)weight_decay, (float)bc1,
+                         (float)std::sqrt(bc2), cur_stream());
+  ST_CHECK_RC(rc, "adamw_step_");
+}
+
+void sumsq_(const at::Tensor& g, at::Tensor out) {
+  TORCH_CHECK(g.is_cuda() && g.is_contiguous() && g.numel() % 4 == 0, "sumsq: contiguous, n%4==0");
+  TORCH_CHECK(g.scalar_type() == at::kFloat || g.scalar_type() == at::kBFloat16, "sumsq: dtype");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= 1, "sumsq: out fp32");
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(g.device());
+  auto partial = at::empty({st_sumsq_partials()}, g.options().dtype(at::kFloat));
+  int rc = st_sumsq(g.data_ptr(), g.scalar_type() == at::kBFloat16 ? 1 : 0, g.numel(),
+                    partial.data_ptr<float>(), out.data_ptr<float>(), cur_stream());
+  ST_CHECK_RC(rc, "sumsq_");
+}
+
+// ---------------------------------------------------------------- cross-entropy
+std::vector<at::Tensor> xent_fwd(const at::Tensor& logits, const at::Tensor& tgt,
+                                 int64_t vocab_start) {
+  check_bf16_cuda(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "xent: logits [N, V] row-major");
+  TORCH_CHECK(tgt.scalar_type() == at::kLong && tgt.is_contiguous() && tgt.numel() == logits.size(0),
+              "xent: targets int64 [N]");
+  const int64_t N = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(V % 8 == 0 && logits.stride(0) % 8 == 0, "xent: V and row stride must be %8");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
+  auto lse = at::empty({N}, logits.options().dtype(at::kFloat));
+  auto tl = at::empty({N}, logits.options().dtype(at::kFloat));
+  int rc = st_xent_fwd(logits.data_ptr(), logits.stride(0), tgt.data_ptr<int64_t>(), N, (int)V,
+                       vocab_start, lse.data_ptr<float>(), tl.data_ptr<float>(), cur_stream());
+  ST_CHECK_RC(rc, "xent_fwd");
+  return {lse, tl};
+}
+
+void xent_bwd_(const at::Tensor& logits, const at::Tensor& tgt, int64_t vocab_start,
+               const at::Tensor& lse, const at::Tensor& dloss, at::Tensor dlogits) {
+  check_bf16_cuda(logits, "logits");
+  check_bf16_cuda(dlogits, "dlogits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && dlogits.sizes() == logits.sizes() &&
+                  dlogits.stride(1) == 1, "xent_bwd: shapes");
+  const int64_t N = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(lse.numel() == N && dloss.numel() == N && tgt.numel() == N, "xent_bwd: row vectors");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && dloss.scalar_type() == at::kFloat &&
+                  lse.is_contiguous() && dloss.is_contiguous(), "xent_bwd: fp32 lse/dloss");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
+  int rc = st_xent_bwd(logits.data_ptr(), logits.stride(0), tgt.data_ptr<int64_t>(), N, (int)V,
+                       vocab_start, lse.data_ptr<float>(), dloss.data_ptr<float>(),
+                       dlogits.data_ptr(), dlogits.stride(0), cur_stream());
+  ST_CHECK_RC(rc, "xent_bwd_");
+}
+
+// ---------------------------------------------------------------- flash attention
+// q [B, Sq, H, D], k/v [B, Sk, Hkv, D] (strided views, D contiguous), out
+// [B, Sq, H, D] contiguous, lse [B, H, Sq] fp32.  q_offset/k_offset are the
+// global positions of row 0 of q / k (context-parallel blocks); causal masks
+// key j > query i in global coordinates.
+void check_qkv(const at::Tensor& t, const char* n, int64_t D) {
+  check_bf16_cuda(t, n);
+  TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1 && t.size(3) == D, n, ": expected [B,S,H,D] with contiguous D");
+  TORCH_CHECK(t.stride(2) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(0) % 8 == 0,
+              n, ": strides must be multiples of 8 elements");
+}
+
+std::vector<at::Tensor> flash_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                  double scale, bool causal, int64_t q_offset, int64_t k_offset) {
+  const int64_t D = q.size(3);
+  TORCH_CHECK(D == 64 || D == 128, "flash_fwd: head_dim must be 64 or 128");
+  check_qkv(q, "q", D);
+  check_qkv(k, "k", D);
+  check_qkv(v, "v", D);
+  const int64_t B = q.size(0), Sq = q.size(1), H = q.size(2), Sk = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(k.size(0) == B && v.size(0) == B && v.size(1) == Sk && v.size(2) == Hkv, "flash_fwd: k/v shapes");
+  TORCH_CHECK(H % Hkv == 0, "flash_fwd: H must be a multiple of Hkv");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  auto o = at::empty({B, Sq, H, D}, q.options());
+  auto lse = at::empty({B, H, Sq}, q.options().dtype(at::kFloat));
+  int rc = st_flash_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
+                        (int)B, (int)Sq, (int)Sk, (int)H, (int)Hkv, (int)D, q.stride(0), q.stride(1),
+                        q.stride(2), k.stride(0), k.stride(1), k.stride(2), v.stride(0), v.stride(1),
+                        v.stride(2), o.stride(0), o.stride(1), o.stride(2), (float)scale,
+                        causal ? 1 : 0, q_offset, k_offset, cur_stream());
+  ST_CHECK_RC(rc, "flash_fwd");
+  return {o, lse};
+}
+
+// Returns (dq, dk, dv) bf16: dq [B,Sq,H,D], dk/dv [B,Sk,Hkv,D].  Optional
+// preallocated outputs (any (b,s,h) strides with contiguous D, e.g. slices of
+// one fused dQKV buffer) are written in place and returned.
+// GQA is native: dk/dv are accumulated over the H/Hkv query heads of each kv
+// head, never expanded.
+std::vector<at::Tensor> flash_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
+                                  const at::Tensor& v, const at::Tensor& o, const at::Tensor& lse,
+                                  double scale, bool causal, int64_t q_offset, int64_t k_offset,
+                                  const c10::optional<at::Tensor>& dq_out,
+                                  const c10::optional<at::Tensor>& dk_out,
+                                  const c10::optional<at::Tensor>& dv_out) {
+  const int64_t D = q.size(3);
+  TORCH_CHECK(D == 64 || D == 128, "flash_bwd: head_dim must be 64 or 128");
+  check_qkv(q, "q", D);
+  check_qkv(k, "k", D);
+  check_qkv(v, "v", D);
+  check_qkv(o, "o", D);
+  check_qkv(dout, "dout", D);
+  const int64_t B = q.size(0), Sq = q.size(1), H = q.size(2), Sk = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(o.sizes() == q.sizes() && dout.sizes() == q.sizes(), "flash_bwd: o/dout shapes");
+  TORCH_CHECK(k.sizes() == v.sizes() && k.size(0) == B, "flash_bwd: k/v shapes");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * H * Sq,
+              "flash_bwd: lse [B,H,Sq] fp32");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  auto delta = at::empty({B, H, Sq}, q.options().dtype(at::kFloat));
+  int rc = st_flash_bwd_preprocess(o.data_ptr(), dout.data_ptr(), delta.data_ptr<float>(), (int)B,
+                                   (int)Sq, (int)H, (int)D, o.stride(0), o.stride(1), o.stride(2),
+                                   dout.stride(0), dout.stride(1), dout.stride(2), cur_stream());
+  ST_CHECK_RC(rc, "flash_bwd_preprocess");
+  auto pick = [&](const c10::optional<at::Tensor>& t, at::IntArrayRef shape, const char* n) {
+    if (t.has_value() && t->defined()) {
+      check_qkv(*t, n, D);
+      TORCH_CHECK(t->sizes() == shape, n, ": wrong shape");
+      return *t;
+    }
+    return at::empty(shape, q.options());
+  };
+  auto dq = pick(dq_out, q.sizes(), "dq_out");
+  auto dk = pick(dk_out, k.sizes(), "dk_out");
+  auto dv = pick(dv_out, v.sizes(), "dv_out");
+  TORCH_CHECK(dk.strides() == dv.strides(), "flash_bwd: dk_out/dv_out must share strides");
+  at::Tensor work;
+  float* wp = nullptr;
+  if (H != Hkv) {
+    work = at::empty({2 * B * Sk * H * D}, q.options().dtype(at::kFloat));
+    wp = work.data_ptr<float>();
+  }
+  rc = st_flash_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
+                    delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), wp,
+                    (int)B, (int)Sq, (int)Sk, (int)H, (int)Hkv, (int)D, q.stride(0), q.stride(1),
+                    q.stride(2), k.stride(0), k.stride(1), k.stride(2), v.stride(0), v.stride(1),
+                    v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2), dq.stride(0),
+                    dq.stride(1), dq.stride(2), dk.stride(0), dk.stride(1), dk.stride(2),
+                    (float)scale, causal ? 1 : 0, q_offset, k_offset, cur_stream());
+  ST_CHECK_RC(rc, "flash_bwd");
+  return {dq, dk, dv};
+}
+
+// In-place online-softmax merge of a partial attention block into a running
+// (out fp32 [B,S,H,D], lse fp32 [B,H,S]) pair -- the ring-attention combine.
+void lse_merge_(at::Tensor out, at::Tensor lse, const at::Tensor& bout, const at::Tensor& blse) {
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.dim() == 4, "lse_merge: out");
+  check_qkv(bout, "block_out", out.size(3));
+  TORCH_CHECK(bout.sizes() == out.sizes(), "lse_merge: block_out shape");
+  const int64_t B = out.size(0), S = out.size(1), H = out.size(2), D = out.size(3);
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && blse.scalar_type() == at::kFloat &&
+                  lse.is_contiguous() && blse.is_contiguous() && lse.numel() == B * H * S &&
+                  blse.numel() == B * H * S, "lse_merge: lse [B,H,S] fp32");
+  TORCH_CHECK(D % 8 == 0, "lse_merge: D % 8");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(out.device());
+  int rc = st_lse_merge(out.data_ptr<float>(), lse.data_ptr<float>(), bout.data_ptr(),
+                        blse.data_ptr<float>(), (int)B, (int)S, (int)H, (int)D, bout.stride(0),
+                        bout.stride(1), bout.stride(2), cur_stream());
+  ST_CHECK_RC(rc, "lse_merge_");
+}
+
+}  // namespace
+
+TORCH_LIBRARY(st_amd, m) {
+  m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor weight, float eps) -> Tensor[]");
+  m.def("rmsnorm_bwd(Tensor dy, Tensor s, Tensor weight, Tensor rstd, Tensor? dres, Tensor(a!) dw_accum) -> Tensor");
+  m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, Tensor? pos, int pos_offset, bool backward) -> ()");
+  m.def("swiglu_fwd(Tensor gate_up) -> Tensor");
+  m.def("swiglu_bwd(Tensor dout, Tensor gate_up) -> Tensor");
+  m.def("adamw_step_(Tensor(a!) master, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor grad, Tensor(d!)? param, Tensor? clip_coef, float lr, float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
+  m.def("sumsq_(Tensor g, Tensor(a!) out) -> ()");
+  m.def("xent_fwd(Tensor logits, Tensor target, int vocab_start) -> Tensor[]");
+  m.def("xent_bwd_(Tensor logits, Tensor target, int vocab_start, Tensor lse, Tensor dloss, Tensor(a!) dlogits) -> ()");
+  m.def("flash_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int q_offset, int k_offset) -> Tensor[]");
+  m.def("flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, int q_offset, int k_offset, Tensor(a!)? dq_out=None, Tensor(b!)? dk_out=None, Tensor(c!)? dv_out=None) -> Tensor[]");
+  m.def("lse_merge_(Tensor(a!) out, Tensor(b!) lse, Tensor block_out, Tensor block_lse) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(st_amd, CUDA, m) {
+  m.impl("rmsnorm_fwd", &rmsnorm_fwd);
+  m.impl("rmsnorm_bwd", &rmsnorm_bwd);
+  m.impl("rope_", &rope_);
+  m.impl("swiglu_fwd", &swiglu_fwd);
+  m.impl("swiglu_bwd", &swiglu_bwd);
+  m.impl("adamw_step_", &adamw_step_);
+  m.impl("sumsq_", &sumsq_);
+  m.impl("xent_fwd", &xent_fwd);
+  m.impl("xent_bwd_", &xent_bwd_);
+  m.impl("flash_fwd", &flash_fwd);
+  m.impl("flash_bwd", &flash_bwd);
+  m.impl("lse_merge_", &lse_merge_);
+}

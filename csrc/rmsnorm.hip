@@ -1,0 +1,263 @@
+// RMSNorm forward / backward for gfx950, optionally fused with the residual add
+// that precedes every pre-norm in a Llama/Qwen3 decoder layer.
+//
+// Reference semantics: scaletorch/models/attention_utils.py:247-271 (fp32
+// variance, rsqrt, scale by weight) and the residual adds in
+// scaletorch/models/llama.py:320-379.  The MI355X design:
+//   * one wave64 owns one row; the whole row lives in VGPRs (h <= 8192), so the
+//     sum of squares is a pure register + DPP/shuffle reduction with no LDS and
+//     no barrier;
+//   * 16-byte (8 x bf16) loads/stores per lane: a wave touches 1 KiB per access;
+//   * the residual add is fused: s = x + r is rounded to bf16 once, written as
+//     the new residual stream and normalised from the rounded value, so the
+//     fused path is bit-compatible with the unfused bf16 graph;
+//   * backward recomputes xhat from s and rstd (fp32, saved by forward), emits
+//     ds (+ an optional incoming residual-stream gradient) and per-wave fp32
+//     partial sums of dy*xhat that a second pass reduces into dweight.
+#include "common.h"
+
+using namespace st;
+
+namespace {
+
+constexpr int kRowsPerBlock = 4;  // 4 waves = 256 threads
+
+template <int NCH, bool RES>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, const bf16_t* __restrict__ w,
+    bf16_t* __restrict__ y, bf16_t* __restrict__ sum_out, float* __restrict__ rstd_out, int rows,
+    int h, float eps) {
+  const int row = blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const size_t base = (size_t)row * h;
+  float v[NCH][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < h) {
+      BF8 a = ld8(x + base + col);
+      unpack8(a, v[c]);
+      if (RES) {
+        float r[8];
+        unpack8(ld8(res + base + col), r);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[c][i] = bf2f(f2bf(v[c][i] + r[i]));
+        st8(sum_out + base + col, pack8(v[c]));
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss += v[c][i] * v[c][i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[c][i] = 0.f;
+    }
+  }
+  ss = wave_sum(ss);
+  const float rs = rsqrtf(ss / (float)h + eps);
+  if (lane == 0) rstd_out[row] = rs;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < h) {
+      float wf[8], o[8];
+      unpack8(ld8(w + col), wf);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = v[c][i] * rs * wf[i];
+      st8(y + base + col, pack8(o));
+    }
+  }
+}
+
+// grid-stride over rows; each wave accumulates its dweight partial in
+// registers and writes it once to partial[wave_global, h].  The row operands
+// are kept packed (bf16) in registers to bound VGPR use at h = 8192.
+template <int NCH, bool DRES>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s, const bf16_t* __restrict__ w,
+    const float* __restrict__ rstd, const bf16_t* __restrict__ dres, bf16_t* __restrict__ ds,
+    float* __restrict__ partial, int rows, int h) {
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  const int nw = gridDim.x * kRowsPerBlock;
+  BF8 wp[NCH];
+  float dwp[NCH][8];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dwp[c][i] = 0.f;
+    if (col < h) wp[c] = ld8(w + col);
+    else wp[c] = BF8{{0u, 0u, 0u, 0u}};
+  }
+  for (int row = gw; row < rows; row += nw) {
+    const size_t base = (size_t)row * h;
+    const float rs = rstd[row];
+    BF8 sp[NCH], dp[NCH];
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < h) {
+        sp[c] = ld8(s + base + col);
+        dp[c] = ld8(dy + base + col);
+      } else {
+        sp[c] = BF8{{0u, 0u, 0u, 0u}};
+        dp[c] = BF8{{0u, 0u, 0u, 0u}};
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      float sv[8], dv[8], wf[8];
+      unpack8(sp[c], sv);
+      unpack8(dp[c], dv);
+      unpack8(wp[c], wf);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float xh = sv[i] * rs;
+        dot += dv[i] * wf[i] * xh;
+        dwp[c][i] += dv[i] * xh;
+      }
+    }
+    dot = wave_sum(dot) / (float)h;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < h) {
+        float sv[8], dv[8], wf[8], o[8];
+        unpack8(sp[c], sv);
+        unpack8(dp[c], dv);
+        unpack8(wp[c], wf);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = rs * (dv[i] * wf[i] - sv[i] * rs * dot);
+        if (DRES) {
+          float r[8];
+          unpack8(ld8(dres + base + col), r);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] += r[i];
+        }
+        st8(ds + base + col, pack8(o));
+      }
+    }
+  }
+  float* pr = partial + (size_t)gw * h;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < h) {
+      st4f(pr + col, make_float4(dwp[c][0], dwp[c][1], dwp[c][2], dwp[c][3]));
+      st4f(pr + col + 4, make_float4(dwp[c][4], dwp[c][5], dwp[c][6], dwp[c][7]));
+    }
+  }
+}
+
+// dw[col] (+)= sum_p partial[p, col].  block = 256 threads covering 256
+// columns (float4 per lane) x 4 waves splitting the partial rows; blockIdx.y
+// splits the partial rows further and combines with one fp32 atomic per
+// column per block (16 adders per address at most).
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ partial,
+                                                     float* __restrict__ out, int P, int h,
+                                                     int splits) {
+  __shared__ float4 red[4][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int col = blockIdx.x * 256 + lane * 4;
+  const int per = (P + splits - 1) / splits;
+  const int p0 = blockIdx.y * per, p1 = min(P, p0 + per);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < h) {
+    for (int p = p0 + wid; p < p1; p += 4) {
+      float4 v = ld4f(partial + (size_t)p * h + col);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  red[wid][lane] = acc;
+  __syncthreads();
+  if (wid == 0 && col < h) {
+    float4 t = red[0][lane];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      t.x += red[k][lane].x; t.y += red[k][lane].y; t.z += red[k][lane].z; t.w += red[k][lane].w;
+    }
+    atomicAdd(out + col + 0, t.x);
+    atomicAdd(out + col + 1, t.y);
+    atomicAdd(out + col + 2, t.z);
+    atomicAdd(out + col + 3, t.w);
+  }
+}
+
+template <bool RES>
+int launch_fwd(const void* x, const void* res, const void* w, void* y, void* sum_out, float* rstd,
+               int rows, int h, float eps, hipStream_t st) {
+  const int nch = (h + 511) / 512;
+  dim3 grid((rows + kRowsPerBlock - 1) / kRowsPerBlock), block(256);
+#define ST_RMS_FWD(N)                                                                      \
+  rmsnorm_fwd_kernel<N, RES><<<grid, block, 0, st>>>(                                      \
+      (const bf16_t*)x, (const bf16_t*)res, (const bf16_t*)w, (bf16_t*)y, (bf16_t*)sum_out, \
+      rstd, rows, h, eps)
+  if (nch <= 1) ST_RMS_FWD(1);
+  else if (nch <= 2) ST_RMS_FWD(2);
+  else if (nch <= 4) ST_RMS_FWD(4);
+  else if (nch <= 8) ST_RMS_FWD(8);
+  else if (nch <= 10) ST_RMS_FWD(10);
+  else if (nch <= 16) ST_RMS_FWD(16);
+  else return -1;
+#undef ST_RMS_FWD
+  return (int)hipGetLastError();
+}
+
+template <bool DRES>
+int launch_bwd(const void* dy, const void* s, const void* w, const float* rstd, const void* dres,
+               void* ds, float* partial, int nwaves, int rows, int h, hipStream_t st) {
+  const int nch = (h + 511) / 512;
+  dim3 grid(nwaves / kRowsPerBlock), block(256);
+#define ST_RMS_BWD(N)                                                                       \
+  rmsnorm_bwd_kernel<N, DRES><<<grid, block, 0, st>>>(                                      \
+      (const bf16_t*)dy, (const bf16_t*)s, (const bf16_t*)w, rstd, (const bf16_t*)dres,     \
+      (bf16_t*)ds, partial, rows, h)
+  if (nch <= 1) ST_RMS_BWD(1);
+  else if (nch <= 2) ST_RMS_BWD(2);
+  else if (nch <= 4) ST_RMS_BWD(4);
+  else if (nch <= 8) ST_RMS_BWD(8);
+  else if (nch <= 10) ST_RMS_BWD(10);
+  else if (nch <= 16) ST_RMS_BWD(16);
+  else return -1;
+#undef ST_RMS_BWD
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+// Number of waves the backward uses (the partial buffer must hold nwaves*h fp32).
+int st_rmsnorm_bwd_nwaves(int rows) {
+  int blocks = (rows + kRowsPerBlock - 1) / kRowsPerBlock;
+  if (blocks > 256) blocks = 256;
+  if (blocks < 1) blocks = 1;
+  return blocks * kRowsPerBlock;
+}
+
+int st_rmsnorm_fwd(const void* x, const void* res, const void* w, void* y, void* sum_out,
+                   float* rstd, int rows, int h, float eps, hipStream_t st) {
+  if (h % 8 != 0) return -2;
+  if (res) return launch_fwd<true>(x, res, w, y, sum_out, rstd, rows, h, eps, st);
+  return launch_fwd<false>(x, nullptr, w, y, nullptr, rstd, rows, h, eps, st);
+}
+
+// dw_out (fp32, length h) is ACCUMULATED into (caller zeroes it or passes a
+// main_grad view).
+int st_rmsnorm_bwd(const void* dy, const void* s, const void* w, const float* rstd,
+                   const void* dres, void* ds, float* partial, float* dw_out, int rows, int h,
+                   hipStream_t st) {
+  if (h % 8 != 0) return -2;
+  const int nw = st_rmsnorm_bwd_nwaves(rows);
+  int rc = dres ? launch_bwd<true>(dy, s, w, rstd, dres, ds, partial, nw, rows, h, st)
+                : launch_bwd<false>(dy, s, w, rstd, nullptr, ds, partial, nw, rows, h, st);
+  if (rc) return rc;
+  const int splits = nw >= 256 ? 16 : 1;
+  dim3 grid((h + 255) / 256, splits);
+  colsum_kernel<<<grid, 256, 0, st>>>(partial, dw_out, nw, h, splits);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,111 @@
+"""In-tree build of the scaletorch_amd HIP kernel library for gfx950.
+
+Every ``csrc/*.hip`` file is compiled by ``hipcc --offload-arch=gfx950`` into an
+object (pure HIP, no torch headers -> seconds per file); ``csrc/bindings.cpp``
+(the TORCH_LIBRARY registrations) is compiled as host C++ against the PyTorch
+headers; everything is linked into ``scaletorch_amd/_st_kernels.so``, which
+``scaletorch_amd.ops`` loads with ``torch.ops.load_library``.  The ``.so``
+lives inside the package so it travels with the repository snapshot to the GPU
+box (it is git-ignored but not gpurun-ignored).
+
+Builds are incremental (object newer than its source and ``common.h``) and
+run in parallel.  No hipify step, no CUDA sources: the kernels are written for
+CDNA4 directly.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+PKG = Path(__file__).resolve().parent
+BUILD = ROOT / "build" / "st_kernels"
+LIB = PKG / "_st_kernels.so"
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+
+
+def _hipcc() -> str:
+    p = ROCM / "bin" / "hipcc"
+    return str(p) if p.exists() else (shutil.which("hipcc") or "hipcc")
+
+
+def _torch_paths():
+    import torch  # noqa: F401
+    from torch.utils import cpp_extension as ce
+
+    try:
+        inc = ce.include_paths(device_type="cuda")
+        libs = ce.library_paths(device_type="cuda")
+    except TypeError:  # older signature
+        inc = ce.include_paths(cuda=True)
+        libs = ce.library_paths(cuda=True)
+    return inc, libs
+
+
+def _stale(obj: Path, deps) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def _run(cmd, verbose: bool):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build step failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -> Path:
+    """Compile all kernels for ``gfx950`` and link ``_st_kernels.so``; returns its path."""
+    BUILD.mkdir(parents=True, exist_ok=True)
+    hip_srcs = sorted(CSRC.glob("*.hip"))
+    headers = sorted(CSRC.glob("*.h"))
+    hipcc = _hipcc()
+    common_flags = ["-O3", "-std=c++17", "-fPIC"]
+    inc, libdirs = _torch_paths()
+
+    jobs_list = []
+    objs = []
+    for src in hip_srcs:
+        obj = BUILD / (src.stem + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [src, *headers]):
+            jobs_list.append([hipcc, f"--offload-arch={ARCH}", *common_flags, "-c", str(src), "-o", str(obj)])
+    bsrc = CSRC / "bindings.cpp"
+    bobj = BUILD / "bindings.o"
+    objs.append(bobj)
+    if force or _stale(bobj, [bsrc]):
+        cxx = shutil.which("g++") or "c++"
+        inc_flags = [f"-I{p}" for p in inc] + [f"-I{ROCM / 'include'}"]
+        jobs_list.append(
+            [cxx, *common_flags, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-D_GLIBCXX_USE_CXX11_ABI=1",
+             *inc_flags, "-c", str(bsrc), "-o", str(bobj)]
+        )
+    n = jobs or min(8, os.cpu_count() or 4)
+    if jobs_list:
+        with cf.ThreadPoolExecutor(max_workers=n) as ex:
+            list(ex.map(lambda c: _run(c, verbose), jobs_list))
+    if force or jobs_list or not LIB.exists() or _stale(LIB, objs):
+        tmp = LIB.with_suffix(".so.tmp")
+        link = [hipcc, "-shared", f"--offload-arch={ARCH}", "-fPIC", *map(str, objs), "-o", str(tmp)]
+        for d in libdirs:
+            link += [f"-L{d}", f"-Wl,-rpath,{d}"]
+        link += ["-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch", "-lamdhip64"]
+        _run(link, verbose)
+        os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    p = build(verbose="-v" in sys.argv, force="--force" in sys.argv)
+    print(p)

@@ -1,0 +1,228 @@
+"""Mixture-of-Experts MLP (Qwen3-MoE / Mixtral) with autograd-aware expert parallelism.
+
+Reference: MoERouter / MoEExperts / MoELayer in scaletorch/models/model_qwen3_moe.py:30-292
+and dispatch/gather in scaletorch/parallel/expert_parallel/ep_comms.py.  Fixes
+and MI355X-first changes:
+
+* dispatch/combine all-to-alls are autograd Functions (backward = the reverse
+  all-to-all), so router and experts receive gradients under EP > 1 (the
+  reference detached them);
+* ONE hidden-state all-to-all each way per layer (expert ids / weights never
+  travel: the permutation is recomputed locally), plus one tiny count exchange;
+* tokens are sorted by expert once (device-side ``argsort``/``bincount``), so
+  every expert runs one contiguous GEMM over its rows (no per-expert
+  ``nonzero`` host syncs, reference model_qwen3_moe.py:143-171);
+* local experts are stored STACKED ([E_local, 2I, h] gate|up and
+  [E_local, h, I] down) for grouped GEMMs; checkpoints expand them to the
+  reference's ``moe.experts.experts.{e}.{gate,up,down}_proj.weight`` keys;
+* the Switch-style load-balancing aux loss is returned to the trainer and added
+  to the LM loss (the reference computed and dropped it).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from ..dist import collectives as C
+from ..parallel import mesh
+from ..parallel.tensor_parallel import (AllGatherFromSequenceParallelRegion, ReduceFromTensorParallelRegion,
+                                        ReduceScatterToSequenceParallelRegion)
+from .config import ModelConfig
+
+
+class _AllToAll(torch.autograd.Function):
+    """Variable-split all-to-all of rows; backward is the reverse exchange."""
+
+    @staticmethod
+    def forward(ctx, x, out_splits, in_splits, group):
+        ctx.splits = (out_splits, in_splits)
+        ctx.group = group
+        return C.all_to_all(x.contiguous(), group=group, output_split_sizes=out_splits, input_split_sizes=in_splits)
+
+    @staticmethod
+    def backward(ctx, g):
+        out_splits, in_splits = ctx.splits
+        return (C.all_to_all(g.contiguous(), group=ctx.group, output_split_sizes=in_splits,
+                             input_split_sizes=out_splits), None, None, None)
+
+
+def all_to_all_rows(x, out_splits, in_splits, group):
+    if C.get_world_size(group) == 1:
+        return x
+    return _AllToAll.apply(x, out_splits, in_splits, group)
+
+
+class MoERouter(nn.Module):
+    """Top-k softmax router (reference model_qwen3_moe.py:30-92)."""
+
+    def __init__(self, hidden: int, num_experts: int, top_k: int, norm_topk_prob: bool, aux_coef: float,
+                 init_std: float = 0.02):
+        super().__init__()
+        self.num_experts, self.top_k = num_experts, top_k
+        self.norm_topk_prob, self.aux_coef = norm_topk_prob, aux_coef
+        self.init_std = init_std
+        self.gate = nn.Linear(hidden, num_experts, bias=False)
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        nn.init.normal_(self.gate.weight, std=self.init_std)
+
+    def forward(self, x2d: torch.Tensor):
+        logits = ops.linear(x2d, self.gate.weight).float()
+        probs = torch.softmax(logits, dim=-1)
+        topw, topi = torch.topk(probs, self.top_k, dim=-1)
+        if self.norm_topk_prob:
+            topw = topw / topw.sum(-1, keepdim=True)
+        # Switch aux loss: coef * E * sum_e f_e * P_e
+        T = x2d.shape[0]
+        counts = torch.zeros(self.num_experts, device=x2d.device, dtype=torch.float32)
+        counts.scatter_add_(0, topi.reshape(-1), torch.ones_like(topi.reshape(-1), dtype=torch.float32))
+        f = counts / max(1, T * self.top_k)
+        P = probs.mean(0)
+        aux = self.aux_coef * self.num_experts * (f * P).sum()
+        return topw, topi, aux
+
+
+class MoEExperts(nn.Module):
+    """Stacked local experts: ``w_gate_up`` [E, 2I/tp, h], ``w_down`` [E, h, I/tp]."""
+
+    def __init__(self, num_local: int, hidden: int, inter: int, init_std: float = 0.02):
+        super().__init__()
+        tp = mesh.tp_size()
+        if inter % tp:
+            raise ValueError(f"moe_intermediate_size {inter} not divisible by tp {tp}")
+        self.num_local, self.hidden, self.inter = num_local, hidden, inter // tp
+        self.init_std = init_std
+        self.w_gate_up = nn.Parameter(torch.empty(num_local, 2 * self.inter, hidden))
+        self.w_down = nn.Parameter(torch.empty(num_local, hidden, self.inter))
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        with torch.no_grad():
+            self.w_gate_up.normal_(0.0, self.init_std)
+            self.w_down.normal_(0.0, self.init_std)
+
+    def forward(self, x: torch.Tensor, counts: list[int]) -> torch.Tensor:
+        """x: rows grouped by local expert (``counts[e]`` rows each)."""
+        outs = []
+        off = 0
+        for e, n in enumerate(counts):
+            if n == 0:
+                continue
+            xe = x[off: off + n]
+            gu = torch.matmul(xe, self.w_gate_up[e].t())
+            outs.append(torch.matmul(ops.swiglu(gu), self.w_down[e].t()))
+            off += n
+        if not outs:
+            return x.new_zeros(0, self.hidden)
+        return torch.cat(outs, 0)
+
+
+class MoELayer(nn.Module):
+    def __init__(self, cfg: ModelConfig, sequence_parallel: bool = False):
+        super().__init__()
+        ep = mesh.ep_size()
+        if cfg.num_experts % ep:
+            raise ValueError(f"num_experts {cfg.num_experts} not divisible by ep {ep}")
+        self.num_experts, self.top_k = cfg.num_experts, cfg.num_experts_per_tok
+        self.ep, self.ep_rank = ep, mesh.ep_rank()
+        self.num_local = cfg.num_experts // ep
+        self.hidden = cfg.hidden_size
+        self.sequence_parallel = sequence_parallel and mesh.tp_size() > 1
+        self.router = MoERouter(cfg.hidden_size, cfg.num_experts, cfg.num_experts_per_tok, cfg.norm_topk_prob,
+                                cfg.router_aux_loss_coef, cfg.initializer_range)
+        self.experts = MoEExperts(self.num_local, cfg.hidden_size, cfg.moe_intermediate_size, cfg.initializer_range)
+        for p in self.experts.parameters():
+            p._st_expert = True  # reduced over the expert-DP group, not dense-DP
+        self.last_aux_loss: torch.Tensor | None = None
+
+    def reset_parameters(self) -> None:
+        self.router.reset_parameters()
+        self.experts.reset_parameters()
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        tp_group = mesh.tp_group()
+        tp = mesh.tp_size()
+        if self.sequence_parallel:
+            # route on the local sequence shard, then gather tokens + routing
+            # results: gradients of both come back summed over TP by the
+            # reduce-scatter, which is exactly the sum of the TP partials.
+            B = x.shape[0]
+            topw, topi, aux = self.router(x.reshape(-1, x.shape[-1]))
+            k = self.top_k
+            topw = AllGatherFromSequenceParallelRegion.apply(topw.view(B, -1, k), tp_group).reshape(-1, k)
+            topi = C.all_gather(topi.view(B, -1, k).transpose(0, 1).contiguous(),
+                                group=tp_group).transpose(0, 1).reshape(-1, k)
+            x = AllGatherFromSequenceParallelRegion.apply(x, tp_group)
+            x2 = x.reshape(-1, x.shape[-1])
+        else:
+            x2 = x.reshape(-1, x.shape[-1])
+            topw, topi, aux = self.router(x2)
+            if tp > 1:
+                # experts see TP-partial intermediate shards: sum their input /
+                # combine-weight gradients over TP in backward
+                from ..parallel.tensor_parallel import CopyToTensorParallelRegion
+
+                x2 = CopyToTensorParallelRegion.apply(x2, tp_group)
+                topw = CopyToTensorParallelRegion.apply(topw, tp_group)
+        shape = x.shape
+        T = x2.shape[0]
+        self.last_aux_loss = aux if self.training else None
+        flat_e = topi.reshape(-1)  # [T*k]
+        order = torch.argsort(flat_e, stable=True)
+        tok = order // self.top_k
+        counts = torch.bincount(flat_e, minlength=self.num_experts)
+        xs = x2.index_select(0, tok)  # rows sorted by global expert
+        if self.ep == 1:
+            y = self.experts(xs, counts.tolist())
+        else:
+            group = mesh.pgm.ep_group
+            # counts per (dest rank, local expert); exchange the full matrix once
+            send_mat = counts.view(self.ep, self.num_local)
+            recv_mat = C.all_to_all(send_mat.contiguous(), group=group)  # [src, local expert]
+            mats = torch.stack([send_mat, recv_mat]).cpu()  # one host sync per layer
+            send_splits = mats[0].sum(1).tolist()
+            recv_mat_h = mats[1]
+            recv_splits = recv_mat_h.sum(1).tolist()
+            xr = all_to_all_rows(xs, recv_splits, send_splits, group)  # grouped [src][expert]
+            # regroup received rows expert-major: [expert][src]
+            idx = []
+            starts = torch.zeros_like(recv_mat_h)
+            flat = recv_mat_h.reshape(-1)
+            starts.view(-1)[1:] = torch.cumsum(flat, 0)[:-1]
+            for e in range(self.num_local):
+                for s in range(self.ep):
+                    n = int(recv_mat_h[s, e])
+                    if n:
+                        b = int(starts[s, e])
+                        idx.append(torch.arange(b, b + n))
+            perm = torch.cat(idx).to(x.device) if idx else torch.zeros(0, dtype=torch.long, device=x.device)
+            ye = self.experts(xr.index_select(0, perm), recv_mat_h.sum(0).tolist())
+            yr = torch.empty_like(ye)
+            yr = yr.index_copy(0, perm, ye) if perm.numel() else ye
+            y = all_to_all_rows(yr, send_splits, recv_splits, group)
+        w = topw.reshape(-1).index_select(0, order).to(y.dtype)
+        out = torch.zeros(T, shape[-1], device=x.device, dtype=y.dtype)
+        out = out.index_add(0, tok, y * w[:, None])
+        out = out.view(shape)
+        # expert down-projections are TP partial sums: reduce once, after the combine
+        if self.sequence_parallel:
+            out = ReduceScatterToSequenceParallelRegion.apply(out, tp_group)
+        elif mesh.tp_size() > 1:
+            out = ReduceFromTensorParallelRegion.apply(out, tp_group)
+        return out
+
+    # reference checkpoint names: experts.experts.{e}.{gate,up,down}_proj.weight
+    def reference_items(self) -> dict[str, torch.Tensor]:
+        out = {}
+        I = self.experts.inter
+        for e in range(self.num_local):
+            gu = self.experts.w_gate_up[e].detach()
+            out[f"experts.experts.{e}.gate_proj.weight"] = gu[:I]
+            out[f"experts.experts.{e}.up_proj.weight"] = gu[I:]
+            out[f"experts.experts.{e}.down_proj.weight"] = self.experts.w_down[e].detach()
+        return out

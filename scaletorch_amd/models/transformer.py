@@ -1,0 +1,264 @@
+"""Decoder-only transformer: Llama-2/3, Qwen3 (QK-norm, tied embeddings),
+Qwen3-MoE and Mixtral (MoE MLP), built TP/SP/CP/PP/EP-aware from the mesh.
+
+Reference: scaletorch/models/llama.py (Llama), model_qwen3.py (Qwen3),
+model_qwen3_moe.py (Qwen3-MoE).  Module / parameter names follow the reference
+contract (``embedding``, ``decoder_layers.{i}.{input_layernorm, attention,
+post_attention_layernorm, mlp|moe}``, ``final_norm``, ``final_proj``) so
+checkpoints map 1:1; the fused QKV / gate-up GEMMs are split back into
+``q_proj/k_proj/v_proj`` and ``gate_proj/up_proj`` by
+``reference_state_dict``.
+
+Hot path per layer on MI355X (all bf16):
+  add+RMSNorm (HIP)  -> QKV GEMM (hipBLASLt) -> RoPE in place + flash fwd (HIP)
+  -> out_proj GEMM -> add+RMSNorm (HIP) -> gate|up GEMM -> SwiGLU (HIP) -> down GEMM
+The residual add of every sub-block is fused into the next norm kernel: layers
+pass ``(x, residual)`` pairs, so no standalone elementwise add kernel runs.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+from torch.utils.checkpoint import checkpoint as torch_checkpoint
+
+from .. import ops
+from ..parallel import mesh
+from ..parallel.tensor_parallel import (ColumnParallelLinear, FusedColumnParallelLinear, RowParallelLinear,
+                                        ScatterToSequenceParallelRegion, VocabParallelEmbedding,
+                                        AllGatherFromSequenceParallelRegion)
+from .config import ModelConfig
+
+
+class Attention(nn.Module):
+    def __init__(self, cfg: ModelConfig, layer_idx: int, sequence_parallel: bool = False):
+        super().__init__()
+        tp = mesh.tp_size()
+        H, Hkv, D = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+        if H % tp or Hkv % tp:
+            raise ValueError(f"heads ({H}, kv {Hkv}) must be divisible by tp={tp}")
+        self.layer_idx = layer_idx
+        self.H, self.Hkv, self.D = H // tp, Hkv // tp, D
+        self.scale = 1.0 / math.sqrt(D)
+        init = dict(init=cfg.init, init_std=cfg.initializer_range)
+        self.qkv_proj = FusedColumnParallelLinear(cfg.hidden_size, [H * D, Hkv * D, Hkv * D],
+                                                  ["q_proj", "k_proj", "v_proj"], bias=cfg.attention_bias,
+                                                  sequence_parallel=sequence_parallel, **init)
+        self.out_proj = RowParallelLinear(H * D, cfg.hidden_size, bias=False, sequence_parallel=sequence_parallel,
+                                          **init)
+        self.qk_norm = cfg.qk_norm
+        if cfg.qk_norm:
+            self.q_norm = ops.RMSNorm(D, eps=cfg.rms_norm_eps)
+            self.k_norm = ops.RMSNorm(D, eps=cfg.rms_norm_eps)
+
+    def reset_parameters(self) -> None:
+        self.qkv_proj.reset_parameters()
+        self.out_proj.reset_parameters()
+        if self.qk_norm:
+            self.q_norm.reset_parameters()
+            self.k_norm.reset_parameters()
+
+    def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor,
+                position_ids: torch.Tensor | None) -> torch.Tensor:
+        qkv = self.qkv_proj(x)
+        B, S = qkv.shape[0], qkv.shape[1]
+        H, Hkv, D = self.H, self.Hkv, self.D
+        if self.qk_norm:
+            q, k, v = qkv.view(B, S, H + 2 * Hkv, D).split([H, Hkv, Hkv], dim=2)
+            q = self.q_norm(q.contiguous())
+            k = self.k_norm(k.contiguous())
+            qkv = torch.cat([q, k, v], dim=2).view(B, S, -1)
+        if mesh.cp_size() > 1:
+            from ..parallel.context_parallel import context_parallel_attention
+
+            out = context_parallel_attention(qkv, cos, sin, position_ids, H, Hkv, D, self.scale)
+        else:
+            out = ops.rope_attention(qkv, cos, sin, position_ids, H, Hkv, D, causal=True, scale=self.scale)
+        return self.out_proj(out)
+
+
+class MLP(nn.Module):
+    """SwiGLU MLP with one fused gate|up GEMM (reference llama.py:207-249)."""
+
+    def __init__(self, cfg: ModelConfig, intermediate_size: int | None = None, sequence_parallel: bool = False):
+        super().__init__()
+        I = intermediate_size or cfg.intermediate_size
+        init = dict(init=cfg.init, init_std=cfg.initializer_range)
+        self.gate_up_proj = FusedColumnParallelLinear(cfg.hidden_size, [I, I], ["gate_proj", "up_proj"],
+                                                      sequence_parallel=sequence_parallel, **init)
+        self.down_proj = RowParallelLinear(I, cfg.hidden_size, sequence_parallel=sequence_parallel, **init)
+
+    def reset_parameters(self) -> None:
+        self.gate_up_proj.reset_parameters()
+        self.down_proj.reset_parameters()
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.down_proj(ops.swiglu(self.gate_up_proj(x)))
+
+
+class DecoderLayer(nn.Module):
+    def __init__(self, cfg: ModelConfig, layer_idx: int, sequence_parallel: bool = False):
+        super().__init__()
+        self.layer_idx = layer_idx
+        self.input_layernorm = ops.RMSNorm(cfg.hidden_size, eps=cfg.rms_norm_eps)
+        self.attention = Attention(cfg, layer_idx, sequence_parallel)
+        self.post_attention_layernorm = ops.RMSNorm(cfg.hidden_size, eps=cfg.rms_norm_eps)
+        self.is_moe = cfg.layer_is_moe(layer_idx)
+        if self.is_moe:
+            from .moe import MoELayer
+
+            self.moe = MoELayer(cfg, sequence_parallel=sequence_parallel)
+        else:
+            self.mlp = MLP(cfg, sequence_parallel=sequence_parallel)
+
+    def reset_parameters(self) -> None:
+        for m in (self.input_layernorm, self.attention, self.post_attention_layernorm,
+                  self.moe if self.is_moe else self.mlp):
+            m.reset_parameters()
+
+    def forward(self, x, residual, cos, sin, position_ids):
+        """(x, residual) -> (block output, residual stream).  ``residual`` None = first layer."""
+        if residual is None:
+            h = self.input_layernorm(x)
+            residual = x
+        else:
+            h, residual = self.input_layernorm(x, residual)
+        a = self.attention(h, cos, sin, position_ids)
+        h, residual = self.post_attention_layernorm(a, residual)
+        out = self.moe(h) if self.is_moe else self.mlp(h)
+        return out, residual
+
+
+def stage_layer_range(num_layers: int, pp_size: int, pp_rank: int,
+                      distribution: list[int] | None = None) -> tuple[int, int]:
+    """Contiguous layer range of a pipeline stage.
+
+    Default split: even, first ``remainder`` stages get one extra layer
+    (reference pipeline_parallel.py:83-133); ``distribution`` overrides it.
+    """
+    if distribution:
+        if len(distribution) != pp_size or sum(distribution) != num_layers:
+            raise ValueError(f"layer distribution {distribution} must have {pp_size} entries summing to {num_layers}")
+        start = sum(distribution[:pp_rank])
+        return start, start + distribution[pp_rank]
+    base, rem = divmod(num_layers, pp_size)
+    start = pp_rank * base + min(pp_rank, rem)
+    return start, start + base + (1 if pp_rank < rem else 0)
+
+
+class TransformerLM(nn.Module):
+    """Causal LM.  ``forward`` returns this TP rank's vocab shard of the logits
+    (last PP stage) or the hidden states to send to the next stage."""
+
+    def __init__(self, cfg: ModelConfig, sequence_parallel: bool = False, layer_distribution: list[int] | None = None):
+        super().__init__()
+        self.config = self.model_config = cfg
+        self.sequence_parallel = sequence_parallel and mesh.tp_size() > 1
+        pp, pr = mesh.pp_size(), (mesh.pgm.pp_rank if mesh.pgm else 0)
+        self.first_stage, self.last_stage = pr == 0, pr == pp - 1
+        self.layer_start, self.layer_end = stage_layer_range(cfg.num_hidden_layers, pp, pr, layer_distribution)
+        sp = self.sequence_parallel
+        std = cfg.initializer_range if cfg.init == "normal" else None
+        if self.first_stage or (cfg.tie_word_embeddings and self.last_stage):
+            self.embedding = VocabParallelEmbedding(cfg.vocab_size, cfg.hidden_size, sequence_parallel=sp, init_std=std)
+        self.decoder_layers = nn.ModuleDict(
+            {str(i): DecoderLayer(cfg, i, sp) for i in range(self.layer_start, self.layer_end)})
+        if self.last_stage:
+            self.final_norm = ops.RMSNorm(cfg.hidden_size, eps=cfg.rms_norm_eps)
+            self.final_proj = ColumnParallelLinear(cfg.hidden_size, cfg.vocab_size, bias=False,
+                                                   sequence_parallel=sp, init=cfg.init,
+                                                   init_std=cfg.initializer_range)
+            if cfg.tie_word_embeddings:
+                self.final_proj.weight = self.embedding.weight
+        cos, sin = ops.rope_tables(cfg.max_position_embeddings, cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
+        self.register_buffer("cos", cos, persistent=False)
+        self.register_buffer("sin", sin, persistent=False)
+
+    # ------------------------------------------------------------------ helpers
+    @property
+    def vocab_start(self) -> int:
+        ref = self.final_proj if self.last_stage else None
+        if ref is None:
+            return 0
+        return mesh.tp_rank() * ref.out_per_rank
+
+    def reset_parameters(self) -> None:
+        if hasattr(self, "embedding"):
+            self.embedding.reset_parameters()
+        for layer in self.decoder_layers.values():
+            layer.reset_parameters()
+        if self.last_stage:
+            self.final_norm.reset_parameters()
+            if not self.config.tie_word_embeddings:
+                self.final_proj.reset_parameters()
+
+    def aux_loss(self) -> torch.Tensor | None:
+        losses = [l.moe.last_aux_loss for l in self.decoder_layers.values()
+                  if l.is_moe and l.moe.last_aux_loss is not None]
+        if not losses:
+            return None
+        return torch.stack([x.float() for x in losses]).sum()
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, input_ids: torch.Tensor | None = None, position_ids: torch.Tensor | None = None,
+                hidden_states: torch.Tensor | None = None, gradient_checkpointing: bool = False,
+                attention_mask: torch.Tensor | None = None) -> torch.Tensor:
+        if self.first_stage:
+            x = self.embedding(input_ids)
+        else:
+            if hidden_states is None:
+                raise ValueError("hidden_states required on non-first pipeline stages")
+            x = hidden_states
+        residual = None
+        for layer in self.decoder_layers.values():
+            if gradient_checkpointing and self.training:
+                x, residual = torch_checkpoint(layer, x, residual, self.cos, self.sin, position_ids,
+                                               use_reentrant=False)
+            else:
+                x, residual = layer(x, residual, self.cos, self.sin, position_ids)
+        if not self.last_stage:
+            return x if residual is None else x + residual
+        x = self.final_norm(x) if residual is None else self.final_norm(x, residual)[0]
+        if self.sequence_parallel:
+            x = AllGatherFromSequenceParallelRegion.apply(x, mesh.tp_group())
+            from ..ops.mlp import linear
+            return linear(x, self.final_proj.weight)
+        return self.final_proj(x)
+
+    # ------------------------------------------------------------------ checkpoints in reference layout
+    def reference_state_dict(self) -> dict[str, torch.Tensor]:
+        """State dict with the reference's key names (fused layers split back)."""
+        out = {}
+        fused = {n: m for n, m in self.named_modules() if isinstance(m, FusedColumnParallelLinear)}
+        for k, v in self.state_dict().items():
+            mod = k.rsplit(".", 1)[0]
+            if mod in fused:
+                m = fused[mod]
+                parent = mod.rsplit(".", 1)[0] + "." if "." in mod else ""
+                suffix = k.rsplit(".", 1)[1]
+                for n, piece in zip(m.names, m.reference_pieces(v)):
+                    out[f"{parent}{n}.{suffix}"] = piece
+            else:
+                out[k] = v
+        if self.config.tie_word_embeddings and "final_proj.weight" in out and "embedding.weight" in out:
+            out.pop("final_proj.weight")
+        return out
+
+    def load_reference_state_dict(self, sd: dict[str, torch.Tensor], strict: bool = True):
+        sd = dict(sd)
+        fused = {n: m for n, m in self.named_modules() if isinstance(m, FusedColumnParallelLinear)}
+        for mod, m in fused.items():
+            parent = mod.rsplit(".", 1)[0] + "." if "." in mod else ""
+            for suffix in ("weight", "bias"):
+                keys = [f"{parent}{n}.{suffix}" for n in m.names]
+                if all(k in sd for k in keys):
+                    sd[f"{mod}.{suffix}"] = torch.cat([sd.pop(k) for k in keys], dim=0)
+        if self.config.tie_word_embeddings and "final_proj.weight" not in sd and hasattr(self, "final_proj"):
+            if "embedding.weight" in sd:
+                sd["final_proj.weight"] = sd["embedding.weight"]
+        return self.load_state_dict(sd, strict=strict)
+
+
+def build_model(cfg: ModelConfig, sequence_parallel: bool = False, layer_distribution=None) -> TransformerLM:
+    return TransformerLM(cfg, sequence_parallel=sequence_parallel, layer_distribution=layer_distribution)

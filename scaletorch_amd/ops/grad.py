@@ -1,0 +1,62 @@
+"""Weight-gradient plumbing shared by every fused op.
+
+When a parameter carries ``main_grad`` (an fp32 view into the flat gradient
+arena owned by :class:`scaletorch_amd.parallel.data_parallel.GradArena`), fused
+backward passes accumulate the weight gradient straight into it -- for linear
+layers with ONE GEMM whose epilogue adds into the fp32 buffer (beta = 1,
+bf16 x bf16 -> fp32), so no bf16 ``.grad`` tensor is ever materialised and no
+separate accumulation kernel runs.  The parameter's ``_st_grad_ready`` hook
+(installed by the DP bucket manager) is then called so the bucket holding the
+parameter can start its all-reduce while the rest of backward runs.
+
+Without ``main_grad`` (plain autograd use, unit tests) the gradient is returned
+normally and autograd accumulates ``.grad``.
+"""
+from __future__ import annotations
+
+import torch
+
+_ADDMM_DTYPE_OK: bool | None = None
+
+
+def _grad_ready(param: torch.Tensor) -> None:
+    hook = getattr(param, "_st_grad_ready", None)
+    if hook is not None:
+        hook(param)
+
+
+def accumulate_grad(param: torch.Tensor, grad: torch.Tensor):
+    """Add ``grad`` into ``param.main_grad`` (returns None) or return it for autograd."""
+    mg = getattr(param, "main_grad", None)
+    if mg is None:
+        return grad.to(param.dtype) if grad.dtype != param.dtype else grad
+    mg.add_(grad.view_as(mg))
+    _grad_ready(param)
+    return None
+
+
+def accumulate_linear_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor):
+    """dW = dy^T x, accumulated into ``param.main_grad`` in fp32 when present.
+
+    Uses ``aten::addmm.dtype_out`` (bf16 operands, fp32 C/D, beta = 1) so the
+    accumulation is fused into the GEMM epilogue on hipBLASLt.
+    """
+    global _ADDMM_DTYPE_OK
+    mg = getattr(param, "main_grad", None)
+    if mg is None:
+        return dy2d.t().mm(x2d)
+    if mg.dtype == dy2d.dtype:
+        mg.addmm_(dy2d.t(), x2d)
+    else:
+        done = False
+        if _ADDMM_DTYPE_OK is not False and dy2d.is_cuda:
+            try:
+                torch.ops.aten.addmm.dtype_out(mg, dy2d.t(), x2d, mg.dtype, beta=1, alpha=1, out=mg)
+                _ADDMM_DTYPE_OK = True
+                done = True
+            except (RuntimeError, NotImplementedError):
+                _ADDMM_DTYPE_OK = False
+        if not done:
+            mg.add_(dy2d.t().mm(x2d))
+    _grad_ready(param)
+    return None

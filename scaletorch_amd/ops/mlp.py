@@ -1,0 +1,69 @@
+"""SwiGLU activation and the main_grad-aware linear layer.
+
+* ``swiglu(gate_up)`` -- csrc/swiglu.hip on the output of ONE fused gate|up GEMM
+  (reference: ``down(silu(gate(x)) * up(x))``, scaletorch/models/llama.py:236-249).
+* ``linear(x, w)`` -- hipBLASLt GEMM forward; backward computes dX with one GEMM
+  and accumulates dW directly into ``w.main_grad`` (fp32) inside a second GEMM's
+  epilogue (see ops/grad.py), which is what lets the DP bucket all-reduce start
+  the moment a weight's gradient is final.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from .grad import accumulate_grad, accumulate_linear_wgrad
+
+
+class _SwiGLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        gu = gu.contiguous()
+        ctx.save_for_backward(gu)
+        return _lib.ops().swiglu_fwd(gu)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (gu,) = ctx.saved_tensors
+        return _lib.ops().swiglu_bwd(dout.contiguous(), gu)
+
+
+def swiglu_ref(gu: torch.Tensor) -> torch.Tensor:
+    g, u = gu.chunk(2, dim=-1)
+    return F.silu(g) * u
+
+
+def swiglu(gu: torch.Tensor) -> torch.Tensor:
+    if _lib.use_native(gu) and gu.dtype == torch.bfloat16 and gu.shape[-1] % 16 == 0:
+        return _SwiGLUFn.apply(gu)
+    return swiglu_ref(gu)
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        ctx.bias = bias
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx = dy.matmul(weight) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = accumulate_linear_wgrad(weight, dy2, x.reshape(-1, x.shape[-1]))
+        db = None
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = accumulate_grad(ctx.bias, dy2.float().sum(0))
+        return dx, dw, db
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """F.linear whose weight gradient goes to ``weight.main_grad`` when it exists."""
+    if getattr(weight, "main_grad", None) is not None and torch.is_grad_enabled():
+        return _LinearFn.apply(x, weight, bias)
+    return F.linear(x, weight, bias)

@@ -1,0 +1,231 @@
+"""Optimizers over flat parameter arenas + global gradient clipping.
+
+Reference: ``create_optimizer`` (scaletorch/trainer/model_builder.py:103-162:
+adamw[fused] / adam / sgd(m=0.9) / lamb->adamw) and ``clip_gradients``
+(scaletorch/trainer/train_step.py:122-136, a LOCAL clip_grad_norm_).
+
+* ``ArenaAdamW``: fp32 master weights + fp32 exp_avg / exp_avg_sq per arena;
+  on GPU one fused HIP kernel (csrc/adamw.hip) per arena updates master, m, v
+  and writes the bf16 model copy -- the whole step is 1-2 launches.  The
+  reference kept bf16 params AND bf16 optimizer states (no master weights).
+* the clip coefficient is computed on device from the GLOBAL norm (squared
+  norms all-reduced over the model-parallel group with TP/EP replicas counted
+  once, data_parallel.py ``grad_sumsq_segments``) and read by the kernel from
+  device memory: no host sync unless the norm is logged.
+* ``ArenaSGD`` / ``ArenaAdam`` / ``ArenaLAMB`` cover the other reference choices.
+Each subclasses ``torch.optim.Optimizer`` so torch LR schedulers drive ``lr``.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .dist import collectives as C
+from .ops import _lib
+
+
+class _ArenaOptimizer(torch.optim.Optimizer):
+    def __init__(self, dp_model, lr: float, defaults: dict):
+        self.dp = dp_model
+        arenas = dp_model.arenas
+        params = [a.param_flat for a in arenas]
+        super().__init__([{"params": [p]} for p in params], dict(lr=lr, **defaults))
+        self.arenas = arenas
+        self._step = 0
+        for a in arenas:
+            a.master = a.param_flat.detach().float().clone() if a.param_flat.dtype != torch.float32 else None
+        self.clip_coef = None
+        self.last_grad_norm = None
+
+    # fp32 view of the weights the update is applied to
+    @staticmethod
+    def _master(a):
+        return a.master if a.master is not None else a.param_flat
+
+    def zero_grad(self, set_to_none: bool = False) -> None:  # noqa: ARG002
+        self.dp.zero_grad()
+
+    # ---------------------------------------------------------------- clipping
+    def grad_norm(self, mp_group=None) -> torch.Tensor:
+        """Global L2 norm of the gradients (device scalar, fp32)."""
+        segs = self.dp.grad_sumsq_segments()
+        dev = segs[0][0].device
+        total = torch.zeros(1, dtype=torch.float32, device=dev)
+        for t, w in segs:
+            if t.numel() == 0:
+                continue
+            if _lib.use_native(t) and t.numel() % 4 == 0:
+                part = torch.zeros(1, dtype=torch.float32, device=dev)
+                _lib.ops().sumsq_(t, part)
+                total += part * w
+            else:
+                total += t.float().pow(2).sum() * w
+        if mp_group is not None and C.get_world_size(mp_group) > 1:
+            C.all_reduce(total, group=mp_group)
+        return total.sqrt()
+
+    def clip_grad_norm_(self, max_norm: float | None, mp_group=None) -> torch.Tensor:
+        norm = self.grad_norm(mp_group)
+        self.last_grad_norm = norm
+        if max_norm is not None and max_norm > 0:
+            self.clip_coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+        else:
+            self.clip_coef = None
+        return norm
+
+    # ---------------------------------------------------------------- state
+    def state_dict(self):
+        return {
+            "step": self._step,
+            "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups],
+            "arenas": [self._arena_state(a) for a in self.arenas],
+        }
+
+    def _arena_state(self, a) -> dict:
+        return {"master": None if a.master is None else a.master.detach().cpu()}
+
+    def load_state_dict(self, sd):
+        self._step = sd["step"]
+        for g, s in zip(self.param_groups, sd["param_groups"]):
+            g.update(s)
+        for a, s in zip(self.arenas, sd["arenas"]):
+            self._load_arena_state(a, s)
+
+    def _load_arena_state(self, a, s) -> None:
+        if s.get("master") is not None and a.master is not None:
+            a.master.copy_(s["master"].to(a.master.device))
+            a.param_flat.copy_(a.master.to(a.param_flat.dtype))
+
+
+class ArenaAdamW(_ArenaOptimizer):
+    def __init__(self, dp_model, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, fused: bool = True, decoupled: bool = True):
+        super().__init__(dp_model, lr, dict(betas=tuple(betas), eps=eps, weight_decay=weight_decay))
+        self.fused = fused
+        self.decoupled = decoupled
+        for a in self.arenas:
+            a.exp_avg = torch.zeros(a.numel, dtype=torch.float32, device=a.param_flat.device)
+            a.exp_avg_sq = torch.zeros_like(a.exp_avg)
+
+    @torch.no_grad()
+    def step(self, closure=None):  # noqa: ARG002
+        self._step += 1
+        t = self._step
+        for g, a in zip(self.param_groups, self.arenas):
+            lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
+            master = self._master(a)
+            if (self.fused and self.decoupled and _lib.use_native(a.param_flat) and a.master is not None
+                    and a.param_flat.dtype == torch.bfloat16):
+                _lib.ops().adamw_step_(master, a.exp_avg, a.exp_avg_sq, a.grad_flat, a.param_flat,
+                                       self.clip_coef, lr, b1, b2, eps, wd, t)
+                continue
+            grad = a.grad_flat.float()
+            if self.clip_coef is not None:
+                grad = grad * self.clip_coef
+            if not self.decoupled and wd:
+                grad = grad + wd * master
+            a.exp_avg.mul_(b1).add_(grad, alpha=1 - b1)
+            a.exp_avg_sq.mul_(b2).addcmul_(grad, grad, value=1 - b2)
+            bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
+            denom = (a.exp_avg_sq.sqrt() / math.sqrt(bc2)).add_(eps)
+            if self.decoupled and wd:
+                master.mul_(1 - lr * wd)
+            master.addcdiv_(a.exp_avg, denom, value=-lr / bc1)
+            if a.master is not None:
+                a.param_flat.copy_(master)
+
+    def _arena_state(self, a) -> dict:
+        d = super()._arena_state(a)
+        d.update(exp_avg=a.exp_avg.detach().cpu(), exp_avg_sq=a.exp_avg_sq.detach().cpu())
+        return d
+
+    def _load_arena_state(self, a, s) -> None:
+        super()._load_arena_state(a, s)
+        a.exp_avg.copy_(s["exp_avg"].to(a.exp_avg.device))
+        a.exp_avg_sq.copy_(s["exp_avg_sq"].to(a.exp_avg_sq.device))
+
+
+class ArenaAdam(ArenaAdamW):
+    """Adam with L2 (coupled) weight decay."""
+
+    def __init__(self, dp_model, **kw):
+        kw.pop("fused", None)
+        super().__init__(dp_model, fused=False, decoupled=False, **kw)
+
+
+class ArenaSGD(_ArenaOptimizer):
+    def __init__(self, dp_model, lr: float = 1e-3, momentum: float = 0.9, weight_decay: float = 0.0):
+        super().__init__(dp_model, lr, dict(momentum=momentum, weight_decay=weight_decay))
+        for a in self.arenas:
+            a.momentum_buf = torch.zeros(a.numel, dtype=torch.float32, device=a.param_flat.device)
+
+    @torch.no_grad()
+    def step(self, closure=None):  # noqa: ARG002
+        self._step += 1
+        for g, a in zip(self.param_groups, self.arenas):
+            master = self._master(a)
+            grad = a.grad_flat.float()
+            if self.clip_coef is not None:
+                grad = grad * self.clip_coef
+            if g["weight_decay"]:
+                grad = grad + g["weight_decay"] * master
+            a.momentum_buf.mul_(g["momentum"]).add_(grad)
+            master.add_(a.momentum_buf, alpha=-g["lr"])
+            if a.master is not None:
+                a.param_flat.copy_(master)
+
+    def _arena_state(self, a) -> dict:
+        d = super()._arena_state(a)
+        d["momentum"] = a.momentum_buf.detach().cpu()
+        return d
+
+    def _load_arena_state(self, a, s) -> None:
+        super()._load_arena_state(a, s)
+        a.momentum_buf.copy_(s["momentum"].to(a.momentum_buf.device))
+
+
+class ArenaLAMB(ArenaAdamW):
+    """LAMB: AdamW update rescaled per parameter by ||w|| / ||update|| (trust ratio)."""
+
+    def __init__(self, dp_model, **kw):
+        kw.pop("fused", None)
+        super().__init__(dp_model, fused=False, **kw)
+
+    @torch.no_grad()
+    def step(self, closure=None):  # noqa: ARG002
+        self._step += 1
+        t = self._step
+        for g, a in zip(self.param_groups, self.arenas):
+            lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
+            master = self._master(a)
+            grad = a.grad_flat.float()
+            if self.clip_coef is not None:
+                grad = grad * self.clip_coef
+            a.exp_avg.mul_(b1).add_(grad, alpha=1 - b1)
+            a.exp_avg_sq.mul_(b2).addcmul_(grad, grad, value=1 - b2)
+            upd = (a.exp_avg / (1 - b1 ** t)) / ((a.exp_avg_sq / (1 - b2 ** t)).sqrt() + eps)
+            if wd:
+                upd.add_(master, alpha=wd)
+            for p, o in zip(a.params, a.offsets):
+                n = p.numel()
+                w, u = master[o: o + n], upd[o: o + n]
+                wn, un = w.norm(), u.norm()
+                ratio = torch.where((wn > 0) & (un > 0), wn / un, torch.ones_like(wn))
+                w.add_(u * ratio, alpha=-lr)
+            if a.master is not None:
+                a.param_flat.copy_(master)
+
+
+def create_optimizer(dp_model, optimizer_type: str = "adamw", lr: float = 1e-3, weight_decay: float = 0.0,
+                     betas=(0.9, 0.999), eps: float = 1e-8, use_fused_adam: bool = True):
+    t = optimizer_type.lower()
+    if t == "adamw":
+        return ArenaAdamW(dp_model, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, fused=use_fused_adam)
+    if t == "adam":
+        return ArenaAdam(dp_model, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+    if t == "sgd":
+        return ArenaSGD(dp_model, lr=lr, momentum=0.9, weight_decay=weight_decay)
+    if t == "lamb":
+        return ArenaLAMB(dp_model, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+    raise ValueError(f"unknown optimizer_type {optimizer_type!r}")

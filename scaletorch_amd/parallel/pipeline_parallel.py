@@ -1,0 +1,218 @@
+"""Pipeline parallelism: stage partitioning + AFAB and 1F1B schedules over RCCL p2p.
+
+Reference: scaletorch/parallel/pipeline_parallel/{pipeline_parallel.py,pp_comms.py}.
+Differences:
+* stages are built stage-local (models/transformer.py ``stage_layer_range``:
+  same even split with the remainder on the first stages, or an explicit
+  ``layer_distribution``); embedding lives on the first stage, final
+  norm + LM head on the last;
+* every exchange is non-blocking (``batch_isend_irecv``); the paired
+  send-forward/recv-backward of the 1F1B steady state is ONE grouped RCCL call;
+* the schedule owns the loss (the reference stored it on the DP wrapper and
+  crashed with PP+DP), losses stay on device (one host sync
+  per step, at logging), and the DP gradient sync is enabled only for the last
+  backward of the stage so its buckets overlap that backward;
+* p2p shapes are known statically ([mbs, S/cp(/tp under SP), h]), no handshake.
+"""
+from __future__ import annotations
+
+from collections import deque
+
+import torch
+import torch.distributed as dist
+
+from ..dist import collectives as C
+from . import mesh
+
+_STATS = {"send_forward": 0, "recv_forward": 0, "send_backward": 0, "recv_backward": 0}
+
+
+def get_communication_stats() -> dict:
+    return dict(_STATS)
+
+
+def reset_communication_stats() -> None:
+    for k in _STATS:
+        _STATS[k] = 0
+
+
+def _p2p(send_fwd=None, send_bwd=None, recv_fwd_shape=None, recv_bwd_shape=None, dtype=torch.bfloat16,
+         device=None):
+    """One grouped exchange with the neighbouring stages; returns (recv_fwd, recv_bwd)."""
+    pg = mesh.pgm
+    group = pg.pp_group
+    ops, rf, rb = [], None, None
+    if send_fwd is not None and pg.pp_next_rank is not None:
+        ops.append(dist.P2POp(dist.isend, send_fwd.contiguous(), pg.pp_next_rank, group))
+        _STATS["send_forward"] += 1
+    if send_bwd is not None and pg.pp_prev_rank is not None:
+        ops.append(dist.P2POp(dist.isend, send_bwd.contiguous(), pg.pp_prev_rank, group))
+        _STATS["send_backward"] += 1
+    if recv_fwd_shape is not None and pg.pp_prev_rank is not None:
+        rf = torch.empty(recv_fwd_shape, dtype=dtype, device=device)
+        ops.append(dist.P2POp(dist.irecv, rf, pg.pp_prev_rank, group))
+        _STATS["recv_forward"] += 1
+    if recv_bwd_shape is not None and pg.pp_next_rank is not None:
+        rb = torch.empty(recv_bwd_shape, dtype=dtype, device=device)
+        ops.append(dist.P2POp(dist.irecv, rb, pg.pp_next_rank, group))
+        _STATS["recv_backward"] += 1
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    if rf is not None:
+        rf.requires_grad_(True)
+    return rf, rb
+
+
+def pipeline_communicate(operation: str, tensor=None, shapes=None, dtype=torch.bfloat16, device=None):
+    """Reference-compatible single-direction API (pp_comms.py:86-190)."""
+    if operation == "recv_forward":
+        return _p2p(recv_fwd_shape=shapes, dtype=dtype, device=device)[0]
+    if operation == "send_forward":
+        _p2p(send_fwd=tensor)
+        return None
+    if operation == "recv_backward":
+        return _p2p(recv_bwd_shape=shapes, dtype=dtype, device=device)[1]
+    if operation == "send_backward":
+        _p2p(send_bwd=tensor)
+        return None
+    raise ValueError(operation)
+
+
+def bidirectional_pipeline_communicate(operation: str, send_tensor, recv_shapes, dtype=torch.bfloat16, device=None):
+    if operation == "send_fwd_recv_bwd":
+        return _p2p(send_fwd=send_tensor, recv_bwd_shape=recv_shapes, dtype=dtype, device=device)[1]
+    if operation == "send_bwd_recv_fwd":
+        return _p2p(send_bwd=send_tensor, recv_fwd_shape=recv_shapes, dtype=dtype, device=device)[0]
+    raise ValueError(operation)
+
+
+class PipelineEngine:
+    """Runs one optimizer step's worth of micro-batches through this stage."""
+
+    def __init__(self, model, loss_fn, tensor_shape, dtype=torch.bfloat16, device=None,
+                 gradient_checkpointing: bool = False, aux_loss_fn=None):
+        self.model = model  # DataParallel-wrapped stage
+        self.loss_fn = loss_fn  # (logits, batch) -> scalar loss
+        self.tensor_shape = tuple(tensor_shape)
+        self.dtype, self.device = dtype, device
+        self.gc = gradient_checkpointing
+        self.aux_loss_fn = aux_loss_fn
+
+    @property
+    def _first(self):
+        return mesh.pgm.pp_is_first_stage
+
+    @property
+    def _last(self):
+        return mesh.pgm.pp_is_last_stage
+
+    def _forward(self, batch, x, num_micro):
+        out = self.model(input_ids=batch["input_ids"] if self._first else None,
+                         position_ids=batch["position_ids"], hidden_states=x, gradient_checkpointing=self.gc)
+        if self._last:
+            loss = self.loss_fn(out, batch) / num_micro
+            if self.aux_loss_fn is not None:
+                aux = self.aux_loss_fn()
+                if aux is not None:
+                    loss = loss + aux / num_micro
+            return loss
+        if self.aux_loss_fn is not None:
+            aux = self.aux_loss_fn()
+            if aux is not None:  # MoE aux loss on non-last stages: fold into the output's graph
+                out = _AttachAux.apply(out, aux / num_micro)
+        return out
+
+    def _backward(self, x, y, dy, last_backward: bool):
+        self.model.require_backward_grad_sync = last_backward
+        if self._last:
+            y.backward()
+        else:
+            torch.autograd.backward(y, dy)
+        self.model.require_backward_grad_sync = True
+        return x.grad if x is not None else None
+
+    def train_step_afab(self, data_iter, num_micro: int) -> torch.Tensor:
+        ins, outs = deque(), deque()
+        loss_sum = torch.zeros((), dtype=torch.float32, device=self.device)
+        for _ in range(num_micro):
+            x = _p2p(recv_fwd_shape=self.tensor_shape, dtype=self.dtype, device=self.device)[0]
+            batch = next(data_iter)
+            y = self._forward(batch, x, num_micro)
+            if not self._last:
+                _p2p(send_fwd=y.detach())
+            else:
+                loss_sum += y.detach().float()
+            ins.append(x)
+            outs.append(y)
+        for i in range(num_micro):
+            dy = _p2p(recv_bwd_shape=self.tensor_shape, dtype=self.dtype, device=self.device)[1]
+            x, y = ins.popleft(), outs.popleft()
+            dx = self._backward(x, y, dy, last_backward=(i == num_micro - 1))
+            _p2p(send_bwd=dx)
+        return loss_sum
+
+    def train_step_1f1b(self, data_iter, num_micro: int) -> torch.Tensor:
+        pg = mesh.pgm
+        warmup = min(pg.pp_world_size - pg.pp_rank - 1, num_micro)
+        steady = num_micro - warmup
+        ins, outs = deque(), deque()
+        loss_sum = torch.zeros((), dtype=torch.float32, device=self.device)
+        n_bwd = 0
+
+        def fwd(x):
+            batch = next(data_iter)
+            y = self._forward(batch, x, num_micro)
+            if self._last:
+                loss_sum.add_(y.detach().float())
+            return y
+
+        for _ in range(warmup):
+            x = _p2p(recv_fwd_shape=self.tensor_shape, dtype=self.dtype, device=self.device)[0]
+            y = fwd(x)
+            _p2p(send_fwd=None if self._last else y.detach())
+            ins.append(x)
+            outs.append(y)
+        x = _p2p(recv_fwd_shape=self.tensor_shape, dtype=self.dtype, device=self.device)[0] if steady > 0 else None
+        for i in range(steady):
+            y = fwd(x)
+            dy = _p2p(send_fwd=None if self._last else y.detach(), recv_bwd_shape=self.tensor_shape,
+                      dtype=self.dtype, device=self.device)[1]
+            ins.append(x)
+            outs.append(y)
+            xo, yo = ins.popleft(), outs.popleft()
+            n_bwd += 1
+            dx = self._backward(xo, yo, dy, last_backward=(n_bwd == num_micro))
+            if i == steady - 1:
+                x = None
+                _p2p(send_bwd=dx)
+            else:
+                x = _p2p(send_bwd=dx, recv_fwd_shape=self.tensor_shape, dtype=self.dtype, device=self.device)[0]
+        for _ in range(warmup):
+            xo, yo = ins.popleft(), outs.popleft()
+            dy = _p2p(recv_bwd_shape=self.tensor_shape, dtype=self.dtype, device=self.device)[1]
+            n_bwd += 1
+            dx = self._backward(xo, yo, dy, last_backward=(n_bwd == num_micro))
+            _p2p(send_bwd=dx)
+        return loss_sum
+
+
+class _AttachAux(torch.autograd.Function):
+    """Identity on ``x`` whose backward also back-propagates d(aux)=1 into the aux loss."""
+
+    @staticmethod
+    def forward(ctx, x, aux):
+        ctx.aux_shape = aux.shape
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, torch.ones(ctx.aux_shape, device=g.device, dtype=torch.float32)
+
+
+def train_step_pipeline_1f1b(engine: PipelineEngine, data_iter, num_micro: int):
+    return engine.train_step_1f1b(data_iter, num_micro)
+
+
+def train_step_pipeline_afab(engine: PipelineEngine, data_iter, num_micro: int):
+    return engine.train_step_afab(data_iter, num_micro)

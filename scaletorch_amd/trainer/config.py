@@ -1,0 +1,223 @@
+"""Training configuration / CLI.
+
+Same flag names and defaults as the reference ``ScaleTorchArguments``
+(scaletorch/trainer/config.py:31-461) so existing launch scripts work; the
+reference's env toggles (FLASH_ATTEN, CONTEXT_PARALLEL, SEQUENCE_PARALLEL, DTYPE)
+are CLI flags here, read once, and every parsed flag is honoured (the reference
+parsed but ignored several).  Extra MI355X-side flags are
+grouped in ``SystemArguments``.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import logging
+from dataclasses import dataclass, field
+
+logger = logging.getLogger(__name__)
+
+_VALID_LR_SCHEDULERS = {"linear", "cosine", "polynomial", "step", "onecycle", "constant"}
+_VALID_OPTIMIZERS = {"adamw", "adam", "sgd", "lamb"}
+
+
+@dataclass
+class DataArguments:
+    data_path: str = field(default="./data", metadata={"help": "local dataset dir / file"})
+    dataset_name: str = field(default="wikitext2", metadata={"help": "dataset name (local only, no hub access)"})
+    tokenizer_name_or_path: str = field(default="facebook/opt-125m", metadata={"help": "local tokenizer path"})
+    subset_name: str | None = field(default=None)
+    split: str = field(default="train")
+    num_proc: int = field(default=1)
+    num_workers: int = field(default=2)
+    num_samples: int | None = field(default=None)
+    pin_memory: bool = field(default=True)
+    synthetic_data: bool = field(default=False, metadata={"help": "random tokens, no dataset/tokenizer needed"})
+
+
+@dataclass
+class ModelArguments:
+    model_name_or_path: str = field(default="facebook/opt-125m",
+                                    metadata={"help": "registry name (llama3-8b, qwen3-8b, mixtral-8x7b, ...) "
+                                                      "or local HF config dir"})
+    num_hidden_layers: int | None = field(default=None)
+    num_attention_heads: int | None = field(default=None)
+    num_key_value_heads: int | None = field(default=None)
+    use_flash_attention: bool = field(default=True)
+    dtype: str = field(default="bfloat16")
+
+
+@dataclass
+class ParallelArguments:
+    tensor_parallel_size: int = field(default=1)
+    pipeline_parallel_size: int = field(default=1)
+    data_parallel_size: int = field(default=1)
+    context_parallel_size: int = field(default=1)
+    expert_parallel_size: int = field(default=1)
+    pipeline_parallel_engine: str = field(default="1f1b", metadata={"help": "1f1b | afab"})
+    backend: str = field(default="nccl", metadata={"help": "nccl (=RCCL) | gloo | hccl (maps to nccl)"})
+    sequence_parallel: bool = field(default=False, metadata={"help": "Megatron-SP over the TP group"})
+    cp_zigzag: bool = field(default=True, metadata={"help": "zig-zag load-balanced CP chunks"})
+    cp_kv_allgather: bool = field(default=False, metadata={"help": "CP via one K/V all-gather instead of a ring"})
+    layer_distribution: str | None = field(default=None, metadata={"help": "comma list of layers per PP stage"})
+
+    def __post_init__(self) -> None:
+        for name in ("data_parallel_size", "tensor_parallel_size", "pipeline_parallel_size",
+                     "context_parallel_size", "expert_parallel_size"):
+            if getattr(self, name) < 1:
+                raise ValueError(f"{name} must be >= 1, got {getattr(self, name)}")
+        if self.pipeline_parallel_engine not in {"1f1b", "afab"}:
+            raise ValueError(f'pipeline_parallel_engine must be "1f1b" or "afab", got {self.pipeline_parallel_engine}')
+        if self.backend not in {"nccl", "gloo", "hccl"}:
+            raise ValueError(f"backend must be one of {{nccl, gloo, hccl}}, got {self.backend}")
+
+
+@dataclass
+class LrSchedulerArguments:
+    lr_scheduler_type: str = field(default="linear")
+    warmup_steps: int = field(default=0)
+    T_max: int | None = field(default=None)
+    eta_min: float = field(default=0.0)
+    power: float = field(default=1.0)
+    step_size: int = field(default=1)
+    gamma: float = field(default=0.1)
+    max_lr: float | None = field(default=None)
+    pct_start: float = field(default=0.3)
+
+    def __post_init__(self) -> None:
+        if self.lr_scheduler_type not in _VALID_LR_SCHEDULERS:
+            raise ValueError(f"lr_scheduler_type must be one of {sorted(_VALID_LR_SCHEDULERS)}, got {self.lr_scheduler_type}")
+        if self.warmup_steps < 0:
+            raise ValueError(f"warmup_steps must be >= 0, got {self.warmup_steps}")
+        t = self.lr_scheduler_type
+        if t == "cosine" and self.eta_min < 0:
+            raise ValueError(f"eta_min must be >= 0, got {self.eta_min}")
+        if t == "polynomial" and self.power <= 0:
+            raise ValueError(f"power must be > 0, got {self.power}")
+        if t == "step":
+            if self.step_size <= 0:
+                raise ValueError(f"step_size must be > 0, got {self.step_size}")
+            if not 0 < self.gamma <= 1:
+                raise ValueError(f"gamma must be in (0, 1], got {self.gamma}")
+        if t == "onecycle" and not 0 < self.pct_start < 1:
+            raise ValueError(f"pct_start must be in (0, 1), got {self.pct_start}")
+
+
+@dataclass
+class OptimizerArguments:
+    optimizer_type: str = field(default="adamw")
+    weight_decay: float = field(default=0.0)
+    use_fused_adam: bool = field(default=True)
+    betas: tuple[float, float] = field(default=(0.9, 0.999))
+    learning_rate: float = field(default=1e-3)
+    adam_eps: float = field(default=1e-8)
+
+    def __post_init__(self) -> None:
+        if self.optimizer_type not in _VALID_OPTIMIZERS:
+            raise ValueError(f"optimizer_type must be one of {sorted(_VALID_OPTIMIZERS)}, got {self.optimizer_type}")
+        if self.learning_rate <= 0:
+            raise ValueError(f"learning_rate must be > 0, got {self.learning_rate}")
+        self.betas = tuple(self.betas)
+
+
+@dataclass
+class TrainingArguments:
+    batch_size: int = field(default=64)
+    test_batch_size: int = field(default=1000)
+    micro_batch_size: int | None = field(default=None)
+    gradient_accumulation_steps: int = field(default=1)
+    gradient_checkpointing: bool = field(default=False)
+    max_grad_norm: float | None = field(default=1.0)
+    epochs: int = field(default=5)
+    seed: int = field(default=1)
+    sequence_length: int | None = field(default=1024)
+    log_interval: int = field(default=1)
+    max_tokens: int | None = field(default=None)
+    total_train_steps: int | None = field(default=None)
+    use_cpu: bool = field(default=False)
+
+    def __post_init__(self) -> None:
+        if self.gradient_accumulation_steps < 1:
+            raise ValueError(f"gradient_accumulation_steps must be >= 1, got {self.gradient_accumulation_steps}")
+        if self.micro_batch_size is not None and self.micro_batch_size < 1:
+            raise ValueError(f"micro_batch_size must be >= 1, got {self.micro_batch_size}")
+        if self.sequence_length is not None and self.sequence_length < 1:
+            raise ValueError(f"sequence_length must be >= 1, got {self.sequence_length}")
+
+
+@dataclass
+class CheckpointArguments:
+    work_dir: str = field(default="./work_dir")
+    save_model_checkpoint: bool = field(default=True)
+    save_frequency: int = field(default=300)
+    resume_path: str = field(default="")
+    auto_resume: bool = field(default=False, metadata={"help": "resume from the newest step dir in work_dir"})
+    async_save: bool = field(default=True, metadata={"help": "write checkpoints from a background thread"})
+
+    def __post_init__(self) -> None:
+        if self.save_frequency < 0:
+            raise ValueError(f"save_frequency must be >= 0, got {self.save_frequency}")
+
+
+@dataclass
+class LoggingArguments:
+    use_wandb: bool = field(default=False)
+    project_name: str = field(default="scaletorch")
+    experiment_name: str | None = field(default=None)
+
+
+@dataclass
+class SystemArguments:
+    grad_reduce_dtype: str = field(default="fp32", metadata={"help": "fp32 | bf16 gradient all-reduce"})
+    bucket_size_mb: int = field(default=256, metadata={"help": "DP bucket size (MiB of fp32 gradient)"})
+    profile: bool = field(default=False, metadata={"help": "torch.profiler trace of steps 3-5"})
+    profile_dir: str = field(default="./profiles/trace")
+    nan_check: bool = field(default=True, metadata={"help": "abort on non-finite loss"})
+    timeout_s: int = field(default=600)
+    debug_collectives: bool = field(default=False, metadata={"help": "cross-check collective order across ranks"})
+
+
+@dataclass
+class ScaleTorchArguments(DataArguments, ModelArguments, ParallelArguments, LrSchedulerArguments,
+                          OptimizerArguments, TrainingArguments, CheckpointArguments, LoggingArguments,
+                          SystemArguments):
+    global_batch_size: int = field(init=False, default=0)
+    global_batch_size_token: int | None = field(init=False, default=None)
+
+    def __post_init__(self) -> None:
+        ParallelArguments.__post_init__(self)
+        LrSchedulerArguments.__post_init__(self)
+        OptimizerArguments.__post_init__(self)
+        TrainingArguments.__post_init__(self)
+        CheckpointArguments.__post_init__(self)
+        if self.micro_batch_size is None:
+            self.micro_batch_size = self.batch_size
+        cp = self.context_parallel_size
+        if self.sequence_length and cp > 1:
+            div = 2 * cp if self.cp_zigzag else cp
+            if self.sequence_length % div:
+                raise ValueError(f"sequence_length ({self.sequence_length}) must be divisible by {div} "
+                                 f"(context_parallel_size={cp}, zigzag={self.cp_zigzag})")
+        # EP ranks are data-parallel replicas (mesh.py)
+        self.global_batch_size = (self.data_parallel_size * self.expert_parallel_size * self.micro_batch_size
+                                  * self.gradient_accumulation_steps)
+        if self.sequence_length is not None:
+            self.global_batch_size_token = self.global_batch_size * self.sequence_length
+
+    def validate_world_size(self, world_size: int) -> None:
+        expected = (self.tensor_parallel_size * self.pipeline_parallel_size * self.data_parallel_size
+                    * self.context_parallel_size * self.expert_parallel_size)
+        if world_size != expected:
+            raise ValueError(f"world_size ({world_size}) != TP({self.tensor_parallel_size}) * "
+                             f"PP({self.pipeline_parallel_size}) * DP({self.data_parallel_size}) * "
+                             f"CP({self.context_parallel_size}) * EP({self.expert_parallel_size}) = {expected}")
+
+    def to_json(self) -> str:
+        return json.dumps(dataclasses.asdict(self), indent=2, default=str)
+
+
+def parse_args(argv: list[str] | None = None) -> ScaleTorchArguments:
+    from transformers import HfArgumentParser
+
+    parser = HfArgumentParser(ScaleTorchArguments)
+    (args,) = parser.parse_args_into_dataclasses(args=argv)
+    return args

@@ -1,0 +1,180 @@
+"""Trainer: builds mesh / model / arenas / optimizer / data and runs training steps.
+
+Reference flow: tools/train.py:55-418 + scaletorch/trainer/{dist_setup,model_builder,train_step}.py.
+Build order here: dist init -> mesh -> seed -> model built sharded on the
+meta-free path directly in bf16 on the GPU -> TP tags -> DataParallel arenas
+(flat bf16 params, fp32 main_grad) -> arena optimizer -> LR schedule -> data.
+
+One training step (non-PP):
+  for each micro-batch: forward -> vocab-parallel CE (+ MoE aux loss) -> backward
+  (DP buckets all-reduce asynchronously during the LAST micro-batch's backward)
+  -> global grad-norm (device) -> fused AdamW (clip coefficient read on device)
+  -> LR schedule.  Losses stay on device; ``.item()`` happens only when logging.
+"""
+from __future__ import annotations
+
+import contextlib
+import logging
+import math
+import os
+import time
+
+import torch
+
+from .. import ops
+from ..data.loader import DeviceSyntheticLoader, MicroBatchDataLoader, SyntheticTokenDataset
+from ..dist import collectives as C
+from ..dist.launch import init_dist
+from ..models import build_model, get_model_config
+from ..optim import create_optimizer
+from ..parallel import mesh
+from ..parallel.data_parallel import DataParallel, mark_tp_sharded
+from ..parallel.pipeline_parallel import PipelineEngine
+from ..utils.misc import set_all_seed
+from .lr_scheduler import create_lr_scheduler
+
+logger = logging.getLogger(__name__)
+
+_DTYPES = {"bfloat16": torch.bfloat16, "bf16": torch.bfloat16, "float16": torch.float16, "fp16": torch.float16,
+           "float32": torch.float32, "fp32": torch.float32}
+
+
+class Trainer:
+    def __init__(self, args, device_data: bool | None = None, build_data: bool = True):
+        self.args = args
+        a = args
+        self.rank, self.local_rank, self.world = init_dist(backend=a.backend, use_cpu=a.use_cpu, timeout_s=a.timeout_s)
+        a.validate_world_size(self.world)
+        if self.world > 1:
+            mesh.setup_process_group_manager(a.tensor_parallel_size, a.context_parallel_size,
+                                             a.pipeline_parallel_size, a.data_parallel_size, a.expert_parallel_size)
+        self.device = torch.device("cuda", self.local_rank) if (torch.cuda.is_available() and not a.use_cpu) \
+            else torch.device("cpu")
+        self.dtype = _DTYPES[a.dtype]
+        if self.device.type == "cpu" and self.dtype == torch.float16:
+            self.dtype = torch.float32
+        set_all_seed(a.seed)
+        overrides = dict(num_hidden_layers=a.num_hidden_layers, num_attention_heads=a.num_attention_heads,
+                         num_key_value_heads=a.num_key_value_heads)
+        self.model_config = get_model_config(a.model_name_or_path, **overrides)
+        cfg = self.model_config
+        if a.sequence_length and a.sequence_length > cfg.max_position_embeddings:
+            cfg.max_position_embeddings = a.sequence_length
+        dist_ = [int(x) for x in a.layer_distribution.split(",")] if a.layer_distribution else None
+        # build directly on the target device in the compute dtype (no meta/CPU materialisation)
+        with torch.device(self.device):
+            prev = torch.get_default_dtype()
+            torch.set_default_dtype(self.dtype if self.dtype.is_floating_point else torch.float32)
+            try:
+                model = build_model(cfg, sequence_parallel=a.sequence_parallel, layer_distribution=dist_)
+            finally:
+                torch.set_default_dtype(prev)
+        model.cos, model.sin = model.cos.float(), model.sin.float()
+        mark_tp_sharded(model)
+        self.raw_model = model
+        bucket = a.bucket_size_mb * 1024 * 1024 // 4
+        self.model = DataParallel(model, bucket_size=bucket, reduce_dtype=a.grad_reduce_dtype)
+        self.optimizer = create_optimizer(self.model, a.optimizer_type, a.learning_rate, a.weight_decay,
+                                          a.betas, a.adam_eps, a.use_fused_adam)
+        self.total_steps = a.total_train_steps or 1000
+        self.lr_scheduler = create_lr_scheduler(self.optimizer, a.lr_scheduler_type, self.total_steps,
+                                                a.warmup_steps, a.T_max, a.eta_min, a.power, a.step_size, a.gamma,
+                                                a.max_lr, a.pct_start)
+        pg = mesh.pgm
+        self.tp_group = pg.tp_group if pg else None
+        self.mp_group = pg.mp_group if pg else None
+        self.pp = pg.pp_world_size if pg else 1
+        self.cp = pg.cp_world_size if pg else 1
+        self.cp_rank = pg.cp_rank if pg else 0
+        self.tokens_per_step = a.global_batch_size * (a.sequence_length or 0)
+        self.step = 0
+        self.trained_tokens = 0
+        self.data = None
+        if build_data:
+            self.data = self._build_data(device_data if device_data is not None else a.synthetic_data)
+        if self.pp > 1:
+            S = a.sequence_length // self.cp
+            if a.sequence_parallel and mesh.tp_size() > 1:
+                S //= mesh.tp_size()
+            self.pipeline = PipelineEngine(self.model, self._loss, (a.micro_batch_size, S, cfg.hidden_size),
+                                           dtype=self.dtype, device=self.device,
+                                           gradient_checkpointing=a.gradient_checkpointing,
+                                           aux_loss_fn=model.aux_loss if cfg.is_moe else None)
+
+    # ---------------------------------------------------------------- data
+    def _build_data(self, synthetic: bool):
+        a, pg = self.args, mesh.pgm
+        data_rank = pg.data_rank if pg else 0
+        data_world = pg.data_world_size if pg else 1
+        if synthetic and self.device.type == "cuda":
+            return DeviceSyntheticLoader(self.model_config.vocab_size, a.micro_batch_size, a.sequence_length,
+                                         self.device, a.gradient_accumulation_steps, self.cp, self.cp_rank,
+                                         a.cp_zigzag, seed=a.seed, data_rank=data_rank)
+        if synthetic:
+            ds = SyntheticTokenDataset(self.model_config.vocab_size, a.sequence_length, seed=a.seed)
+        else:
+            from ..data.dataset import build_dataset
+
+            ds = build_dataset(a, a.sequence_length)
+        return MicroBatchDataLoader(ds, a.micro_batch_size, a.sequence_length, a.gradient_accumulation_steps,
+                                    data_rank, data_world, self.cp_rank, self.cp, a.cp_zigzag, seed=a.seed,
+                                    num_workers=0 if synthetic else a.num_workers,
+                                    pin_memory=a.pin_memory and self.device.type == "cuda")
+
+    def _to_device(self, batch: dict) -> dict:
+        out = {}
+        for k, v in batch.items():
+            out[k] = v.to(self.device, non_blocking=True) if isinstance(v, torch.Tensor) else v
+        return out
+
+    # ---------------------------------------------------------------- loss
+    def _loss(self, logits: torch.Tensor, batch: dict) -> torch.Tensor:
+        tgt = batch["target_ids"].to(logits.device)
+        group = self.tp_group if mesh.tp_size() > 1 else None
+        return ops.cross_entropy(logits, tgt, vocab_start=self.raw_model.vocab_start, group=group)
+
+    # ---------------------------------------------------------------- step
+    def train_step(self) -> torch.Tensor:
+        """One optimizer step; returns the mean loss as a DEVICE tensor."""
+        a = self.args
+        ga = a.gradient_accumulation_steps
+        self.optimizer.zero_grad()
+        if self.pp > 1:
+            it = (self._to_device(next(self.data)) for _ in iter(int, 1))
+            eng = self.pipeline
+            if a.pipeline_parallel_engine == "1f1b":
+                loss = eng.train_step_1f1b(it, ga)
+            else:
+                loss = eng.train_step_afab(it, ga)
+        else:
+            loss = torch.zeros((), dtype=torch.float32, device=self.device)
+            for i in range(ga):
+                batch = self._to_device(next(self.data))
+                ctx = self.model.no_sync() if i < ga - 1 else contextlib.nullcontext()
+                with ctx:
+                    logits = self.model(input_ids=batch["input_ids"], position_ids=batch["position_ids"],
+                                        gradient_checkpointing=a.gradient_checkpointing)
+                    l = self._loss(logits, batch) / ga
+                    del logits
+                    if self.model_config.is_moe:
+                        aux = self.raw_model.aux_loss()
+                        if aux is not None:
+                            l = l + aux / ga
+                    l.backward()
+                loss += l.detach().float()
+        self.optimizer.clip_grad_norm_(a.max_grad_norm, self.mp_group)
+        self.optimizer.step()
+        self.lr_scheduler.step()
+        self.step += 1
+        self.trained_tokens += self.tokens_per_step
+        return loss
+
+    def reduced_loss(self, loss: torch.Tensor) -> float:
+        """Mean loss over data-parallel replicas (last PP stage holds it); host sync."""
+        pg = mesh.pgm
+        t = loss.detach().float().clone().reshape(1)
+        if pg:
+            if pg.pp_world_size > 1:
+                C.all_reduce(t, group=pg.pp_group)  # only the last stage is non-zero
+            C.all_reduce(t, op="mean", group=pg.dense_dp_group)
+        return float(t.item())

@@ -1,0 +1,207 @@
+"""Numerics of every HIP kernel vs a plain PyTorch fp32 reference of the same op (GPU only)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from scaletorch_amd import ops  # noqa: E402
+from scaletorch_amd.ops import _lib  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    assert _lib.load(), f"HIP kernel library not loaded: {_lib.load_error()}"
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("h", [256, 4096, 5120])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_rmsnorm(h, with_res):
+    torch.manual_seed(0)
+    x = torch.randn(3, 77, h, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn_like(x, requires_grad=True) if with_res else None
+    w = (1 + 0.1 * torch.randn(h, device="cuda")).to(torch.bfloat16).requires_grad_(True)
+    if with_res:
+        y, s = ops.add_rms_norm(x, r, w, 1e-5)
+        gy, gs = torch.randn_like(y), torch.randn_like(s)
+        (y.float() * gy.float()).sum().add((s.float() * gs.float()).sum()).backward()
+    else:
+        y = ops.rms_norm(x, w, 1e-5)
+        gy = torch.randn_like(y)
+        (y.float() * gy.float()).sum().backward()
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True) if with_res else None
+    sr = xr + rr if with_res else xr
+    yr = sr * torch.rsqrt(sr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    loss = (yr * gy.float()).sum()
+    if with_res:
+        loss = loss + (sr * gs.float()).sum()
+    loss.backward()
+    assert rel(y, yr) < 1e-2
+    assert rel(x.grad, xr.grad) < 2e-2
+    assert rel(w.grad, wr.grad) < 2e-2
+    if with_res:
+        assert rel(r.grad, rr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_rope_inplace(D):
+    torch.manual_seed(0)
+    B, S, NH = 2, 100, 6
+    cos, sin = ops.rope_tables(512, D, 10000.0, device="cuda")
+    base = torch.randn(B, S, NH + 3, D, device="cuda", dtype=torch.bfloat16)
+    x = base.clone()
+    view = x[:, :, :NH]
+    pos = torch.randint(0, 512, (B, S), device="cuda")
+    _lib.ops().rope_(view, cos, sin, pos, 0, False)
+    ref = ops.apply_rope_ref(base[:, :, :NH].float(), cos, sin, pos).float()
+    assert rel(view, ref) < 1e-2
+    assert torch.equal(x[:, :, NH:], base[:, :, NH:])  # untouched tail
+    _lib.ops().rope_(view, cos, sin, pos, 0, True)  # inverse
+    assert rel(view, base[:, :, :NH]) < 1e-2
+
+
+def test_swiglu():
+    torch.manual_seed(0)
+    gu = torch.randn(5, 33, 2 * 384, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    y = ops.swiglu(gu)
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    gr = gu.detach().float().requires_grad_(True)
+    a, b = gr.chunk(2, -1)
+    yr = torch.nn.functional.silu(a) * b
+    (yr * g.float()).sum().backward()
+    assert rel(y, yr) < 1e-2
+    assert rel(gu.grad, gr.grad) < 2e-2
+
+
+def test_adamw_and_sumsq():
+    torch.manual_seed(0)
+    n = 4096 * 33
+    master = torch.randn(n, device="cuda")
+    m, v = torch.randn(n, device="cuda") * 0.01, torch.rand(n, device="cuda") * 0.01
+    g = torch.randn(n, device="cuda")
+    p = master.to(torch.bfloat16)
+    clip = torch.tensor([0.5], device="cuda")
+    mr, vr, wr = m.clone(), v.clone(), master.clone()
+    lr, b1, b2, eps, wd, t = 1e-3, 0.9, 0.95, 1e-8, 0.1, 7
+    _lib.ops().adamw_step_(master, m, v, g, p, clip, lr, b1, b2, eps, wd, t)
+    gg = g * 0.5
+    mr.mul_(b1).add_(gg, alpha=1 - b1)
+    vr.mul_(b2).addcmul_(gg, gg, value=1 - b2)
+    wr.mul_(1 - lr * wd)
+    wr.addcdiv_(mr / (1 - b1 ** t), (vr / (1 - b2 ** t)).sqrt() + eps, value=-lr)
+    assert rel(m, mr) < 1e-6 and rel(v, vr) < 1e-6
+    assert (master - wr).abs().max().item() < 1e-6
+    assert rel(p, wr) < 1e-2
+    out = torch.zeros(1, device="cuda")
+    _lib.ops().sumsq_(g, out)
+    assert abs(out.item() - g.double().pow(2).sum().item()) / g.double().pow(2).sum().item() < 1e-5
+    gb = g.to(torch.bfloat16)
+    out.zero_()
+    _lib.ops().sumsq_(gb, out)
+    ref = gb.double().pow(2).sum().item()
+    assert abs(out.item() - ref) / ref < 1e-5
+
+
+@pytest.mark.parametrize("V", [512, 32000])
+def test_cross_entropy(V):
+    torch.manual_seed(0)
+    N = 300
+    logits = (3 * torch.randn(N, V, device="cuda")).to(torch.bfloat16).requires_grad_(True)
+    tgt = torch.randint(0, V, (N,), device="cuda")
+    tgt[::17] = -100
+    loss = ops.cross_entropy(logits, tgt)
+    loss.backward()
+    lr = logits.detach().float().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(lr, tgt, ignore_index=-100)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-3 * max(1.0, ref.item())
+    assert rel(logits.grad, lr.grad) < 2e-2
+
+
+FLASH_CASES = [
+    # B, Sq, Sk, H, Hkv, D, causal
+    (2, 256, 256, 4, 4, 128, True),
+    (1, 333, 333, 8, 2, 128, True),
+    (2, 200, 320, 4, 1, 128, False),
+    (1, 128, 128, 4, 4, 64, True),
+    (2, 257, 257, 4, 2, 64, False),
+    (1, 1024, 1024, 8, 2, 128, True),
+]
+
+
+@pytest.mark.parametrize("B,Sq,Sk,H,Hkv,D,causal", FLASH_CASES)
+def test_flash_fwd_bwd(B, Sq, Sk, H, Hkv, D, causal):
+    torch.manual_seed(0)
+    q = torch.randn(B, Sq, H, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, Sk, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, Sk, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    off = Sk - Sq if causal else 0  # bottom-right aligned causal when Sq != Sk
+    out, lse = ops.flash_attn_fwd(q, k, v, scale, causal, off, 0)
+    ref_out, ref_lse = ops.sdpa_ref(q, k, v, causal, scale, off, 0)
+    assert rel(out, ref_out) < 1e-2
+    assert (lse - ref_lse).abs().max().item() < 1e-2
+    dout = torch.randn_like(out)
+    dq, dk, dv = ops.flash_attn_bwd(dout, q, k, v, out, lse, scale, causal, off, 0)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    o2, _ = ops.attention._sdpa_fp32(qr, kr, vr, causal, scale, off, 0)
+    o2.backward(dout.float())
+    assert rel(dq, qr.grad) < 2e-2
+    assert rel(dk, kr.grad) < 2e-2
+    assert rel(dv, vr.grad) < 2e-2
+
+
+def test_flash_offsets_blockwise_equals_full():
+    """Ring-attention building block: attention split into K/V blocks with global
+    offsets and merged by lse_merge_ equals full causal attention."""
+    torch.manual_seed(0)
+    B, S, H, Hkv, D = 1, 512, 4, 2, 128
+    q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    full, full_lse = ops.flash_attn_fwd(q, k, v, scale, True)
+    qs = q[:, 256:]  # second half of queries, global offset 256
+    acc = torch.zeros(B, 256, H, D, device="cuda")
+    lse = torch.full((B, H, 256), float("-inf"), device="cuda")
+    for kb in range(2):
+        ks, vs = k[:, kb * 256:(kb + 1) * 256], v[:, kb * 256:(kb + 1) * 256]
+        bo, bl = ops.flash_attn_fwd(qs, ks, vs, scale, True, 256, kb * 256)
+        _lib.ops().lse_merge_(acc, lse, bo, bl)
+    assert rel(acc, full[:, 256:]) < 1e-2
+    assert (lse - full_lse[:, :, 256:]).abs().max().item() < 1e-2
+
+
+def test_rope_attention_autograd_matches_reference():
+    torch.manual_seed(0)
+    B, S, H, Hkv, D = 2, 192, 4, 2, 128
+    cos, sin = ops.rope_tables(1024, D, 500000.0, device="cuda")
+    qkv = torch.randn(B, S, (H + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    out = ops.rope_attention(qkv.clone(), cos, sin, None, H, Hkv, D)
+    g = torch.randn_like(out)
+    (out.float() * g.float()).sum().backward()
+    gq = qkv.grad.clone()
+    qkv.grad = None
+    import os
+
+    os.environ["ST_DISABLE_NATIVE"] = "1"
+    try:
+        qf = qkv.detach().float().requires_grad_(True)
+        ref = ops.rope_attention(qf, cos, sin, None, H, Hkv, D)
+        (ref * g.float()).sum().backward()
+    finally:
+        os.environ["ST_DISABLE_NATIVE"] = "0"
+    assert rel(out, ref) < 2e-2
+    assert rel(gq, qf.grad) < 3e-2
