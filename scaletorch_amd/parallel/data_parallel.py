@@ -69,6 +69,9 @@ class GradArena:
                  use_counts: dict | None = None):
         self.name, self.group = name, group
         self.world = C.get_world_size(group)
+        # expert grads already SUM the contributions of the ep data replicas that routed tokens
+        # to them (all-to-all); dividing by ep turns that into the data-parallel mean
+        self.post_scale = 1.0 / mesh.ep_size() if name == "expert" else 1.0
         self.reduce_dtype = reduce_dtype
         self.params = params
         if not params:
@@ -161,6 +164,8 @@ class GradArena:
                 b.handle = None
             if b.comm_buf is not None and self.world > 1:
                 self.grad_flat[b.start: b.end].copy_(b.comm_buf)
+        if self.post_scale != 1.0:
+            self.grad_flat.mul_(self.post_scale)
 
     def mark_ready(self, p) -> bool:
         """Returns True when this call completed the bucket (and launched it)."""
@@ -221,6 +226,10 @@ class DataParallel(nn.Module):
                 continue
             g = dense_group if name == "dense" else expert_group
             self.arenas.append(GradArena(ps, g, name, bucket_size, reduce_dtype, use_counts=uses))
+        # TP-replicated params whose grads are TP-partial (per-head QK-norm weights; every
+        # norm / router weight under sequence parallelism): summed over TP after backward
+        self.tp_group = mesh.tp_group() if mesh.pgm else C.SINGLE
+        self.tp_partial = [p for p in params if getattr(p, "_st_tp_partial_grad", False)]
         self._arena_of = {}
         for a in self.arenas:
             for p in a.params:
@@ -260,6 +269,18 @@ class DataParallel(nn.Module):
             for a in self.arenas:
                 a.finish()
                 a.reset_counts()
+            self._reduce_tp_partial()
+
+    def _reduce_tp_partial(self) -> None:
+        if not self.tp_partial or C.get_world_size(self.tp_group) == 1:
+            return
+        flat = torch.cat([p.main_grad.reshape(-1) for p in self.tp_partial])
+        C.all_reduce(flat, group=self.tp_group)
+        off = 0
+        for p in self.tp_partial:
+            n = p.numel()
+            p.main_grad.copy_(flat[off: off + n].view_as(p.main_grad))
+            off += n
 
     # ---------------------------------------------------------------- API
     def forward(self, *args, **kwargs):
@@ -288,6 +309,7 @@ class DataParallel(nn.Module):
                 a.launch(b)
             a.finish()
             a.reset_counts()
+        self._reduce_tp_partial()
 
     reset = zero_grad
 

@@ -270,8 +270,22 @@ class ColumnParallelLinear(nn.Module):
         self.bias = nn.Parameter(torch.zeros(self.out_per_rank)) if bias else None
         self.reset_parameters()
 
+    def _row_pieces(self) -> list[int]:
+        return [self.out_features]
+
     def reset_parameters(self) -> None:
-        _init_shard_(self.weight, self.init, self.init_std, self.in_features)
+        from .init import init_full
+
+        key = getattr(self, "_st_init_key", None)
+        if key is None:
+            _init_shard_(self.weight, self.init, self.init_std, self.in_features)
+        else:
+            full = init_full((self.out_features, self.in_features), self.init, self.init_std, self.in_features,
+                             key, self.weight.device)
+            r = C.get_rank(self.group) if self.tp > 1 else 0
+            shards = [p.chunk(self.tp, dim=0)[r] for p in full.split(self._row_pieces(), dim=0)]
+            with torch.no_grad():
+                self.weight.copy_(torch.cat(shards, dim=0))
         if self.bias is not None:
             nn.init.zeros_(self.bias)
 
@@ -307,7 +321,17 @@ class RowParallelLinear(nn.Module):
         self.reset_parameters()
 
     def reset_parameters(self) -> None:
-        _init_shard_(self.weight, self.init, self.init_std, self.in_features)
+        from .init import init_full
+
+        key = getattr(self, "_st_init_key", None)
+        if key is None:
+            _init_shard_(self.weight, self.init, self.init_std, self.in_features)
+        else:
+            full = init_full((self.out_features, self.in_features), self.init, self.init_std, self.in_features,
+                             key, self.weight.device)
+            r = C.get_rank(self.group) if self.tp > 1 else 0
+            with torch.no_grad():
+                self.weight.copy_(full.chunk(self.tp, dim=1)[r])
         if self.bias is not None:
             nn.init.zeros_(self.bias)
 
@@ -343,6 +367,9 @@ class FusedColumnParallelLinear(ColumnParallelLinear):
                 raise ValueError(f"fused piece {s} not divisible by tp {self.tp}")
         self.local_splits = [s // self.tp for s in splits]
 
+    def _row_pieces(self) -> list[int]:
+        return self.splits
+
     def split_output(self, y: torch.Tensor) -> list[torch.Tensor]:
         return list(y.split(self.local_splits, dim=-1))
 
@@ -375,9 +402,17 @@ class VocabParallelEmbedding(nn.Module):
         self.reset_parameters()
 
     def reset_parameters(self) -> None:
+        from .init import init_full
+
         std = self.init_std if self.init_std is not None else 1.0 / math.sqrt(self.embedding_dim)
+        key = getattr(self, "_st_init_key", None)
         with torch.no_grad():
-            self.weight.normal_(0.0, std)
+            if key is None:
+                self.weight.normal_(0.0, std)
+            else:
+                full = init_full((self.num_embeddings, self.embedding_dim), "normal", std, self.embedding_dim, key,
+                                 self.weight.device)
+                self.weight.copy_(full.chunk(self.tp, dim=0)[self.rank])
 
     def forward(self, ids: torch.Tensor) -> torch.Tensor:
         from .embedding import embedding

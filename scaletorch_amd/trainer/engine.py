@@ -48,12 +48,19 @@ class Trainer:
         if self.world > 1:
             mesh.setup_process_group_manager(a.tensor_parallel_size, a.context_parallel_size,
                                              a.pipeline_parallel_size, a.data_parallel_size, a.expert_parallel_size)
+        if a.context_parallel_size > 1:
+            from ..parallel.context_parallel import set_cp_zigzag
+
+            set_cp_zigzag(a.cp_zigzag)
         self.device = torch.device("cuda", self.local_rank) if (torch.cuda.is_available() and not a.use_cpu) \
             else torch.device("cpu")
         self.dtype = _DTYPES[a.dtype]
         if self.device.type == "cpu" and self.dtype == torch.float16:
             self.dtype = torch.float32
         set_all_seed(a.seed)
+        from ..parallel.init import set_init_seed
+
+        set_init_seed(a.seed)
         overrides = dict(num_hidden_layers=a.num_hidden_layers, num_attention_heads=a.num_attention_heads,
                          num_key_value_heads=a.num_key_value_heads)
         self.model_config = get_model_config(a.model_name_or_path, **overrides)
