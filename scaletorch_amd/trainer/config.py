@@ -107,7 +107,7 @@ class OptimizerArguments:
     optimizer_type: str = field(default="adamw")
     weight_decay: float = field(default=0.0)
     use_fused_adam: bool = field(default=True)
-    betas: tuple[float, float] = field(default=(0.9, 0.999))
+    betas: list[float] = field(default_factory=lambda: [0.9, 0.999], metadata={"help": "two floats"})
     learning_rate: float = field(default=1e-3)
     adam_eps: float = field(default=1e-8)
 

@@ -1,0 +1,208 @@
+"""Checkpoint save / resume in the reference layout + HF safetensors import.
+
+Reference: CheckpointManager and init helpers in scaletorch/utils/checkpoint.py:23-560.
+Layout (kept byte-for-byte so tooling and resume scripts carry over):
+  {work_dir}/{step}/weights_tp_rank_world_size={tp}_{tpws}_pp_rank_world_size={pp}_{ppws}.pth
+  {work_dir}/{step}/scheduler.pt
+with ``{"model", "optimizer", "trained_steps", "trained_tokens"}`` per file and
+model keys in the reference naming (``reference_state_dict``).  Additions:
+``_ep_rank_world_size={ep}_{epws}`` is appended only when EP > 1 (the
+reference's EP shards overwrote each other); writes can run on a background
+thread after a device->host copy so the training loop does not stall on disk;
+``latest_checkpoint`` enables torchrun auto-resume.  Loading always uses
+``torch.load(weights_only=True)``.
+"""
+from __future__ import annotations
+
+import glob
+import json
+import logging
+import os
+import re
+import threading
+from pathlib import Path
+
+import torch
+
+from ..dist import collectives as C
+from ..parallel import mesh
+
+logger = logging.getLogger(__name__)
+
+
+def checkpoint_filename(tp_rank: int, tp_ws: int, pp_rank: int, pp_ws: int, ep_rank: int = 0, ep_ws: int = 1) -> str:
+    name = f"weights_tp_rank_world_size={tp_rank}_{tp_ws}_pp_rank_world_size={pp_rank}_{pp_ws}"
+    if ep_ws > 1:
+        name += f"_ep_rank_world_size={ep_rank}_{ep_ws}"
+    return name + ".pth"
+
+
+def _coords():
+    pg = mesh.pgm
+    if not pg:
+        return 0, 1, 0, 1, 0, 1, 0, 0
+    return (pg.tp_rank, pg.tp_world_size, pg.pp_rank, pg.pp_world_size, pg.ep_rank, pg.ep_world_size,
+            pg.dp_rank, pg.cp_rank)
+
+
+def _to_cpu(obj):
+    if isinstance(obj, torch.Tensor):
+        return obj.detach().to("cpu", copy=True)
+    if isinstance(obj, dict):
+        return {k: _to_cpu(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_cpu(v) for v in obj)
+    return obj
+
+
+def latest_checkpoint(work_dir: str) -> str | None:
+    steps = []
+    for d in glob.glob(os.path.join(work_dir, "*")):
+        b = os.path.basename(d)
+        if b.isdigit() and glob.glob(os.path.join(d, "weights_*.pth")):
+            steps.append(int(b))
+    return os.path.join(work_dir, str(max(steps))) if steps else None
+
+
+class CheckpointManager:
+    def __init__(self, work_dir: str = "./work_dir", async_save: bool = True):
+        self.work_dir = work_dir
+        self.async_save = async_save
+        self._thread: threading.Thread | None = None
+
+    def wait(self) -> None:
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+
+    def save_checkpoint(self, model, optimizer, trained_steps: int, trained_tokens: int, out_dir: str | None = None,
+                        lr_scheduler=None) -> str:
+        tp, tpws, pp, ppws, ep, epws, dp, cp = _coords()
+        out_dir = out_dir or os.path.join(self.work_dir, str(trained_steps))
+        path = os.path.join(out_dir, checkpoint_filename(tp, tpws, pp, ppws, ep, epws))
+        raw = getattr(model, "module", model)
+        writer = dp == 0 and cp == 0  # one copy per (tp, pp, ep) shard
+        if writer:
+            os.makedirs(out_dir, exist_ok=True)
+            sd = raw.reference_state_dict() if hasattr(raw, "reference_state_dict") else raw.state_dict()
+            payload = {"model": _to_cpu(sd), "optimizer": _to_cpu(optimizer.state_dict()),
+                       "trained_steps": trained_steps, "trained_tokens": trained_tokens}
+            sched = _to_cpu(lr_scheduler.state_dict()) if lr_scheduler is not None else None
+            self.wait()
+
+            def _write():
+                tmp = path + ".tmp"
+                torch.save(payload, tmp, _use_new_zipfile_serialization=True)
+                os.replace(tmp, path)
+                if sched is not None and tp == 0 and pp == 0 and ep == 0:
+                    torch.save(sched, os.path.join(out_dir, "scheduler.pt"))
+
+            if self.async_save:
+                self._thread = threading.Thread(target=_write, daemon=False)
+                self._thread.start()
+            else:
+                _write()
+        return path
+
+    def load_checkpoint(self, model, optimizer, resume_path: str, lr_scheduler=None, strict: bool = True):
+        """Returns (trained_steps, trained_tokens)."""
+        tp, tpws, pp, ppws, ep, epws, _, _ = _coords()
+        path = os.path.join(resume_path, checkpoint_filename(tp, tpws, pp, ppws, ep, epws))
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"checkpoint {path} not found")
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        for k in ("model", "optimizer", "trained_steps", "trained_tokens"):
+            if k not in ck:
+                raise KeyError(f"checkpoint {path} missing key {k!r}")
+        raw = getattr(model, "module", model)
+        with torch.no_grad():
+            if hasattr(raw, "load_reference_state_dict"):
+                raw.load_reference_state_dict(ck["model"], strict=strict)
+            else:
+                raw.load_state_dict(ck["model"], strict=strict)
+        if optimizer is not None:
+            optimizer.load_state_dict(ck["optimizer"])
+        sp = os.path.join(resume_path, "scheduler.pt")
+        if lr_scheduler is not None and os.path.exists(sp):
+            lr_scheduler.load_state_dict(torch.load(sp, weights_only=True))
+        return int(ck["trained_steps"]), int(ck["trained_tokens"])
+
+
+# ------------------------------------------------------------------ HF safetensors import
+_HF_MAP = [
+    (r"^model\.embed_tokens\.weight$", "embedding.weight"),
+    (r"^model\.norm\.weight$", "final_norm.weight"),
+    (r"^lm_head\.weight$", "final_proj.weight"),
+    (r"^model\.layers\.(\d+)\.self_attn\.o_proj\.", r"decoder_layers.\1.attention.out_proj."),
+    (r"^model\.layers\.(\d+)\.self_attn\.([qkv])_proj\.", r"decoder_layers.\1.attention.\2_proj."),
+    (r"^model\.layers\.(\d+)\.self_attn\.([qk])_norm\.", r"decoder_layers.\1.attention.\2_norm."),
+    (r"^model\.layers\.(\d+)\.mlp\.gate\.weight$", r"decoder_layers.\1.moe.router.gate.weight"),
+    (r"^model\.layers\.(\d+)\.block_sparse_moe\.gate\.weight$", r"decoder_layers.\1.moe.router.gate.weight"),
+    (r"^model\.layers\.(\d+)\.mlp\.experts\.(\d+)\.(gate|up|down)_proj\.", r"decoder_layers.\1.moe.experts.experts.\2.\3_proj."),
+    (r"^model\.layers\.(\d+)\.block_sparse_moe\.experts\.(\d+)\.w1\.", r"decoder_layers.\1.moe.experts.experts.\2.gate_proj."),
+    (r"^model\.layers\.(\d+)\.block_sparse_moe\.experts\.(\d+)\.w3\.", r"decoder_layers.\1.moe.experts.experts.\2.up_proj."),
+    (r"^model\.layers\.(\d+)\.block_sparse_moe\.experts\.(\d+)\.w2\.", r"decoder_layers.\1.moe.experts.experts.\2.down_proj."),
+    (r"^model\.layers\.(\d+)\.mlp\.(gate|up|down)_proj\.", r"decoder_layers.\1.mlp.\2_proj."),
+    (r"^model\.layers\.(\d+)\.(input_layernorm|post_attention_layernorm)\.", r"decoder_layers.\1.\2."),
+]
+
+
+def hf_to_internal_name(name: str) -> str | None:
+    for pat, rep in _HF_MAP:
+        if re.search(pat, name):
+            return re.sub(pat, rep, name)
+    return None
+
+
+def _tp_slice(name: str, t: torch.Tensor, tp: int, rank: int) -> torch.Tensor:
+    if tp == 1:
+        return t
+    if any(s in name for s in ("q_proj", "k_proj", "v_proj", "gate_proj", "up_proj", "final_proj", "embedding")):
+        if "experts.experts" in name and "down_proj" not in name:
+            return t.chunk(tp, 0)[rank]
+        return t.chunk(tp, 0)[rank]
+    if any(s in name for s in ("out_proj", "down_proj")):
+        return t.chunk(tp, 1)[rank]
+    return t
+
+
+def load_hf_safetensors(model, path: str, strict: bool = False) -> list[str]:
+    """Load this rank's shard of an HF checkpoint dir (single file or sharded index) into ``model``.
+
+    Only the tensors of this PP stage / EP shard are read (safetensors memory-maps the files).
+    Returns the list of internal names loaded.
+    """
+    from safetensors import safe_open
+
+    raw = getattr(model, "module", model)
+    tp = mesh.tp_size()
+    tpr = mesh.tp_rank()
+    ep, epr = mesh.ep_size(), mesh.ep_rank()
+    files = sorted(glob.glob(os.path.join(path, "*.safetensors")))
+    if not files:
+        raise FileNotFoundError(f"no *.safetensors under {path}")
+    wanted = set(raw.reference_state_dict().keys())
+    sd = {}
+    for f in files:
+        with safe_open(f, framework="pt") as fh:
+            for name in fh.keys():
+                iname = hf_to_internal_name(name)
+                if iname is None:
+                    continue
+                m = re.match(r"(.*moe\.experts\.experts\.)(\d+)(\..*)", iname)
+                if m and ep > 1:
+                    e = int(m.group(2))
+                    per = raw.config.num_experts // ep
+                    if e // per != epr:
+                        continue
+                    iname = f"{m.group(1)}{e % per}{m.group(3)}"
+                if iname not in wanted and not (iname == "embedding.weight" and "final_proj.weight" in wanted):
+                    continue
+                sd[iname] = _tp_slice(iname, fh.get_tensor(name), tp, tpr)
+    if raw.config.tie_word_embeddings and "final_proj.weight" in wanted and "final_proj.weight" not in sd \
+            and "embedding.weight" in sd:
+        sd["final_proj.weight"] = sd["embedding.weight"]
+    with torch.no_grad():
+        raw.load_reference_state_dict({k: v.to(next(raw.parameters()).dtype) for k, v in sd.items()}, strict=strict)
+    # arenas: params are views into the flat buffer, so the copy landed there; refresh fp32 masters
+    return sorted(sd)
