@@ -200,9 +200,13 @@ class DataParallel(nn.Module):
     """
 
     def __init__(self, module: nn.Module, bucket_size: int = 64 * 1024 * 1024,
-                 reduce_dtype: torch.dtype | str = torch.float32, dense_group=None, expert_group=None):
+                 reduce_dtype: torch.dtype | str = torch.float32, dense_group=None, expert_group=None,
+                 expose_grads: bool = False):
         super().__init__()
         self.module = module
+        # expose_grads: after the sync, point ``p.grad`` at the reduced main_grad so stock
+        # torch.optim optimizers can be used (examples); the arena optimizers read main_grad
+        self.expose_grads = expose_grads
         if isinstance(reduce_dtype, str):
             reduce_dtype = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
                             "bfloat16": torch.bfloat16}[reduce_dtype]
@@ -244,6 +248,10 @@ class DataParallel(nn.Module):
         """Params whose grads come through plain autograd (no fused op)."""
         if p.grad is None:
             return
+        if self.expose_grads and p.grad.data_ptr() == p.main_grad.data_ptr():
+            p.grad = None  # stale exposed view from the previous step: autograd accumulated into main_grad
+            self._grad_ready(p)
+            return
         p.main_grad.add_(p.grad.view_as(p.main_grad))
         p.grad = None
         self._grad_ready(p)
@@ -270,6 +278,14 @@ class DataParallel(nn.Module):
                 a.finish()
                 a.reset_counts()
             self._reduce_tp_partial()
+            self._expose()
+
+    def _expose(self) -> None:
+        if not self.expose_grads:
+            return
+        for a in self.arenas:
+            for p in a.params:
+                p.grad = p.main_grad if p.main_grad.dtype == p.dtype else p.main_grad.to(p.dtype)
 
     def _reduce_tp_partial(self) -> None:
         if not self.tp_partial or C.get_world_size(self.tp_group) == 1:
