@@ -135,12 +135,7 @@ def flash_attn_bwd(dout, q, k, v, out, lse, scale: float, causal: bool, q_offset
     if _lib.use_native(q):
         return _lib.ops().flash_bwd(dout.contiguous(), q, k, v, out, lse, scale, causal, q_offset,
                                     k_offset, dq, dk, dv)
-    with torch.enable_grad():
-        qq = q.detach().float().requires_grad_(True)
-        kk = k.detach().float().requires_grad_(True)
-        vv = v.detach().float().requires_grad_(True)
-        o, _ = _sdpa_fp32(qq, kk, vv, causal, scale, q_offset, k_offset)
-        gq, gk, gv = torch.autograd.grad(o, (qq, kk, vv), dout.float())
+    gq, gk, gv = flash_bwd_ref(dout, q, k, v, out, lse, scale, causal, q_offset, k_offset)
     res = []
     for g, dst, ref in ((gq, dq, q), (gk, dk, k), (gv, dv, v)):
         if dst is not None:
@@ -149,6 +144,34 @@ def flash_attn_bwd(dout, q, k, v, out, lse, scale: float, causal: bool, q_offset
         else:
             res.append(g.to(ref.dtype))
     return tuple(res)
+
+
+def flash_bwd_ref(dout, q, k, v, out, lse, scale, causal, q_offset=0, k_offset=0):
+    """fp32 reference of the flash backward for one K/V block, using the GIVEN
+    (possibly global, ring-merged) ``out`` and ``lse`` -- exactly what the HIP kernel computes."""
+    B, Sq, H, D = q.shape
+    Sk, Hkv = k.shape[1], k.shape[2]
+    g = H // Hkv
+    qf = q.float().permute(0, 2, 1, 3)
+    kf = k.float().permute(0, 2, 1, 3).repeat_interleave(g, dim=1)
+    vf = v.float().permute(0, 2, 1, 3).repeat_interleave(g, dim=1)
+    do = dout.float().permute(0, 2, 1, 3)
+    o = out.float().permute(0, 2, 1, 3)
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if causal:
+        qi = torch.arange(Sq, device=q.device)[:, None] + q_offset
+        ki = torch.arange(Sk, device=q.device)[None, :] + k_offset
+        s = s.masked_fill(ki > qi, float("-inf"))
+    p = torch.exp(s - lse.float()[..., None]).nan_to_num(0.0)
+    dv = torch.matmul(p.transpose(-1, -2), do)
+    dp = torch.matmul(do, vf.transpose(-1, -2))
+    delta = (do * o).sum(-1, keepdim=True)
+    ds = p * (dp - delta)
+    dq = torch.matmul(ds, kf) * scale
+    dk = torch.matmul(ds.transpose(-1, -2), qf) * scale
+    dk = dk.view(B, Hkv, g, Sk, D).sum(2)
+    dv = dv.view(B, Hkv, g, Sk, D).sum(2)
+    return dq.permute(0, 2, 1, 3), dk.permute(0, 2, 1, 3), dv.permute(0, 2, 1, 3)
 
 
 def _sdpa_fp32(q, k, v, causal, scale, q_offset, k_offset):

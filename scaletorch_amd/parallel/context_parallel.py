@@ -125,6 +125,128 @@ class _CPAttnFn(torch.autograd.Function):
         return dq, dkv_local.contiguous(), None, None, None, None, None
 
 
+def _chunks_of(rank: int, S: int, cp: int, s: int, zigzag: bool):
+    """[(local offset, length, global start)] of one rank's sequence shard."""
+    if zigzag:
+        a, b, c = zigzag_chunk_starts(S, cp, rank)
+        return [(0, c, a), (c, c, b)]
+    return [(0, s, rank * s)]
+
+
+def _ring_exchange(tensors: list[torch.Tensor], group, cp: int, rank: int):
+    """Async send of ``tensors`` to the next CP rank / receive from the previous one."""
+    import torch.distributed as dist
+
+    nxt = C.global_rank_of(group, (rank + 1) % cp)
+    prv = C.global_rank_of(group, (rank - 1) % cp)
+    recv = [torch.empty_like(t) for t in tensors]
+    ops = []
+    for t, r in zip(tensors, recv):
+        ops.append(dist.P2POp(dist.isend, t, nxt, group))
+        ops.append(dist.P2POp(dist.irecv, r, prv, group))
+    return recv, dist.batch_isend_irecv(ops)
+
+
+class _RingAttnFn(torch.autograd.Function):
+    """Ring transport: K/V (GQA-sized, packed) rotate around the CP ring; each
+    step's block attention runs the flash kernel with global offsets while the
+    next block is in flight (async RCCL p2p); partial results are combined by
+    the LSE-merge kernel.  Backward rotates K/V again together with an fp32
+    dK/dV accumulator that arrives back at its owner after cp hops."""
+
+    @staticmethod
+    def forward(ctx, q, kv, H, Hkv, D, scale, zigzag):
+        group, cp, rank = _cp()
+        B, s = q.shape[0], q.shape[1]
+        S = s * cp
+        qch = _chunks_of(rank, S, cp, s, zigzag)
+        acc = [torch.zeros(B, n, H, D, dtype=torch.float32, device=q.device) for _, n, _ in qch]
+        lse = [torch.full((B, H, n), float("-inf"), dtype=torch.float32, device=q.device) for _, n, _ in qch]
+        cur = kv.contiguous()
+        for j in range(cp):
+            src = (rank - j) % cp
+            pending = None
+            if j < cp - 1:
+                nxt_kv, pending = _ring_exchange([cur], group, cp, rank)
+            for (ko, kn, kg) in _chunks_of(src, S, cp, s, zigzag):
+                kc, vc = cur[:, ko: ko + kn, :Hkv], cur[:, ko: ko + kn, Hkv:]
+                for i, (qo, qn, qg) in enumerate(qch):
+                    if kg > qg + qn - 1:
+                        continue  # block entirely in the future
+                    bo, bl = ops.flash_attn_fwd(q[:, qo: qo + qn], kc, vc, scale, True, qg, kg)
+                    _merge(acc[i], lse[i], bo, bl)
+            if pending is not None:
+                for w in pending:
+                    w.wait()
+                cur = nxt_kv[0]
+        out = torch.cat([a.to(q.dtype) for a in acc], dim=1) if len(acc) > 1 else acc[0].to(q.dtype)
+        ctx.save_for_backward(q, kv, out, *lse)
+        ctx.meta = (H, Hkv, D, scale, zigzag)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, kv, out = ctx.saved_tensors[:3]
+        lses = ctx.saved_tensors[3:]
+        H, Hkv, D, scale, zigzag = ctx.meta
+        group, cp, rank = _cp()
+        B, s = q.shape[0], q.shape[1]
+        S = s * cp
+        qch = _chunks_of(rank, S, cp, s, zigzag)
+        dout = dout.contiguous()
+        dq = torch.zeros(q.shape, dtype=torch.float32, device=q.device)
+        cur = kv.contiguous()
+        dkv = torch.zeros(kv.shape, dtype=torch.float32, device=q.device)
+        for j in range(cp):
+            src = (rank - j) % cp
+            pending = None
+            if j < cp - 1:
+                nxt_kv, pending = _ring_exchange([cur], group, cp, rank)
+            for (ko, kn, kg) in _chunks_of(src, S, cp, s, zigzag):
+                kc, vc = cur[:, ko: ko + kn, :Hkv], cur[:, ko: ko + kn, Hkv:]
+                for i, (qo, qn, qg) in enumerate(qch):
+                    if kg > qg + qn - 1:
+                        continue
+                    g_q, g_k, g_v = ops.flash_attn_bwd(dout[:, qo: qo + qn], q[:, qo: qo + qn], kc, vc,
+                                                       out[:, qo: qo + qn].contiguous(), lses[i], scale, True,
+                                                       qg, kg)
+                    dq[:, qo: qo + qn] += g_q.float()
+                    dkv[:, ko: ko + kn, :Hkv] += g_k.float()
+                    dkv[:, ko: ko + kn, Hkv:] += g_v.float()
+            # the dK/dV accumulator travels with its K/V block (cp hops in total -> back home)
+            moved, pend2 = _ring_exchange([dkv], group, cp, rank)
+            if pending is not None:
+                for w in pending:
+                    w.wait()
+                cur = nxt_kv[0]
+            for w in pend2:
+                w.wait()
+            dkv = moved[0]
+        return dq.to(q.dtype), dkv.to(kv.dtype), None, None, None, None, None
+
+
+def _merge(acc: torch.Tensor, lse: torch.Tensor, bo: torch.Tensor, bl: torch.Tensor) -> None:
+    """acc/lse <- online-softmax combination with a block result (HIP kernel on GPU)."""
+    if _lib.use_native(acc):
+        _lib.ops().lse_merge_(acc, lse, bo, bl)
+        return
+    L = torch.logaddexp(lse, bl)
+    wa = torch.exp(lse - L).nan_to_num(0.0).transpose(1, 2)[..., None]
+    wb = torch.exp(bl - L).nan_to_num(0.0).transpose(1, 2)[..., None]
+    acc.copy_(acc * wa + bo.float() * wb)
+    lse.copy_(L)
+
+
+_CP_COMM = "allgather"
+
+
+def set_cp_comm(mode: str) -> None:
+    global _CP_COMM
+    if mode not in ("allgather", "ring"):
+        raise ValueError(f"cp_comm must be 'allgather' or 'ring', got {mode!r}")
+    _CP_COMM = mode
+
+
 def context_parallel_attention(qkv: torch.Tensor, cos, sin, position_ids, H: int, Hkv: int, D: int,
                                scale: float, zigzag: bool | None = None) -> torch.Tensor:
     """qkv [B, s, (H+2Hkv)*D] local CP shard -> attention output [B, s, H*D]."""
@@ -135,7 +257,8 @@ def context_parallel_attention(qkv: torch.Tensor, cos, sin, position_ids, H: int
     q = ops.apply_rope(qkv4[:, :, :H], cos, sin, position_ids)
     k = ops.apply_rope(qkv4[:, :, H: H + Hkv], cos, sin, position_ids)
     kv = torch.cat([k, qkv4[:, :, H + Hkv:]], dim=2)
-    out = _CPAttnFn.apply(q.contiguous(), kv.contiguous(), H, Hkv, D, scale, zigzag)
+    fn = _RingAttnFn if _CP_COMM == "ring" else _CPAttnFn
+    out = fn.apply(q.contiguous(), kv.contiguous(), H, Hkv, D, scale, zigzag)
     return out.reshape(B, s, H * D)
 
 

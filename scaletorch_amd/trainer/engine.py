@@ -49,9 +49,10 @@ class Trainer:
             mesh.setup_process_group_manager(a.tensor_parallel_size, a.context_parallel_size,
                                              a.pipeline_parallel_size, a.data_parallel_size, a.expert_parallel_size)
         if a.context_parallel_size > 1:
-            from ..parallel.context_parallel import set_cp_zigzag
+            from ..parallel.context_parallel import set_cp_comm, set_cp_zigzag
 
             set_cp_zigzag(a.cp_zigzag)
+            set_cp_comm(a.cp_comm)
         self.device = torch.device("cuda", self.local_rank) if (torch.cuda.is_available() and not a.use_cpu) \
             else torch.device("cpu")
         self.dtype = _DTYPES[a.dtype]

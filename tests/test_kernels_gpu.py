@@ -184,6 +184,23 @@ def test_flash_offsets_blockwise_equals_full():
     assert (lse - full_lse[:, :, 256:]).abs().max().item() < 1e-2
 
 
+def test_flash_bwd_block_with_global_lse():
+    """Ring-attention backward building block: one K/V block, global (merged) out/lse."""
+    torch.manual_seed(0)
+    B, S, H, Hkv, D = 2, 256, 4, 2, 128
+    q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, 2 * S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, 2 * S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    out, lse = ops.flash_attn_fwd(q, k, v, scale, True, S, 0)  # queries at global [S, 2S)
+    dout = torch.randn_like(out)
+    for kb in range(2):
+        ks, vs = k[:, kb * S:(kb + 1) * S], v[:, kb * S:(kb + 1) * S]
+        dq, dk, dv = ops.flash_attn_bwd(dout, q, ks, vs, out, lse, scale, True, S, kb * S)
+        rq, rk, rv = ops.attention.flash_bwd_ref(dout, q, ks, vs, out, lse, scale, True, S, kb * S)
+        assert rel(dq, rq) < 2e-2 and rel(dk, rk) < 2e-2 and rel(dv, rv) < 2e-2
+
+
 def test_rope_attention_autograd_matches_reference():
     torch.manual_seed(0)
     B, S, H, Hkv, D = 2, 192, 4, 2, 128

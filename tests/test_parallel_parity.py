@@ -117,9 +117,11 @@ def _compare(ref, results, atol=2e-5, rtol=2e-3):
     dict(tensor_parallel_size=2, micro_batch_size=4),
     dict(tensor_parallel_size=2, micro_batch_size=4, sequence_parallel=True),
     dict(context_parallel_size=2, micro_batch_size=4),
+    dict(context_parallel_size=2, micro_batch_size=4, cp_comm="ring"),
+    dict(context_parallel_size=2, micro_batch_size=4, cp_comm="ring", cp_zigzag=False),
     dict(pipeline_parallel_size=2, micro_batch_size=2, gradient_accumulation_steps=2),
     dict(pipeline_parallel_size=2, micro_batch_size=2, gradient_accumulation_steps=2, pipeline_parallel_engine="afab"),
-], ids=["dp2", "dp2_ga2", "tp2", "tp2_sp", "cp2", "pp2_1f1b", "pp2_afab"])
+], ids=["dp2", "dp2_ga2", "tp2", "tp2_sp", "cp2", "cp2_ring", "cp2_ring_contig", "pp2_1f1b", "pp2_afab"])
 def test_dense_parity_world2(kw):
     ref = _reference("tiny-llama")
     res = run_workers(_worker, 2, "tiny-llama", kw)
