@@ -23,7 +23,7 @@ int st_rmsnorm_bwd(const void* dy, const void* s, const void* w, const float* rs
 int st_rmsnorm_bwd_nwaves(int rows);
 int st_rope_inplace(void* x, const float* cos_t, const float* sin_t, const int64_t* pos, int B,
                     int S, int NH, int D, int64_t sB, int64_t sS, int64_t sH, int pos_offset,
-                    int backward, hipStream_t st);
+                    int backward, int64_t max_pos, hipStream_t st);
 int st_swiglu_fwd(const void* gu, void* out, int64_t N, int64_t I, hipStream_t st);
 int st_swiglu_bwd(const void* dout, const void* gu, void* dgu, int64_t N, int64_t I,
                   hipStream_t st);
@@ -68,6 +68,14 @@ void check_bf16_cuda(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16, got ", t.scalar_type());
 }
 
+// Every auxiliary tensor a kernel dereferences must live on the same GPU as
+// the primary operand: a host pointer handed to a kernel is an illegal-address
+// fault on the device, so it is rejected here instead.
+void check_same_gpu(const at::Tensor& t, const at::Tensor& ref, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.device() == ref.device(), name, " must be on ", ref.device(), ", got ",
+              t.device());
+}
+
 // ---------------------------------------------------------------- RMSNorm
 std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& res,
                                     const at::Tensor& w, double eps) {
@@ -110,6 +118,10 @@ at::Tensor rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& s, const at::Tens
   TORCH_CHECK(rstd.numel() == rows && rstd.scalar_type() == at::kFloat, "rmsnorm_bwd: rstd");
   TORCH_CHECK(dw_accum.numel() == h && dw_accum.scalar_type() == at::kFloat &&
                   dw_accum.is_contiguous(), "rmsnorm_bwd: dw_accum must be fp32 [h]");
+  check_same_gpu(dy, s, "dy");
+  check_same_gpu(w, s, "weight");
+  check_same_gpu(rstd, s, "rstd");
+  check_same_gpu(dw_accum, s, "dw_accum");
   c10::hip::HIPGuardMasqueradingAsCUDA g(s.device());
   const void* dp = nullptr;
   if (dres.has_value() && dres->defined()) {
@@ -138,10 +150,14 @@ void rope_(at::Tensor x, const at::Tensor& cos_t, const at::Tensor& sin_t,
                   cos_t.is_contiguous() && sin_t.is_contiguous() && cos_t.size(-1) == D / 2,
               "rope: tables must be fp32 contiguous [max_pos, D/2]");
   const int64_t maxpos = cos_t.size(0);
+  check_same_gpu(cos_t, x, "cos table");
+  check_same_gpu(sin_t, x, "sin table");
+  TORCH_CHECK(sin_t.sizes() == cos_t.sizes(), "rope: cos/sin tables differ in shape");
   const int64_t* pp = nullptr;
   if (pos.has_value() && pos->defined()) {
     TORCH_CHECK(pos->scalar_type() == at::kLong && pos->is_contiguous() && pos->numel() == B * S,
                 "rope: position_ids must be int64 [B,S]");
+    check_same_gpu(*pos, x, "position_ids");
     pp = pos->data_ptr<int64_t>();
   } else {
     TORCH_CHECK(S + pos_offset <= maxpos && pos_offset >= 0, "rope: positions exceed table");
@@ -149,7 +165,7 @@ void rope_(at::Tensor x, const at::Tensor& cos_t, const at::Tensor& sin_t,
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   int rc = st_rope_inplace(x.data_ptr(), cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), pp,
                            (int)B, (int)S, (int)NH, (int)D, x.stride(0), x.stride(1), x.stride(2),
-                           (int)pos_offset, backward ? 1 : 0, cur_stream());
+                           (int)pos_offset, backward ? 1 : 0, maxpos, cur_stream());
   ST_CHECK_RC(rc, "rope_");
 }
 
@@ -196,15 +212,20 @@ void adamw_step_(at::Tensor master, at::Tensor exp_avg, at::Tensor exp_avg_sq,
   TORCH_CHECK(grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16,
               "adamw: grad must be fp32 or bf16");
   TORCH_CHECK(n % 4 == 0, "adamw: arena length must be a multiple of 4");
+  check_same_gpu(exp_avg, master, "exp_avg");
+  check_same_gpu(exp_avg_sq, master, "exp_avg_sq");
+  check_same_gpu(grad, master, "grad");
   void* pp = nullptr;
   if (param.has_value() && param->defined()) {
     check_bf16_cuda(*param, "param");
+    check_same_gpu(*param, master, "param");
     TORCH_CHECK(param->numel() == n && param->is_contiguous(), "adamw: param arena");
     pp = param->data_ptr();
   }
   const float* cp = nullptr;
   if (clip_coef.has_value() && clip_coef->defined()) {
     TORCH_CHECK(clip_coef->scalar_type() == at::kFloat && clip_coef->numel() == 1, "adamw: clip");
+    check_same_gpu(*clip_coef, master, "clip_coef");
     cp = clip_coef->data_ptr<float>();
   }
   const double bc1 = 1.0 - std::pow(beta1, (double)step);
@@ -222,6 +243,7 @@ void sumsq_(const at::Tensor& g, at::Tensor out) {
   TORCH_CHECK(g.is_cuda() && g.is_contiguous() && g.numel() % 4 == 0, "sumsq: contiguous, n%4==0");
   TORCH_CHECK(g.scalar_type() == at::kFloat || g.scalar_type() == at::kBFloat16, "sumsq: dtype");
   TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= 1, "sumsq: out fp32");
+  check_same_gpu(out, g, "out");
   c10::hip::HIPGuardMasqueradingAsCUDA gd(g.device());
   auto partial = at::empty({st_sumsq_partials()}, g.options().dtype(at::kFloat));
   int rc = st_sumsq(g.data_ptr(), g.scalar_type() == at::kBFloat16 ? 1 : 0, g.numel(),
@@ -236,6 +258,7 @@ std::vector<at::Tensor> xent_fwd(const at::Tensor& logits, const at::Tensor& tgt
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "xent: logits [N, V] row-major");
   TORCH_CHECK(tgt.scalar_type() == at::kLong && tgt.is_contiguous() && tgt.numel() == logits.size(0),
               "xent: targets int64 [N]");
+  check_same_gpu(tgt, logits, "target");
   const int64_t N = logits.size(0), V = logits.size(1);
   TORCH_CHECK(V % 8 == 0 && logits.stride(0) % 8 == 0, "xent: V and row stride must be %8");
   c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
@@ -257,6 +280,11 @@ void xent_bwd_(const at::Tensor& logits, const at::Tensor& tgt, int64_t vocab_st
   TORCH_CHECK(lse.numel() == N && dloss.numel() == N && tgt.numel() == N, "xent_bwd: row vectors");
   TORCH_CHECK(lse.scalar_type() == at::kFloat && dloss.scalar_type() == at::kFloat &&
                   lse.is_contiguous() && dloss.is_contiguous(), "xent_bwd: fp32 lse/dloss");
+  TORCH_CHECK(tgt.scalar_type() == at::kLong && tgt.is_contiguous(), "xent_bwd: targets int64");
+  check_same_gpu(tgt, logits, "target");
+  check_same_gpu(lse, logits, "lse");
+  check_same_gpu(dloss, logits, "dloss");
+  check_same_gpu(dlogits, logits, "dlogits");
   c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
   int rc = st_xent_bwd(logits.data_ptr(), logits.stride(0), tgt.data_ptr<int64_t>(), N, (int)V,
                        vocab_start, lse.data_ptr<float>(), dloss.data_ptr<float>(),
@@ -286,6 +314,8 @@ std::vector<at::Tensor> flash_fwd(const at::Tensor& q, const at::Tensor& k, cons
   const int64_t B = q.size(0), Sq = q.size(1), H = q.size(2), Sk = k.size(1), Hkv = k.size(2);
   TORCH_CHECK(k.size(0) == B && v.size(0) == B && v.size(1) == Sk && v.size(2) == Hkv, "flash_fwd: k/v shapes");
   TORCH_CHECK(H % Hkv == 0, "flash_fwd: H must be a multiple of Hkv");
+  check_same_gpu(k, q, "k");
+  check_same_gpu(v, q, "v");
   c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   auto o = at::empty({B, Sq, H, D}, q.options());
   auto lse = at::empty({B, H, Sq}, q.options().dtype(at::kFloat));
@@ -321,6 +351,8 @@ std::vector<at::Tensor> flash_bwd(const at::Tensor& dout, const at::Tensor& q, c
   TORCH_CHECK(k.sizes() == v.sizes() && k.size(0) == B, "flash_bwd: k/v shapes");
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * H * Sq,
               "flash_bwd: lse [B,H,Sq] fp32");
+  TORCH_CHECK(H % Hkv == 0, "flash_bwd: H must be a multiple of Hkv");
+  for (auto* t : {&k, &v, &o, &dout, &lse}) check_same_gpu(*t, q, "flash_bwd operand");
   c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   auto delta = at::empty({B, H, Sq}, q.options().dtype(at::kFloat));
   int rc = st_flash_bwd_preprocess(o.data_ptr(), dout.data_ptr(), delta.data_ptr<float>(), (int)B,
@@ -330,6 +362,7 @@ std::vector<at::Tensor> flash_bwd(const at::Tensor& dout, const at::Tensor& q, c
   auto pick = [&](const c10::optional<at::Tensor>& t, at::IntArrayRef shape, const char* n) {
     if (t.has_value() && t->defined()) {
       check_qkv(*t, n, D);
+      check_same_gpu(*t, q, n);
       TORCH_CHECK(t->sizes() == shape, n, ": wrong shape");
       return *t;
     }
@@ -367,6 +400,10 @@ void lse_merge_(at::Tensor out, at::Tensor lse, const at::Tensor& bout, const at
                   lse.is_contiguous() && blse.is_contiguous() && lse.numel() == B * H * S &&
                   blse.numel() == B * H * S, "lse_merge: lse [B,H,S] fp32");
   TORCH_CHECK(D % 8 == 0, "lse_merge: D % 8");
+  TORCH_CHECK(out.is_cuda(), "lse_merge: out must be a GPU tensor");
+  check_same_gpu(lse, out, "lse");
+  check_same_gpu(bout, out, "block_out");
+  check_same_gpu(blse, out, "block_lse");
   c10::hip::HIPGuardMasqueradingAsCUDA g(out.device());
   int rc = st_lse_merge(out.data_ptr<float>(), lse.data_ptr<float>(), bout.data_ptr(),
                         blse.data_ptr<float>(), (int)B, (int)S, (int)H, (int)D, bout.stride(0),

@@ -20,7 +20,8 @@ __global__ __launch_bounds__(256) void rope_kernel(bf16_t* __restrict__ x, const
                                                     const float* __restrict__ sin_t,
                                                     const int64_t* __restrict__ pos, int B, int S, int NH,
                                                     int D, int64_t sB, int64_t sS, int64_t sH,
-                                                    int pos_offset, float sin_sign, int64_t total) {
+                                                    int pos_offset, float sin_sign, int64_t total,
+                                                    int64_t max_pos) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
   const int half = D >> 1;
@@ -31,7 +32,9 @@ __global__ __launch_bounds__(256) void rope_kernel(bf16_t* __restrict__ x, const
   r /= NH;
   const int s = (int)(r % S);
   const int b = (int)(r / S);
-  const int64_t p = pos ? pos[(int64_t)b * S + s] : (int64_t)(s + pos_offset);
+  int64_t p = pos ? pos[(int64_t)b * S + s] : (int64_t)(s + pos_offset);
+  // position ids are data: clamp into the table instead of reading out of bounds
+  p = p < 0 ? 0 : (p >= max_pos ? max_pos - 1 : p);
   bf16_t* base = x + b * sB + s * sS + h * sH + j * 8;
   float x1[8], x2[8], c[8], sn[8];
   unpack8(ld8(base), x1);
@@ -56,13 +59,13 @@ __global__ __launch_bounds__(256) void rope_kernel(bf16_t* __restrict__ x, const
 
 extern "C" int st_rope_inplace(void* x, const float* cos_t, const float* sin_t, const int64_t* pos,
                                int B, int S, int NH, int D, int64_t sB, int64_t sS, int64_t sH,
-                               int pos_offset, int backward, hipStream_t st) {
+                               int pos_offset, int backward, int64_t max_pos, hipStream_t st) {
   if (D % 16 != 0) return -2;
   const int64_t total = (int64_t)B * S * NH * (D / 16);
   if (total == 0) return 0;
   const int64_t blocks = (total + 255) / 256;
   rope_kernel<<<dim3((unsigned)blocks), dim3(256), 0, st>>>((bf16_t*)x, cos_t, sin_t, pos, B, S, NH, D,
                                                              sB, sS, sH, pos_offset,
-                                                             backward ? -1.f : 1.f, total);
+                                                             backward ? -1.f : 1.f, total, max_pos);
   return (int)hipGetLastError();
 }

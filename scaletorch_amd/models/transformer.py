@@ -187,7 +187,9 @@ class TransformerLM(nn.Module):
 
         assign_init_keys(self)
         self.reset_parameters()
-        cos, sin = ops.rope_tables(cfg.max_position_embeddings, cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
+        dev = next(self.parameters()).device  # tables live with the weights (kernels read them on device)
+        cos, sin = ops.rope_tables(cfg.max_position_embeddings, cfg.head_dim, cfg.rope_theta, cfg.rope_scaling,
+                                   device=dev)
         self.register_buffer("cos", cos, persistent=False)
         self.register_buffer("sin", sin, persistent=False)
 

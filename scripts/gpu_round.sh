@@ -18,7 +18,7 @@ run() {  # name timeout cmd...
   return $rc
 }
 has() { [[ " $STAGES " == *" $1 "* ]]; }
-rc_ok() { [ "$1" -le 1 ]; }
+rc_ok() { [ "$1" -eq 0 ]; }
 if has kernels; then run pytest_kernels 600 python -m pytest tests/test_kernels_gpu.py -x -q -m gpu; rc=$?; rc_ok $rc || exit $rc; fi
 if has train; then HIP_LAUNCH_BLOCKING=1 run pytest_train 400 python -m pytest tests/test_train_gpu.py -x -q -m gpu; rc=$?; rc_ok $rc || exit $rc; fi
 if has smoke; then run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; [ $rc -eq 0 ] || exit $rc; fi

@@ -71,6 +71,16 @@ def test_rope_inplace(D):
     assert rel(view, base[:, :, :NH]) < 1e-2
 
 
+def test_host_pointer_rejected_before_launch():
+    """A CPU tensor handed to a kernel must raise on the host, never reach the device."""
+    cos, sin = ops.rope_tables(64, 64, 10000.0, device="cpu")
+    x = torch.randn(1, 8, 2, 64, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        _lib.ops().rope_(x, cos, sin, None, 0, False)
+    with pytest.raises(RuntimeError):
+        _lib.ops().xent_fwd(torch.randn(4, 64, device="cuda", dtype=torch.bfloat16), torch.zeros(4, dtype=torch.long), 0)
+
+
 def test_swiglu():
     torch.manual_seed(0)
     gu = torch.randn(5, 33, 2 * 384, device="cuda", dtype=torch.bfloat16, requires_grad=True)
