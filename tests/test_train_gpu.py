@@ -32,6 +32,18 @@ def test_linear_main_grad_accumulation():
     assert rel(w.main_grad, ref) < 1e-2
 
 
+def test_wgrad_fp32_epilogue_gemm():
+    """bf16 x bf16 -> fp32 accumulate (beta=1) straight into main_grad: aten::addmm.dtype_out on hipBLASLt."""
+    torch.manual_seed(0)
+    dy = torch.randn(512, 384, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(512, 256, device="cuda", dtype=torch.bfloat16)
+    mg = torch.randn(384, 256, device="cuda", dtype=torch.float32)
+    ref = mg + dy.float().t() @ x.float()
+    torch.ops.aten.addmm.dtype_out(mg, dy.t(), x, torch.float32, beta=1, alpha=1, out=mg)
+    torch.cuda.synchronize()
+    assert rel(mg, ref) < 1e-3
+
+
 def test_embedding_main_grad():
     from scaletorch_amd.parallel.embedding import embedding
 
