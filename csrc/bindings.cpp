@@ -46,7 +46,7 @@ int st_flash_bwd_preprocess(const void* o, const void* dout, float* delta, int B
                             int D, int64_t sob, int64_t sos, int64_t soh, int64_t sdb, int64_t sds,
                             int64_t sdh, hipStream_t st);
 int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse,
-                 const float* delta, void* dq, void* dk, void* dv, float* work, int B, int Sq, int Sk,
+                 const float* delta, void* dq, void* dk, void* dv, int B, int Sq, int Sk,
                  int H, int Hkv, int D, int64_t sqb, int64_t sqs, int64_t sqh, int64_t skb,
                  int64_t sks, int64_t skh, int64_t svb, int64_t svs, int64_t svh, int64_t sdb,
                  int64_t sds, int64_t sdh, int64_t sdqb, int64_t sdqs, int64_t sdqh, int64_t sdkb,
@@ -372,15 +372,8 @@ std::vector<at::Tensor> flash_bwd(const at::Tensor& dout, const at::Tensor& q, c
   auto dk = pick(dk_out, k.sizes(), "dk_out");
   auto dv = pick(dv_out, v.sizes(), "dv_out");
   TORCH_CHECK(dk.strides() == dv.strides(), "flash_bwd: dk_out/dv_out must share strides");
-  at::Tensor work;
-  float* wp = nullptr;
-  if (H != Hkv) {
-    work = at::empty({2 * B * Sk * H * D}, q.options().dtype(at::kFloat));
-    wp = work.data_ptr<float>();
-  }
   rc = st_flash_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
-                    delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), wp,
-                    (int)B, (int)Sq, (int)Sk, (int)H, (int)Hkv, (int)D, q.stride(0), q.stride(1),
+                    delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), (int)B, (int)Sq, (int)Sk, (int)H, (int)Hkv, (int)D, q.stride(0), q.stride(1),
                     q.stride(2), k.stride(0), k.stride(1), k.stride(2), v.stride(0), v.stride(1),
                     v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2), dq.stride(0),
                     dq.stride(1), dq.stride(2), dk.stride(0), dk.stride(1), dk.stride(2),

@@ -18,18 +18,26 @@
 //     B operand (registers 8s..8s+7 -> k-step s, cdna_hip_programming.md §3);
 //     the other operand is read with ds_read_b64_tr_b16 from a row-major LDS
 //     image (T10), so no product needs an explicit transpose.
-//   * one LDS image per K/V (or Q/dO) tile, XOR-swizzled so both the 16-byte
-//     row reads and the transposed reads are bank-conflict free (T10 (b)).
-//   * register-staged double buffering (T14): the next tile's global loads are
-//     issued before the MFMAs of the current tile and written to the other LDS
-//     buffer after them -- one barrier per tile.
-//   * online softmax in base 2 with the scale folded into one multiply.
-//   * backward = 3 kernels: delta = rowsum(dO*O); dQ (per 128-query tile,
-//     iterating keys); dK/dV (per 128-key tile x query head, iterating
-//     queries) -- no atomics anywhere, bitwise deterministic; GQA groups are
-//     summed by a final bandwidth-bound pass.
-//   * causal: workgroups are launched heaviest-first and skip blocks that are
-//     entirely masked; only diagonal blocks evaluate the mask.
+//   * one LDS image per tile, XOR-swizzled so both the 16-byte row reads and the
+//     transposed reads are bank-conflict free (T2/T10).  Every LDS read in the
+//     loops is `ds_read* vaddr offset:<imm>` on a lane-constant VGPR computed
+//     once (LdsAddr); the double-buffer index is a template constant (the loop
+//     is unrolled by two), so the loops carry no LDS address arithmetic.
+//   * global -> LDS through registers (T14: issue the next tile's loads before
+//     this tile's MFMAs, write them to the other buffer after), with buffer
+//     descriptors (T8/T20): 32-bit offsets, and rows past the end of a
+//     sequence read as zero by the hardware range check -- no branches.
+//   * online softmax in base 2 with raw v_exp_f32; the O rescale is deferred
+//     until the running max grows by 2^8 (T13) and decided wave-uniformly.
+//   * only the diagonal / tail blocks evaluate the causal mask.
+//   * backward = delta = rowsum(dO*O); dQ kernel (per 128-query tile, iterating
+//     key blocks); dK/dV kernel (per 128-key tile of one kv head, iterating
+//     every query head of its GQA group x query blocks, so dK/dV are summed in
+//     registers) -- no atomics, no partial buffers, bitwise deterministic.
+//   * causal: workgroups are numbered heaviest-first so the dispatcher's
+//     greedy fill is a longest-job-first schedule.
+#include <type_traits>
+
 #include "common.h"
 
 using namespace st;
@@ -39,48 +47,87 @@ namespace {
 typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bfx4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) char lds_t;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
+constexpr float kRescaleThr = 8.f;  // log2 units: P entries stay <= 2^8 between rescales
 
 // ---- LDS tile geometry: rows of D bf16, 16-byte chunks, XOR swizzle ----
 template <int D>
+ST_DEVICE int swz(int row) {
+  if constexpr (D == 128) return ((row & 3) << 2) | ((row >> 2) & 3);
+  else return (row >> 1) & 7;
+}
+template <int D>
 ST_DEVICE int lds_off(int row, int ch) {
-  if constexpr (D == 128) {
-    return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
-  } else {
-    return row * 128 + 16 * (ch ^ ((row >> 1) & 7));
+  return row * (2 * D) + 16 * (ch ^ swz<D>(row));
+}
+
+ST_DEVICE bfx8 lds_row(const lds_t* p) {
+  return *reinterpret_cast<const bfx8 __attribute__((address_space(3)))*>(p);
+}
+ST_DEVICE bfx8 lds_tr(const lds_t* p0, const lds_t* p1) {
+  bfx4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((bfx4 __attribute__((address_space(3)))*)p0);
+  bfx4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((bfx4 __attribute__((address_space(3)))*)p1);
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// Lane-constant LDS offsets into one tile image.
+//  rowf(tile, t, kk): 8 contiguous bf16 of tile row 32t + (lane&31), chunk
+//    2kk + (lane>>5)  -- an MFMA A/B fragment in natural k order.
+//  trf(tile, rbase, s, dt): element j of lane (r = lane&31, h = lane>>5) is
+//    tile[rbase + 16s + 8(j>>2) + 4h + (j&3)][32dt + r] -- the operand whose k
+//    index runs over tile ROWS, permuted to match an accumulator fed back as
+//    the other operand (k-step s).
+// Swizzle rows only depend on row & 15 (D=128) / bits 1..3 (D=64), so the
+// 32-row sub-tile and 16-row k-step offsets are compile-time immediates.
+template <int D>
+struct LdsAddr {
+  static constexpr int NKK = D / 16, NDT = D / 32, RB = 2 * D;
+  int row[NKK];
+  int tr[NDT][2];
+  ST_DEVICE void init(int lane) {
+    const int r = lane & 31, h = lane >> 5, g = (lane >> 4) & 1, q = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) row[kk] = lds_off<D>(r, 2 * kk + h);
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+        tr[dt][hf] = lds_off<D>(4 * h + q + 8 * hf, 4 * dt + 2 * g + (pp >> 1)) + 8 * (pp & 1);
   }
-}
-
-// 8 contiguous bf16 of row `row`, chunk `ch` (MFMA A or B fragment, natural k order).
-template <int D>
-ST_DEVICE bfx8 row_frag(const lds_t* tile, int row, int ch) {
-  return *reinterpret_cast<const bfx8 __attribute__((address_space(3)))*>(tile + lds_off<D>(row, ch));
-}
-
-// Transposed fragment: element j of lane (r = lane&31, h = lane>>5) is
-//   tile[rbase + 16 s + 8 (j>>2) + 4 h + (j&3)][32 dt + r]
-// i.e. the operand whose k index runs over tile ROWS, permuted to match an
-// accumulator fed back as the other operand.
-template <int D>
-ST_DEVICE bfx8 tr_frag(const lds_t* tile, int rbase, int s, int dt, int lane) {
-  const int h = lane >> 5, g = (lane >> 4) & 1, q = (lane >> 2) & 3, p = lane & 3;
-  const int col = 32 * dt + 16 * g + 4 * p;
-  const int row0 = rbase + 16 * s + 4 * h + q;
-  const int ch = col >> 3, sub = (col & 7) * 2;
-  bfx4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-      (bfx4 __attribute__((address_space(3)))*)(tile + lds_off<D>(row0, ch) + sub));
-  bfx4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-      (bfx4 __attribute__((address_space(3)))*)(tile + lds_off<D>(row0 + 8, ch) + sub));
-  bfx8 r;
-  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
-  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
-  return r;
-}
+  ST_DEVICE bfx8 rowf(const lds_t* tile, int t, int kk) const {
+    return lds_row(tile + t * 32 * RB + row[kk]);
+  }
+  ST_DEVICE bfx8 trf(const lds_t* tile, int rbase, int s, int dt) const {
+    const lds_t* b = tile + (rbase + 16 * s) * RB;
+    return lds_tr(b + tr[dt][0], b + tr[dt][1]);
+  }
+};
 
 ST_DEVICE f32x16 mfma(bfx8 a, bfx8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// Long-lived accumulators (dQ, dK, dV) live in the AGPR file for the whole
+// loop: this file is built with -mllvm -amdgpu-mfma-vgpr-form so the
+// compiler's own MFMAs (S, dP: read by VALU right away) stay in VGPRs, and
+// these asm MFMAs pin the accumulate chains to AGPRs -- no per-iteration
+// v_accvgpr copies.  `s_nop 1` covers the VALU-write -> MFMA-read hazard of
+// the freshly converted B operand (cdna_hip_programming.md §5.7 item 2);
+// MFMA -> MFMA on the same C needs none.
+ST_DEVICE void mfma_acc(f32x16& c, bfx8 a, bfx8 b) {
+  asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+// Ends the AGPR chains before compiler code reads them (8-pass XDL result ->
+// any reader: >= 12 wait states).
+template <int N>
+ST_DEVICE void agpr_fence(f32x16 (&c)[N]) {
+  if constexpr (N == 4)
+    asm volatile("s_nop 15\n\ts_nop 3" : "+a"(c[0]), "+a"(c[1]), "+a"(c[2]), "+a"(c[3]));
+  else
+    asm volatile("s_nop 15\n\ts_nop 3" : "+a"(c[0]), "+a"(c[1]));
 }
 
 ST_DEVICE f32x16 zero16() {
@@ -90,49 +137,67 @@ ST_DEVICE f32x16 zero16() {
   return z;
 }
 
+typedef __bf16 bfx2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+ST_DEVICE bfx2 cvt2(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
+  f32x2 v = {a, b};
+  return __builtin_convertvector(v, bfx2);
+}
+
 // registers 8s..8s+7 of an accumulator -> bf16 fragment for k-step s
 ST_DEVICE bfx8 acc_frag(const f32x16& a, int s) {
-  bfx8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = static_cast<__bf16>(a[8 * s + j]);
-  return r;
+  const int o = 8 * s;
+  const bfx2 p0 = cvt2(a[o], a[o + 1]), p1 = cvt2(a[o + 2], a[o + 3]);
+  const bfx2 p2 = cvt2(a[o + 4], a[o + 5]), p3 = cvt2(a[o + 6], a[o + 7]);
+  return __builtin_shufflevector(__builtin_shufflevector(p0, p1, 0, 1, 2, 3),
+                                 __builtin_shufflevector(p2, p3, 0, 1, 2, 3), 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-// accumulator register -> row index inside the 32x32 C tile
-ST_DEVICE int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+// accumulator register -> row inside the 32x32 C tile, minus the 4h lane part
+ST_DEVICE constexpr int acc_row0(int reg) { return (reg & 3) + 8 * (reg >> 2); }
 
-// Global 16-byte row chunk of a [rows, D] tile starting at `row0`, zero past `nrows`.
-ST_DEVICE BF8 ld_chunk(const bf16_t* base, int64_t row_stride, int row, int ch, int nrows) {
-  if (row < nrows) return ld8(base + (int64_t)row * row_stride + ch * 8);
-  return BF8{{0u, 0u, 0u, 0u}};
+ST_DEVICE float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Buffer descriptor over rows [0, rows) of a [rows, D] view with a row stride
+// (elements); built from wave-uniform values only (T20) so no waterfall loops.
+ST_DEVICE rsrc_t make_rsrc(const bf16_t* base, int rows, int64_t row_stride, int D) {
+  const uint32_t bytes = rows > 0 ? (uint32_t)(((int64_t)(rows - 1) * row_stride + D) * 2) : 0u;
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
-template <int D>
-ST_DEVICE void st_chunk(lds_t* tile, int row, int ch, const BF8& v) {
-  u32x4 w;
-  w[0] = v.w[0]; w[1] = v.w[1]; w[2] = v.w[2]; w[3] = v.w[3];
-  *reinterpret_cast<u32x4 __attribute__((address_space(3)))*>(tile + lds_off<D>(row, ch)) = w;
+ST_DEVICE bfx8 bload_frag(rsrc_t rs, uint32_t off) {
+  return __builtin_bit_cast(bfx8, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
 }
 
-// Cooperative tile staging: ROWS x D bf16 by 256 threads, register-staged.
+// Cooperative register-staged copy of a ROWS x D tile (256 threads, 16 B per
+// thread per pass); rows outside the descriptor's range arrive as zeros.
 template <int D, int ROWS>
-struct Stage {
-  static constexpr int NCH = D / 8;
-  static constexpr int N = ROWS * NCH / 256;  // 16-byte chunks per thread
-  BF8 r[N];
-  ST_DEVICE void load(const bf16_t* base, int64_t row_stride, int row0, int nrows, int tid) {
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int c = tid + 256 * i, row = c / NCH, ch = c % NCH;
-      r[i] = ld_chunk(base, row_stride, row0 + row, ch, nrows);
-    }
+struct Stager {
+  static constexpr int NCH = D / 8, RPP = 256 / NCH, N = ROWS / RPP;
+  static_assert(N >= 1 && ROWS % RPP == 0, "tile rows");
+  u32x4 v[N];
+  uint32_t voff, pass_bytes, stride_bytes;
+  int lds;
+  ST_DEVICE void init(int tid, int64_t row_stride) {
+    stride_bytes = (uint32_t)(row_stride * 2);
+    voff = (uint32_t)(tid / NCH) * stride_bytes + (uint32_t)(tid % NCH) * 16u;
+    pass_bytes = RPP * stride_bytes;
+    lds = lds_off<D>(tid / NCH, tid % NCH);
   }
-  ST_DEVICE void store(lds_t* tile, int tid) const {
+  ST_DEVICE void load(rsrc_t rs, int row0) {
+    const uint32_t o = voff + (uint32_t)row0 * stride_bytes;
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int c = tid + 256 * i, row = c / NCH, ch = c % NCH;
-      st_chunk<D>(tile, row, ch, r[i]);
-    }
+    for (int i = 0; i < N; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, o + i * pass_bytes, 0, 0);
+  }
+  ST_DEVICE void store(lds_t* tile) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      *reinterpret_cast<u32x4 __attribute__((address_space(3)))*>(tile + lds + i * RPP * 2 * D) = v[i];
   }
 };
 
@@ -148,40 +213,71 @@ struct AttnParams {
   int64_t sxb, sxs, sxh;  // output strides (dQ for the dQ kernel, dK/dV for the dK/dV kernel)
 };
 
+template <int BUF>
+using Buf = std::integral_constant<int, BUF>;
+
+// Key-block range of a query tile [q0, q0+BM): blocks [0, nkb) are visible,
+// blocks >= kb_mask need the per-element mask (diagonal, or the Sk tail when
+// `tail_mask`).
+template <int BM, int BN>
+ST_DEVICE void key_blocks(const AttnParams& p, int q0, bool tail_mask, int& nkb, int& kb_mask) {
+  nkb = (p.Sk + BN - 1) / BN;
+  kb_mask = tail_mask ? p.Sk / BN : nkb;
+  if (p.causal) {
+    const int64_t last = p.q_offset + q0 + BM - 1 - p.k_offset;  // last key any row of the tile sees
+    const int64_t lim = last < 0 ? 0 : last / BN + 1;
+    if (lim < nkb) nkb = (int)lim;
+    const int64_t full = p.q_offset + q0 - p.k_offset + 1;  // keys [0, full) visible to every row
+    const int64_t fb = full <= 0 ? 0 : full / BN;
+    if (fb < kb_mask) kb_mask = (int)fb;
+  }
+}
+
+// Per-lane key limit inside key block kb for query row qg (global): key
+// 32t + acc_row0(i) + 4h is visible iff it is <= the returned value.
+ST_DEVICE int key_limit(const AttnParams& p, int kb, int BN, int64_t qg, int h, bool tail) {
+  int64_t lim = tail ? (int64_t)p.Sk - 1 - (int64_t)kb * BN : (int64_t)BN;
+  if (p.causal) {
+    const int64_t c = qg - p.k_offset - (int64_t)kb * BN;
+    if (c < lim) lim = c;
+  }
+  if (lim < -1) lim = -1;
+  return (int)lim - 4 * h;
+}
+
 // ============================================================== forward
 template <int D>
 __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(AttnParams p, bf16_t* __restrict__ o,
                                                            int64_t sob, int64_t sos, int64_t soh,
                                                            float* __restrict__ lse) {
   constexpr int BM = 128, BN = 64, NKK = D / 16, NDT = D / 32;
-  constexpr int TILE = BN * D * 2;
-  __shared__ __attribute__((aligned(16))) char smem_raw[4 * TILE];
+  constexpr int TB = BN * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];  // K0 K1 V0 V1
   lds_t* smem = (lds_t*)smem_raw;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, h = lane >> 5;
-  const int nqt = gridDim.x;
-  const int qt = p.causal ? (nqt - 1 - (int)blockIdx.x) : (int)blockIdx.x;
-  const int bh = blockIdx.y, b = bh / p.H, hq = bh % p.H, hk = hq / (p.H / p.Hkv);
-  const int q0 = qt * BM, qw = q0 + wid * 32, my_q = qw + r;
+  const int BH = p.B * p.H, nqt = (p.Sq + BM - 1) / BM, id = blockIdx.x;
+  const int qt = p.causal ? nqt - 1 - id / BH : id / BH;
+  const int bh = id % BH, b = bh / p.H, hq = bh % p.H, hk = hq / (p.H / p.Hkv);
+  const int q0 = qt * BM, my_q = q0 + wid * 32 + r;
 
-  const bf16_t* qbase = p.q + (int64_t)b * p.sqb + (int64_t)hq * p.sqh;
-  const bf16_t* kbase = p.k + (int64_t)b * p.skb + (int64_t)hk * p.skh;
-  const bf16_t* vbase = p.v + (int64_t)b * p.svb + (int64_t)hk * p.svh;
+  const rsrc_t rq = make_rsrc(p.q + (int64_t)b * p.sqb + (int64_t)hq * p.sqh, p.Sq, p.sqs, D);
+  const rsrc_t rk = make_rsrc(p.k + (int64_t)b * p.skb + (int64_t)hk * p.skh, p.Sk, p.sks, D);
+  const rsrc_t rv = make_rsrc(p.v + (int64_t)b * p.svb + (int64_t)hk * p.svh, p.Sk, p.svs, D);
 
   // Q fragments (B operand of S^T = K Q^T): lane holds Q[my_q][16kk + 8h .. +8]
   bfx8 qf[NKK];
 #pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) {
-    BF8 c = ld_chunk(qbase, p.sqs, my_q, 2 * kk + h, p.Sq);
-    qf[kk] = __builtin_bit_cast(bfx8, c);
-  }
+  for (int kk = 0; kk < NKK; ++kk)
+    qf[kk] = bload_frag(rq, (uint32_t)my_q * (uint32_t)(p.sqs * 2) + (2 * kk + h) * 16);
 
-  // key blocks this query tile needs
-  int nkb = (p.Sk + BN - 1) / BN;
-  if (p.causal) {
-    const int64_t last_key = p.q_offset + q0 + BM - 1 - p.k_offset;  // local index of last visible key
-    const int64_t lim = last_key < 0 ? 0 : last_key / BN + 1;
-    if (lim < nkb) nkb = (int)lim;
-  }
+  int nkb, kb_mask;
+  key_blocks<BM, BN>(p, q0, true, nkb, kb_mask);
+
+  LdsAddr<D> la;
+  la.init(lane);
+  Stager<D, BN> sk, sv;
+  sk.init(tid, p.sks);
+  sv.init(tid, p.svs);
 
   f32x16 oacc[NDT];
 #pragma unroll
@@ -190,80 +286,89 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(AttnParams p, bf16_t*
   const float c2 = p.scale * kLog2e;
   const int64_t qg = p.q_offset + my_q;
 
-  Stage<D, BN> sk, sv;
   if (nkb > 0) {
-    sk.load(kbase, p.sks, 0, p.Sk, tid);
-    sv.load(vbase, p.svs, 0, p.Sk, tid);
-    sk.store(smem, tid);
-    sv.store(smem + 2 * TILE, tid);
+    sk.load(rk, 0);
+    sv.load(rv, 0);
+    sk.store(smem);
+    sv.store(smem + 2 * TB);
   }
   __syncthreads();
-  int cur = 0;
-  for (int kb = 0; kb < nkb; ++kb) {
+
+  auto step = [&](auto bufc, int kb) {
+    constexpr int BUF = decltype(bufc)::value;
     const bool more = kb + 1 < nkb;
     if (more) {
-      sk.load(kbase, p.sks, (kb + 1) * BN, p.Sk, tid);
-      sv.load(vbase, p.svs, (kb + 1) * BN, p.Sk, tid);
+      sk.load(rk, (kb + 1) * BN);
+      sv.load(rv, (kb + 1) * BN);
     }
-    const lds_t* kt = smem + cur * TILE;
-    const lds_t* vt = smem + 2 * TILE + cur * TILE;
-    // S^T tiles: rows = keys 32t + acc_row, col = query (lane)
+    const lds_t* kt = smem + BUF * TB;
+    const lds_t* vt = smem + (2 + BUF) * TB;
     f32x16 s0 = zero16(), s1 = zero16();
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) {
-      s0 = mfma(row_frag<D>(kt, r, 2 * kk + h), qf[kk], s0);
-      s1 = mfma(row_frag<D>(kt, 32 + r, 2 * kk + h), qf[kk], s1);
+      s0 = mfma(la.rowf(kt, 0, kk), qf[kk], s0);
+      s1 = mfma(la.rowf(kt, 1, kk), qf[kk], s1);
     }
-    const int kbase_l = kb * BN;
-    const bool need_mask =
-        (kbase_l + BN > p.Sk) || (p.causal && (p.k_offset + kbase_l + BN - 1 > p.q_offset + q0));
-    float mx = -INFINITY;
+    if (kb >= kb_mask) {
+      const int lim = key_limit(p, kb, BN, qg, h, true);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float a = s0[i] * c2, bb = s1[i] * c2;
-      if (need_mask) {
-        const int k0 = kbase_l + acc_row(i, h), k1 = k0 + 32;
-        if (k0 >= p.Sk || (p.causal && p.k_offset + k0 > qg)) a = -INFINITY;
-        if (k1 >= p.Sk || (p.causal && p.k_offset + k1 > qg)) bb = -INFINITY;
+      for (int i = 0; i < 16; ++i) {
+        if (acc_row0(i) > lim) s0[i] = -INFINITY;
+        if (acc_row0(i) + 32 > lim) s1[i] = -INFINITY;
       }
-      s0[i] = a;
-      s1[i] = bb;
-      mx = fmaxf(mx, fmaxf(a, bb));
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m, mx);
-    const float m_use = m_new == -INFINITY ? 0.f : m_new;
-    const float alpha = exp2f(m - m_use);
-    float rs = 0.f;
+    float mx0 = fmaxf(s0[0], s1[0]), mx1 = fmaxf(s0[1], s1[1]);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      s0[i] = exp2f(s0[i] - m_use);
-      s1[i] = exp2f(s1[i] - m_use);
-      rs += s0[i] + s1[i];
+    for (int i = 2; i < 16; i += 2) {
+      mx0 = fmaxf(mx0, fmaxf(s0[i], s1[i]));
+      mx1 = fmaxf(mx1, fmaxf(s0[i + 1], s1[i + 1]));
     }
-    rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
-    m = m_new;
-    if (alpha != 1.f) {
+    float mx = fmaxf(mx0, mx1);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mxs = mx * c2;
+    if (__any(mxs > m + kRescaleThr)) {  // T13: rare after the first blocks
+      const float m_new = fmaxf(m, mxs);
+      const float alpha = (m == m_new) ? 1.f : fast_exp2(m - m_new);
+      l *= alpha;
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+      m = m_new;
     }
+    const float mu = (m == -INFINITY) ? 0.f : m;
+    float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+      s0[i] = fast_exp2(fmaf(s0[i], c2, -mu));
+      s1[i] = fast_exp2(fmaf(s1[i], c2, -mu));
+      s0[i + 1] = fast_exp2(fmaf(s0[i + 1], c2, -mu));
+      s1[i + 1] = fast_exp2(fmaf(s1[i + 1], c2, -mu));
+      r0 += s0[i];
+      r1 += s1[i];
+      r2 += s0[i + 1];
+      r3 += s1[i + 1];
+    }
+    float rs = (r0 + r1) + (r2 + r3);
+    rs += __shfl_xor(rs, 32, 64);
+    l += rs;
     const bfx8 p00 = acc_frag(s0, 0), p01 = acc_frag(s0, 1), p10 = acc_frag(s1, 0), p11 = acc_frag(s1, 1);
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) {
-      oacc[dt] = mfma(tr_frag<D>(vt, 0, 0, dt, lane), p00, oacc[dt]);
-      oacc[dt] = mfma(tr_frag<D>(vt, 0, 1, dt, lane), p01, oacc[dt]);
-      oacc[dt] = mfma(tr_frag<D>(vt, 32, 0, dt, lane), p10, oacc[dt]);
-      oacc[dt] = mfma(tr_frag<D>(vt, 32, 1, dt, lane), p11, oacc[dt]);
+      oacc[dt] = mfma(la.trf(vt, 0, 0, dt), p00, oacc[dt]);
+      oacc[dt] = mfma(la.trf(vt, 0, 1, dt), p01, oacc[dt]);
+      oacc[dt] = mfma(la.trf(vt, 32, 0, dt), p10, oacc[dt]);
+      oacc[dt] = mfma(la.trf(vt, 32, 1, dt), p11, oacc[dt]);
     }
     if (more) {
-      sk.store(smem + (cur ^ 1) * TILE, tid);
-      sv.store(smem + 2 * TILE + (cur ^ 1) * TILE, tid);
+      sk.store(smem + (BUF ^ 1) * TB);
+      sv.store(smem + (2 + (BUF ^ 1)) * TB);
     }
     __syncthreads();
-    cur ^= 1;
+  };
+  for (int kb = 0; kb < nkb; kb += 2) {
+    step(Buf<0>(), kb);
+    if (kb + 1 < nkb) step(Buf<1>(), kb + 1);
   }
 
   if (my_q < p.Sq) {
@@ -319,7 +424,9 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
 // ============================================================== backward: dQ
 // One workgroup = 128 queries of one (b, q-head); iterates the visible key
 // blocks.  S^T and dP^T keep the query on the lane, so lse/delta are scalars
-// per lane; dQ^T += K^T dS^T feeds dS^T back as the B operand.
+// per lane; dQ^T += K^T dS^T feeds dS^T back as the B operand.  Keys past Sk
+// read as zero (K = V = 0 => dS^T K^T contributes nothing), so only the causal
+// diagonal is masked.
 template <int D>
 __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
                                                               const bf16_t* __restrict__ dout,
@@ -328,25 +435,25 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
                                                               const float* __restrict__ delta,
                                                               bf16_t* __restrict__ dq) {
   constexpr int BM = 128, BN = 64, NKK = D / 16, NDT = D / 32;
-  constexpr int TILE = BN * D * 2;
-  __shared__ __attribute__((aligned(16))) char smem_raw[4 * TILE];
+  constexpr int TB = BN * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];  // K0 K1 V0 V1
   lds_t* smem = (lds_t*)smem_raw;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, h = lane >> 5;
-  const int nqt = gridDim.x;
-  const int qt = p.causal ? (nqt - 1 - (int)blockIdx.x) : (int)blockIdx.x;
-  const int bh = blockIdx.y, b = bh / p.H, hq = bh % p.H, hk = hq / (p.H / p.Hkv);
-  const int q0 = qt * BM, qw = q0 + wid * 32, my_q = qw + r;
+  const int BH = p.B * p.H, nqt = (p.Sq + BM - 1) / BM, id = blockIdx.x;
+  const int qt = p.causal ? nqt - 1 - id / BH : id / BH;
+  const int bh = id % BH, b = bh / p.H, hq = bh % p.H, hk = hq / (p.H / p.Hkv);
+  const int q0 = qt * BM, my_q = q0 + wid * 32 + r;
 
-  const bf16_t* qbase = p.q + (int64_t)b * p.sqb + (int64_t)hq * p.sqh;
-  const bf16_t* dobase = dout + (int64_t)b * sdb + (int64_t)hq * sdh;
-  const bf16_t* kbase = p.k + (int64_t)b * p.skb + (int64_t)hk * p.skh;
-  const bf16_t* vbase = p.v + (int64_t)b * p.svb + (int64_t)hk * p.svh;
+  const rsrc_t rq = make_rsrc(p.q + (int64_t)b * p.sqb + (int64_t)hq * p.sqh, p.Sq, p.sqs, D);
+  const rsrc_t rdo = make_rsrc(dout + (int64_t)b * sdb + (int64_t)hq * sdh, p.Sq, sds, D);
+  const rsrc_t rk = make_rsrc(p.k + (int64_t)b * p.skb + (int64_t)hk * p.skh, p.Sk, p.sks, D);
+  const rsrc_t rv = make_rsrc(p.v + (int64_t)b * p.svb + (int64_t)hk * p.svh, p.Sk, p.svs, D);
 
   bfx8 qf[NKK], df[NKK];
 #pragma unroll
   for (int kk = 0; kk < NKK; ++kk) {
-    qf[kk] = __builtin_bit_cast(bfx8, ld_chunk(qbase, p.sqs, my_q, 2 * kk + h, p.Sq));
-    df[kk] = __builtin_bit_cast(bfx8, ld_chunk(dobase, sds, my_q, 2 * kk + h, p.Sq));
+    qf[kk] = bload_frag(rq, (uint32_t)my_q * (uint32_t)(p.sqs * 2) + (2 * kk + h) * 16);
+    df[kk] = bload_frag(rdo, (uint32_t)my_q * (uint32_t)(sds * 2) + (2 * kk + h) * 16);
   }
   const int64_t li = ((int64_t)b * p.H + hq) * p.Sq + my_q;
   const float lse2 = my_q < p.Sq ? lse[li] * kLog2e : 0.f;
@@ -354,73 +461,81 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
   const float c2 = p.scale * kLog2e;
   const int64_t qg = p.q_offset + my_q;
 
-  int nkb = (p.Sk + BN - 1) / BN;
-  if (p.causal) {
-    const int64_t last_key = p.q_offset + q0 + BM - 1 - p.k_offset;
-    const int64_t lim = last_key < 0 ? 0 : last_key / BN + 1;
-    if (lim < nkb) nkb = (int)lim;
-  }
+  int nkb, kb_mask;
+  key_blocks<BM, BN>(p, q0, false, nkb, kb_mask);
+
+  LdsAddr<D> la;
+  la.init(lane);
+  Stager<D, BN> sk, sv;
+  sk.init(tid, p.sks);
+  sv.init(tid, p.svs);
 
   f32x16 dqacc[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) dqacc[dt] = zero16();
 
-  Stage<D, BN> sk, sv;
   if (nkb > 0) {
-    sk.load(kbase, p.sks, 0, p.Sk, tid);
-    sv.load(vbase, p.svs, 0, p.Sk, tid);
-    sk.store(smem, tid);
-    sv.store(smem + 2 * TILE, tid);
+    sk.load(rk, 0);
+    sv.load(rv, 0);
+    sk.store(smem);
+    sv.store(smem + 2 * TB);
   }
   __syncthreads();
-  int cur = 0;
-  for (int kb = 0; kb < nkb; ++kb) {
+
+  auto step = [&](auto bufc, int kb) {
+    constexpr int BUF = decltype(bufc)::value;
     const bool more = kb + 1 < nkb;
     if (more) {
-      sk.load(kbase, p.sks, (kb + 1) * BN, p.Sk, tid);
-      sv.load(vbase, p.svs, (kb + 1) * BN, p.Sk, tid);
+      sk.load(rk, (kb + 1) * BN);
+      sv.load(rv, (kb + 1) * BN);
     }
-    const lds_t* kt = smem + cur * TILE;
-    const lds_t* vt = smem + 2 * TILE + cur * TILE;
+    const lds_t* kt = smem + BUF * TB;
+    const lds_t* vt = smem + (2 + BUF) * TB;
     f32x16 s0 = zero16(), s1 = zero16(), d0 = zero16(), d1 = zero16();
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) {
-      s0 = mfma(row_frag<D>(kt, r, 2 * kk + h), qf[kk], s0);
-      s1 = mfma(row_frag<D>(kt, 32 + r, 2 * kk + h), qf[kk], s1);
-      d0 = mfma(row_frag<D>(vt, r, 2 * kk + h), df[kk], d0);
-      d1 = mfma(row_frag<D>(vt, 32 + r, 2 * kk + h), df[kk], d1);
+      s0 = mfma(la.rowf(kt, 0, kk), qf[kk], s0);
+      s1 = mfma(la.rowf(kt, 1, kk), qf[kk], s1);
+      d0 = mfma(la.rowf(vt, 0, kk), df[kk], d0);
+      d1 = mfma(la.rowf(vt, 1, kk), df[kk], d1);
     }
-    const int kbase_l = kb * BN;
-    const bool need_mask =
-        (kbase_l + BN > p.Sk) || (p.causal && (p.k_offset + kbase_l + BN - 1 > p.q_offset + q0));
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      float pa = exp2f(s0[i] * c2 - lse2), pb = exp2f(s1[i] * c2 - lse2);
-      if (need_mask) {
-        const int k0 = kbase_l + acc_row(i, h), k1 = k0 + 32;
-        if (k0 >= p.Sk || (p.causal && p.k_offset + k0 > qg)) pa = 0.f;
-        if (k1 >= p.Sk || (p.causal && p.k_offset + k1 > qg)) pb = 0.f;
-      }
+      const float pa = fast_exp2(fmaf(s0[i], c2, -lse2));
+      const float pb = fast_exp2(fmaf(s1[i], c2, -lse2));
       s0[i] = pa * (d0[i] - dlt);
       s1[i] = pb * (d1[i] - dlt);
+    }
+    if (kb >= kb_mask) {
+      const int lim = key_limit(p, kb, BN, qg, h, false);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (acc_row0(i) > lim) s0[i] = 0.f;
+        if (acc_row0(i) + 32 > lim) s1[i] = 0.f;
+      }
     }
     const bfx8 g00 = acc_frag(s0, 0), g01 = acc_frag(s0, 1), g10 = acc_frag(s1, 0), g11 = acc_frag(s1, 1);
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) {
-      dqacc[dt] = mfma(tr_frag<D>(kt, 0, 0, dt, lane), g00, dqacc[dt]);
-      dqacc[dt] = mfma(tr_frag<D>(kt, 0, 1, dt, lane), g01, dqacc[dt]);
-      dqacc[dt] = mfma(tr_frag<D>(kt, 32, 0, dt, lane), g10, dqacc[dt]);
-      dqacc[dt] = mfma(tr_frag<D>(kt, 32, 1, dt, lane), g11, dqacc[dt]);
+      mfma_acc(dqacc[dt], la.trf(kt, 0, 0, dt), g00);
+      mfma_acc(dqacc[dt], la.trf(kt, 0, 1, dt), g01);
+      mfma_acc(dqacc[dt], la.trf(kt, 32, 0, dt), g10);
+      mfma_acc(dqacc[dt], la.trf(kt, 32, 1, dt), g11);
     }
     if (more) {
-      sk.store(smem + (cur ^ 1) * TILE, tid);
-      sv.store(smem + 2 * TILE + (cur ^ 1) * TILE, tid);
+      sk.store(smem + (BUF ^ 1) * TB);
+      sv.store(smem + (2 + (BUF ^ 1)) * TB);
     }
     __syncthreads();
-    cur ^= 1;
+  };
+  for (int kb = 0; kb < nkb; kb += 2) {
+    step(Buf<0>(), kb);
+    if (kb + 1 < nkb) step(Buf<1>(), kb + 1);
   }
+
+  agpr_fence(dqacc);
   if (my_q < p.Sq) {
-    bf16_t* row = dq + (int64_t)b * p.sxb + (int64_t)my_q * p.sxs + (int64_t)hq * p.sxh;
+    bf16_t* row = dq +(int64_t)b * p.sxb + (int64_t)my_q * p.sxs + (int64_t)hq * p.sxh;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) {
 #pragma unroll
@@ -436,184 +551,176 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
 }
 
 // ============================================================== backward: dK, dV
-// One workgroup = 128 keys (4 waves x 32) of one (b, q-head); iterates query
-// blocks of 32 rows staged in LDS (Q, dO, lse, delta).  Output is this query
-// head's contribution, fp32 [B, Sk, H, D] (summed over the GQA group later)
-// or bf16 directly when H == Hkv.
-template <int D, bool DIRECT>
+// One workgroup = 128 keys (4 waves x 32) of one (b, kv-head); iterates every
+// query head of the GQA group x query blocks of 64 rows staged in LDS (Q, dO,
+// lse, delta), so dK/dV of the kv head are summed in registers and written
+// once as bf16.  Rows past Sq read as zero with lse = +inf => P = dS = 0.
+template <int D>
 __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
     AttnParams p, const bf16_t* __restrict__ dout, int64_t sdb, int64_t sds, int64_t sdh,
-    const float* __restrict__ lse, const float* __restrict__ delta, void* __restrict__ dk_out,
-    void* __restrict__ dv_out) {
-  constexpr int BKW = 128, BQ = 32, NKK = D / 16, NDT = D / 32;
-  constexpr int TILE = BQ * D * 2;
-  __shared__ __attribute__((aligned(16))) char smem_raw[4 * TILE + 4 * BQ * 4];
-  lds_t* smem = (lds_t*)smem_raw;
-  float* stats = (float*)(smem_raw + 4 * TILE);  // [2 buf][lse2 | delta][BQ]
+    const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dk,
+    bf16_t* __restrict__ dv) {
+  constexpr int BKW = 128, BQ = 64, NKK = D / 16, NDT = D / 32;
+  constexpr int TB = BQ * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB + 2 * 2 * BQ * 4];
+  lds_t* smem = (lds_t*)smem_raw;  // Q0 Q1 dO0 dO1 | stats[buf][lse2 | delta][BQ]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, h = lane >> 5;
-  const int nkt = gridDim.x;
-  const int kt_i = p.causal ? (int)blockIdx.x : (int)blockIdx.x;  // early keys = heaviest (causal)
-  (void)nkt;
-  const int bh = blockIdx.y, b = bh / p.H, hq = bh % p.H, hk = hq / (p.H / p.Hkv);
+  const int G = p.H / p.Hkv, BHk = p.B * p.Hkv, id = blockIdx.x;
+  const int kt_i = id / BHk;  // causal: early keys are the heaviest -> launched first
+  const int bhk = id % BHk, b = bhk / p.Hkv, hk = bhk % p.Hkv;
   const int k0 = kt_i * BKW, kw = k0 + wid * 32, my_k = kw + r;
 
-  const bf16_t* qbase = p.q + (int64_t)b * p.sqb + (int64_t)hq * p.sqh;
-  const bf16_t* dobase = dout + (int64_t)b * sdb + (int64_t)hq * sdh;
-  const bf16_t* kbase = p.k + (int64_t)b * p.skb + (int64_t)hk * p.skh;
-  const bf16_t* vbase = p.v + (int64_t)b * p.svb + (int64_t)hk * p.svh;
-  const float* lse_row = lse + ((int64_t)b * p.H + hq) * p.Sq;
-  const float* dlt_row = delta + ((int64_t)b * p.H + hq) * p.Sq;
-
+  const rsrc_t rk = make_rsrc(p.k + (int64_t)b * p.skb + (int64_t)hk * p.skh, p.Sk, p.sks, D);
+  const rsrc_t rv = make_rsrc(p.v + (int64_t)b * p.svb + (int64_t)hk * p.svh, p.Sk, p.svs, D);
   // K^T / V^T as B operands: lane holds K[my_k][16kk + 8h .. +8]
   bfx8 kf[NKK], vf[NKK];
 #pragma unroll
   for (int kk = 0; kk < NKK; ++kk) {
-    kf[kk] = __builtin_bit_cast(bfx8, ld_chunk(kbase, p.sks, my_k, 2 * kk + h, p.Sk));
-    vf[kk] = __builtin_bit_cast(bfx8, ld_chunk(vbase, p.svs, my_k, 2 * kk + h, p.Sk));
+    kf[kk] = bload_frag(rk, (uint32_t)my_k * (uint32_t)(p.sks * 2) + (2 * kk + h) * 16);
+    vf[kk] = bload_frag(rv, (uint32_t)my_k * (uint32_t)(p.svs * 2) + (2 * kk + h) * 16);
   }
   const int64_t kg = p.k_offset + my_k;
   const float c2 = p.scale * kLog2e;
 
-  // query blocks that can see any key of this tile
+  // query blocks that can see any key of this tile; from qb_full on, every
+  // query of the block sees every key of the tile
   int qb0 = 0;
   if (p.causal) {
-    const int64_t first_q = p.k_offset + k0 - p.q_offset;  // local query index of first visible row
-    qb0 = first_q <= 0 ? 0 : (int)(first_q / BQ);
+    const int64_t first_q = p.k_offset + k0 - p.q_offset;
+    qb0 = first_q <= 0 ? 0 : (int)((first_q) / BQ);
   }
   const int nqb = (p.Sq + BQ - 1) / BQ;
+  const int nq = nqb > qb0 ? nqb - qb0 : 0;
+  const int total = G * nq;
+
+  LdsAddr<D> la;
+  la.init(lane);
+  Stager<D, BQ> sq, sd;
+  sq.init(tid, p.sqs);
+  sd.init(tid, sds);
+  float* stats = (float*)(smem_raw + 4 * TB);
 
   f32x16 dkacc[NDT], dvacc[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) dkacc[dt] = dvacc[dt] = zero16();
 
-  // staging: Q and dO tiles (32 x D each = 256 threads x N chunks), stats by threads < 64
-  Stage<D, BQ> sq, sd;
   float st_v = 0.f;
-  auto load_stats = [&](int qb) {
-    if (tid < 2 * BQ) {
-      const int qi = qb * BQ + (tid & (BQ - 1));
-      if (tid < BQ) st_v = qi < p.Sq ? lse_row[qi] * kLog2e : INFINITY;
-      else st_v = qi < p.Sq ? dlt_row[qi] : 0.f;
+  auto issue = [&](int g, int qb) {  // global loads of step (g, qb) into registers
+    const int hq = hk * G + g;
+    sq.load(make_rsrc(p.q + (int64_t)b * p.sqb + (int64_t)hq * p.sqh, p.Sq, p.sqs, D), qb * BQ);
+    sd.load(make_rsrc(dout + (int64_t)b * sdb + (int64_t)hq * sdh, p.Sq, sds, D), qb * BQ);
+    if (wid < 2) {
+      const int qi = qb * BQ + lane;
+      const int64_t row = ((int64_t)b * p.H + hq) * p.Sq;
+      if (wid == 0) st_v = qi < p.Sq ? lse[row + qi] * kLog2e : INFINITY;
+      else st_v = qi < p.Sq ? delta[row + qi] : 0.f;
     }
   };
-  auto store_stats = [&](int buf) {
-    if (tid < 2 * BQ) stats[buf * 2 * BQ + tid] = st_v;
+  auto commit = [&](int buf) {
+    sq.store(smem + buf * TB);
+    sd.store(smem + (2 + buf) * TB);
+    if (wid < 2) stats[buf * 2 * BQ + wid * BQ + lane] = st_v;
   };
-  if (qb0 < nqb) {
-    sq.load(qbase, p.sqs, qb0 * BQ, p.Sq, tid);
-    sd.load(dobase, sds, qb0 * BQ, p.Sq, tid);
-    load_stats(qb0);
-    sq.store(smem, tid);
-    sd.store(smem + 2 * TILE, tid);
-    store_stats(0);
+  if (total > 0) {
+    issue(0, qb0);
+    commit(0);
   }
   __syncthreads();
-  int cur = 0;
-  for (int qb = qb0; qb < nqb; ++qb) {
-    const bool more = qb + 1 < nqb;
-    if (more) {
-      sq.load(qbase, p.sqs, (qb + 1) * BQ, p.Sq, tid);
-      sd.load(dobase, sds, (qb + 1) * BQ, p.Sq, tid);
-      load_stats(qb + 1);
+
+  int g_c = 0, qb_c = qb0;
+  auto step = [&](auto bufc, int it) {
+    constexpr int BUF = decltype(bufc)::value;
+    const bool more = it + 1 < total;
+    int g_n = g_c, qb_n = qb_c + 1;
+    if (qb_n == nqb) {
+      qb_n = qb0;
+      ++g_n;
     }
-    const lds_t* qt = smem + cur * TILE;
-    const lds_t* dt_ = smem + 2 * TILE + cur * TILE;
-    const float* lse2 = stats + cur * 2 * BQ;
-    const float* dl = lse2 + BQ;
-    const int qbase_l = qb * BQ;
+    if (more) issue(g_n, qb_n);
+    const lds_t* qt = smem + BUF * TB;
+    const lds_t* dt_ = smem + (2 + BUF) * TB;
+    const lds_t* st = (const lds_t*)(stats + BUF * 2 * BQ);
+    const int64_t qstart = p.q_offset + (int64_t)qb_c * BQ;  // global index of the block's row 0
     // this wave's keys vs this query block: skip when every key is in the future
-    const bool wave_dead = p.causal && (p.k_offset + kw > p.q_offset + qbase_l + BQ - 1);
-    if (!wave_dead) {
-      // S = Q K^T, dP = dO V^T : rows = queries (acc_row), col = key (lane)
-      f32x16 s = zero16(), dp = zero16();
+    const bool dead = p.causal && (kg - r > qstart + BQ - 1);
+    if (!dead) {
+      const bool need_mask = p.causal && (kg - r + 31 > qstart);
+      bfx8 pf[2][2], gf[2][2];
 #pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) {
-        s = mfma(row_frag<D>(qt, r, 2 * kk + h), kf[kk], s);
-        dp = mfma(row_frag<D>(dt_, r, 2 * kk + h), vf[kk], dp);
-      }
-      const bool need_mask = (qbase_l + BQ > p.Sq) || (my_k >= p.Sk) ||
-                             (p.causal && (p.k_offset + kw + 31 > p.q_offset + qbase_l));
+      for (int u = 0; u < 2; ++u) {
+        // S = Q K^T, dP = dO V^T : rows = queries (acc rows), col = key (lane)
+        f32x16 s = zero16(), dp = zero16();
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qi = acc_row(i, h);
-        float pv = exp2f(s[i] * c2 - lse2[qi]);
-        if (need_mask) {
-          const int64_t qgl = p.q_offset + qbase_l + qi;
-          if (qbase_l + qi >= p.Sq || my_k >= p.Sk || (p.causal && kg > qgl)) pv = 0.f;
+        for (int kk = 0; kk < NKK; ++kk) {
+          s = mfma(la.rowf(qt, u, kk), kf[kk], s);
+          dp = mfma(la.rowf(dt_, u, kk), vf[kk], dp);
         }
-        s[i] = pv;
-        dp[i] = pv * (dp[i] - dl[qi]);
+        // query row of register i: 32u + acc_row0(i) + 4h
+        int thr = 0;
+        if (need_mask) {
+          const int64_t t = kg - qstart - 32 * u - 4 * h;  // row visible iff acc_row0(i) >= t
+          thr = t > 64 ? 64 : (int)t;
+        }
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int rowo = 32 * u + 8 * gq + 4 * h;
+          const f32x4 L = *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * rowo);
+          const f32x4 Dl =
+              *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * (BQ + rowo));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int i = 4 * gq + j;
+            float pv = fast_exp2(fmaf(s[i], c2, -L[j]));
+            if (need_mask && acc_row0(i) < thr) pv = 0.f;
+            s[i] = pv;
+            dp[i] = pv * (dp[i] - Dl[j]);
+          }
+        }
+        pf[u][0] = acc_frag(s, 0);
+        pf[u][1] = acc_frag(s, 1);
+        gf[u][0] = acc_frag(dp, 0);
+        gf[u][1] = acc_frag(dp, 1);
       }
-      const bfx8 p0 = acc_frag(s, 0), p1 = acc_frag(s, 1);
-      const bfx8 g0 = acc_frag(dp, 0), g1 = acc_frag(dp, 1);
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
-        dvacc[dt] = mfma(tr_frag<D>(dt_, 0, 0, dt, lane), p0, dvacc[dt]);
-        dvacc[dt] = mfma(tr_frag<D>(dt_, 0, 1, dt, lane), p1, dvacc[dt]);
-        dkacc[dt] = mfma(tr_frag<D>(qt, 0, 0, dt, lane), g0, dkacc[dt]);
-        dkacc[dt] = mfma(tr_frag<D>(qt, 0, 1, dt, lane), g1, dkacc[dt]);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          mfma_acc(dvacc[dt], la.trf(dt_, 32 * u, 0, dt), pf[u][0]);
+          mfma_acc(dvacc[dt], la.trf(dt_, 32 * u, 1, dt), pf[u][1]);
+          mfma_acc(dkacc[dt], la.trf(qt, 32 * u, 0, dt), gf[u][0]);
+          mfma_acc(dkacc[dt], la.trf(qt, 32 * u, 1, dt), gf[u][1]);
+        }
       }
     }
-    if (more) {
-      sq.store(smem + (cur ^ 1) * TILE, tid);
-      sd.store(smem + 2 * TILE + (cur ^ 1) * TILE, tid);
-      store_stats(cur ^ 1);
-    }
+    if (more) commit(BUF ^ 1);
     __syncthreads();
-    cur ^= 1;
+    g_c = g_n;
+    qb_c = qb_n;
+  };
+  for (int it = 0; it < total; it += 2) {
+    step(Buf<0>(), it);
+    if (it + 1 < total) step(Buf<1>(), it + 1);
   }
+
+  agpr_fence(dkacc);
+  agpr_fence(dvacc);
   if (my_k < p.Sk) {
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int d = 32 * dt + 8 * g + 4 * h;
-        if (DIRECT) {
-          const int64_t off = (int64_t)b * p.sxb + (int64_t)my_k * p.sxs + (int64_t)hk * p.sxh + d;
-          uint2 wk, wv;
-          wk.x = pack_bf16x2(dkacc[dt][4 * g] * p.scale, dkacc[dt][4 * g + 1] * p.scale);
-          wk.y = pack_bf16x2(dkacc[dt][4 * g + 2] * p.scale, dkacc[dt][4 * g + 3] * p.scale);
-          wv.x = pack_bf16x2(dvacc[dt][4 * g], dvacc[dt][4 * g + 1]);
-          wv.y = pack_bf16x2(dvacc[dt][4 * g + 2], dvacc[dt][4 * g + 3]);
-          *reinterpret_cast<uint2*>((bf16_t*)dk_out + off) = wk;
-          *reinterpret_cast<uint2*>((bf16_t*)dv_out + off) = wv;
-        } else {
-          const int64_t off = (((int64_t)b * p.Sk + my_k) * p.H + hq) * D + d;
-          st4f((float*)dk_out + off,
-               make_float4(dkacc[dt][4 * g] * p.scale, dkacc[dt][4 * g + 1] * p.scale,
-                           dkacc[dt][4 * g + 2] * p.scale, dkacc[dt][4 * g + 3] * p.scale));
-          st4f((float*)dv_out + off,
-               make_float4(dvacc[dt][4 * g], dvacc[dt][4 * g + 1], dvacc[dt][4 * g + 2],
-                           dvacc[dt][4 * g + 3]));
-        }
+        const int64_t off = (int64_t)b * p.sxb + (int64_t)my_k * p.sxs + (int64_t)hk * p.sxh + d;
+        uint2 wk, wv;
+        wk.x = pack_bf16x2(dkacc[dt][4 * g] * p.scale, dkacc[dt][4 * g + 1] * p.scale);
+        wk.y = pack_bf16x2(dkacc[dt][4 * g + 2] * p.scale, dkacc[dt][4 * g + 3] * p.scale);
+        wv.x = pack_bf16x2(dvacc[dt][4 * g], dvacc[dt][4 * g + 1]);
+        wv.y = pack_bf16x2(dvacc[dt][4 * g + 2], dvacc[dt][4 * g + 3]);
+        *reinterpret_cast<uint2*>(dk + off) = wk;
+        *reinterpret_cast<uint2*>(dv + off) = wv;
       }
     }
   }
-}
-
-// Sum the per-query-head fp32 dK/dV partials over each GQA group -> bf16.
-// in: [B*Sk, H, D] fp32, out: [B, Sk, Hkv, D] with strides (bf16).
-__global__ __launch_bounds__(256) void gqa_reduce_kernel(const float* __restrict__ in,
-                                                         bf16_t* __restrict__ out, int64_t rows,
-                                                         int H, int Hkv, int D, int64_t sob,
-                                                         int64_t sos, int64_t soh, int Sk) {
-  const int G = H / Hkv, D8 = D / 8;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t total = rows * Hkv * D8;
-  if (t >= total) return;
-  const int c = (int)(t % D8);
-  const int64_t rh = t / D8;
-  const int hk = (int)(rh % Hkv);
-  const int64_t row = rh / Hkv;  // b*Sk + s
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int g = 0; g < G; ++g) {
-    const float* src = in + (row * H + hk * G + g) * D + c * 8;
-    float4 a = ld4f(src), bq = ld4f(src + 4);
-    acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
-    acc[4] += bq.x; acc[5] += bq.y; acc[6] += bq.z; acc[7] += bq.w;
-  }
-  const int64_t b = row / Sk, s = row % Sk;
-  st8(out + b * sob + s * sos + hk * soh + c * 8, pack8(acc));
 }
 
 // ============================================================== ring-attention merge
@@ -672,6 +779,12 @@ AttnParams make_params(const void* q, const void* k, const void* v, int B, int S
   return p;
 }
 
+// Buffer offsets are 32-bit: every row read (plus one tile of overrun) must
+// stay below 2^31 bytes from its (batch, head) base.
+bool offsets_fit(int64_t rows, int64_t stride) {
+  return (rows + 256) * stride * 2 < (int64_t(1) << 31);
+}
+
 }  // namespace
 
 extern "C" {
@@ -683,9 +796,10 @@ int st_flash_fwd(const void* q, const void* k, const void* v, void* o, float* ls
                  int64_t k_offset, hipStream_t st) {
   if (H % Hkv != 0) return -2;
   if (Sq == 0 || B == 0) return 0;
+  if (!offsets_fit(Sq, sqs) || !offsets_fit(Sk, sks) || !offsets_fit(Sk, svs)) return -5;
   AttnParams p = make_params(q, k, v, B, Sq, Sk, H, Hkv, sqb, sqs, sqh, skb, sks, skh, svb, svs, svh,
                              scale, causal, q_offset, k_offset);
-  dim3 grid((Sq + 127) / 128, B * H);
+  const unsigned grid = (unsigned)(((Sq + 127) / 128) * B * H);
   if (D == 128)
     flash_fwd_kernel<128><<<grid, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
   else if (D == 64)
@@ -713,50 +827,36 @@ int st_flash_bwd_preprocess(const void* o, const void* dout, float* delta, int B
 }
 
 // dq / dk / dv: bf16 outputs with arbitrary (b, s, h) strides (D contiguous) so
-// they can be slices of one fused dQKV buffer.  `work` must hold
-// 2*B*Sk*H*D floats when H != Hkv (per-query-head partials of the GQA sum).
+// they can be slices of one fused dQKV buffer.
 int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse,
-                 const float* delta, void* dq, void* dk, void* dv, float* work, int B, int Sq,
-                 int Sk, int H, int Hkv, int D, int64_t sqb, int64_t sqs, int64_t sqh, int64_t skb,
-                 int64_t sks, int64_t skh, int64_t svb, int64_t svs, int64_t svh, int64_t sdb,
-                 int64_t sds, int64_t sdh, int64_t sdqb, int64_t sdqs, int64_t sdqh, int64_t sdkb,
-                 int64_t sdks, int64_t sdkh, float scale, int causal, int64_t q_offset,
-                 int64_t k_offset, hipStream_t st) {
+                 const float* delta, void* dq, void* dk, void* dv, int B, int Sq, int Sk, int H,
+                 int Hkv, int D, int64_t sqb, int64_t sqs, int64_t sqh, int64_t skb, int64_t sks,
+                 int64_t skh, int64_t svb, int64_t svs, int64_t svh, int64_t sdb, int64_t sds,
+                 int64_t sdh, int64_t sdqb, int64_t sdqs, int64_t sdqh, int64_t sdkb, int64_t sdks,
+                 int64_t sdkh, float scale, int causal, int64_t q_offset, int64_t k_offset,
+                 hipStream_t st) {
   if (H % Hkv != 0) return -2;
   if (B == 0 || Sq == 0 || Sk == 0) return 0;
+  if (!offsets_fit(Sq, sqs) || !offsets_fit(Sq, sds) || !offsets_fit(Sk, sks) || !offsets_fit(Sk, svs))
+    return -5;
   AttnParams p = make_params(q, k, v, B, Sq, Sk, H, Hkv, sqb, sqs, sqh, skb, sks, skh, svb, svs, svh,
                              scale, causal, q_offset, k_offset);
   AttnParams pq = p, pk = p;
   pq.sxb = sdqb; pq.sxs = sdqs; pq.sxh = sdqh;
   pk.sxb = sdkb; pk.sxs = sdks; pk.sxh = sdkh;
-  dim3 gq((Sq + 127) / 128, B * H);
-  dim3 gk((Sk + 127) / 128, B * H);
-  const bool direct = (H == Hkv);
-  if (!direct && work == nullptr) return -4;
-  float* wk = work;
-  float* wv = direct ? nullptr : work + (int64_t)B * Sk * H * D;
+  const unsigned gq = (unsigned)(((Sq + 127) / 128) * B * H);
+  const unsigned gk = (unsigned)(((Sk + 127) / 128) * B * Hkv);
   const bf16_t* dop = (const bf16_t*)dout;
   if (D == 128) {
     flash_bwd_dq_kernel<128><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq);
-    if (direct)
-      flash_bwd_dkdv_kernel<128, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, dk, dv);
-    else
-      flash_bwd_dkdv_kernel<128, false><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, wk, wv);
+    flash_bwd_dkdv_kernel<128><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
+                                                   (bf16_t*)dv);
   } else if (D == 64) {
     flash_bwd_dq_kernel<64><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq);
-    if (direct)
-      flash_bwd_dkdv_kernel<64, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, dk, dv);
-    else
-      flash_bwd_dkdv_kernel<64, false><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, wk, wv);
+    flash_bwd_dkdv_kernel<64><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
+                                                  (bf16_t*)dv);
   } else {
     return -3;
-  }
-  if (!direct) {
-    const int64_t rows = (int64_t)B * Sk;
-    const int64_t total = rows * Hkv * (D / 8);
-    const unsigned blocks = (unsigned)((total + 255) / 256);
-    gqa_reduce_kernel<<<blocks, 256, 0, st>>>(wk, (bf16_t*)dk, rows, H, Hkv, D, sdkb, sdks, sdkh, Sk);
-    gqa_reduce_kernel<<<blocks, 256, 0, st>>>(wv, (bf16_t*)dv, rows, H, Hkv, D, sdkb, sdks, sdkh, Sk);
   }
   return (int)hipGetLastError();
 }

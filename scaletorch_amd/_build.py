@@ -30,6 +30,13 @@ LIB = PKG / "_st_kernels.so"
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 
+# Per-file flags.  flash_attn: scores never hold NaN by construction (masked
+# entries are -inf, never inf - inf), so -fno-honor-nans drops the v_max
+# canonicalisation hipcc inserts before every fmaxf on an MFMA result;
+# -amdgpu-mfma-vgpr-form keeps compiler-emitted MFMAs in VGPRs (their results
+# feed VALU) while the asm accumulate chains own the AGPRs (see mfma_acc).
+FILE_FLAGS = {"flash_attn.hip": ["-fno-honor-nans", "-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
 
 def _hipcc() -> str:
     p = ROCM / "bin" / "hipcc"
@@ -79,8 +86,10 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     for src in hip_srcs:
         obj = BUILD / (src.stem + ".o")
         objs.append(obj)
-        if force or _stale(obj, [src, *headers]):
-            jobs_list.append([hipcc, f"--offload-arch={ARCH}", *common_flags, "-c", str(src), "-o", str(obj)])
+        if force or _stale(obj, [src, *headers, Path(__file__)]):
+            extra = FILE_FLAGS.get(src.name, [])
+            jobs_list.append([hipcc, f"--offload-arch={ARCH}", *common_flags, *extra, "-c", str(src), "-o",
+                              str(obj)])
     bsrc = CSRC / "bindings.cpp"
     bobj = BUILD / "bindings.o"
     objs.append(bobj)

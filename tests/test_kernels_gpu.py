@@ -148,13 +148,27 @@ FLASH_CASES = [
     (1, 128, 128, 4, 4, 64, True),
     (2, 257, 257, 4, 2, 64, False),
     (1, 1024, 1024, 8, 2, 128, True),
+    (1, 64, 1000, 4, 1, 128, True),     # short query block at the end of a long key range
+    (1, 300, 300, 8, 1, 128, True),     # GQA group of 8 summed in one dK/dV workgroup
+    (1, 2048, 2048, 4, 1, 64, True),
+    (2, 96, 96, 2, 2, 128, False),
 ]
 
 
 @pytest.mark.parametrize("B,Sq,Sk,H,Hkv,D,causal", FLASH_CASES)
 def test_flash_fwd_bwd(B, Sq, Sk, H, Hkv, D, causal):
+    _flash_case(B, Sq, Sk, H, Hkv, D, causal, 1.0)
+
+
+@pytest.mark.parametrize("qscale", [6.0, 30.0])
+def test_flash_large_logits(qscale):
+    """Peaked softmax: exercises the deferred (thresholded) O rescale."""
+    _flash_case(1, 700, 700, 4, 2, 128, True, qscale)
+
+
+def _flash_case(B, Sq, Sk, H, Hkv, D, causal, qscale):
     torch.manual_seed(0)
-    q = torch.randn(B, Sq, H, D, device="cuda", dtype=torch.bfloat16)
+    q = (torch.randn(B, Sq, H, D, device="cuda") * qscale).to(torch.bfloat16)
     k = torch.randn(B, Sk, Hkv, D, device="cuda", dtype=torch.bfloat16)
     v = torch.randn(B, Sk, Hkv, D, device="cuda", dtype=torch.bfloat16)
     scale = 1 / math.sqrt(D)
