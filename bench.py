@@ -44,7 +44,9 @@ def main() -> int:
     ap.add_argument("--sp", action="store_true")
     ap.add_argument("--gc", action="store_true", help="activation checkpointing")
     ap.add_argument("--grad_reduce_dtype", default="bf16")
-    ap.add_argument("--bucket_mb", type=int, default=256)
+    ap.add_argument("--bucket_mb", type=float, default=256)
+    ap.add_argument("--zero", type=int, default=1, help="ZeRO stage when DP > 1 (0: replicated optimizer, "
+                                                         "1: sharded optimizer / reduce-scatter + all-gather)")
     ap.add_argument("--layers", type=int, default=None, help="(debug only; result marked invalid)")
     args = ap.parse_args()
 
@@ -72,6 +74,7 @@ def main() -> int:
         gradient_checkpointing=args.gc, learning_rate=3e-4, lr_scheduler_type="cosine", warmup_steps=0,
         max_grad_norm=1.0, grad_reduce_dtype=args.grad_reduce_dtype, bucket_size_mb=args.bucket_mb,
         num_hidden_layers=args.layers, dtype="bfloat16", weight_decay=0.1, betas=(0.9, 0.95),
+        zero_stage=args.zero,
     )
     tr = Trainer(a)
     rank = tr.rank
@@ -127,7 +130,7 @@ def main() -> int:
         "config": {"model": args.model, "global_batch": dp * args.ep * args.micro_batch_size * ga,
                    "micro_batch": args.micro_batch_size, "grad_accum": ga, "seq_len": args.seq_len,
                    "parallelism": par, "sequence_parallel": args.sp, "activation_checkpointing": args.gc,
-                   "grad_reduce_dtype": args.grad_reduce_dtype},
+                   "grad_reduce_dtype": args.grad_reduce_dtype, "zero_stage": args.zero if dp > 1 else 0},
         "tokens_per_s_per_gpu": round(per_gpu, 1),
         "mfu_pct": round(mfu, 2),
         "mfu_pct_causal_flops": round(per_gpu * fpt_causal / peak * 100, 2),

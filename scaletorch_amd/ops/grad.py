@@ -51,7 +51,7 @@ def accumulate_linear_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
         mg.addmm_(dy2d.t(), x2d)
     else:
         done = False
-        if _ADDMM_DTYPE_OK is not False and dy2d.is_cuda and os.environ.get("ST_WGRAD_FP32_GEMM", "0") == "1":
+        if _ADDMM_DTYPE_OK is not False and dy2d.is_cuda and os.environ.get("ST_WGRAD_FP32_GEMM", "1") == "1":
             try:
                 torch.ops.aten.addmm.dtype_out(mg, dy2d.t(), x2d, mg.dtype, beta=1, alpha=1, out=mg)
                 _ADDMM_DTYPE_OK = True

@@ -26,6 +26,10 @@ from .ops import _lib
 
 
 class _ArenaOptimizer(torch.optim.Optimizer):
+    """Base: per-arena optimizer state over the arena's SEGMENTS -- the whole
+    arena, or under ZeRO-1 (data_parallel.GradArena ``zero1``) this rank's
+    shard of every bucket, with state tensors sized to the shard."""
+
     def __init__(self, dp_model, lr: float, defaults: dict):
         self.dp = dp_model
         arenas = dp_model.arenas
@@ -34,14 +38,29 @@ class _ArenaOptimizer(torch.optim.Optimizer):
         self.arenas = arenas
         self._step = 0
         for a in arenas:
-            a.master = a.param_flat.detach().float().clone() if a.param_flat.dtype != torch.float32 else None
+            if a.param_flat.dtype == torch.float32:
+                a.master = None
+            elif a.zero1:
+                a.master = torch.cat([a.param_flat[lo:hi].float() for lo, hi, _ in a.segments()])
+            else:
+                a.master = a.param_flat.detach().float().clone()
         self.clip_coef = None
         self.last_grad_norm = None
 
-    # fp32 view of the weights the update is applied to
-    @staticmethod
-    def _master(a):
-        return a.master if a.master is not None else a.param_flat
+    @property
+    def sharded(self) -> bool:
+        return any(a.zero1 for a in self.arenas)
+
+    def _views(self, a, states: tuple):
+        """Yield (param_seg, grad_seg, master_seg, *state_segs) for every segment."""
+        for lo, hi, so in a.segments():
+            n = hi - lo
+            master = a.master[so: so + n] if a.master is not None else a.param_flat[lo:hi]
+            yield (a.param_flat[lo:hi], a.grad_flat[lo:hi], master) + tuple(s[so: so + n] for s in states)
+
+    def _finish_step(self) -> None:
+        for a in self.arenas:
+            a.gather_params()
 
     def zero_grad(self, set_to_none: bool = False) -> None:  # noqa: ARG002
         self.dp.zero_grad()
@@ -61,7 +80,10 @@ class _ArenaOptimizer(torch.optim.Optimizer):
                 total += part * w
             else:
                 total += t.float().pow(2).sum() * w
-        if mp_group is not None and C.get_world_size(mp_group) > 1:
+        if self.sharded:  # shard shares sum over every rank (grad_sumsq_segments)
+            if C.get_world_size() > 1:
+                C.all_reduce(total)
+        elif mp_group is not None and C.get_world_size(mp_group) > 1:
             C.all_reduce(total, group=mp_group)
         return total.sqrt()
 
@@ -95,7 +117,10 @@ class _ArenaOptimizer(torch.optim.Optimizer):
     def _load_arena_state(self, a, s) -> None:
         if s.get("master") is not None and a.master is not None:
             a.master.copy_(s["master"].to(a.master.device))
-            a.param_flat.copy_(a.master.to(a.param_flat.dtype))
+            for lo, hi, so in a.segments():
+                a.param_flat[lo:hi].copy_(a.master[so: so + hi - lo])
+            a.gather_params()
+            a.wait_params()
 
 
 class ArenaAdamW(_ArenaOptimizer):
@@ -105,7 +130,7 @@ class ArenaAdamW(_ArenaOptimizer):
         self.fused = fused
         self.decoupled = decoupled
         for a in self.arenas:
-            a.exp_avg = torch.zeros(a.numel, dtype=torch.float32, device=a.param_flat.device)
+            a.exp_avg = torch.zeros(a.state_numel, dtype=torch.float32, device=a.param_flat.device)
             a.exp_avg_sq = torch.zeros_like(a.exp_avg)
 
     @torch.no_grad()
@@ -114,26 +139,27 @@ class ArenaAdamW(_ArenaOptimizer):
         t = self._step
         for g, a in zip(self.param_groups, self.arenas):
             lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
-            master = self._master(a)
-            if (self.fused and self.decoupled and _lib.use_native(a.param_flat) and a.master is not None
-                    and a.param_flat.dtype == torch.bfloat16):
-                _lib.ops().adamw_step_(master, a.exp_avg, a.exp_avg_sq, a.grad_flat, a.param_flat,
-                                       self.clip_coef, lr, b1, b2, eps, wd, t)
-                continue
-            grad = a.grad_flat.float()
-            if self.clip_coef is not None:
-                grad = grad * self.clip_coef
-            if not self.decoupled and wd:
-                grad = grad + wd * master
-            a.exp_avg.mul_(b1).add_(grad, alpha=1 - b1)
-            a.exp_avg_sq.mul_(b2).addcmul_(grad, grad, value=1 - b2)
-            bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
-            denom = (a.exp_avg_sq.sqrt() / math.sqrt(bc2)).add_(eps)
-            if self.decoupled and wd:
-                master.mul_(1 - lr * wd)
-            master.addcdiv_(a.exp_avg, denom, value=-lr / bc1)
-            if a.master is not None:
-                a.param_flat.copy_(master)
+            native = (self.fused and self.decoupled and _lib.use_native(a.param_flat) and a.master is not None
+                      and a.param_flat.dtype == torch.bfloat16)
+            for param, gseg, master, m, v in self._views(a, (a.exp_avg, a.exp_avg_sq)):
+                if native:
+                    _lib.ops().adamw_step_(master, m, v, gseg, param, self.clip_coef, lr, b1, b2, eps, wd, t)
+                    continue
+                grad = gseg.float()
+                if self.clip_coef is not None:
+                    grad = grad * self.clip_coef
+                if not self.decoupled and wd:
+                    grad = grad + wd * master
+                m.mul_(b1).add_(grad, alpha=1 - b1)
+                v.mul_(b2).addcmul_(grad, grad, value=1 - b2)
+                bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
+                denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+                if self.decoupled and wd:
+                    master.mul_(1 - lr * wd)
+                master.addcdiv_(m, denom, value=-lr / bc1)
+                if a.master is not None:
+                    param.copy_(master)
+        self._finish_step()
 
     def _arena_state(self, a) -> dict:
         d = super()._arena_state(a)
@@ -158,22 +184,23 @@ class ArenaSGD(_ArenaOptimizer):
     def __init__(self, dp_model, lr: float = 1e-3, momentum: float = 0.9, weight_decay: float = 0.0):
         super().__init__(dp_model, lr, dict(momentum=momentum, weight_decay=weight_decay))
         for a in self.arenas:
-            a.momentum_buf = torch.zeros(a.numel, dtype=torch.float32, device=a.param_flat.device)
+            a.momentum_buf = torch.zeros(a.state_numel, dtype=torch.float32, device=a.param_flat.device)
 
     @torch.no_grad()
     def step(self, closure=None):  # noqa: ARG002
         self._step += 1
         for g, a in zip(self.param_groups, self.arenas):
-            master = self._master(a)
-            grad = a.grad_flat.float()
-            if self.clip_coef is not None:
-                grad = grad * self.clip_coef
-            if g["weight_decay"]:
-                grad = grad + g["weight_decay"] * master
-            a.momentum_buf.mul_(g["momentum"]).add_(grad)
-            master.add_(a.momentum_buf, alpha=-g["lr"])
-            if a.master is not None:
-                a.param_flat.copy_(master)
+            for param, gseg, master, mom in self._views(a, (a.momentum_buf,)):
+                grad = gseg.float()
+                if self.clip_coef is not None:
+                    grad = grad * self.clip_coef
+                if g["weight_decay"]:
+                    grad = grad + g["weight_decay"] * master
+                mom.mul_(g["momentum"]).add_(grad)
+                master.add_(mom, alpha=-g["lr"])
+                if a.master is not None:
+                    param.copy_(master)
+        self._finish_step()
 
     def _arena_state(self, a) -> dict:
         d = super()._arena_state(a)
@@ -190,6 +217,8 @@ class ArenaLAMB(ArenaAdamW):
 
     def __init__(self, dp_model, **kw):
         kw.pop("fused", None)
+        if any(a.zero1 for a in dp_model.arenas):
+            raise ValueError("LAMB needs whole-parameter norms; use it without zero1")
         super().__init__(dp_model, fused=False, **kw)
 
     @torch.no_grad()
@@ -198,7 +227,7 @@ class ArenaLAMB(ArenaAdamW):
         t = self._step
         for g, a in zip(self.param_groups, self.arenas):
             lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
-            master = self._master(a)
+            master = a.master if a.master is not None else a.param_flat
             grad = a.grad_flat.float()
             if self.clip_coef is not None:
                 grad = grad * self.clip_coef

@@ -51,24 +51,45 @@ def _is_tp_sharded(p) -> bool:
 
 
 class Bucket:
-    __slots__ = ("start", "end", "params", "pending", "handle", "comm_buf", "launched")
+    __slots__ = ("start", "end", "params", "pending", "handle", "comm_buf", "comm_out", "launched",
+                 "shard_lo", "shard_hi", "state_lo", "ag_handle")
 
     def __init__(self, start: int, end: int, params: list):
         self.start, self.end, self.params = start, end, params
         self.pending = 0
         self.handle = None
         self.comm_buf = None
+        self.comm_out = None
         self.launched = False
+        self.shard_lo, self.shard_hi, self.state_lo = start, end, start
+        self.ag_handle = None
+
+
+def _aligned(n: int) -> int:
+    return math.ceil(n / ALIGN) * ALIGN
 
 
 class GradArena:
-    """Flat parameter + fp32 gradient storage for one reduction group."""
+    """Flat parameter + fp32 gradient storage for one reduction group.
+
+    ``zero1``: ZeRO stage-1 / distributed optimizer.  Every bucket is padded to
+    a multiple of ``world * ALIGN`` and split evenly over the group; backward
+    REDUCE-SCATTERS each bucket (half the bytes of an all-reduce land on this
+    rank: only its shard is reduced), the optimizer updates only this rank's
+    shards (fp32 master / m / v are 1/world of the arena), and the updated bf16
+    shards are ALL-GATHERED back bucket by bucket in forward order, each
+    forward layer waiting only for the bucket that holds its weights.
+    Reference: the FSDP/ZeRO examples (examples/FSDP2/*, SURVEY.md §2.1);
+    design is Megatron's distributed optimizer on our arenas.
+    """
 
     def __init__(self, params: list[nn.Parameter], group, name: str, bucket_size: int = 64 * 1024 * 1024,
                  reduce_dtype: torch.dtype = torch.float32, grad_dtype: torch.dtype = torch.float32,
-                 use_counts: dict | None = None):
+                 use_counts: dict | None = None, zero1: bool = False):
         self.name, self.group = name, group
         self.world = C.get_world_size(group)
+        self.rank = C.get_rank(group) if self.world > 1 else 0
+        self.zero1 = bool(zero1) and self.world > 1
         # expert grads already SUM the contributions of the ep data replicas that routed tokens
         # to them (all-to-all); dividing by ep turns that into the data-parallel mean
         self.post_scale = 1.0 / mesh.ep_size() if name == "expert" else 1.0
@@ -80,11 +101,27 @@ class GradArena:
         device = params[0].device
         if any(p.dtype != dtype for p in params):
             raise ValueError(f"arena {name}: mixed parameter dtypes")
-        # layout: TP-sharded / expert params first, TP-replicated last (grad-norm dedup segments)
-        offs, off = [], 0
+        # bucket membership first (contiguous runs in registration = backward order, params
+        # never split), then the layout: TP-sharded / expert params first, TP-replicated last
+        # (grad-norm dedup segments); under ZeRO-1 each bucket is padded to world * ALIGN
+        runs, cur, size = [], [], 0
         for p in params:
-            offs.append(off)
-            off += math.ceil(p.numel() / ALIGN) * ALIGN
+            cur.append(p)
+            size += _aligned(p.numel())
+            if size >= bucket_size:
+                runs.append(cur)
+                cur, size = [], 0
+        if cur:
+            runs.append(cur)
+        quantum = ALIGN * (self.world if self.zero1 else 1)
+        offs, off, spans = [], 0, []
+        for run in runs:
+            start = off
+            for p in run:
+                offs.append(off)
+                off += _aligned(p.numel())
+            off = start + math.ceil((off - start) / quantum) * quantum
+            spans.append((start, off, run))
         self.numel = off
         self.offsets = offs
         self.param_flat = torch.zeros(self.numel, dtype=dtype, device=device)
@@ -101,17 +138,18 @@ class GradArena:
             if not (_is_tp_sharded(p) or _is_expert(p)):
                 self.repl_start = o
                 break
-        # buckets over contiguous arena ranges, params never split
-        self.buckets: list[Bucket] = []
-        cur, cur_start = [], 0
-        for p, o in zip(params, offs):
-            end = o + math.ceil(p.numel() / ALIGN) * ALIGN
-            cur.append(p)
-            if end - cur_start >= bucket_size:
-                self.buckets.append(Bucket(cur_start, end, cur))
-                cur, cur_start = [], end
-        if cur:
-            self.buckets.append(Bucket(cur_start, self.numel, cur))
+        self.buckets: list[Bucket] = [Bucket(s, e, run) for s, e, run in spans]
+        # optimizer segments: (arena_lo, arena_hi, state_lo); the whole arena, or this
+        # rank's shard of every bucket under ZeRO-1
+        state = 0
+        for b in self.buckets:
+            if self.zero1:
+                n = (b.end - b.start) // self.world
+                b.shard_lo = b.start + self.rank * n
+                b.shard_hi = b.shard_lo + n
+            b.state_lo = state
+            state += b.shard_hi - b.shard_lo
+        self.state_numel = state
         self.expected = {}
         self.bucket_of = {}
         for i, b in enumerate(self.buckets):
@@ -147,11 +185,20 @@ class GradArena:
             buf = b.comm_buf
         else:
             buf = g
-        if nccl:
-            b.handle = dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
-        else:
+        if not nccl:
             buf.div_(self.world)
-            b.handle = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        op = dist.ReduceOp.AVG if nccl else dist.ReduceOp.SUM
+        if self.zero1:
+            n = b.shard_hi - b.shard_lo
+            if buf is g and nccl:  # in place: this rank's chunk of the bucket is the output
+                out = self.grad_flat[b.shard_lo: b.shard_hi]
+            else:
+                if b.comm_out is None or b.comm_out.numel() != n:
+                    b.comm_out = torch.empty(n, dtype=buf.dtype, device=buf.device)
+                out = b.comm_out
+            b.handle = dist.reduce_scatter_tensor(out, buf, op=op, group=self.group, async_op=True)
+        else:
+            b.handle = dist.all_reduce(buf, op=op, group=self.group, async_op=True)
 
     def finish(self) -> None:
         """Launch whatever did not fire (unused params) and join every bucket."""
@@ -162,10 +209,42 @@ class GradArena:
             if b.handle is not None:
                 b.handle.wait()  # stream-ordered join (no host block on RCCL)
                 b.handle = None
-            if b.comm_buf is not None and self.world > 1:
+            if self.world == 1:
+                continue
+            if self.zero1:
+                if b.comm_out is not None:
+                    self.grad_flat[b.shard_lo: b.shard_hi].copy_(b.comm_out)
+            elif b.comm_buf is not None:
                 self.grad_flat[b.start: b.end].copy_(b.comm_buf)
         if self.post_scale != 1.0:
-            self.grad_flat.mul_(self.post_scale)
+            for lo, hi, _ in self.segments():
+                self.grad_flat[lo:hi].mul_(self.post_scale)
+
+    # ---------------------------------------------------------------- ZeRO-1
+    def segments(self) -> list[tuple[int, int, int]]:
+        """(arena_lo, arena_hi, state_lo) ranges the optimizer owns on this rank."""
+        if not self.zero1:
+            return [(0, self.numel, 0)]
+        return [(b.shard_lo, b.shard_hi, b.state_lo) for b in self.buckets]
+
+    def gather_params(self) -> None:
+        """All-gather the updated bf16 shards, first-used (last registered) bucket first."""
+        if not self.zero1:
+            return
+        for b in reversed(self.buckets):
+            b.ag_handle = dist.all_gather_into_tensor(self.param_flat[b.start: b.end],
+                                                      self.param_flat[b.shard_lo: b.shard_hi],
+                                                      group=self.group, async_op=True)
+
+    def wait_bucket(self, i: int) -> None:
+        b = self.buckets[i]
+        if b.ag_handle is not None:
+            b.ag_handle.wait()
+            b.ag_handle = None
+
+    def wait_params(self) -> None:
+        for i in range(len(self.buckets)):
+            self.wait_bucket(i)
 
     def mark_ready(self, p) -> bool:
         """Returns True when this call completed the bucket (and launched it)."""
@@ -201,9 +280,11 @@ class DataParallel(nn.Module):
 
     def __init__(self, module: nn.Module, bucket_size: int = 64 * 1024 * 1024,
                  reduce_dtype: torch.dtype | str = torch.float32, dense_group=None, expert_group=None,
-                 expose_grads: bool = False):
+                 expose_grads: bool = False, zero1: bool = False):
         super().__init__()
         self.module = module
+        if zero1 and expose_grads:
+            raise ValueError("zero1 keeps only a gradient shard per rank; expose_grads needs full grads")
         # expose_grads: after the sync, point ``p.grad`` at the reduced main_grad so stock
         # torch.optim optimizers can be used (examples); the arena optimizers read main_grad
         self.expose_grads = expose_grads
@@ -229,7 +310,10 @@ class DataParallel(nn.Module):
             if not ps:
                 continue
             g = dense_group if name == "dense" else expert_group
-            self.arenas.append(GradArena(ps, g, name, bucket_size, reduce_dtype, use_counts=uses))
+            self.arenas.append(GradArena(ps, g, name, bucket_size, reduce_dtype, use_counts=uses, zero1=zero1))
+        self.zero1 = any(a.zero1 for a in self.arenas)
+        if self.zero1:
+            self._install_param_waits()
         # TP-replicated params whose grads are TP-partial (per-head QK-norm weights; every
         # norm / router weight under sequence parallelism): summed over TP after backward
         self.tp_group = mesh.tp_group() if mesh.pgm else C.SINGLE
@@ -244,6 +328,36 @@ class DataParallel(nn.Module):
                     p._st_hooked = True
 
     # ---------------------------------------------------------------- hooks
+    def _install_param_waits(self) -> None:
+        """ZeRO-1: each module waits (stream-ordered) for the all-gather of the
+        buckets holding its own parameters right before its forward, so the
+        parameter all-gather after the optimizer step overlaps the next forward."""
+        where = {}
+        for a in self.arenas:
+            for i, b in enumerate(a.buckets):
+                for p in b.params:
+                    where[id(p)] = (a, i)
+
+        def make_hook(needs):
+            def hook(_mod, _inp):
+                for a, i in needs:
+                    a.wait_bucket(i)
+            return hook
+
+        for m in self.module.modules():
+            needs = sorted({where[id(p)] for p in m.parameters(recurse=False) if id(p) in where},
+                           key=lambda t: (id(t[0]), t[1]))
+            if needs:
+                m.register_forward_pre_hook(make_hook(needs))
+
+    def gather_params(self) -> None:
+        for a in self.arenas:
+            a.gather_params()
+
+    def wait_params(self) -> None:
+        for a in self.arenas:
+            a.wait_params()
+
     def _post_accumulate(self, p) -> None:
         """Params whose grads come through plain autograd (no fused op)."""
         if p.grad is None:
@@ -331,10 +445,27 @@ class DataParallel(nn.Module):
 
     def grad_sumsq_segments(self):
         """(tensor, weight) pairs whose weighted squared norms sum to this rank's
-        de-duplicated share of the global gradient norm."""
+        de-duplicated share of the global gradient norm.
+
+        Without ZeRO-1 the shares are summed over the model-parallel group (dense
+        grads are replicated over EP); with ZeRO-1 every rank holds a distinct
+        shard of its reduction group and the shares are summed over ALL ranks
+        (``norm_over_world``): sharded dense / expert weight 1, TP-replicated 1/tp."""
         tp = mesh.tp_size()
         ep = mesh.ep_size()
         out = []
+        if self.zero1:
+            for a in self.arenas:
+                for lo, hi, _ in a.segments():
+                    if a.name == "expert":
+                        out.append((a.grad_flat[lo:hi], 1.0))
+                        continue
+                    r = a.repl_start
+                    if lo < min(hi, r):
+                        out.append((a.grad_flat[lo: min(hi, r)], 1.0))
+                    if max(lo, r) < hi:
+                        out.append((a.grad_flat[max(lo, r): hi], 1.0 / tp))
+            return out
         for a in self.arenas:
             if a.name == "expert":
                 out.append((a.grad_flat, 1.0))
@@ -346,6 +477,7 @@ class DataParallel(nn.Module):
         return out
 
     def state_dict(self, *args, **kwargs):
+        self.wait_params()
         return self.module.state_dict(*args, **kwargs)
 
     def load_state_dict(self, *args, **kwargs):

@@ -168,7 +168,10 @@ class LoggingArguments:
 @dataclass
 class SystemArguments:
     grad_reduce_dtype: str = field(default="fp32", metadata={"help": "fp32 | bf16 gradient all-reduce"})
-    bucket_size_mb: int = field(default=256, metadata={"help": "DP bucket size (MiB of fp32 gradient)"})
+    bucket_size_mb: float = field(default=256, metadata={"help": "DP bucket size (MiB of fp32 gradient)"})
+    zero_stage: int = field(default=0, metadata={"help": "0: replicated optimizer; 1: ZeRO-1 distributed "
+                                                         "optimizer (reduce-scatter grads, sharded states, "
+                                                         "all-gather params)"})
     profile: bool = field(default=False, metadata={"help": "torch.profiler trace of steps 3-5"})
     profile_dir: str = field(default="./profiles/trace")
     nan_check: bool = field(default=True, metadata={"help": "abort on non-finite loss"})

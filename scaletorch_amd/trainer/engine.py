@@ -80,8 +80,9 @@ class Trainer:
         model.cos, model.sin = model.cos.float(), model.sin.float()
         mark_tp_sharded(model)
         self.raw_model = model
-        bucket = a.bucket_size_mb * 1024 * 1024 // 4
-        self.model = DataParallel(model, bucket_size=bucket, reduce_dtype=a.grad_reduce_dtype)
+        bucket = max(1, int(a.bucket_size_mb * 1024 * 1024) // 4)
+        self.model = DataParallel(model, bucket_size=bucket, reduce_dtype=a.grad_reduce_dtype,
+                                  zero1=a.zero_stage >= 1)
         self.optimizer = create_optimizer(self.model, a.optimizer_type, a.learning_rate, a.weight_decay,
                                           a.betas, a.adam_eps, a.use_fused_adam)
         self.total_steps = a.total_train_steps or 1000

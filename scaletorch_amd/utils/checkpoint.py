@@ -37,6 +37,10 @@ def checkpoint_filename(tp_rank: int, tp_ws: int, pp_rank: int, pp_ws: int, ep_r
     return name + ".pth"
 
 
+def _shard_filename() -> str:
+    return f"optimizer_shard_rank_world_size={C.get_rank()}_{C.get_world_size()}.pth"
+
+
 def _coords():
     pg = mesh.pgm
     if not pg:
@@ -81,19 +85,29 @@ class CheckpointManager:
         out_dir = out_dir or os.path.join(self.work_dir, str(trained_steps))
         path = os.path.join(out_dir, checkpoint_filename(tp, tpws, pp, ppws, ep, epws))
         raw = getattr(model, "module", model)
+        if hasattr(model, "wait_params"):  # ZeRO-1: parameter all-gathers may still be in flight
+            model.wait_params()
         writer = dp == 0 and cp == 0  # one copy per (tp, pp, ep) shard
+        sharded = bool(getattr(optimizer, "sharded", False))
+        writes = []
         if writer:
-            os.makedirs(out_dir, exist_ok=True)
             sd = raw.reference_state_dict() if hasattr(raw, "reference_state_dict") else raw.state_dict()
-            payload = {"model": _to_cpu(sd), "optimizer": _to_cpu(optimizer.state_dict()),
+            opt = {"zero1_sharded": True, "world": C.get_world_size()} if sharded else _to_cpu(optimizer.state_dict())
+            payload = {"model": _to_cpu(sd), "optimizer": opt,
                        "trained_steps": trained_steps, "trained_tokens": trained_tokens}
-            sched = _to_cpu(lr_scheduler.state_dict()) if lr_scheduler is not None else None
+            writes.append((path, payload))
+        if sharded:  # ZeRO-1: every rank owns a distinct optimizer shard
+            writes.append((os.path.join(out_dir, _shard_filename()), _to_cpu(optimizer.state_dict())))
+        if writes:
+            os.makedirs(out_dir, exist_ok=True)
+            sched = _to_cpu(lr_scheduler.state_dict()) if (lr_scheduler is not None and writer) else None
             self.wait()
 
             def _write():
-                tmp = path + ".tmp"
-                torch.save(payload, tmp, _use_new_zipfile_serialization=True)
-                os.replace(tmp, path)
+                for pth, obj in writes:
+                    tmp = pth + ".tmp"
+                    torch.save(obj, tmp, _use_new_zipfile_serialization=True)
+                    os.replace(tmp, pth)
                 if sched is not None and tp == 0 and pp == 0 and ep == 0:
                     torch.save(sched, os.path.join(out_dir, "scheduler.pt"))
 
@@ -121,7 +135,12 @@ class CheckpointManager:
             else:
                 raw.load_state_dict(ck["model"], strict=strict)
         if optimizer is not None:
-            optimizer.load_state_dict(ck["optimizer"])
+            opt = ck["optimizer"]
+            if isinstance(opt, dict) and opt.get("zero1_sharded"):
+                if opt.get("world") != C.get_world_size():
+                    raise ValueError("ZeRO-1 checkpoint was written with a different world size")
+                opt = torch.load(os.path.join(resume_path, _shard_filename()), map_location="cpu", weights_only=True)
+            optimizer.load_state_dict(opt)
         sp = os.path.join(resume_path, "scheduler.pt")
         if lr_scheduler is not None and os.path.exists(sp):
             lr_scheduler.load_state_dict(torch.load(sp, weights_only=True))
