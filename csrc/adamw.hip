@@ -37,29 +37,46 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, 
                                                      int64_t n4, float lr, float b1, float b2, float eps,
                                                      float wd, float bc1, float bc2_sqrt) {
   const float cs = clip ? *clip : 1.f;
-  const float step = lr / bc1;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n4;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t i = t * 4;
-    float4 w = ld4f(master + i), mm = ld4f(m + i), vv = ld4f(v + i), gg = load_g4<G>(g, i);
-    float wa[4] = {w.x, w.y, w.z, w.w}, ma[4] = {mm.x, mm.y, mm.z, mm.w};
-    float va[4] = {vv.x, vv.y, vv.z, vv.w}, ga[4] = {gg.x, gg.y, gg.z, gg.w};
+  const float step = lr / bc1, decay = 1.f - lr * wd;
+  // Two 16-B chunks per thread per iteration, all loads issued before any math
+  // (10 independent HBM streams in flight per thread); every byte is touched
+  // exactly once, so loads/stores are non-temporal (no L2 pollution).
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n4; t += 2 * stride) {
+    int64_t ii[2] = {t * 4, (t + stride) * 4};
+    const int nv = (t + stride < n4) ? 2 : 1;
+    f32x4 w[2], mm[2], vv[2];
+    float4 gg[2];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float gk = ga[k] * cs;
-      ma[k] = b1 * ma[k] + (1.f - b1) * gk;
-      va[k] = b2 * va[k] + (1.f - b2) * gk * gk;
-      const float denom = sqrtf(va[k]) / bc2_sqrt + eps;
-      wa[k] = wa[k] * (1.f - lr * wd) - step * ma[k] / denom;
+    for (int u = 0; u < 2; ++u) {
+      if (u < nv) {
+        w[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(master + ii[u]));
+        mm[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(m + ii[u]));
+        vv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(v + ii[u]));
+        gg[u] = load_g4<G>(g, ii[u]);
+      }
     }
-    st4f(master + i, make_float4(wa[0], wa[1], wa[2], wa[3]));
-    st4f(m + i, make_float4(ma[0], ma[1], ma[2], ma[3]));
-    st4f(v + i, make_float4(va[0], va[1], va[2], va[3]));
-    if (p) {
-      uint2 o;
-      o.x = pack_bf16x2(wa[0], wa[1]);
-      o.y = pack_bf16x2(wa[2], wa[3]);
-      *reinterpret_cast<uint2*>(p + i) = o;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (u >= nv) continue;
+      const float ga[4] = {gg[u].x, gg[u].y, gg[u].z, gg[u].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float gk = ga[k] * cs;
+        mm[u][k] = b1 * mm[u][k] + (1.f - b1) * gk;
+        vv[u][k] = b2 * vv[u][k] + (1.f - b2) * gk * gk;
+        const float denom = sqrtf(vv[u][k]) / bc2_sqrt + eps;
+        w[u][k] = w[u][k] * decay - step * mm[u][k] / denom;
+      }
+      __builtin_nontemporal_store(w[u], reinterpret_cast<f32x4*>(master + ii[u]));
+      __builtin_nontemporal_store(mm[u], reinterpret_cast<f32x4*>(m + ii[u]));
+      __builtin_nontemporal_store(vv[u], reinterpret_cast<f32x4*>(v + ii[u]));
+      if (p) {
+        uint2 o;
+        o.x = pack_bf16x2(w[u][0], w[u][1]);
+        o.y = pack_bf16x2(w[u][2], w[u][3]);
+        *reinterpret_cast<uint2*>(p + ii[u]) = o;
+      }
     }
   }
 }

@@ -90,16 +90,17 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
             extra = FILE_FLAGS.get(src.name, [])
             jobs_list.append([hipcc, f"--offload-arch={ARCH}", *common_flags, *extra, "-c", str(src), "-o",
                               str(obj)])
-    bsrc = CSRC / "bindings.cpp"
-    bobj = BUILD / "bindings.o"
-    objs.append(bobj)
-    if force or _stale(bobj, [bsrc]):
-        cxx = shutil.which("g++") or "c++"
-        inc_flags = [f"-I{p}" for p in inc] + [f"-I{ROCM / 'include'}"]
-        jobs_list.append(
-            [cxx, *common_flags, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-D_GLIBCXX_USE_CXX11_ABI=1",
-             *inc_flags, "-c", str(bsrc), "-o", str(bobj)]
-        )
+    # host C++ (torch op registrations, hipBLASLt tuner): g++ against the PyTorch headers
+    cxx = shutil.which("g++") or "c++"
+    inc_flags = [f"-I{p}" for p in inc] + [f"-I{ROCM / 'include'}"]
+    for bsrc in sorted(CSRC.glob("*.cpp")):
+        bobj = BUILD / (bsrc.stem + ".o")
+        objs.append(bobj)
+        if force or _stale(bobj, [bsrc]):
+            jobs_list.append(
+                [cxx, *common_flags, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-D_GLIBCXX_USE_CXX11_ABI=1",
+                 *inc_flags, "-c", str(bsrc), "-o", str(bobj)]
+            )
     n = jobs or min(8, os.cpu_count() or 4)
     if jobs_list:
         with cf.ThreadPoolExecutor(max_workers=n) as ex:
@@ -109,7 +110,8 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         link = [hipcc, "-shared", f"--offload-arch={ARCH}", "-fPIC", *map(str, objs), "-o", str(tmp)]
         for d in libdirs:
             link += [f"-L{d}", f"-Wl,-rpath,{d}"]
-        link += ["-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch", "-lamdhip64"]
+        link += ["-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch", "-lamdhip64",
+                 f"-L{ROCM / 'lib'}", "-lhipblaslt"]
         _run(link, verbose)
         os.replace(tmp, LIB)
     return LIB

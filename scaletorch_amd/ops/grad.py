@@ -27,12 +27,29 @@ def _grad_ready(param: torch.Tensor) -> None:
         hook(param)
 
 
+def take_fresh(param: torch.Tensor) -> bool:
+    """True (once per step) if ``param.main_grad`` holds last step's values.
+
+    The arena does not zero its fp32 gradients between steps (a 4-byte/param
+    fill pass); instead every parameter is marked fresh and its FIRST gradient
+    write of the step overwrites (GEMM beta = 0, copy) rather than accumulates.
+    Parameters nobody wrote are zeroed before their bucket is reduced
+    (data_parallel.GradArena.zero_fresh)."""
+    if getattr(param, "_st_fresh", False):
+        param._st_fresh = False
+        return True
+    return False
+
+
 def accumulate_grad(param: torch.Tensor, grad: torch.Tensor):
     """Add ``grad`` into ``param.main_grad`` (returns None) or return it for autograd."""
     mg = getattr(param, "main_grad", None)
     if mg is None:
         return grad.to(param.dtype) if grad.dtype != param.dtype else grad
-    mg.add_(grad.view_as(mg))
+    if take_fresh(param):
+        mg.copy_(grad.view_as(mg))
+    else:
+        mg.add_(grad.view_as(mg))
     _grad_ready(param)
     return None
 
@@ -47,18 +64,22 @@ def accumulate_linear_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
     mg = getattr(param, "main_grad", None)
     if mg is None:
         return dy2d.t().mm(x2d)
+    beta = 0 if take_fresh(param) else 1
     if mg.dtype == dy2d.dtype:
-        mg.addmm_(dy2d.t(), x2d)
+        mg.addmm_(dy2d.t(), x2d, beta=beta)
     else:
         done = False
         if _ADDMM_DTYPE_OK is not False and dy2d.is_cuda and os.environ.get("ST_WGRAD_FP32_GEMM", "1") == "1":
             try:
-                torch.ops.aten.addmm.dtype_out(mg, dy2d.t(), x2d, mg.dtype, beta=1, alpha=1, out=mg)
+                torch.ops.aten.addmm.dtype_out(mg, dy2d.t(), x2d, mg.dtype, beta=beta, alpha=1, out=mg)
                 _ADDMM_DTYPE_OK = True
                 done = True
             except (RuntimeError, NotImplementedError):
                 _ADDMM_DTYPE_OK = False
         if not done:
-            mg.add_(dy2d.t().mm(x2d))
+            if beta == 0:
+                mg.copy_(dy2d.t().mm(x2d))
+            else:
+                mg.add_(dy2d.t().mm(x2d))
     _grad_ready(param)
     return None

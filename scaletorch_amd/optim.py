@@ -66,8 +66,13 @@ class _ArenaOptimizer(torch.optim.Optimizer):
         self.dp.zero_grad()
 
     # ---------------------------------------------------------------- clipping
+    def _zero_unwritten(self) -> None:
+        for a in self.arenas:  # normally a no-op: the DP sync already zeroed untouched grads
+            a.zero_fresh()
+
     def grad_norm(self, mp_group=None) -> torch.Tensor:
         """Global L2 norm of the gradients (device scalar, fp32)."""
+        self._zero_unwritten()
         segs = self.dp.grad_sumsq_segments()
         dev = segs[0][0].device
         total = torch.zeros(1, dtype=torch.float32, device=dev)
@@ -135,6 +140,7 @@ class ArenaAdamW(_ArenaOptimizer):
 
     @torch.no_grad()
     def step(self, closure=None):  # noqa: ARG002
+        self._zero_unwritten()
         self._step += 1
         t = self._step
         for g, a in zip(self.param_groups, self.arenas):
@@ -188,6 +194,7 @@ class ArenaSGD(_ArenaOptimizer):
 
     @torch.no_grad()
     def step(self, closure=None):  # noqa: ARG002
+        self._zero_unwritten()
         self._step += 1
         for g, a in zip(self.param_groups, self.arenas):
             for param, gseg, master, mom in self._views(a, (a.momentum_buf,)):
@@ -223,6 +230,7 @@ class ArenaLAMB(ArenaAdamW):
 
     @torch.no_grad()
     def step(self, closure=None):  # noqa: ARG002
+        self._zero_unwritten()
         self._step += 1
         t = self._step
         for g, a in zip(self.param_groups, self.arenas):

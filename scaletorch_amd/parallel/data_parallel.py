@@ -168,12 +168,28 @@ class GradArena:
 
     def zero_grad(self) -> None:
         self.grad_flat.zero_()
+        for p in self.params:
+            p._st_fresh = False
+
+    def mark_fresh(self) -> None:
+        """Lazy zeroing: the first gradient write of the next step overwrites
+        (ops/grad.py ``take_fresh``), so no fill pass over the fp32 arena."""
+        for p in self.params:
+            p._st_fresh = True
+
+    def zero_fresh(self, params=None) -> None:
+        """Zero the gradients nobody wrote this step (before they are reduced / read)."""
+        for p in (self.params if params is None else params):
+            if getattr(p, "_st_fresh", False):
+                p.main_grad.zero_()
+                p._st_fresh = False
 
     # ---------------------------------------------------------------- comm
     def launch(self, b: Bucket) -> None:
         if b.launched:
             return
         b.launched = True
+        self.zero_fresh(b.params)
         if self.world == 1:
             return
         g = self.grad_flat[b.start: b.end]
@@ -366,7 +382,11 @@ class DataParallel(nn.Module):
             p.grad = None  # stale exposed view from the previous step: autograd accumulated into main_grad
             self._grad_ready(p)
             return
-        p.main_grad.add_(p.grad.view_as(p.main_grad))
+        if getattr(p, "_st_fresh", False):
+            p._st_fresh = False
+            p.main_grad.copy_(p.grad.view_as(p.main_grad))
+        else:
+            p.main_grad.add_(p.grad.view_as(p.main_grad))
         p.grad = None
         self._grad_ready(p)
 
@@ -427,7 +447,7 @@ class DataParallel(nn.Module):
 
     def zero_grad(self, set_to_none: bool = False) -> None:  # noqa: ARG002 - arenas are persistent
         for a in self.arenas:
-            a.zero_grad()
+            a.mark_fresh()
             a.reset_counts()
         for p in self.module.parameters():
             p.grad = None

@@ -7,7 +7,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
-from ..ops.grad import _grad_ready
+from ..ops.grad import _grad_ready, take_fresh
 
 
 class _EmbeddingFn(torch.autograd.Function):
@@ -22,6 +22,8 @@ class _EmbeddingFn(torch.autograd.Function):
         (ids,) = ctx.saved_tensors
         w = ctx.weight
         mg = w.main_grad
+        if take_fresh(w):
+            mg.zero_()
         mg.index_add_(0, ids.reshape(-1), dy.reshape(-1, dy.shape[-1]).to(mg.dtype))
         _grad_ready(w)
         return None, None

@@ -43,11 +43,14 @@ def main():
     ap.add_argument("--seq", type=int, default=4096)
     ap.add_argument("--batch", type=int, default=2)
     ap.add_argument("--only", default="")
+    ap.add_argument("--blas", default="", help="torch BLAS backend for the reference GEMMs: hipblaslt | rocblas")
     args = ap.parse_args()
     from scaletorch_amd import ops
     from scaletorch_amd.ops import _lib
 
     assert _lib.load(), _lib.load_error()
+    if args.blas:
+        torch.backends.cuda.preferred_blas_library(args.blas)
     st = _lib.ops()
     B, S, H, Hkv, D, h, I = args.batch, args.seq, 32, 8, 128, 4096, 14336
     res = {"shape": dict(B=B, S=S, H=H, Hkv=Hkv, D=D)}
@@ -102,6 +105,37 @@ def main():
                 res["addmm_dtype_error"] = str(e)[:200]
             t = timeit(lambda: mg.add_(dy.t().mm(xi)))
             res[f"gemm_{name}_wgrad_plus_add_tflops"] = 2 * N * o_ * i_ / t / 1e9
+    if not args.only or "tgemm" in args.only:
+        # autotuned hipBLASLt (st_amd.gemm_) vs torch's default solution, same problems
+        N = B * S
+        for name, (o_, i_) in {"qkv": (6144, h), "out": (h, h), "gate_up": (2 * I, h), "down": (h, I),
+                               "lm_head": (128256, h)}.items():
+            w = torch.randn(o_, i_, device=dev, dtype=torch.bfloat16)
+            xi = torch.randn(N, i_, device=dev, dtype=torch.bfloat16)
+            dy = torch.randn(N, o_, device=dev, dtype=torch.bfloat16)
+            fl = 2 * N * o_ * i_ / 1e9
+            y = torch.empty(N, o_, device=dev, dtype=torch.bfloat16)
+            st.gemm_(y, xi, w, False, True, 1.0, 0.0)
+            res[f"tg_{name}_fwd_err"] = ((y.float() - F.linear(xi, w).float()).norm() / y.float().norm()).item()
+            res[f"tg_{name}_fwd_tflops"] = fl / timeit(lambda: st.gemm_(y, xi, w, False, True, 1.0, 0.0))
+            res[f"torch_{name}_fwd_tflops"] = fl / timeit(lambda: F.linear(xi, w))
+            dx = torch.empty(N, i_, device=dev, dtype=torch.bfloat16)
+            res[f"tg_{name}_dgrad_tflops"] = fl / timeit(lambda: st.gemm_(dx, dy, w, False, False, 1.0, 0.0))
+            res[f"torch_{name}_dgrad_tflops"] = fl / timeit(lambda: dy.mm(w))
+            mg = torch.zeros(o_, i_, device=dev, dtype=torch.float32)
+            st.gemm_(mg, dy, xi, True, False, 1.0, 1.0)
+            res[f"tg_{name}_wgrad_err"] = ((mg - dy.float().t() @ xi.float()).norm() / mg.norm()).item()
+            res[f"tg_{name}_wgrad_fp32acc_tflops"] = fl / timeit(lambda: st.gemm_(mg, dy, xi, True, False, 1.0, 1.0))
+            res[f"torch_{name}_wgrad_fp32acc_tflops"] = fl / timeit(
+                lambda: torch.ops.aten.addmm.dtype_out(mg, dy.t(), xi, torch.float32, beta=1, alpha=1, out=mg))
+            # same product with token-contiguous (pre-transposed) operands: the fwd-like layout
+            dyT, xT = dy.t().contiguous(), xi.t().contiguous()
+            res[f"tg_{name}_wgradT_fp32acc_tflops"] = fl / timeit(
+                lambda: st.gemm_(mg, dyT, xT, False, True, 1.0, 1.0))
+            res[f"transpose_{name}_ms"] = timeit(lambda: (dy.t().contiguous(), xi.t().contiguous()))
+            del w, xi, dy, y, dx, mg, dyT, xT
+        rep = st.gemm_tuning_report()
+        res["tuning"] = [rep[i:i + 7] for i in range(0, len(rep), 7)]
     if not args.only or "elt" in args.only:
         N = B * S
         x = torch.randn(N, h, device=dev, dtype=torch.bfloat16)
