@@ -176,6 +176,8 @@ class SystemArguments:
     profile_dir: str = field(default="./profiles/trace")
     nan_check: bool = field(default=True, metadata={"help": "abort on non-finite loss"})
     timeout_s: int = field(default=600)
+    watchdog_s: float = field(default=0.0, metadata={"help": "abort (exit 75, torchrun restarts + --auto_resume) "
+                                                            "when a step makes no progress for this long; 0 = off"})
     debug_collectives: bool = field(default=False, metadata={"help": "cross-check collective order across ranks"})
 
 

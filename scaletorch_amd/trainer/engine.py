@@ -30,6 +30,7 @@ from ..optim import create_optimizer
 from ..parallel import mesh
 from ..parallel.data_parallel import DataParallel, mark_tp_sharded
 from ..parallel.pipeline_parallel import PipelineEngine
+from ..utils import profiling
 from ..utils.misc import set_all_seed
 from .lr_scheduler import create_lr_scheduler
 
@@ -48,6 +49,10 @@ class Trainer:
         if self.world > 1:
             mesh.setup_process_group_manager(a.tensor_parallel_size, a.context_parallel_size,
                                              a.pipeline_parallel_size, a.data_parallel_size, a.expert_parallel_size)
+            if a.debug_collectives:
+                from ..dist import debug
+
+                debug.enable(timeout_s=a.timeout_s)
         if a.context_parallel_size > 1:
             from ..parallel.context_parallel import set_cp_comm, set_cp_zigzag
 
@@ -161,18 +166,21 @@ class Trainer:
                 batch = self._to_device(next(self.data))
                 ctx = self.model.no_sync() if i < ga - 1 else contextlib.nullcontext()
                 with ctx:
-                    logits = self.model(input_ids=batch["input_ids"], position_ids=batch["position_ids"],
-                                        gradient_checkpointing=a.gradient_checkpointing)
-                    l = self._loss(logits, batch) / ga
-                    del logits
-                    if self.model_config.is_moe:
-                        aux = self.raw_model.aux_loss()
-                        if aux is not None:
-                            l = l + aux / ga
-                    l.backward()
+                    with profiling.range("forward"):
+                        logits = self.model(input_ids=batch["input_ids"], position_ids=batch["position_ids"],
+                                            gradient_checkpointing=a.gradient_checkpointing)
+                        l = self._loss(logits, batch) / ga
+                        del logits
+                        if self.model_config.is_moe:
+                            aux = self.raw_model.aux_loss()
+                            if aux is not None:
+                                l = l + aux / ga
+                    with profiling.range("backward"):
+                        l.backward()
                 loss += l.detach().float()
-        self.optimizer.clip_grad_norm_(a.max_grad_norm, self.mp_group)
-        self.optimizer.step()
+        with profiling.range("optimizer"):
+            self.optimizer.clip_grad_norm_(a.max_grad_norm, self.mp_group)
+            self.optimizer.step()
         self.lr_scheduler.step()
         self.step += 1
         self.trained_tokens += self.tokens_per_step

@@ -16,6 +16,7 @@ fault-injection env ST_FAULT_STEP / ST_FAULT_RANK used by the resume tests.
 from __future__ import annotations
 
 import json
+import math
 import os
 import signal
 import sys
@@ -89,6 +90,14 @@ def main(argv=None) -> int:
                        schedule=schedule(wait=2, warmup=1, active=3, repeat=1),
                        on_trace_ready=tensorboard_trace_handler(args.profile_dir), record_shapes=False)
         prof.start()
+        from scaletorch_amd.utils import profiling
+
+        profiling.set_enabled(True)  # roctx ranges around fwd / bwd / optimizer in the trace
+    watchdog = None
+    if args.watchdog_s and args.watchdog_s > 0:
+        from scaletorch_amd.utils.watchdog import StepWatchdog
+
+        watchdog = StepWatchdog(args.watchdog_s).start()
     stop = {"flag": False}
     signal.signal(signal.SIGTERM, lambda *_: stop.__setitem__("flag", True))
     try:
@@ -101,6 +110,8 @@ def main(argv=None) -> int:
             monitor.start_iteration()
             loss_t = tr.train_step()
             rec = monitor.end_iteration(tr.tokens_per_step)
+            if watchdog is not None:
+                watchdog.kick(tr.step)
             if prof is not None:
                 prof.step()
             if tr.step % max(1, args.log_interval) == 0 or tr.step == total:
@@ -109,6 +120,8 @@ def main(argv=None) -> int:
                     raise FloatingPointError(f"non-finite loss at step {tr.step}")
                 gn = tr.optimizer.last_grad_norm
                 gn = float(gn.item()) if gn is not None else None
+                if args.nan_check and gn is not None and not math.isfinite(gn):
+                    raise FloatingPointError(f"non-finite gradient norm {gn} at step {tr.step}")
                 tok_s = rec["tokens_per_s"]
                 per_gpu = tok_s / world
                 mfu = per_gpu * fpt / peak * 100
@@ -134,6 +147,8 @@ def main(argv=None) -> int:
     except KeyboardInterrupt:
         log.warning("interrupted; cleaning up")
     finally:
+        if watchdog is not None:
+            watchdog.stop()
         if prof is not None:
             prof.stop()
         ckpt.wait()
