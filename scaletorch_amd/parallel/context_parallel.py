@@ -237,13 +237,114 @@ def _merge(acc: torch.Tensor, lse: torch.Tensor, bo: torch.Tensor, bl: torch.Ten
     lse.copy_(L)
 
 
+# ---------------------------------------------------------------- Ulysses (all-to-all) transport
+def _a2a(x: torch.Tensor, group) -> torch.Tensor:
+    """all_to_all_single over dim 0 (= destination rank on input, source rank on output)."""
+    return C.all_to_all(x.contiguous(), group=group)
+
+
+def _kv_heads_for(Hkv: int, P: int) -> int:
+    """kv heads per rank after the head scatter (GQA groups stay whole)."""
+    if Hkv % P == 0:
+        return Hkv // P
+    if P % Hkv == 0:
+        return 1  # kv heads replicated P/Hkv times, one per rank
+    raise ValueError(f"ulysses needs Hkv % cp == 0 or cp % Hkv == 0 (Hkv={Hkv}, cp={P})")
+
+
+def _scatter_heads(x: torch.Tensor, P: int, group) -> torch.Tensor:
+    """[B, s, P*h, D] sequence shard -> [B, P*s, h, D] head shard (rank order of sequence)."""
+    B, s, HH, D = x.shape
+    h = HH // P
+    t = x.view(B, s, P, h, D).permute(2, 0, 1, 3, 4)  # [P(dst), B, s, h, D]
+    r = _a2a(t, group)  # [P(src), B, s, h, D]
+    return r.permute(1, 0, 2, 3, 4).reshape(B, P * s, h, D)
+
+
+def _gather_heads(x: torch.Tensor, P: int, group) -> torch.Tensor:
+    """Inverse of _scatter_heads: [B, P*s, h, D] -> [B, s, P*h, D]."""
+    B, S, h, D = x.shape
+    s = S // P
+    t = x.view(B, P, s, h, D).permute(1, 0, 2, 3, 4)  # [P(dst: seq owner), B, s, h, D]
+    r = _a2a(t, group)  # [P(src: head owner), B, s, h, D]
+    return r.permute(1, 2, 0, 3, 4).reshape(B, s, P * h, D)
+
+
+class _UlyssesAttnFn(torch.autograd.Function):
+    """DeepSpeed-Ulysses sequence parallelism (absent in the reference):
+    one all-to-all turns the sequence-sharded q/k/v into head-sharded full
+    sequences, the HIP flash kernel runs plain causal attention on H/cp heads,
+    and one all-to-all returns the output to sequence shards.  4 all-to-alls
+    per layer (fwd 2, bwd 2) of activation size / cp each -- per-link traffic
+    independent of cp, versus the K/V all-gather's (cp-1)/cp of the sequence;
+    best when heads >= cp and the sequence is long."""
+
+    @staticmethod
+    def forward(ctx, q, kv, H, Hkv, D, scale, zigzag):
+        group, P, rank = _cp()
+        if H % P:
+            raise ValueError(f"ulysses needs num_attention_heads % cp == 0 (H={H}, cp={P})")
+        B, s = q.shape[0], q.shape[1]
+        S = s * P
+        hk = _kv_heads_for(Hkv, P)
+        k, v = kv[:, :, :Hkv], kv[:, :, Hkv:]
+        rep = (P * hk) // Hkv
+        if rep > 1:  # every rank needs the kv head of its query-head block
+            k, v = k.repeat_interleave(rep, dim=2), v.repeat_interleave(rep, dim=2)
+        qf = _scatter_heads(q, P, group)  # [B, S, H/P, D]
+        kvf = _scatter_heads(torch.cat([k.reshape(B, s, P, hk, D), v.reshape(B, s, P, hk, D)], dim=3)
+                             .reshape(B, s, P * 2 * hk, D), P, group)  # [B, S, 2hk, D]
+        if zigzag:
+            idx = _global_order_index(S, P, q.device)
+            qf, kvf = qf.index_select(1, idx), kvf.index_select(1, idx)
+        kf, vf = kvf[:, :, :hk], kvf[:, :, hk:]
+        o, lse = ops.flash_attn_fwd(qf, kf, vf, scale, True, 0, 0)
+        ctx.save_for_backward(qf, kvf, o, lse)
+        ctx.meta = (H, Hkv, hk, rep, D, scale, zigzag, S)
+        if zigzag:
+            o = o.index_select(1, _inverse(idx))
+        return _gather_heads(o, P, group)  # [B, s, H, D]
+
+    @staticmethod
+    def backward(ctx, dout):
+        qf, kvf, o, lse = ctx.saved_tensors
+        H, Hkv, hk, rep, D, scale, zigzag, S = ctx.meta
+        group, P, rank = _cp()
+        B, s = dout.shape[0], dout.shape[1]
+        dof = _scatter_heads(dout.contiguous(), P, group)
+        if zigzag:
+            idx = _global_order_index(S, P, dout.device)
+            dof = dof.index_select(1, idx)
+        kf, vf = kvf[:, :, :hk], kvf[:, :, hk:]
+        dq, dk, dv = ops.flash_attn_bwd(dof.contiguous(), qf, kf, vf, o, lse, scale, True, 0, 0)
+        dkv = torch.cat([dk, dv], dim=2)
+        if zigzag:
+            inv = _inverse(idx)
+            dq, dkv = dq.index_select(1, inv), dkv.index_select(1, inv)
+        dq = _gather_heads(dq, P, group)  # [B, s, H, D]
+        dkv = _gather_heads(dkv, P, group).view(B, s, P, 2, hk, D)  # per rank block [k heads | v heads]
+        dk = dkv[:, :, :, 0].reshape(B, s, P * hk, D)
+        dv = dkv[:, :, :, 1].reshape(B, s, P * hk, D)
+        if rep > 1:  # sum the replicas of each kv head
+            dk = dk.float().view(B, s, Hkv, rep, D).sum(3).to(dout.dtype)
+            dv = dv.float().view(B, s, Hkv, rep, D).sum(3).to(dout.dtype)
+        return dq, torch.cat([dk, dv], dim=2), None, None, None, None, None
+
+
+def _inverse(idx: torch.Tensor) -> torch.Tensor:
+    inv = torch.empty_like(idx)
+    inv[idx] = torch.arange(idx.numel(), device=idx.device)
+    return inv
+
+
 _CP_COMM = "allgather"
+_CP_FNS = {"allgather": "_CPAttnFn", "ring": "_RingAttnFn", "ulysses": "_UlyssesAttnFn"}
 
 
 def set_cp_comm(mode: str) -> None:
     global _CP_COMM
-    if mode not in ("allgather", "ring"):
-        raise ValueError(f"cp_comm must be 'allgather' or 'ring', got {mode!r}")
+    if mode not in _CP_FNS:
+        raise ValueError(f"cp_comm must be one of {sorted(_CP_FNS)}, got {mode!r}")
     _CP_COMM = mode
 
 
@@ -257,7 +358,7 @@ def context_parallel_attention(qkv: torch.Tensor, cos, sin, position_ids, H: int
     q = ops.apply_rope(qkv4[:, :, :H], cos, sin, position_ids)
     k = ops.apply_rope(qkv4[:, :, H: H + Hkv], cos, sin, position_ids)
     kv = torch.cat([k, qkv4[:, :, H + Hkv:]], dim=2)
-    fn = _RingAttnFn if _CP_COMM == "ring" else _CPAttnFn
+    fn = globals()[_CP_FNS[_CP_COMM]]
     out = fn.apply(q.contiguous(), kv.contiguous(), H, Hkv, D, scale, zigzag)
     return out.reshape(B, s, H * D)
 

@@ -122,12 +122,23 @@ def _compare(ref, results, atol=2e-5, rtol=2e-3):
     dict(context_parallel_size=2, micro_batch_size=4),
     dict(context_parallel_size=2, micro_batch_size=4, cp_comm="ring"),
     dict(context_parallel_size=2, micro_batch_size=4, cp_comm="ring", cp_zigzag=False),
+    dict(context_parallel_size=2, micro_batch_size=4, cp_comm="ulysses"),
+    dict(context_parallel_size=2, micro_batch_size=4, cp_comm="ulysses", cp_zigzag=False),
     dict(pipeline_parallel_size=2, micro_batch_size=2, gradient_accumulation_steps=2),
     dict(pipeline_parallel_size=2, micro_batch_size=2, gradient_accumulation_steps=2, pipeline_parallel_engine="afab"),
-], ids=["dp2", "dp2_ga2", "tp2", "tp2_sp", "cp2", "cp2_ring", "cp2_ring_contig", "pp2_1f1b", "pp2_afab"])
+], ids=["dp2", "dp2_ga2", "tp2", "tp2_sp", "cp2", "cp2_ring", "cp2_ring_contig", "cp2_ulysses",
+        "cp2_ulysses_contig", "pp2_1f1b", "pp2_afab"])
 def test_dense_parity_world2(kw):
     ref = _reference("tiny-llama")
     res = run_workers(_worker, 2, "tiny-llama", kw)
+    _compare(ref, res)
+
+
+@pytest.mark.parametrize("comm", ["ulysses", "allgather"])
+def test_cp4_parity_world4(comm):
+    """cp=4 > Hkv=2: Ulysses replicates each kv head over 2 ranks and sums their dK/dV."""
+    ref = _reference("tiny-llama")
+    res = run_workers(_worker, 4, "tiny-llama", dict(context_parallel_size=4, micro_batch_size=4, cp_comm=comm))
     _compare(ref, res)
 
 
