@@ -79,14 +79,12 @@ class MoERouter(nn.Module):
 
     def forward(self, x2d: torch.Tensor):
         logits = ops.linear(x2d, self.gate.weight).float()
-        probs = torch.softmax(logits, dim=-1)
-        topw, topi = torch.topk(probs, self.top_k, dim=-1)
-        if self.norm_topk_prob:
-            topw = topw / topw.sum(-1, keepdim=True)
+        # fused softmax + top-k + renorm (one wave per token, csrc/moe.hip)
+        probs, topw, topi = ops.moe.router_topk(logits, self.top_k, self.norm_topk_prob)
         # Switch aux loss: coef * E * sum_e f_e * P_e
         T = x2d.shape[0]
         counts = torch.zeros(self.num_experts, device=x2d.device, dtype=torch.float32)
-        counts.scatter_add_(0, topi.reshape(-1), torch.ones_like(topi.reshape(-1), dtype=torch.float32))
+        counts.scatter_add_(0, topi.reshape(-1).long(), torch.ones(topi.numel(), device=x2d.device))
         f = counts / max(1, T * self.top_k)
         P = probs.mean(0)
         aux = self.aux_coef * self.num_experts * (f * P).sum()
@@ -194,13 +192,11 @@ class MoELayer(nn.Module):
                 x2 = CopyToTensorParallelRegion.apply(x2, tp_group)
                 topw = CopyToTensorParallelRegion.apply(topw, tp_group)
         shape = x.shape
-        T = x2.shape[0]
         self.last_aux_loss = aux if self.training else None
-        flat_e = topi.reshape(-1)  # [T*k]
-        order = torch.argsort(flat_e, stable=True)
-        tok = order // self.top_k
-        counts = torch.bincount(flat_e, minlength=self.num_experts)
-        xs = x2.index_select(0, tok)  # rows sorted by global expert
+        # stable sort of the T*k (token, slot) entries by global expert + row gather
+        perm = ops.moe.permutation(topi, self.num_experts)
+        counts = perm.counts
+        xs = ops.moe.gather_rows(x2, perm)  # rows sorted by global expert
         if self.ep == 1:
             y = self.experts(xs, counts.tolist())
         else:
@@ -224,15 +220,12 @@ class MoELayer(nn.Module):
                     if n:
                         b = int(starts[s, e])
                         idx.append(torch.arange(b, b + n))
-            perm = torch.cat(idx).to(x.device) if idx else torch.zeros(0, dtype=torch.long, device=x.device)
-            ye = self.experts(xr.index_select(0, perm), recv_mat_h.sum(0).tolist())
+            regroup = torch.cat(idx).to(x.device) if idx else torch.zeros(0, dtype=torch.long, device=x.device)
+            ye = self.experts(xr.index_select(0, regroup), recv_mat_h.sum(0).tolist())
             yr = torch.empty_like(ye)
-            yr = yr.index_copy(0, perm, ye) if perm.numel() else ye
+            yr = yr.index_copy(0, regroup, ye) if regroup.numel() else ye
             y = all_to_all_rows(yr, send_splits, recv_splits, group)
-        w = topw.reshape(-1).index_select(0, order).to(y.dtype)
-        out = torch.zeros(T, shape[-1], device=x.device, dtype=y.dtype)
-        out = out.index_add(0, tok, y * w[:, None])
-        out = out.view(shape)
+        out = ops.moe.combine(y, topw, perm).view(shape)
         # expert down-projections are TP partial sums: reduce once, after the combine
         if self.sequence_parallel:
             out = ReduceScatterToSequenceParallelRegion.apply(out, tp_group)

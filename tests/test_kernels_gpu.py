@@ -246,3 +246,55 @@ def test_rope_attention_autograd_matches_reference():
         os.environ["ST_DISABLE_NATIVE"] = "0"
     assert rel(out, ref) < 2e-2
     assert rel(gq, qf.grad) < 3e-2
+
+
+@pytest.mark.parametrize("T,E,k,renorm", [(3000, 8, 2, True), (2500, 128, 8, True), (700, 60, 4, False)])
+def test_moe_router_topk(T, E, k, renorm):
+    from scaletorch_amd.ops import moe
+
+    torch.manual_seed(0)
+    logits = torch.randn(T, E, device="cuda") * 2
+    probs, topw, topi = moe.router_topk(logits, k, renorm)
+    rp, rw, ri = moe._router_ref(logits, k, renorm)
+    assert torch.allclose(probs, rp, atol=1e-6, rtol=1e-5)
+    assert torch.equal(topi.long().sort(-1).values, ri.long().sort(-1).values)
+    assert torch.allclose(topw, rw, atol=1e-6, rtol=1e-5)
+    # gradients: topw and the aux-loss path through probs
+    lg = logits.clone().requires_grad_(True)
+    p, w, _ = moe.router_topk(lg, k, renorm)
+    gw, gp = torch.randn_like(w), torch.randn_like(p)
+    ((w * gw).sum() + (p * gp).sum()).backward()
+    lr = logits.clone().requires_grad_(True)
+    p2, w2, _ = moe._router_ref(lr, k, renorm)
+    ((w2 * gw).sum() + (p2 * gp).sum()).backward()
+    assert rel(lg.grad, lr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("T,E,k,h", [(3000, 8, 2, 256), (1500, 128, 8, 512), (5, 64, 4, 64)])
+def test_moe_permute_gather_combine(T, E, k, h):
+    from scaletorch_amd.ops import moe
+
+    torch.manual_seed(0)
+    topi = torch.randint(0, E, (T, k), device="cuda", dtype=torch.int32)
+    perm = moe.permutation(topi, E)
+    order = torch.argsort(topi.reshape(-1).long(), stable=True)
+    assert torch.equal(perm.sorted_entry.long(), order)
+    assert torch.equal(perm.counts.long(), torch.bincount(topi.reshape(-1).long(), minlength=E))
+    assert torch.equal(perm.pos.long()[order], torch.arange(T * k, device="cuda"))
+    x = torch.randn(T, h, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    xs = moe.gather_rows(x, perm)
+    assert torch.equal(xs, x.detach().index_select(0, order // k))
+    w = torch.rand(T, k, device="cuda", requires_grad=True)
+    y = (xs.float() * 1.5).to(torch.bfloat16)  # an "expert"
+    out = moe.combine(y, w, perm)
+    ref_y = y.detach().float().requires_grad_(True)
+    ref_w = w.detach().clone().requires_grad_(True)
+    ref = (ref_y.index_select(0, perm.pos.long()).view(T, k, h) * ref_w.unsqueeze(-1)).sum(1)
+    assert rel(out, ref) < 1e-2
+    g = torch.randn(T, h, device="cuda", dtype=torch.bfloat16)
+    out.backward(g)
+    ref.backward(g.float())
+    assert rel(w.grad, ref_w.grad) < 1e-2
+    # dx: every token receives sum over its slots of 1.5 * w * g
+    exp_dx = 1.5 * (ref_w.detach().sum(-1, keepdim=True) * g.float())
+    assert rel(x.grad, exp_dx) < 2e-2
