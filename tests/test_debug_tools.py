@@ -101,3 +101,21 @@ def test_bench_comm_gloo():
     ops = {r["op"] for r in rows}
     assert ops == {"all_reduce", "reduce_scatter", "all_gather", "all_to_all", "broadcast", "sendrecv"}
     assert all(r["busbw_GBps"] >= 0 and r["time_us"] > 0 for r in rows)
+
+
+def test_benchmark_sweep_list_and_dry_run(capsys):
+    import importlib.util
+    import os
+
+    spec = importlib.util.spec_from_file_location(
+        "benchmark_sweep", os.path.join(os.path.dirname(os.path.dirname(__file__)), "scripts", "benchmark_sweep.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    cfgs = mod.build_configs(8)
+    names = [c["name"] for c in cfgs]
+    assert "llama3-8b-dp8" in names and "qwen3-8b-tp2-dp4" in names and "mixtral-8x7b-ep8" in names
+    assert all(8 % (c["tp"] * c["pp"] * c["cp"] * c["ep"]) == 0 for c in cfgs)
+    assert mod.main(["--gpus", "8", "--dry-run", "--filter", "^llama3-8b-tp2-pp2"]) == 0
+    out = capsys.readouterr().out
+    assert "--tp 2" in out and "--pp 2" in out and "--nproc-per-node=8" in out
+    assert mod.parse_result('noise\n{"metric": "x", "value": 1}\n') == {"metric": "x", "value": 1}
