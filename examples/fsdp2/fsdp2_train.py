@@ -1,0 +1,149 @@
+#!/usr/bin/env python3
+"""FSDP2 (``torch.distributed.fsdp.fully_shard``) training of a scaletorch_amd
+transformer -- the framework's HIP kernels (flash attention, RMSNorm, SwiGLU,
+RoPE, vocab-parallel CE) running under PyTorch's per-parameter sharding.
+
+Reference: examples/FSDP2/fsdp2_main.py + checkpoint.py (toy Transformer,
+MixedPrecisionPolicy, explicit prefetching, DTensor and DCP checkpoints).
+Here the model is a real registry model (``--model tiny-llama`` ... ``llama3-8b``)
+and the step uses RCCL reduce-scatter / all-gather over xGMI (gloo on CPU).
+
+  torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/fsdp2/fsdp2_train.py \
+      --model llama3-8b --seq 4096 --mbs 1 --steps 10 --mixed-precision
+  torchrun --nproc-per-node 2 --master-addr 127.0.0.1 examples/fsdp2/fsdp2_train.py --cpu  # gloo smoke
+
+Checkpoints: ``--dcp`` writes a sharded torch.distributed.checkpoint directory
+(each rank its shards, resumable at any world size); the default writes one
+full (unsharded) state dict from rank 0 gathered with
+``get_model_state_dict(full_state_dict=True, cpu_offload=True)``.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.realpath(__file__))))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="tiny-llama")
+    ap.add_argument("--layers", type=int, default=None)
+    ap.add_argument("--seq", type=int, default=128)
+    ap.add_argument("--mbs", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--lr", type=float, default=3e-4)
+    ap.add_argument("--mixed-precision", action="store_true", help="bf16 params in compute, fp32 reduce")
+    ap.add_argument("--explicit-prefetching", action="store_true")
+    ap.add_argument("--dcp", action="store_true", help="sharded torch.distributed.checkpoint instead of full")
+    ap.add_argument("--ckpt-dir", default="")
+    ap.add_argument("--resume", action="store_true")
+    ap.add_argument("--cpu", action="store_true")
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> dict:
+    args = parse(argv)
+    from torch.distributed.device_mesh import init_device_mesh
+    from torch.distributed.fsdp import MixedPrecisionPolicy, fully_shard
+
+    from scaletorch_amd import ops
+    from scaletorch_amd.dist.launch import init_dist
+    from scaletorch_amd.models import build_model, get_model_config
+
+    rank, local_rank, world = init_dist(backend="gloo" if args.cpu else None, use_cpu=args.cpu)
+    dev = torch.device("cpu") if (args.cpu or not torch.cuda.is_available()) else torch.device("cuda", local_rank)
+    mesh = init_device_mesh(dev.type, (world,), mesh_dim_names=("dp",))
+    torch.manual_seed(0)
+    cfg = get_model_config(args.model, num_hidden_layers=args.layers)
+    cfg.max_position_embeddings = max(cfg.max_position_embeddings, args.seq)
+    dtype = torch.float32 if (dev.type == "cpu" or args.mixed_precision) else torch.bfloat16
+    with torch.device(dev):
+        prev = torch.get_default_dtype()
+        torch.set_default_dtype(dtype)
+        model = build_model(cfg)
+        torch.set_default_dtype(prev)
+    model.cos, model.sin = model.cos.float(), model.sin.float()
+    mp = MixedPrecisionPolicy(param_dtype=torch.bfloat16, reduce_dtype=torch.float32) \
+        if (args.mixed_precision and dev.type == "cuda") else MixedPrecisionPolicy()
+    layers = list(model.decoder_layers.values())
+    for layer in layers:  # one FSDP unit per decoder layer: all-gather / reduce-scatter per layer
+        fully_shard(layer, mesh=mesh, mp_policy=mp)
+    fully_shard(model, mesh=mesh, mp_policy=mp)
+    if args.explicit_prefetching:  # issue layer i+1's all-gather while layer i computes
+        for a, b in zip(layers[:-1], layers[1:]):
+            a.set_modules_to_forward_prefetch([b])
+            b.set_modules_to_backward_prefetch([a])
+    opt = torch.optim.AdamW(model.parameters(), lr=args.lr, weight_decay=0.1, betas=(0.9, 0.95),
+                            foreach=dev.type == "cuda")
+    start = 0
+    ckpt_dir = args.ckpt_dir or os.path.join(ROOT, "work_dir", "fsdp2_ckpt")
+    if args.resume:
+        start = load(model, opt, ckpt_dir, args.dcp)
+    g = torch.Generator(device="cpu").manual_seed(1234 + rank)
+    losses = []
+    t0 = time.perf_counter()
+    for step in range(start, start + args.steps):
+        ids = torch.randint(0, cfg.vocab_size, (args.mbs, args.seq + 1), generator=g).to(dev)
+        logits = model(input_ids=ids[:, :-1])
+        loss = ops.cross_entropy(logits, ids[:, 1:])
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)  # DTensor-aware global norm
+        opt.step()
+        opt.zero_grad()
+        losses.append(float(loss.detach().float()))
+        if rank == 0:
+            print(f"step {step} loss {losses[-1]:.4f}", flush=True)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    save(model, opt, ckpt_dir, args.dcp, start + args.steps)
+    if rank == 0:
+        tok = args.steps * args.mbs * args.seq * world
+        print(f"fsdp2 done: {tok / dt:.0f} tokens/s on {world} ranks, final loss {losses[-1]:.4f}", flush=True)
+    return {"losses": losses, "world": world}
+
+
+def save(model, opt, path: str, use_dcp: bool, step: int) -> None:
+    from torch.distributed.checkpoint.state_dict import StateDictOptions, get_model_state_dict, get_state_dict
+
+    if use_dcp:
+        import torch.distributed.checkpoint as dcp
+
+        msd, osd = get_state_dict(model, opt)
+        dcp.save({"model": msd, "optim": osd, "step": torch.tensor(step)}, checkpoint_id=path)
+        return
+    full = get_model_state_dict(model, options=StateDictOptions(full_state_dict=True, cpu_offload=True))
+    if dist.get_rank() == 0:
+        os.makedirs(path, exist_ok=True)
+        torch.save({"model": full, "step": step}, os.path.join(path, "full_model.pt"))
+    dist.barrier()
+
+
+def load(model, opt, path: str, use_dcp: bool) -> int:
+    from torch.distributed.checkpoint.state_dict import (StateDictOptions, get_state_dict, set_model_state_dict,
+                                                         set_state_dict)
+
+    if use_dcp:
+        import torch.distributed.checkpoint as dcp
+
+        msd, osd = get_state_dict(model, opt)
+        state = {"model": msd, "optim": osd, "step": torch.tensor(0)}
+        dcp.load(state, checkpoint_id=path)
+        set_state_dict(model, opt, model_state_dict=state["model"], optim_state_dict=state["optim"])
+        return int(state["step"])
+    ck = torch.load(os.path.join(path, "full_model.pt"), map_location="cpu", weights_only=True)
+    set_model_state_dict(model, ck["model"], options=StateDictOptions(full_state_dict=True, broadcast_from_rank0=False))
+    return int(ck["step"])
+
+
+if __name__ == "__main__":
+    main()
+    if dist.is_initialized():
+        dist.destroy_process_group()

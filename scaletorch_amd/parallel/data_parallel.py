@@ -307,10 +307,13 @@ class DataParallel(nn.Module):
         if isinstance(reduce_dtype, str):
             reduce_dtype = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
                             "bfloat16": torch.bfloat16}[reduce_dtype]
+        # no 5-D mesh configured: plain data parallelism over every rank of the job
+        # (examples wrap a model without building a ProcessGroupManager)
+        world_default = None if C.is_distributed() and C.get_world_size() > 1 else C.SINGLE
         if dense_group is None:
-            dense_group = mesh.pgm.dense_dp_group if mesh.pgm else C.SINGLE
+            dense_group = mesh.pgm.dense_dp_group if mesh.pgm else world_default
         if expert_group is None:
-            expert_group = mesh.pgm.expert_dp_group if mesh.pgm else C.SINGLE
+            expert_group = mesh.pgm.expert_dp_group if mesh.pgm else world_default
         self.require_backward_grad_sync = True
         self._callback_queued = False
         uses = _use_counts(module)

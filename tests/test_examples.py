@@ -21,3 +21,82 @@ def test_mingpt_dp2_cpu_gloo(tmp_path):
     m = re.search(r"final train loss ([0-9.]+) val loss ([0-9.]+)", out.stdout)
     assert m, out.stdout[-2000:]
     assert float(m.group(1)) < 2.5  # char vocab ~ 20: ln(20)=3.0 at init
+
+
+def _torchrun(script, args, port, timeout=600):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, script), *args]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    return out.stdout
+
+
+@pytest.mark.slow
+def test_fsdp2_example_dcp_resume(tmp_path):
+    ck = str(tmp_path / "dcp")
+    out = _torchrun("examples/fsdp2/fsdp2_train.py", ["--cpu", "--steps", "2", "--dcp", "--ckpt-dir", ck], 29641)
+    assert "fsdp2 done" in out
+    out = _torchrun("examples/fsdp2/fsdp2_train.py", ["--cpu", "--steps", "1", "--dcp", "--resume", "--ckpt-dir", ck],
+                    29642)
+    assert "step 2 loss" in out  # resumed at step 2
+
+
+@pytest.mark.slow
+def test_device_mesh_demos():
+    out = _torchrun("examples/device_mesh/demos.py", ["all", "--cpu"], 29643)
+    for d in ("mesh", "dtensor", "manual", "tp", "sp", "fsdp_tp"):
+        assert f"[device_mesh] {d}: ok" in out
+
+
+@pytest.mark.slow
+def test_mnist_arena_equals_ddp():
+    accs = []
+    for mode, port in (("ddp", 29644), ("arena", 29645)):
+        out = _torchrun("examples/mnist/mnist_ddp.py", ["--mode", mode, "--cpu", "--epochs", "1", "--max-steps", "12"],
+                        port)
+        accs.append(float(re.search(r"test accuracy ([0-9.]+)", out).group(1)))
+    assert accs[0] == accs[1], accs
+
+
+@pytest.mark.slow
+def test_resnet_example():
+    out = _torchrun("examples/imagenet/resnet_ddp.py", ["--cpu", "--arch", "resnet18", "--dummy", "--image-size", "64",
+                                                         "--steps", "2", "--batch-size", "4", "--classes", "10"], 29646)
+    assert "images/s" in out
+
+
+def _arena_vs_local(rank, world, mode):
+    import torch
+    import torch.distributed as dist
+    import torch.nn.functional as F
+
+    from scaletorch_amd.models.attention_variants import LeNet
+    from scaletorch_amd.parallel.data_parallel import DataParallel
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(1)
+    m = LeNet().eval()
+    g = torch.Generator().manual_seed(rank)
+    x, y = torch.randn(8, 1, 28, 28, generator=g), torch.randint(0, 10, (8,), generator=g)
+    if mode == "local":
+        F.nll_loss(m(x), y).backward()
+        gl = torch.cat([p.grad.reshape(-1) for p in m.parameters()])
+        dist.all_reduce(gl)
+        return gl / world
+    mm = DataParallel(m, bucket_size=1 << 20, expose_grads=True)
+    mm.zero_grad()
+    F.nll_loss(mm(x), y).backward()
+    return torch.cat([p.grad.reshape(-1) for p in m.parameters()])
+
+
+def test_arena_dp_without_mesh_reduces_over_world():
+    """Regression: DataParallel on a bare process group (no 5-D mesh) must average over all ranks."""
+    import torch
+
+    from tests.dist_harness import run_workers
+
+    ref = run_workers(_arena_vs_local, 2, "local")
+    got = run_workers(_arena_vs_local, 2, "arena")
+    for a, b in zip(ref, got):
+        torch.testing.assert_close(b, a)
