@@ -492,12 +492,23 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
     const lds_t* kt = smem + BUF * TB;
     const lds_t* vt = smem + (2 + BUF) * TB;
     f32x16 s0 = zero16(), s1 = zero16(), d0 = zero16(), d1 = zero16();
+    // K/V row fragments one k-step ahead, pinned above the MFMAs (1 wave/SIMD)
+    bfx8 fk[NKK][2], fv[NKK][2];
+    auto load_k = [&](int kk) {
+      fk[kk][0] = la.rowf(kt, 0, kk);
+      fk[kk][1] = la.rowf(kt, 1, kk);
+      fv[kk][0] = la.rowf(vt, 0, kk);
+      fv[kk][1] = la.rowf(vt, 1, kk);
+    };
+    load_k(0);
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) {
-      s0 = mfma(la.rowf(kt, 0, kk), qf[kk], s0);
-      s1 = mfma(la.rowf(kt, 1, kk), qf[kk], s1);
-      d0 = mfma(la.rowf(vt, 0, kk), df[kk], d0);
-      d1 = mfma(la.rowf(vt, 1, kk), df[kk], d1);
+      if (kk + 1 < NKK) load_k(kk + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      s0 = mfma(fk[kk][0], qf[kk], s0);
+      s1 = mfma(fk[kk][1], qf[kk], s1);
+      d0 = mfma(fv[kk][0], df[kk], d0);
+      d1 = mfma(fv[kk][1], df[kk], d1);
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -515,12 +526,22 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
       }
     }
     const bfx8 g00 = acc_frag(s0, 0), g01 = acc_frag(s0, 1), g10 = acc_frag(s1, 0), g11 = acc_frag(s1, 1);
+    bfx8 tk[NDT][4];
+    auto load_t = [&](int dt) {
+      tk[dt][0] = la.trf(kt, 0, 0, dt);
+      tk[dt][1] = la.trf(kt, 0, 1, dt);
+      tk[dt][2] = la.trf(kt, 32, 0, dt);
+      tk[dt][3] = la.trf(kt, 32, 1, dt);
+    };
+    load_t(0);
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) {
-      mfma_acc(dqacc[dt], la.trf(kt, 0, 0, dt), g00);
-      mfma_acc(dqacc[dt], la.trf(kt, 0, 1, dt), g01);
-      mfma_acc(dqacc[dt], la.trf(kt, 32, 0, dt), g10);
-      mfma_acc(dqacc[dt], la.trf(kt, 32, 1, dt), g11);
+      if (dt + 1 < NDT) load_t(dt + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_acc(dqacc[dt], tk[dt][0], g00);
+      mfma_acc(dqacc[dt], tk[dt][1], g01);
+      mfma_acc(dqacc[dt], tk[dt][2], g10);
+      mfma_acc(dqacc[dt], tk[dt][3], g11);
     }
     if (more) {
       sk.store(smem + (BUF ^ 1) * TB);
@@ -648,12 +669,26 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
       bfx8 pf[2][2], gf[2][2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        // S = Q K^T, dP = dO V^T : rows = queries (acc rows), col = key (lane)
+        // S = Q K^T, dP = dO V^T : rows = queries (acc rows), col = key (lane).
+        // Fragments are read two k-steps ahead and a sched_barrier pins each
+        // read group above the MFMAs that precede its use: with one wave per
+        // SIMD nothing else hides the LDS latency (hipcc otherwise emits
+        // read -> wait -> MFMA for every k-step).
         f32x16 s = zero16(), dp = zero16();
+        bfx8 qa[NKK], da[NKK];
+        qa[0] = la.rowf(qt, u, 0);
+        da[0] = la.rowf(dt_, u, 0);
+        qa[1] = la.rowf(qt, u, 1);
+        da[1] = la.rowf(dt_, u, 1);
 #pragma unroll
         for (int kk = 0; kk < NKK; ++kk) {
-          s = mfma(la.rowf(qt, u, kk), kf[kk], s);
-          dp = mfma(la.rowf(dt_, u, kk), vf[kk], dp);
+          if (kk + 2 < NKK) {
+            qa[kk + 2] = la.rowf(qt, u, kk + 2);
+            da[kk + 2] = la.rowf(dt_, u, kk + 2);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          s = mfma(qa[kk], kf[kk], s);
+          dp = mfma(da[kk], vf[kk], dp);
         }
         // query row of register i: 32u + acc_row0(i) + 4h
         int thr = 0;
@@ -681,15 +716,27 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
         gf[u][0] = acc_frag(dp, 0);
         gf[u][1] = acc_frag(dp, 1);
       }
+      // dV^T += dO^T P, dK^T += Q^T dS: 8 (dt, u) groups of 4 MFMAs; transposed
+      // fragments read one group ahead (same pinning as above)
+      constexpr int NG = NDT * 2;
+      bfx8 tv[NG][2], tk[NG][2];
+      auto load_group = [&](int gidx) {
+        const int dt = gidx >> 1, u = gidx & 1;
+        tv[gidx][0] = la.trf(dt_, 32 * u, 0, dt);
+        tv[gidx][1] = la.trf(dt_, 32 * u, 1, dt);
+        tk[gidx][0] = la.trf(qt, 32 * u, 0, dt);
+        tk[gidx][1] = la.trf(qt, 32 * u, 1, dt);
+      };
+      load_group(0);
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          mfma_acc(dvacc[dt], la.trf(dt_, 32 * u, 0, dt), pf[u][0]);
-          mfma_acc(dvacc[dt], la.trf(dt_, 32 * u, 1, dt), pf[u][1]);
-          mfma_acc(dkacc[dt], la.trf(qt, 32 * u, 0, dt), gf[u][0]);
-          mfma_acc(dkacc[dt], la.trf(qt, 32 * u, 1, dt), gf[u][1]);
-        }
+      for (int gi = 0; gi < NG; ++gi) {
+        if (gi + 1 < NG) load_group(gi + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        const int dt = gi >> 1, u = gi & 1;
+        mfma_acc(dvacc[dt], tv[gi][0], pf[u][0]);
+        mfma_acc(dvacc[dt], tv[gi][1], pf[u][1]);
+        mfma_acc(dkacc[dt], tk[gi][0], gf[u][0]);
+        mfma_acc(dkacc[dt], tk[gi][1], gf[u][1]);
       }
     }
     if (more) commit(BUF ^ 1);

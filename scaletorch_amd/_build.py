@@ -72,8 +72,17 @@ def _run(cmd, verbose: bool):
     return r
 
 
-def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -> Path:
-    """Compile all kernels for ``gfx950`` and link ``_st_kernels.so``; returns its path."""
+def build(verbose: bool = False, jobs: int | None = None, force: bool = False, variant: str | None = None,
+          variant_flags: dict | None = None) -> Path:
+    """Compile all kernels for ``gfx950`` and link ``_st_kernels.so``; returns its path.
+
+    ``variant``: build an A/B copy into ``build/variants/<variant>.so`` with extra
+    per-file flags (``variant_flags = {"flash_attn.hip": [...]}``); load it with
+    ``ST_KERNEL_LIB=<path>`` (tools/bench_kernels.py)."""
+    global BUILD, LIB
+    if variant:
+        BUILD = ROOT / "build" / "variants" / variant
+        LIB = ROOT / "build" / "variants" / f"{variant}.so"
     BUILD.mkdir(parents=True, exist_ok=True)
     hip_srcs = sorted(CSRC.glob("*.hip"))
     headers = sorted(CSRC.glob("*.h"))
@@ -87,7 +96,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         obj = BUILD / (src.stem + ".o")
         objs.append(obj)
         if force or _stale(obj, [src, *headers, Path(__file__)]):
-            extra = FILE_FLAGS.get(src.name, [])
+            extra = FILE_FLAGS.get(src.name, []) + (variant_flags or {}).get(src.name, [])
             jobs_list.append([hipcc, f"--offload-arch={ARCH}", *common_flags, *extra, "-c", str(src), "-o",
                               str(obj)])
     # host C++ (torch op registrations, hipBLASLt tuner): g++ against the PyTorch headers
@@ -118,5 +127,13 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
 
 
 if __name__ == "__main__":
-    p = build(verbose="-v" in sys.argv, force="--force" in sys.argv)
+    # python -m scaletorch_amd._build [--force] [-v] [--variant NAME file.hip="-flag -flag" ...]
+    var, vflags = None, {}
+    for a in sys.argv[1:]:
+        if a.startswith("--variant="):
+            var = a.split("=", 1)[1]
+        elif "=" in a and a.split("=", 1)[0].endswith(".hip"):
+            f, fl = a.split("=", 1)
+            vflags[f] = fl.split()
+    p = build(verbose="-v" in sys.argv, force="--force" in sys.argv, variant=var, variant_flags=vflags)
     print(p)

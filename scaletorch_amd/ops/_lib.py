@@ -15,7 +15,8 @@ from pathlib import Path
 
 import torch
 
-_LIB_PATH = Path(__file__).resolve().parent.parent / "_st_kernels.so"
+# ST_KERNEL_LIB: load an alternative build (kernel A/B experiments, tools/bench_kernels.py)
+_LIB_PATH = Path(os.environ.get("ST_KERNEL_LIB") or Path(__file__).resolve().parent.parent / "_st_kernels.so")
 _lock = threading.Lock()
 _loaded: bool | None = None
 _load_error: str | None = None
