@@ -174,30 +174,42 @@ ST_DEVICE bfx8 bload_frag(rsrc_t rs, uint32_t off) {
   return __builtin_bit_cast(bfx8, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
 }
 
-// Cooperative register-staged copy of a ROWS x D tile (256 threads, 16 B per
-// thread per pass); rows outside the descriptor's range arrive as zeros.
+// Direct global -> LDS staging (buffer_load_dwordx4 ... lds): each wave
+// instruction writes 1 KiB of LDS lane-linearly, so the XOR swizzle is applied
+// on the SOURCE side -- lane l of a wave fetches the global chunk that belongs
+// at LDS byte (base + 16 l) of the swizzled image.  No staging registers, no
+// ds_write; rows past the descriptor's range land as zeros.  The loads are
+// issued at the top of a step and retired by the end-of-step barrier
+// (__syncthreads waits vmcnt(0)), so they overlap the step's MFMAs.
+ST_DEVICE void lds_dma16(rsrc_t rs, lds_t* dst, uint32_t voff) {
+  // device pass only: in the host pass this target builtin poisons the enclosing
+  // kernel templates and hipcc silently drops their host launch stubs
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, voff, 0, 0, 0);
+#endif
+}
+
 template <int D, int ROWS>
-struct Stager {
-  static constexpr int NCH = D / 8, RPP = 256 / NCH, N = ROWS / RPP;
-  static_assert(N >= 1 && ROWS % RPP == 0, "tile rows");
-  u32x4 v[N];
-  uint32_t voff, pass_bytes, stride_bytes;
-  int lds;
-  ST_DEVICE void init(int tid, int64_t row_stride) {
+struct DmaStager {
+  static constexpr int RB = 2 * D, BYTES = ROWS * RB, PER_WAVE = BYTES / 4, NI = PER_WAVE / 1024;
+  static_assert(NI >= 1 && PER_WAVE % 1024 == 0, "tile must be whole KiB per wave");
+  uint32_t voff[NI];
+  uint32_t stride_bytes;
+  int wave_base;
+  ST_DEVICE void init(int wid, int lane, int64_t row_stride) {
     stride_bytes = (uint32_t)(row_stride * 2);
-    voff = (uint32_t)(tid / NCH) * stride_bytes + (uint32_t)(tid % NCH) * 16u;
-    pass_bytes = RPP * stride_bytes;
-    lds = lds_off<D>(tid / NCH, tid % NCH);
-  }
-  ST_DEVICE void load(rsrc_t rs, int row0) {
-    const uint32_t o = voff + (uint32_t)row0 * stride_bytes;
+    wave_base = wid * PER_WAVE;
 #pragma unroll
-    for (int i = 0; i < N; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, o + i * pass_bytes, 0, 0);
+    for (int i = 0; i < NI; ++i) {
+      const int a = wave_base + i * 1024 + lane * 16;
+      const int row = a / RB, pos = (a % RB) / 16;
+      voff[i] = (uint32_t)row * stride_bytes + (uint32_t)((pos ^ swz<D>(row)) * 16);
+    }
   }
-  ST_DEVICE void store(lds_t* tile) const {
+  ST_DEVICE void load(rsrc_t rs, lds_t* tile, int row0) const {
+    const uint32_t o = (uint32_t)row0 * stride_bytes;
 #pragma unroll
-    for (int i = 0; i < N; ++i)
-      *reinterpret_cast<u32x4 __attribute__((address_space(3)))*>(tile + lds + i * RPP * 2 * D) = v[i];
+    for (int i = 0; i < NI; ++i) lds_dma16(rs, tile + wave_base + i * 1024, voff[i] + o);
   }
 };
 
@@ -275,9 +287,9 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(AttnParams p, bf16_t*
 
   LdsAddr<D> la;
   la.init(lane);
-  Stager<D, BN> sk, sv;
-  sk.init(tid, p.sks);
-  sv.init(tid, p.svs);
+  DmaStager<D, BN> sk, sv;
+  sk.init(wid, lane, p.sks);
+  sv.init(wid, lane, p.svs);
 
   f32x16 oacc[NDT];
 #pragma unroll
@@ -287,10 +299,8 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(AttnParams p, bf16_t*
   const int64_t qg = p.q_offset + my_q;
 
   if (nkb > 0) {
-    sk.load(rk, 0);
-    sv.load(rv, 0);
-    sk.store(smem);
-    sv.store(smem + 2 * TB);
+    sk.load(rk, smem, 0);
+    sv.load(rv, smem + 2 * TB, 0);
   }
   __syncthreads();
 
@@ -298,8 +308,8 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(AttnParams p, bf16_t*
     constexpr int BUF = decltype(bufc)::value;
     const bool more = kb + 1 < nkb;
     if (more) {
-      sk.load(rk, (kb + 1) * BN);
-      sv.load(rv, (kb + 1) * BN);
+      sk.load(rk, smem + (BUF ^ 1) * TB, (kb + 1) * BN);
+      sv.load(rv, smem + (2 + (BUF ^ 1)) * TB, (kb + 1) * BN);
     }
     const lds_t* kt = smem + BUF * TB;
     const lds_t* vt = smem + (2 + BUF) * TB;
@@ -360,11 +370,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(AttnParams p, bf16_t*
       oacc[dt] = mfma(la.trf(vt, 32, 0, dt), p10, oacc[dt]);
       oacc[dt] = mfma(la.trf(vt, 32, 1, dt), p11, oacc[dt]);
     }
-    if (more) {
-      sk.store(smem + (BUF ^ 1) * TB);
-      sv.store(smem + (2 + (BUF ^ 1)) * TB);
-    }
-    __syncthreads();
+    __syncthreads();  // also retires this step's LDS-DMA (vmcnt(0))
   };
   for (int kb = 0; kb < nkb; kb += 2) {
     step(Buf<0>(), kb);
@@ -466,19 +472,17 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
 
   LdsAddr<D> la;
   la.init(lane);
-  Stager<D, BN> sk, sv;
-  sk.init(tid, p.sks);
-  sv.init(tid, p.svs);
+  DmaStager<D, BN> sk, sv;
+  sk.init(wid, lane, p.sks);
+  sv.init(wid, lane, p.svs);
 
   f32x16 dqacc[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) dqacc[dt] = zero16();
 
   if (nkb > 0) {
-    sk.load(rk, 0);
-    sv.load(rv, 0);
-    sk.store(smem);
-    sv.store(smem + 2 * TB);
+    sk.load(rk, smem, 0);
+    sv.load(rv, smem + 2 * TB, 0);
   }
   __syncthreads();
 
@@ -486,8 +490,8 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
     constexpr int BUF = decltype(bufc)::value;
     const bool more = kb + 1 < nkb;
     if (more) {
-      sk.load(rk, (kb + 1) * BN);
-      sv.load(rv, (kb + 1) * BN);
+      sk.load(rk, smem + (BUF ^ 1) * TB, (kb + 1) * BN);
+      sv.load(rv, smem + (2 + (BUF ^ 1)) * TB, (kb + 1) * BN);
     }
     const lds_t* kt = smem + BUF * TB;
     const lds_t* vt = smem + (2 + BUF) * TB;
@@ -543,11 +547,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
       mfma_acc(dqacc[dt], tk[dt][2], g10);
       mfma_acc(dqacc[dt], tk[dt][3], g11);
     }
-    if (more) {
-      sk.store(smem + (BUF ^ 1) * TB);
-      sv.store(smem + (2 + (BUF ^ 1)) * TB);
-    }
-    __syncthreads();
+    __syncthreads();  // also retires this step's LDS-DMA (vmcnt(0))
   };
   for (int kb = 0; kb < nkb; kb += 2) {
     step(Buf<0>(), kb);
@@ -616,9 +616,9 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
 
   LdsAddr<D> la;
   la.init(lane);
-  Stager<D, BQ> sq, sd;
-  sq.init(tid, p.sqs);
-  sd.init(tid, sds);
+  DmaStager<D, BQ> sq, sd;
+  sq.init(wid, lane, p.sqs);
+  sd.init(wid, lane, sds);
   float* stats = (float*)(smem_raw + 4 * TB);
 
   f32x16 dkacc[NDT], dvacc[NDT];
@@ -626,10 +626,11 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
   for (int dt = 0; dt < NDT; ++dt) dkacc[dt] = dvacc[dt] = zero16();
 
   float st_v = 0.f;
-  auto issue = [&](int g, int qb) {  // global loads of step (g, qb) into registers
+  // Q / dO tiles of step (g, qb) DMA'd straight into LDS buffer `buf`; lse / delta into a register
+  auto issue = [&](int g, int qb, int buf) {
     const int hq = hk * G + g;
-    sq.load(make_rsrc(p.q + (int64_t)b * p.sqb + (int64_t)hq * p.sqh, p.Sq, p.sqs, D), qb * BQ);
-    sd.load(make_rsrc(dout + (int64_t)b * sdb + (int64_t)hq * sdh, p.Sq, sds, D), qb * BQ);
+    sq.load(make_rsrc(p.q + (int64_t)b * p.sqb + (int64_t)hq * p.sqh, p.Sq, p.sqs, D), smem + buf * TB, qb * BQ);
+    sd.load(make_rsrc(dout + (int64_t)b * sdb + (int64_t)hq * sdh, p.Sq, sds, D), smem + (2 + buf) * TB, qb * BQ);
     if (wid < 2) {
       const int qi = qb * BQ + lane;
       const int64_t row = ((int64_t)b * p.H + hq) * p.Sq;
@@ -638,12 +639,10 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
     }
   };
   auto commit = [&](int buf) {
-    sq.store(smem + buf * TB);
-    sd.store(smem + (2 + buf) * TB);
     if (wid < 2) stats[buf * 2 * BQ + wid * BQ + lane] = st_v;
   };
   if (total > 0) {
-    issue(0, qb0);
+    issue(0, qb0, 0);
     commit(0);
   }
   __syncthreads();
@@ -657,7 +656,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
       qb_n = qb0;
       ++g_n;
     }
-    if (more) issue(g_n, qb_n);
+    if (more) issue(g_n, qb_n, BUF ^ 1);
     const lds_t* qt = smem + BUF * TB;
     const lds_t* dt_ = smem + (2 + BUF) * TB;
     const lds_t* st = (const lds_t*)(stats + BUF * 2 * BQ);

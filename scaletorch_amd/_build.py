@@ -122,6 +122,12 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False, v
         link += ["-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch", "-lamdhip64",
                  f"-L{ROCM / 'lib'}", "-lhipblaslt"]
         _run(link, verbose)
+        # a library with an unresolved symbol links fine (-shared) and only fails at dlopen:
+        # load it once here so a broken build is a build error, not a GPU-box surprise
+        chk = subprocess.run([sys.executable, "-c", f"import torch; torch.ops.load_library({str(tmp)!r})"],
+                             capture_output=True, text=True)
+        if chk.returncode != 0:
+            raise RuntimeError(f"built {tmp} does not load:\n{chk.stderr[-2000:]}")
         os.replace(tmp, LIB)
     return LIB
 
