@@ -23,10 +23,14 @@
 //     loops is `ds_read* vaddr offset:<imm>` on a lane-constant VGPR computed
 //     once (LdsAddr); the double-buffer index is a template constant (the loop
 //     is unrolled by two), so the loops carry no LDS address arithmetic.
-//   * global -> LDS through registers (T14: issue the next tile's loads before
-//     this tile's MFMAs, write them to the other buffer after), with buffer
-//     descriptors (T8/T20): 32-bit offsets, and rows past the end of a
-//     sequence read as zero by the hardware range check -- no branches.
+//   * global -> LDS by LDS-DMA (`buffer_load_dwordx4 ... lds`, DmaStager): the
+//     next tile is requested at the top of a step into the other buffer and
+//     retired by the end-of-step barrier; buffer descriptors (T8/T20) give
+//     32-bit offsets and zero-fill rows past the end of a sequence -- no
+//     staging registers, no ds_write, no branches.
+//   * with one wave per SIMD (backward kernels) fragment reads are issued a
+//     k-step ahead and pinned above the MFMAs that precede their use
+//     (sched_barrier); hipcc otherwise serialises read -> wait -> MFMA.
 //   * online softmax in base 2 with raw v_exp_f32; the O rescale is deferred
 //     until the running max grows by 2^8 (T13) and decided wave-uniformly.
 //   * only the diagonal / tail blocks evaluate the causal mask.
