@@ -56,6 +56,30 @@ def all_to_all_rows(x, out_splits, in_splits, group):
     return _AllToAll.apply(x, out_splits, in_splits, group)
 
 
+_GMM_OK: bool | None = None
+
+
+def _grouped_mm_available() -> bool:
+    """torch._grouped_mm (device offsets, autograd) exists and runs on this device;
+    ST_MOE_GROUPED_GEMM=0 forces the per-expert loop."""
+    global _GMM_OK
+    import os
+
+    if os.environ.get("ST_MOE_GROUPED_GEMM", "1") == "0":
+        return False
+    if _GMM_OK is None:
+        _GMM_OK = False
+        if hasattr(torch, "_grouped_mm") and torch.cuda.is_available():
+            try:
+                a = torch.randn(32, 64, device="cuda", dtype=torch.bfloat16)
+                b = torch.randn(2, 64, 32, device="cuda", dtype=torch.bfloat16)
+                torch._grouped_mm(a, b, offs=torch.tensor([16, 32], device="cuda", dtype=torch.int32))
+                _GMM_OK = True
+            except (RuntimeError, NotImplementedError, TypeError):
+                _GMM_OK = False
+    return _GMM_OK
+
+
 class MoERouter(nn.Module):
     """Top-k softmax router (reference model_qwen3_moe.py:30-92)."""
 
@@ -127,8 +151,23 @@ class MoEExperts(nn.Module):
             dn.normal_(0.0, self.init_std, generator=keyed_generator(key and key + ".down", dev))
             self.w_down.copy_(dn[e0:e0 + self.num_local].chunk(self.tp, 2)[self.tp_rank])
 
-    def forward(self, x: torch.Tensor, counts: list[int]) -> torch.Tensor:
-        """x: rows grouped by local expert (``counts[e]`` rows each)."""
+    def forward(self, x: torch.Tensor, counts) -> torch.Tensor:
+        """x: rows grouped by local expert (``counts[e]`` rows each; list or device tensor).
+
+        GPU: two grouped GEMMs over all local experts (``torch._grouped_mm`` with
+        device-side group offsets -> hipBLASLt grouped kernels): no per-expert
+        launches and no host read of the routing counts.  CPU / fallback: one GEMM
+        pair per expert."""
+        if x.is_cuda and _grouped_mm_available() and x.dtype == torch.bfloat16:
+            if not isinstance(counts, torch.Tensor):
+                counts = torch.tensor(counts, dtype=torch.int32)
+            offs = torch.cumsum(counts.to(device=x.device, dtype=torch.int32), 0, dtype=torch.int32)
+            if x.shape[0] == 0:
+                return x.new_zeros(0, self.hidden)
+            gu = torch._grouped_mm(x.contiguous(), self.w_gate_up.transpose(-2, -1), offs=offs)
+            return torch._grouped_mm(ops.swiglu(gu), self.w_down.transpose(-2, -1), offs=offs)
+        if isinstance(counts, torch.Tensor):
+            counts = counts.tolist()
         outs = []
         off = 0
         for e, n in enumerate(counts):
@@ -198,7 +237,7 @@ class MoELayer(nn.Module):
         counts = perm.counts
         xs = ops.moe.gather_rows(x2, perm)  # rows sorted by global expert
         if self.ep == 1:
-            y = self.experts(xs, counts.tolist())
+            y = self.experts(xs, counts)  # device counts: no host sync on the grouped-GEMM path
         else:
             group = mesh.pgm.ep_group
             # counts per (dest rank, local expert); exchange the full matrix once
@@ -221,7 +260,7 @@ class MoELayer(nn.Module):
                         b = int(starts[s, e])
                         idx.append(torch.arange(b, b + n))
             regroup = torch.cat(idx).to(x.device) if idx else torch.zeros(0, dtype=torch.long, device=x.device)
-            ye = self.experts(xr.index_select(0, regroup), recv_mat_h.sum(0).tolist())
+            ye = self.experts(xr.index_select(0, regroup), recv_mat_h.sum(0))
             yr = torch.empty_like(ye)
             yr = yr.index_copy(0, regroup, ye) if regroup.numel() else ye
             y = all_to_all_rows(yr, send_splits, recv_splits, group)
