@@ -43,6 +43,7 @@ def main() -> int:
     ap.add_argument("--ep", type=int, default=1)
     ap.add_argument("--sp", action="store_true")
     ap.add_argument("--cp_comm", default="allgather", help="allgather | ring | ulysses")
+    ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) | gloo (debug rehearsals only)")
     ap.add_argument("--gc", action="store_true", help="activation checkpointing")
     ap.add_argument("--grad_reduce_dtype", default="bf16")
     ap.add_argument("--bucket_mb", type=float, default=256)
@@ -72,7 +73,7 @@ def main() -> int:
         sequence_length=args.seq_len, gradient_accumulation_steps=ga, total_train_steps=args.warmup + args.steps,
         tensor_parallel_size=args.tp, pipeline_parallel_size=args.pp, context_parallel_size=args.cp,
         expert_parallel_size=args.ep, data_parallel_size=dp, sequence_parallel=args.sp,
-        cp_comm=args.cp_comm,
+        cp_comm=args.cp_comm, backend=args.backend,
         gradient_checkpointing=args.gc, learning_rate=3e-4, lr_scheduler_type="cosine", warmup_steps=0,
         max_grad_norm=1.0, grad_reduce_dtype=args.grad_reduce_dtype, bucket_size_mb=args.bucket_mb,
         num_hidden_layers=args.layers, dtype="bfloat16", weight_decay=0.1, betas=(0.9, 0.95),

@@ -112,15 +112,19 @@ def init_dist(launcher: str | None = None, backend: str | None = None, use_cpu: 
         backend = device_backend(use_cpu)
     if backend == "nccl" and not torch.cuda.is_available():
         backend = "gloo"
+    # ST_GPU_OVERSUBSCRIBE=1 (tests only): several ranks share the visible GPUs
+    gpu = local_rank
+    if os.environ.get("ST_GPU_OVERSUBSCRIBE", "0") == "1" and torch.cuda.is_available():
+        gpu = local_rank % max(1, torch.cuda.device_count())
     if backend == "nccl":
         _apply_rccl_env()
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(gpu)
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = dict(backend=backend, init_method="env://", world_size=world, rank=rank,
                   timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
-            kw["device_id"] = torch.device("cuda", local_rank)
+            kw["device_id"] = torch.device("cuda", gpu)
         dist.init_process_group(**kw)
     return rank, local_rank, world
 

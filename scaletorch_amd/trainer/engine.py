@@ -58,7 +58,7 @@ class Trainer:
 
             set_cp_zigzag(a.cp_zigzag)
             set_cp_comm(a.cp_comm)
-        self.device = torch.device("cuda", self.local_rank) if (torch.cuda.is_available() and not a.use_cpu) \
+        self.device = torch.device("cuda", torch.cuda.current_device()) if (torch.cuda.is_available() and not a.use_cpu) \
             else torch.device("cpu")
         self.dtype = _DTYPES[a.dtype]
         if self.device.type == "cpu" and self.dtype == torch.float16:
