@@ -27,5 +27,20 @@ if has prof; then
   export TMPDIR=/tmp
   run rocprof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
       python bench.py --gpus 1 --steps 3 --warmup 1 ${BENCH_ARGS:-}; rc=$?
+  [ $rc -eq 0 ] || exit $rc
+fi
+if has pmc; then
+  # hardware counters: one rocprofv3 run per counter group, --pmc with --kernel-trace only
+  export TMPDIR=/tmp
+  KB="python3 tools/bench_kernels.py --only attn,elt --no-ref --iters 3"
+  run pmc_mfma 240 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU_MFMA_MOPS_BF16 \
+      -d gpurun_out/pmc_mfma -o run --output-format csv -- $KB || exit $?
+  run pmc_lds 240 rocprofv3 --kernel-trace --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
+      -d gpurun_out/pmc_lds -o run --output-format csv -- $KB || exit $?
+  # (derived FETCH_SIZE/WRITE_SIZE hung rocprofv3 on this pool: raw TCC request counts instead)
+  run pmc_hbm 240 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum \
+      -d gpurun_out/pmc_hbm -o run --output-format csv -- $KB || exit $?
+  run pmc_step 400 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU_MFMA_MOPS_BF16 \
+      -d gpurun_out/pmc_step -o run --output-format csv -- python3 bench.py --gpus 1 --steps 1 --warmup 1 || exit $?
 fi
 exit 0

@@ -22,7 +22,11 @@ import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
 
-def timeit(fn, iters=20, warmup=3):
+_ITERS = 20
+
+
+def timeit(fn, iters=None, warmup=3):
+    iters = min(iters or _ITERS, _ITERS)
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
@@ -44,7 +48,11 @@ def main():
     ap.add_argument("--batch", type=int, default=2)
     ap.add_argument("--only", default="")
     ap.add_argument("--blas", default="", help="torch BLAS backend for the reference GEMMs: hipblaslt | rocblas")
+    ap.add_argument("--no-ref", action="store_true", help="skip the vendor reference paths (for counter runs)")
+    ap.add_argument("--iters", type=int, default=20)
     args = ap.parse_args()
+    global _ITERS
+    _ITERS = args.iters
     from scaletorch_amd import ops
     from scaletorch_amd.ops import _lib
 
@@ -71,10 +79,12 @@ def main():
         res["flash_bwd_ms"] = t
         res["flash_bwd_tflops_5mm"] = 5 * flop_mm / t / 1e9
         # vendor SDPA for context (expanded GQA as the reference does)
-        qt = q.transpose(1, 2)
+        qt = None if args.no_ref else q.transpose(1, 2)
         kt = k.transpose(1, 2).repeat_interleave(H // Hkv, 1)
         vt = v.transpose(1, 2).repeat_interleave(H // Hkv, 1)
         try:
+            if qt is None:
+                raise RuntimeError("skipped (--no-ref)")
             t = timeit(lambda: F.scaled_dot_product_attention(qt, kt, vt, is_causal=True))
             res["torch_sdpa_fwd_ms"] = t
             qr, kr, vr = (x.detach().requires_grad_(True) for x in (qt, kt, vt))
