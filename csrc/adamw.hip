@@ -13,6 +13,8 @@
 //   * grads may be fp32 (main_grad arena) or bf16.
 #include "common.h"
 
+#include <cstdlib>
+
 using namespace st;
 
 namespace {
@@ -120,6 +122,18 @@ inline unsigned grid_for(int64_t n4) {
 
 extern "C" {
 
+// ST_ADAMW_BLOCKS caps the grid (grid-stride loop): a small grid leaves most CUs
+// to the GEMMs of the forward pass the side-stream update overlaps (optim.py).
+static unsigned adamw_grid(int64_t n4) {
+  static const long cap = [] {
+    const char* e = std::getenv("ST_ADAMW_BLOCKS");
+    return e ? std::atol(e) : 0L;
+  }();
+  unsigned g = grid_for(n4);
+  if (cap > 0 && g > (unsigned)cap) g = (unsigned)cap;
+  return g;
+}
+
 int st_adamw_step(float* master, float* m, float* v, const void* g, int g_is_bf16, void* p,
                   const float* clip, int64_t n, float lr, float b1, float b2, float eps, float wd,
                   float bc1, float bc2_sqrt, hipStream_t st) {
@@ -127,10 +141,10 @@ int st_adamw_step(float* master, float* m, float* v, const void* g, int g_is_bf1
   const int64_t n4 = n / 4;
   if (n4 == 0) return 0;
   if (g_is_bf16)
-    adamw_kernel<bf16_t><<<grid_for(n4), 256, 0, st>>>(master, m, v, (const bf16_t*)g, (bf16_t*)p,
+    adamw_kernel<bf16_t><<<adamw_grid(n4), 256, 0, st>>>(master, m, v, (const bf16_t*)g, (bf16_t*)p,
                                                        clip, n4, lr, b1, b2, eps, wd, bc1, bc2_sqrt);
   else
-    adamw_kernel<float><<<grid_for(n4), 256, 0, st>>>(master, m, v, (const float*)g, (bf16_t*)p,
+    adamw_kernel<float><<<adamw_grid(n4), 256, 0, st>>>(master, m, v, (const float*)g, (bf16_t*)p,
                                                       clip, n4, lr, b1, b2, eps, wd, bc1, bc2_sqrt);
   return (int)hipGetLastError();
 }

@@ -12,6 +12,14 @@ adamw[fused] / adam / sgd(m=0.9) / lamb->adamw) and ``clip_gradients``
   norms all-reduced over the model-parallel group with TP/EP replicas counted
   once, data_parallel.py ``grad_sumsq_segments``) and read by the kernel from
   device memory: no host sync unless the norm is logged.
+* overlap (GPU, ``ST_OVERLAP_OPT=1`` default): the update is enqueued bucket by
+  bucket, in FORWARD order, on the model's side stream (data_parallel.py); each
+  module of the next forward waits only for the buckets holding its own weights,
+  so the HBM-bound AdamW pass (~30 B/param) runs under the next step's MFMA-bound
+  GEMMs instead of between steps.  Under ZeRO-1 the bucket's parameter all-gather
+  is issued right behind its update on the same stream.  The squared gradient
+  norm is likewise accumulated per bucket on that stream during backward
+  (world size 1), so clipping costs one scalar reduction after backward.
 * ``ArenaSGD`` / ``ArenaAdam`` / ``ArenaLAMB`` cover the other reference choices.
 Each subclasses ``torch.optim.Optimizer`` so torch LR schedulers drive ``lr``.
 """
@@ -46,6 +54,7 @@ class _ArenaOptimizer(torch.optim.Optimizer):
                 a.master = a.param_flat.detach().float().clone()
         self.clip_coef = None
         self.last_grad_norm = None
+        self.side_stream = getattr(dp_model, "side_stream", None)
 
     @property
     def sharded(self) -> bool:
@@ -73,6 +82,12 @@ class _ArenaOptimizer(torch.optim.Optimizer):
     def grad_norm(self, mp_group=None) -> torch.Tensor:
         """Global L2 norm of the gradients (device scalar, fp32)."""
         self._zero_unwritten()
+        pre = [a.take_sumsq() for a in self.arenas]
+        if pre and all(x is not None for x in pre) and C.get_world_size() <= 1:
+            total = pre[0].clone()  # accumulated on the side stream during backward
+            for x in pre[1:]:
+                total += x
+            return total.sqrt()
         segs = self.dp.grad_sumsq_segments()
         dev = segs[0][0].device
         total = torch.zeros(1, dtype=torch.float32, device=dev)
@@ -102,7 +117,13 @@ class _ArenaOptimizer(torch.optim.Optimizer):
         return norm
 
     # ---------------------------------------------------------------- state
+    def sync(self) -> None:
+        """Join the side-stream update (before reading master / states on the host)."""
+        if self.side_stream is not None:
+            torch.cuda.current_stream().wait_stream(self.side_stream)
+
     def state_dict(self):
+        self.sync()
         return {
             "step": self._step,
             "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups],
@@ -113,6 +134,7 @@ class _ArenaOptimizer(torch.optim.Optimizer):
         return {"master": None if a.master is None else a.master.detach().cpu()}
 
     def load_state_dict(self, sd):
+        self.sync()
         self._step = sd["step"]
         for g, s in zip(self.param_groups, sd["param_groups"]):
             g.update(s)
@@ -138,11 +160,48 @@ class ArenaAdamW(_ArenaOptimizer):
             a.exp_avg = torch.zeros(a.state_numel, dtype=torch.float32, device=a.param_flat.device)
             a.exp_avg_sq = torch.zeros_like(a.exp_avg)
 
+    def _native(self, a) -> bool:
+        return (self.fused and self.decoupled and _lib.use_native(a.param_flat) and a.master is not None
+                and a.param_flat.dtype == torch.bfloat16)
+
+    def _step_overlapped(self, t: int) -> None:
+        """Enqueue every bucket's fused update on the side stream in forward order
+        (first-used bucket first); record per-bucket completion for the forward
+        pre-hooks, or chain the ZeRO-1 all-gather of the bucket behind it."""
+        import torch.distributed as dist
+
+        ev = torch.cuda.Event()
+        ev.record()  # gradients final + clip coefficient computed
+        st = self.side_stream
+        if self.clip_coef is not None:
+            self.clip_coef.record_stream(st)
+        with torch.cuda.stream(st):
+            st.wait_event(ev)
+            for g, a in zip(self.param_groups, self.arenas):
+                lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
+                for b in reversed(a.buckets):
+                    lo, hi, so = b.shard_lo, b.shard_hi, b.state_lo
+                    n = hi - lo
+                    if n:
+                        _lib.ops().adamw_step_(a.master[so: so + n], a.exp_avg[so: so + n],
+                                               a.exp_avg_sq[so: so + n], a.grad_flat[lo:hi],
+                                               a.param_flat[lo:hi], self.clip_coef, lr, b1, b2, eps, wd, t)
+                    if a.zero1:
+                        b.ag_handle = dist.all_gather_into_tensor(a.param_flat[b.start: b.end],
+                                                                  a.param_flat[b.shard_lo: b.shard_hi],
+                                                                  group=a.group, async_op=True)
+                    else:
+                        b.opt_event = torch.cuda.Event()
+                        b.opt_event.record(st)
+
     @torch.no_grad()
     def step(self, closure=None):  # noqa: ARG002
         self._zero_unwritten()
         self._step += 1
         t = self._step
+        if self.side_stream is not None and all(self._native(a) for a in self.arenas):
+            self._step_overlapped(t)
+            return
         for g, a in zip(self.param_groups, self.arenas):
             lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
             native = (self.fused and self.decoupled and _lib.use_native(a.param_flat) and a.master is not None

@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os
 from collections import defaultdict
 
 import torch
@@ -52,7 +53,7 @@ def _is_tp_sharded(p) -> bool:
 
 class Bucket:
     __slots__ = ("start", "end", "params", "pending", "handle", "comm_buf", "comm_out", "launched",
-                 "shard_lo", "shard_hi", "state_lo", "ag_handle")
+                 "shard_lo", "shard_hi", "state_lo", "ag_handle", "opt_event")
 
     def __init__(self, start: int, end: int, params: list):
         self.start, self.end, self.params = start, end, params
@@ -63,6 +64,7 @@ class Bucket:
         self.launched = False
         self.shard_lo, self.shard_hi, self.state_lo = start, end, start
         self.ag_handle = None
+        self.opt_event = None  # side-stream optimizer update of this bucket (optim.py overlap)
 
 
 def _aligned(n: int) -> int:
@@ -157,6 +159,11 @@ class GradArena:
                 self.bucket_of[id(p)] = i
                 self.expected[id(p)] = (use_counts or {}).get(id(p), 1)
         self.remaining = {}
+        # optimizer side stream (set by DataParallel on GPU): per-bucket grad sum-of-squares
+        # during backward (world == 1) and the overlapped optimizer update (optim.py)
+        self.side_stream = None
+        self.sq_acc = None
+        self.sq_count = 0
         self.reset_counts()
 
     def reset_counts(self) -> None:
@@ -191,6 +198,7 @@ class GradArena:
         b.launched = True
         self.zero_fresh(b.params)
         if self.world == 1:
+            self._bucket_sumsq(b)
             return
         g = self.grad_flat[b.start: b.end]
         nccl = dist.get_backend(self.group) == "nccl"
@@ -215,6 +223,40 @@ class GradArena:
             b.handle = dist.reduce_scatter_tensor(out, buf, op=op, group=self.group, async_op=True)
         else:
             b.handle = dist.all_reduce(buf, op=op, group=self.group, async_op=True)
+
+    def _bucket_sumsq(self, b: Bucket) -> None:
+        """world == 1: this bucket's gradients are final -> add their squared norm
+        into ``sq_acc`` on the side stream while the rest of backward runs (the
+        global-norm pass after backward then reads one scalar per arena)."""
+        st = self.side_stream
+        if st is None:
+            return
+        from ..ops import _lib
+
+        g = self.grad_flat[b.start: b.end]
+        if not _lib.use_native(g) or g.numel() % 4:
+            return
+        ev = torch.cuda.Event()
+        ev.record()
+        with torch.cuda.stream(st):
+            st.wait_event(ev)
+            if self.sq_count == 0:
+                if self.sq_acc is None:
+                    self.sq_acc = torch.zeros(1, dtype=torch.float32, device=g.device)
+                else:
+                    self.sq_acc.zero_()
+            _lib.ops().sumsq_(g, self.sq_acc)
+        self.sq_count += 1
+
+    def take_sumsq(self):
+        """The backward-accumulated sum of squares (device scalar) if every bucket
+        contributed this step, else None; joins the side stream."""
+        if self.side_stream is None or self.world != 1 or self.sq_count != len(self.buckets):
+            self.sq_count = 0
+            return None
+        self.sq_count = 0
+        torch.cuda.current_stream().wait_stream(self.side_stream)
+        return self.sq_acc
 
     def finish(self) -> None:
         """Launch whatever did not fire (unused params) and join every bucket."""
@@ -257,6 +299,9 @@ class GradArena:
         if b.ag_handle is not None:
             b.ag_handle.wait()
             b.ag_handle = None
+        if b.opt_event is not None:
+            torch.cuda.current_stream().wait_event(b.opt_event)
+            b.opt_event = None
 
     def wait_params(self) -> None:
         for i in range(len(self.buckets)):
@@ -331,7 +376,16 @@ class DataParallel(nn.Module):
             g = dense_group if name == "dense" else expert_group
             self.arenas.append(GradArena(ps, g, name, bucket_size, reduce_dtype, use_counts=uses, zero1=zero1))
         self.zero1 = any(a.zero1 for a in self.arenas)
-        if self.zero1:
+        # one side stream per model on GPU: per-bucket gradient norms during backward and the
+        # optimizer update overlapped with the NEXT forward (optim.py); each module's forward
+        # pre-hook waits only for the buckets holding its own parameters
+        dev = params[0].device if params else torch.device("cpu")
+        self.side_stream = None
+        if dev.type == "cuda" and os.environ.get("ST_OVERLAP_OPT", "1") == "1":
+            self.side_stream = torch.cuda.Stream(device=dev)
+            for a in self.arenas:
+                a.side_stream = self.side_stream
+        if self.zero1 or self.side_stream is not None:
             self._install_param_waits()
         # TP-replicated params whose grads are TP-partial (per-head QK-norm weights; every
         # norm / router weight under sequence parallelism): summed over TP after backward
@@ -348,9 +402,10 @@ class DataParallel(nn.Module):
 
     # ---------------------------------------------------------------- hooks
     def _install_param_waits(self) -> None:
-        """ZeRO-1: each module waits (stream-ordered) for the all-gather of the
-        buckets holding its own parameters right before its forward, so the
-        parameter all-gather after the optimizer step overlaps the next forward."""
+        """Each module waits (stream-ordered) for the buckets holding its own
+        parameters right before its forward: the ZeRO-1 parameter all-gather and/or
+        the side-stream optimizer update of the previous step overlap the next
+        forward instead of preceding it."""
         where = {}
         for a in self.arenas:
             for i, b in enumerate(a.buckets):
@@ -437,7 +492,11 @@ class DataParallel(nn.Module):
 
     # ---------------------------------------------------------------- API
     def forward(self, *args, **kwargs):
-        return self.module(*args, **kwargs)
+        out = self.module(*args, **kwargs)
+        # parameters no forward hook covered (unused this step) must not be written by
+        # backward while the previous optimizer update may still read their gradients
+        self.wait_params()
+        return out
 
     @contextlib.contextmanager
     def no_sync(self):

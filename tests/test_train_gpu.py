@@ -111,3 +111,32 @@ def test_moe_grouped_gemm_matches_expert_loop():
     assert rel(y, y2) < 1e-2
     assert rel(gx, x.grad) < 2e-2
     assert rel(gw1, ex.w_gate_up.grad) < 2e-2 and rel(gw2, ex.w_down.grad) < 2e-2
+
+
+@pytest.mark.parametrize("ga", [1, 2])
+def test_overlapped_optimizer_matches_serial(ga):
+    """Side-stream AdamW (forward-order buckets, per-module waits) + backward-time
+    grad norms == the serial step: same losses, grad norms and parameters."""
+    def run(overlap):
+        os.environ["ST_OVERLAP_OPT"] = "1" if overlap else "0"
+        try:
+            # no clipping: the norm's summation order (per bucket vs per arena) must then not
+            # touch the parameters at all -> bitwise-equal training
+            tr = _tiny_trainer(gradient_accumulation_steps=ga, bucket_size_mb=0.25, max_grad_norm=0.0)
+        finally:
+            os.environ["ST_OVERLAP_OPT"] = "1"
+        assert (tr.model.side_stream is not None) == overlap
+        losses, norms = [], []
+        for _ in range(4):
+            losses.append(tr.reduced_loss(tr.train_step()))
+            norms.append(float(tr.optimizer.last_grad_norm))
+        tr.optimizer.sync()
+        torch.cuda.synchronize()
+        return losses, norms, torch.cat([a.param_flat.float() for a in tr.model.arenas])
+
+    l0, n0, p0 = run(False)
+    l1, n1, p1 = run(True)
+    for a, b in zip(n0, n1):
+        assert abs(a - b) <= 1e-5 * abs(a), (n0, n1)
+    assert l0 == l1, (l0, l1)
+    assert torch.equal(p0, p1)
