@@ -52,6 +52,8 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
                  int64_t sds, int64_t sdh, int64_t sdqb, int64_t sdqs, int64_t sdqh, int64_t sdkb,
                  int64_t sdks, int64_t sdkh, float scale, int causal, int64_t q_offset,
                  int64_t k_offset, hipStream_t st);
+int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int M,
+                  int N, int T, int beta, hipStream_t st);
 int st_lse_merge(float* out, float* lse, const void* bout, const float* blse, int B, int S, int H,
                  int D, int64_t sbb, int64_t sbs, int64_t sbh, hipStream_t st);
 }
@@ -251,6 +253,29 @@ void sumsq_(const at::Tensor& g, at::Tensor out) {
   ST_CHECK_RC(rc, "sumsq_");
 }
 
+// ---------------------------------------------------------------- weight-gradient GEMM
+// out[M,N] fp32 (+)= dy[T,M]^T @ x[T,N]; returns false when the shape is not one the
+// kernel tiles (caller falls back to hipBLASLt).
+bool wgrad_gemm_(at::Tensor out, const at::Tensor& dy, const at::Tensor& x, int64_t beta) {
+  check_bf16_cuda(dy, "dy");
+  check_bf16_cuda(x, "x");
+  check_same_gpu(x, dy, "x");
+  check_same_gpu(out, dy, "out");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && out.dim() == 2, "wgrad_gemm: 2-D operands");
+  TORCH_CHECK(out.scalar_type() == at::kFloat, "wgrad_gemm: out must be fp32");
+  TORCH_CHECK(dy.size(0) == x.size(0) && out.size(0) == dy.size(1) && out.size(1) == x.size(1),
+              "wgrad_gemm: shapes ", dy.sizes(), " x ", x.sizes(), " -> ", out.sizes());
+  if (dy.stride(1) != 1 || x.stride(1) != 1 || out.stride(1) != 1) return false;
+  const int64_t T = dy.size(0), M = dy.size(1), N = x.size(1);
+  if (T > INT32_MAX || M > INT32_MAX || N > INT32_MAX) return false;
+  c10::hip::HIPGuardMasqueradingAsCUDA g(out.device());
+  int rc = st_wgrad_gemm(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr<float>(),
+                         out.stride(0), (int)M, (int)N, (int)T, beta ? 1 : 0, cur_stream());
+  if (rc == -2) return false;
+  ST_CHECK_RC(rc, "wgrad_gemm_");
+  return true;
+}
+
 // ---------------------------------------------------------------- cross-entropy
 std::vector<at::Tensor> xent_fwd(const at::Tensor& logits, const at::Tensor& tgt,
                                  int64_t vocab_start) {
@@ -418,6 +443,7 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("xent_bwd_(Tensor logits, Tensor target, int vocab_start, Tensor lse, Tensor dloss, Tensor(a!) dlogits) -> ()");
   m.def("flash_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int q_offset, int k_offset) -> Tensor[]");
   m.def("flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, int q_offset, int k_offset, Tensor(a!)? dq_out=None, Tensor(b!)? dk_out=None, Tensor(c!)? dv_out=None) -> Tensor[]");
+  m.def("wgrad_gemm_(Tensor(a!) out, Tensor dy, Tensor x, int beta) -> bool");
   m.def("lse_merge_(Tensor(a!) out, Tensor(b!) lse, Tensor block_out, Tensor block_lse) -> ()");
 }
 
@@ -434,4 +460,5 @@ TORCH_LIBRARY_IMPL(st_amd, CUDA, m) {
   m.impl("flash_fwd", &flash_fwd);
   m.impl("flash_bwd", &flash_bwd);
   m.impl("lse_merge_", &lse_merge_);
+  m.impl("wgrad_gemm_", &wgrad_gemm_);
 }

@@ -57,8 +57,11 @@ def accumulate_grad(param: torch.Tensor, grad: torch.Tensor):
 def accumulate_linear_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor):
     """dW = dy^T x, accumulated into ``param.main_grad`` in fp32 when present.
 
-    Uses ``aten::addmm.dtype_out`` (bf16 operands, fp32 C/D, beta = 1) so the
-    accumulation is fused into the GEMM epilogue on hipBLASLt.
+    On GPU the product runs on the hand-written gfx950 weight-gradient GEMM
+    (csrc/wgrad_gemm.hip: both operands token-major, read with LDS transpose
+    reads, fp32 epilogue accumulating into main_grad); shapes it does not tile
+    go to ``aten::addmm.dtype_out`` (hipBLASLt, bf16 operands, fp32 C/D).
+    ``ST_WGRAD_KERNEL=0`` forces the hipBLASLt path (A/B).
     """
     global _ADDMM_DTYPE_OK
     mg = getattr(param, "main_grad", None)
@@ -69,7 +72,13 @@ def accumulate_linear_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
         mg.addmm_(dy2d.t(), x2d, beta=beta)
     else:
         done = False
-        if _ADDMM_DTYPE_OK is not False and dy2d.is_cuda and os.environ.get("ST_WGRAD_FP32_GEMM", "1") == "1":
+        if (mg.dtype == torch.float32 and dy2d.is_cuda and dy2d.dtype == torch.bfloat16
+                and x2d.dtype == torch.bfloat16 and os.environ.get("ST_WGRAD_KERNEL", "1") == "1"):
+            from . import _lib
+
+            if _lib.use_native(dy2d):
+                done = bool(_lib.ops().wgrad_gemm_(mg.view(mg.shape[0], -1), dy2d, x2d, beta))
+        if not done and _ADDMM_DTYPE_OK is not False and dy2d.is_cuda and os.environ.get("ST_WGRAD_FP32_GEMM", "1") == "1":
             try:
                 torch.ops.aten.addmm.dtype_out(mg, dy2d.t(), x2d, mg.dtype, beta=beta, alpha=1, out=mg)
                 _ADDMM_DTYPE_OK = True

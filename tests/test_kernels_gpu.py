@@ -298,3 +298,29 @@ def test_moe_permute_gather_combine(T, E, k, h):
     # dx: every token receives sum over its slots of 1.5 * w * g
     exp_dx = 1.5 * (ref_w.detach().sum(-1, keepdim=True) * g.float())
     assert rel(x.grad, exp_dx) < 2e-2
+
+
+@pytest.mark.parametrize("mfma", ["32", "16"])
+@pytest.mark.parametrize("T,M,N,beta", [(64, 256, 256, 0), (512, 512, 768, 1), (1024, 768, 512, 0), (96, 256, 512, 1)])
+def test_wgrad_gemm(T, M, N, beta, mfma, monkeypatch):
+    monkeypatch.setenv("ST_WGRAD_MFMA", mfma)
+    """dW (+)= dY^T X with token-major operands (csrc/wgrad_gemm.hip) vs fp32 reference;
+    strided operands (column slices of wider activations) and asymmetric data."""
+    torch.manual_seed(0)
+    dy_full = torch.randn(T, M + 64, device="cuda", dtype=torch.bfloat16)
+    x_full = torch.randn(T, N + 128, device="cuda", dtype=torch.bfloat16)
+    dy, x = dy_full[:, 32: 32 + M], x_full[:, 64: 64 + N]
+    ramp = torch.arange(M, device="cuda", dtype=torch.float32)[:, None] * 1e-3
+    out = torch.randn(M, N, device="cuda") + ramp
+    ref = dy.float().t() @ x.float() + (out if beta else 0)
+    assert _lib.ops().wgrad_gemm_(out, dy, x, beta)
+    torch.cuda.synchronize()
+    assert rel(out, ref) < 1e-5
+
+
+def test_wgrad_gemm_unsupported_shape_declines():
+    dy = torch.randn(64, 200, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(64, 256, device="cuda", dtype=torch.bfloat16)
+    out = torch.zeros(200, 256, device="cuda")
+    assert not _lib.ops().wgrad_gemm_(out, dy, x, 0)
+    assert out.abs().sum().item() == 0

@@ -20,7 +20,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def set_variant(tr, name: str, side) -> None:
-    """overlap: side-stream optimizer + backward-time norms; serial: both off."""
+    """overlap: side-stream optimizer + backward-time norms; serial: both off;
+    ``K=V[+K=V...]``: environment toggles read per call (e.g. ST_WGRAD_KERNEL=0)."""
+    if "=" in name:
+        for kv in name.split("+"):
+            k, v = kv.split("=", 1)
+            os.environ[k] = v
+        return
+    for k in list(os.environ):
+        if k.startswith("ST_WGRAD"):
+            del os.environ[k]
     on = name == "overlap"
     tr.optimizer.side_stream = side if on else None
     tr.model.side_stream = side if on else None
