@@ -12,8 +12,10 @@
 // and autograd's F.linear backward.
 //
 // Design (CDNA4-first):
-//   * 256x256 output tile, 8 waves (2 along M x 4 along N, 128x64 per wave),
-//     v_mfma_f32_32x32x16_bf16, 8 accumulators (128 acc registers) per lane.
+//   * 256x256 output tile, 8 waves (2 along M x 4 along N, 128x64 per wave), or
+//     256x128 (4 x 2 waves, 64x64 per wave) when the 256-wide grid would leave a
+//     partial last wave of workgroups on the 256 CUs; v_mfma_f32_16x16x32_bf16
+//     (on random operands it holds a higher clock than 32x32x16: +5-8 % here).
 //   * the K loop walks T in 64-token tiles; each tile of A and B is staged
 //     global -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds) EXACTLY as stored
 //     (rows = tokens, 256-byte rows of 128 features, XOR-swizzled on the source
@@ -21,8 +23,9 @@
 //     delivers the token (reduction) index down a lane's fragment: no transpose
 //     pass, no staging registers, no ds_write.  The same permuted k order is
 //     used for A and B, so the pairing inside the MFMA is consistent.
-//   * two LDS stages (2 x 64 KiB): the next tile's DMA is issued at the top of
-//     a step and retired by the end-of-step barrier.
+//   * K loop over 32-token tiles through a ring of 4 LDS stages with 3 tiles in
+//     flight: the DMA is issued from inline asm (so hipcc does not drain it
+//     before the transposed reads) and retired by a counted vmcnt + s_barrier.
 //   * XCD-aware tile order: the dispatcher deals workgroups round-robin to the
 //     8 XCDs; the bijective remap gives each XCD a contiguous range of tiles,
 //     grouped 4 M-blocks x N so the ~32 tiles an XCD runs at once share their
@@ -40,12 +43,10 @@ typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bfx4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) char lds_t;
 
-constexpr int BM = 256, BN = 256, BK = 32, NT = 512;
+constexpr int BM = 256, BK = 32, NT = 512;
 constexpr int RB = 256;               // bytes per LDS image row: 128 bf16 features
 constexpr int IMG = BK * RB;          // one [32 tokens][128 features] image: 8 KiB
-constexpr int STAGE = 4 * IMG;        // A0 A1 B0 B1: 32 KiB
-constexpr int NBUF = 4;               // ring of 4 stages = 128 KiB, 3 in flight
-constexpr int NDMA = STAGE / (NT * 16);  // LDS-DMA instructions per lane per stage (4)
+constexpr int NBUF = 4;               // ring of 4 stages, 3 tiles in flight
 constexpr int GROUP_M = 4;
 
 // 256-B rows, 16-B chunks: both the transposed reads and the DMA fill are
@@ -73,9 +74,9 @@ ST_DEVICE i32x4 make_rsrc(const bf16_t* base, uint32_t bytes) {
 
 // LDS-DMA issued from inline asm: hipcc does not see it as an LDS write, so it
 // does not drain it (vmcnt(0)) before the tile's transposed reads the way it
-// does for the builtin form -- the wait is placed by hand (end of step), which
-// is what lets the next tile's DMA overlap this tile's MFMAs.  M0 = the wave's
-// LDS destination base; lane l lands at base + 16 l.
+// does for the builtin form -- the wait is placed by hand, which is what lets
+// the next tiles' DMA overlap this tile's MFMAs.  M0 = the wave's LDS
+// destination base; lane l lands at base + 16 l.
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved: nothing else in this kernel uses it
 ST_DEVICE void lds_dma16(const i32x4& rs, uint32_t lds_base, uint32_t voff) {
@@ -86,14 +87,28 @@ ST_DEVICE void lds_dma16(const i32x4& rs, uint32_t lds_base, uint32_t voff) {
 }
 #pragma clang diagnostic pop
 
-template <int PROBE, int MF>
+template <int BN>
+struct Geo {
+  static constexpr int WM = BN == 256 ? 2 : 4, WN = 8 / WM;  // wave grid
+  static constexpr int TM = BM / WM, TN = BN / WN;           // per-wave tile
+  static constexpr int FM = TM / 16, FN = TN / 16;           // 16x16 fragments per wave
+  static constexpr int NIMG = (BM + BN) / 128;               // 128-feature images per stage
+  static constexpr int STAGE = NIMG * IMG;
+  static constexpr int PIECES = STAGE / 1024;                // 1 KiB DMA pieces per stage
+  static constexpr int NDMA = PIECES / 8;                    // per wave (and per lane)
+  static_assert(PIECES % 8 == 0, "stage must split evenly over 8 waves");
+};
+
+template <int PROBE, int BN>
 __global__ __launch_bounds__(NT, 2) void wgrad_gemm_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                            const bf16_t* __restrict__ B, int64_t ldb,
                                                            float* __restrict__ C, int64_t ldc, int M, int N,
                                                            int T, int beta) {
-  __shared__ __attribute__((aligned(16))) char smem_raw[NBUF * STAGE];
+  using Gm = Geo<BN>;
+  __shared__ __attribute__((aligned(16))) char smem_raw[NBUF * Gm::STAGE];
   lds_t* smem = (lds_t*)smem_raw;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int nbm = M / BM, nbn = N / BN, nwg = nbm * nbn;
 
   // ---- tile of this workgroup: XCD remap, then GROUP_M x nbn grouping
@@ -105,77 +120,66 @@ __global__ __launch_bounds__(NT, 2) void wgrad_gemm_kernel(const bf16_t* __restr
   const int bm = first_bm + in_group % gsz, bn = in_group / gsz;
   const int m0 = bm * BM, n0 = bn * BN;
 
-  // ---- DMA plan: wave w fills rows [16 (w&1), +16) of image (w>>1) of a stage
-  const int img = wid >> 1, part = wid & 1;
-  const bf16_t* src = img < 2 ? A + m0 + 128 * img : B + n0 + 128 * (img - 2);
-  const int64_t ld = img < 2 ? lda : ldb;
-  const uint32_t stride_b = (uint32_t)(ld * 2);
-  const i32x4 rs = make_rsrc(src, (uint32_t)(((int64_t)(T - 1) * ld + 128) * 2));
-  uint32_t voff[NDMA];
+  // ---- DMA plan: a stage is NIMG images [32 tokens][128 features] (A images
+  // first); wave w fills the 1 KiB pieces [w NDMA, (w+1) NDMA) of it.  Image
+  // boundaries are 8 KiB, so a piece never straddles two images.
+  const i32x4 rsA = make_rsrc(A + m0, (uint32_t)(((int64_t)(T - 1) * lda + BM) * 2));
+  const i32x4 rsB = make_rsrc(B + n0, (uint32_t)(((int64_t)(T - 1) * ldb + BN) * 2));
+  const uint32_t sA = (uint32_t)(lda * 2), sB = (uint32_t)(ldb * 2);
+  uint32_t voff[Gm::NDMA];
+  bool isA[Gm::NDMA];
 #pragma unroll
-  for (int i = 0; i < NDMA; ++i) {
-    const int a = part * (IMG / 2) + i * 1024 + lane * 16;
-    const int row = a / RB, pos = (a % RB) / 16;
-    voff[i] = (uint32_t)row * stride_b + (uint32_t)((pos ^ swz(row)) * 16);
+  for (int i = 0; i < Gm::NDMA; ++i) {
+    const int piece = (wid * Gm::NDMA + i) * 1024;  // wave-uniform
+    const int a = piece + lane * 16;
+    const int im = piece / IMG, row = (a % IMG) / RB, pos = (a % RB) / 16;
+    isA[i] = im < BM / 128;
+    const int col_b = 256 * (isA[i] ? im : im - BM / 128);
+    voff[i] = (uint32_t)row * (isA[i] ? sA : sB) + (uint32_t)(col_b + 16 * (pos ^ swz(row)));
   }
-  const uint32_t dma_base = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)smem + (uint32_t)(img * IMG + part * (IMG / 2)));
+  const uint32_t dma_base =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem + (uint32_t)(wid * Gm::NDMA * 1024));
   auto dma = [&](int buf, int kt) {
-    const uint32_t o = (uint32_t)(kt * BK) * stride_b;
+    const uint32_t oA = (uint32_t)(kt * BK) * sA, oB = (uint32_t)(kt * BK) * sB;
 #pragma unroll
-    for (int i = 0; i < NDMA; ++i) lds_dma16(rs, dma_base + buf * STAGE + i * 1024, voff[i] + o);
+    for (int i = 0; i < Gm::NDMA; ++i)
+      lds_dma16(isA[i] ? rsA : rsB, dma_base + buf * Gm::STAGE + i * 1024, voff[i] + (isA[i] ? oA : oB));
   };
 
-  // ---- fragment read plan (lane-constant offsets): element j of lane (r, h) of a
-  // transposed read at k-step s is image[16s + 8(j>>2) + 4h + (j&3)][32 dt + r]
-  const int h = lane >> 5, g = (lane >> 4) & 1, q = (lane >> 2) & 3, pp = lane & 3;
-  const int wm = wid >> 2, wn = wid & 3;
-  const int a_img = wm * IMG, b_img = (2 + (wn >> 1)) * IMG, b_dt0 = (wn & 1) * 2;
-  int atr[4][2], btr[2][2];  // never indexed by a runtime value (registers, not scratch)
-  // 16x16x32 plan: lane group G = lane>>4 reads token rows 8G..8G+7 (natural k
-  // order) of 16 feature columns 16 f .. 16 f + 15
-  const int G = lane >> 4;
-  int atr16[8][2], btr16[4][2];
-  if constexpr (MF == 32) {
+  // ---- fragment read plan (16x16x32): lane group G = lane>>4 reads token rows
+  // 8G..8G+7 (natural k order) of 16 feature columns; lane 4q+p of the group
+  // addresses row q, columns 4p..4p+3 (T10).
+  const int G = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int wm = wid / Gm::WN, wn = wid % Gm::WN;
+  const int am = wm * Gm::TM, bnn = wn * Gm::TN;  // wave's first row / column inside the tile
+  int atr[Gm::FM][2], btr[Gm::FN][2];             // never indexed by a runtime value
 #pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
+  for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-        atr[dt][hf] = lds_off(4 * h + q + 8 * hf, 4 * dt + 2 * g + (pp >> 1)) + 8 * (pp & 1);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        btr[j][hf] = lds_off(4 * h + q + 8 * hf, 4 * (b_dt0 + j) + 2 * g + (pp >> 1)) + 8 * (pp & 1);
+    for (int f = 0; f < Gm::FM; ++f) {
+      const int col = am + 16 * f;  // feature column inside the A half-images
+      atr[f][hf] = (col / 128) * IMG + lds_off(8 * G + 4 * hf + q, ((col % 128) / 8) + (pp >> 1)) + 8 * (pp & 1);
     }
-  } else {
 #pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-#pragma unroll
-      for (int f = 0; f < 8; ++f) atr16[f][hf] = lds_off(8 * G + 4 * hf + q, 2 * f + (pp >> 1)) + 8 * (pp & 1);
-#pragma unroll
-      for (int f = 0; f < 4; ++f)
-        btr16[f][hf] = lds_off(8 * G + 4 * hf + q, 2 * (4 * (wn & 1) + f) + (pp >> 1)) + 8 * (pp & 1);
+    for (int f = 0; f < Gm::FN; ++f) {
+      const int col = bnn + 16 * f;
+      btr[f][hf] = (BM / 128 + col / 128) * IMG + lds_off(8 * G + 4 * hf + q, ((col % 128) / 8) + (pp >> 1)) +
+                   8 * (pp & 1);
     }
   }
 
-  f32x16 acc[4][2];
-  f32x4 acc16[8][4];
+  f32x4 acc[Gm::FM][Gm::FN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < Gm::FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < Gm::FN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc16[i][j][r] = 0.f;
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
 
   // ---- K loop: a ring of NBUF stages, NBUF-1 tiles in flight.  Top of step kt:
   // wait (counted vmcnt) until this wave's DMA of tile kt landed, barrier (every
   // wave's DMA landed + every wave finished reading tile kt-1), refill the stage
-  // tile kt-1 used with tile kt+NBUF-1, then 2 k-steps of MFMAs on tile kt.
+  // tile kt-1 used with tile kt+NBUF-1, then the tile's MFMAs.
   const int KT = T / BK;
 #pragma unroll
   for (int p = 0; p < NBUF - 1; ++p)
@@ -183,47 +187,25 @@ __global__ __launch_bounds__(NT, 2) void wgrad_gemm_kernel(const bf16_t* __restr
 
   auto step = [&](auto bufc, int kt) {
     constexpr int BUF = decltype(bufc)::value;
-    if (kt + 2 < KT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NDMA) : "memory");
-    else if (kt + 1 < KT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
+    if (kt + 2 < KT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * Gm::NDMA) : "memory");
+    else if (kt + 1 < KT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Gm::NDMA) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (kt + NBUF - 1 < KT && PROBE != 1) dma((BUF + NBUF - 1) % NBUF, kt + NBUF - 1);
-    const lds_t* st = smem + BUF * STAGE;
-    if constexpr (MF == 16) {
-      const lds_t* ab = st + a_img;
-      const lds_t* bb = st + b_img;
-      bfx8 af[8], bf[4];
+    const lds_t* st = smem + BUF * Gm::STAGE;
+    bfx8 af[Gm::FM], bf[Gm::FN];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bf[j] = lds_tr(bb + btr16[j][0], bb + btr16[j][1]);
+    for (int j = 0; j < Gm::FN; ++j) bf[j] = lds_tr(st + btr[j][0], st + btr[j][1]);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) af[i] = lds_tr(ab + atr16[i][0], ab + atr16[i][1]);
-      __builtin_amdgcn_s_setprio(1);
+    for (int i = 0; i < Gm::FM; ++i) af[i] = lds_tr(st + atr[i][0], st + atr[i][1]);
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < Gm::FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc16[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      asm volatile("" ::: "memory");
-      return;
-    }
-#pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
-      const lds_t* ab = st + a_img + 16 * s * RB;
-      const lds_t* bb = st + b_img + 16 * s * RB;
-      bfx8 af[4], bf[2];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = lds_tr(ab + atr[i][0], ab + atr[i][1]);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bf[j] = lds_tr(bb + btr[j][0], bb + btr[j][1]);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
+      for (int j = 0; j < Gm::FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
     asm volatile("" ::: "memory");
   };
   for (int kt = 0; kt < KT; kt += NBUF) {
@@ -233,29 +215,15 @@ __global__ __launch_bounds__(NT, 2) void wgrad_gemm_kernel(const bf16_t* __restr
     if (kt + 3 < KT) step(std::integral_constant<int, 3>(), kt + 3);
   }
 
-  const int mb = m0 + wm * 128, nb = n0 + wn * 64, c = lane & 31;
-  if constexpr (MF == 16) {  // C/D: row = 4 (lane>>4) + reg (M), column = lane&15 (N)
+  // ---- epilogue: 16x16 C/D row = 4 (lane>>4) + reg (M), column = lane&15 (N)
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < Gm::FM; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < Gm::FN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = mb + 16 * i + 4 * G + r;
-          float* p = C + (int64_t)m * ldc + nb + 16 * j + (lane & 15);
-          *p = beta ? *p + acc16[i][j][r] : acc16[i][j][r];
-        }
-    return;
-  }
-  // ---- epilogue: C/D row = (reg&3) + 8(reg>>2) + 4h (M), column = lane&31 (N)
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mb + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-        float* p = C + (int64_t)m * ldc + nb + 32 * j + c;
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + am + 16 * i + 4 * G + r;
+        float* p = C + (int64_t)m * ldc + n0 + bnn + 16 * j + (lane & 15);
         *p = beta ? *p + acc[i][j][r] : acc[i][j][r];
       }
 }
@@ -265,30 +233,40 @@ __global__ __launch_bounds__(NT, 2) void wgrad_gemm_kernel(const bf16_t* __restr
 extern "C" {
 
 // 0 on success; -2: shape not supported by this kernel (caller falls back).
+// Tile width: 256 unless only 128 divides N or the 256-wide grid would end in a
+// partial wave of workgroups that the 128-wide one avoids (qkv 6144x4096: 384
+// vs 768 tiles; down 4096x14336: 896 vs 1792 on 256 CUs).
 int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int M,
                   int N, int T, int beta, hipStream_t st) {
   if (M <= 0 || N <= 0 || T <= 0) return -2;
-  if (M % BM || N % BN || T % BK) return -2;
+  if (M % BM || N % 128 || T % BK) return -2;
   if (lda % 8 || ldb % 8 || lda < M || ldb < N || ldc < N) return -2;
   if (((uintptr_t)A | (uintptr_t)B) % 16 || (uintptr_t)C % 4) return -2;
   // 32-bit buffer offsets: the last row of each operand must be addressable
   if (((int64_t)(T - 1) * lda + M) * 2 >= (int64_t)1 << 32) return -2;
   if (((int64_t)(T - 1) * ldb + N) * 2 >= (int64_t)1 << 32) return -2;
-  const int nwg = (M / BM) * (N / BN);
-  // ST_WGRAD_PROBE=1: timing probe only (no K-loop DMA: compute ceiling) -- wrong results
-  const char* pe = std::getenv("ST_WGRAD_PROBE");
+  const char* pe = std::getenv("ST_WGRAD_PROBE");  // 1: no K-loop DMA (timing probe, wrong results)
   const int probe = pe ? std::atoi(pe) : 0;
-  // ST_WGRAD_MFMA=32: v_mfma_f32_32x32x16_bf16 variant (default 16x16x32: ~+5-8 % on random data)
-  const char* me = std::getenv("ST_WGRAD_MFMA");
-  const int mf = me ? std::atoi(me) : 16;
+  const char* be = std::getenv("ST_WGRAD_BN");     // force 128 / 256 (A/B)
+  int bn = be ? std::atoi(be) : 0;
+  const int cus = 256;
+  if (bn != 128 && bn != 256) {
+    const int64_t t256 = (N % 256 == 0) ? (int64_t)(M / BM) * (N / 256) : -1;
+    const int64_t t128 = (int64_t)(M / BM) * (N / 128);
+    auto eff = [&](int64_t t) { return (double)t / (double)(((t + cus - 1) / cus) * cus); };
+    // a 256x128 tile streams ~10 % less MFMA work per LDS byte: switch only for a real tail win
+    bn = (t256 > 0 && eff(t256) * 1.08 >= eff(t128)) ? 256 : 128;
+  }
+  if (bn == 256 && N % 256) return -2;
   const bf16_t *a = (const bf16_t*)A, *b = (const bf16_t*)B;
   const int bt = beta ? 1 : 0;
-  if (mf == 16) {
-    if (probe == 1) wgrad_gemm_kernel<1, 16><<<nwg, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
-    else wgrad_gemm_kernel<0, 16><<<nwg, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
+  const int nwg = (M / BM) * (N / bn);
+  if (bn == 256) {
+    if (probe == 1) wgrad_gemm_kernel<1, 256><<<nwg, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
+    else wgrad_gemm_kernel<0, 256><<<nwg, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
   } else {
-    if (probe == 1) wgrad_gemm_kernel<1, 32><<<nwg, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
-    else wgrad_gemm_kernel<0, 32><<<nwg, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
+    if (probe == 1) wgrad_gemm_kernel<1, 128><<<nwg, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
+    else wgrad_gemm_kernel<0, 128><<<nwg, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
   }
   return (int)hipGetLastError();
 }

@@ -19,6 +19,10 @@ import os
 import torch
 
 _ADDMM_DTYPE_OK: bool | None = None
+# per-shape winner of the weight-gradient GEMM: True = csrc/wgrad_gemm.hip, False = hipBLASLt
+_WGRAD_CHOICE: dict = {}
+_WGRAD_TIMES: dict = {}  # tuning measurements (ms for two calls), for tools/ab_step.py
+_TUNE_MAX_BYTES = 512 << 20
 
 
 def _grad_ready(param: torch.Tensor) -> None:
@@ -54,6 +58,52 @@ def accumulate_grad(param: torch.Tensor, grad: torch.Tensor):
     return None
 
 
+def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> bool:
+    """First call per (shape, strides): time the HIP kernel against the hipBLASLt
+    fp32-epilogue GEMM on a scratch output (5 x 2 runs, same stream) and keep the
+    faster one -- on gfx950 neither wins every projection shape."""
+    from . import _lib
+
+    key = (tuple(dy2d.shape), dy2d.stride(0), tuple(x2d.shape), x2d.stride(0), dy2d.device.index)
+    got = _WGRAD_CHOICE.get(key)
+    if got is not None:
+        return got
+    M, N = dy2d.shape[1], x2d.shape[1]
+    if M * N * 4 > _TUNE_MAX_BYTES or os.environ.get("ST_WGRAD_TUNE", "1") != "1":
+        _WGRAD_CHOICE[key] = True
+        return True
+    scratch = torch.zeros(M, N, dtype=torch.float32, device=dy2d.device)
+    if not _lib.ops().wgrad_gemm_(scratch, dy2d, x2d, 0):
+        _WGRAD_CHOICE[key] = False
+        return False
+
+    def ours():
+        _lib.ops().wgrad_gemm_(scratch, dy2d, x2d, 1)
+
+    def blas():
+        torch.ops.aten.addmm.dtype_out(scratch, dy2d.t(), x2d, torch.float32, beta=1, alpha=1, out=scratch)
+
+    best = {}
+    try:
+        blas()
+        for _ in range(5):
+            for name, fn in (("ours", ours), ("blas", blas)):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                fn()
+                fn()
+                e.record()
+                e.synchronize()
+                best[name] = min(best.get(name, 1e30), s.elapsed_time(e))
+        choice = best["ours"] <= best["blas"]
+    except (RuntimeError, NotImplementedError):
+        choice = True
+    del scratch
+    _WGRAD_CHOICE[key] = choice
+    _WGRAD_TIMES[key] = best
+    return choice
+
+
 def accumulate_linear_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor):
     """dW = dy^T x, accumulated into ``param.main_grad`` in fp32 when present.
 
@@ -76,7 +126,7 @@ def accumulate_linear_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
                 and x2d.dtype == torch.bfloat16 and os.environ.get("ST_WGRAD_KERNEL", "1") == "1"):
             from . import _lib
 
-            if _lib.use_native(dy2d):
+            if _lib.use_native(dy2d) and _wgrad_pick(dy2d, x2d):
                 done = bool(_lib.ops().wgrad_gemm_(mg.view(mg.shape[0], -1), dy2d, x2d, beta))
         if not done and _ADDMM_DTYPE_OK is not False and dy2d.is_cuda and os.environ.get("ST_WGRAD_FP32_GEMM", "1") == "1":
             try:

@@ -300,10 +300,12 @@ def test_moe_permute_gather_combine(T, E, k, h):
     assert rel(x.grad, exp_dx) < 2e-2
 
 
-@pytest.mark.parametrize("mfma", ["32", "16"])
-@pytest.mark.parametrize("T,M,N,beta", [(64, 256, 256, 0), (512, 512, 768, 1), (1024, 768, 512, 0), (96, 256, 512, 1)])
-def test_wgrad_gemm(T, M, N, beta, mfma, monkeypatch):
-    monkeypatch.setenv("ST_WGRAD_MFMA", mfma)
+@pytest.mark.parametrize("bn", ["auto", "128", "256"])
+@pytest.mark.parametrize("T,M,N,beta", [(64, 256, 256, 0), (512, 512, 768, 1), (1024, 768, 512, 0), (96, 256, 512, 1),
+                                        (160, 512, 384, 1)])
+def test_wgrad_gemm(T, M, N, beta, bn, monkeypatch):
+    if bn != "auto":
+        monkeypatch.setenv("ST_WGRAD_BN", bn)
     """dW (+)= dY^T X with token-major operands (csrc/wgrad_gemm.hip) vs fp32 reference;
     strided operands (column slices of wider activations) and asymmetric data."""
     torch.manual_seed(0)
@@ -313,6 +315,9 @@ def test_wgrad_gemm(T, M, N, beta, mfma, monkeypatch):
     ramp = torch.arange(M, device="cuda", dtype=torch.float32)[:, None] * 1e-3
     out = torch.randn(M, N, device="cuda") + ramp
     ref = dy.float().t() @ x.float() + (out if beta else 0)
+    if bn == "256" and N % 256:
+        assert not _lib.ops().wgrad_gemm_(out, dy, x, beta)
+        return
     assert _lib.ops().wgrad_gemm_(out, dy, x, beta)
     torch.cuda.synchronize()
     assert rel(out, ref) < 1e-5
@@ -320,7 +325,7 @@ def test_wgrad_gemm(T, M, N, beta, mfma, monkeypatch):
 
 def test_wgrad_gemm_unsupported_shape_declines():
     dy = torch.randn(64, 200, device="cuda", dtype=torch.bfloat16)
-    x = torch.randn(64, 256, device="cuda", dtype=torch.bfloat16)
-    out = torch.zeros(200, 256, device="cuda")
+    x = torch.randn(64, 192, device="cuda", dtype=torch.bfloat16)
+    out = torch.zeros(200, 192, device="cuda")
     assert not _lib.ops().wgrad_gemm_(out, dy, x, 0)
     assert out.abs().sum().item() == 0

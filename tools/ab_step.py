@@ -76,6 +76,11 @@ def main() -> int:
             torch.cuda.synchronize()
             times[v].append((time.perf_counter() - t0) / args.steps * 1e3)
             print(f"round {r} {v}: {times[v][-1]:.2f} ms/step", flush=True)
+    from scaletorch_amd.ops import grad as G
+
+    for k, v in G._WGRAD_TIMES.items():
+        print("wgrad tune", k[0], k[2], {a: round(b, 3) for a, b in v.items()}, "->",
+              "hip" if G._WGRAD_CHOICE.get(k) else "hipblaslt")
     print(json.dumps({v: round(statistics.median(t), 2) for v, t in times.items()}))
     return 0
 
