@@ -54,6 +54,18 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
                  int64_t k_offset, hipStream_t st);
 int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int M,
                   int N, int T, int beta, hipStream_t st);
+int st_xgmi_header_bytes();
+int st_xgmi_max_ranks();
+int64_t st_xgmi_create(int rank, int world, int64_t cap, int64_t epoch_base);
+int st_xgmi_handle(int64_t id, void* out64);
+int st_xgmi_open(int64_t id, int r, const void* handle64);
+int st_xgmi_set_peer(int64_t id, int r, int64_t peer_id);
+int st_xgmi_all_reduce(int64_t id, const void* in, void* out, int64_t n, int dtype, int mode, int blocks,
+                       hipStream_t st);
+int st_xgmi_all_reduce_sim(const int64_t* ids, const void* const* ins, void* const* outs, int world, int64_t n,
+                           int dtype, int mode, int blocks, hipStream_t st);
+int st_xgmi_error(int64_t id);
+int st_xgmi_destroy(int64_t id);
 int st_lse_merge(float* out, float* lse, const void* bout, const float* blse, int B, int S, int H,
                  int D, int64_t sbb, int64_t sbs, int64_t sbh, hipStream_t st);
 }
@@ -276,6 +288,63 @@ bool wgrad_gemm_(at::Tensor out, const at::Tensor& dy, const at::Tensor& x, int6
   return true;
 }
 
+// ---------------------------------------------------------------- xGMI all-reduce
+// Stateful helpers around csrc/xgmi_allreduce.hip (catch-all kernels: most take no tensor).
+int64_t xgmi_create(int64_t rank, int64_t world, int64_t cap, int64_t epoch_base) {
+  int64_t id = st_xgmi_create((int)rank, (int)world, cap, epoch_base);
+  TORCH_CHECK(id >= 0, "xgmi_create failed (", id, ")");
+  return id;
+}
+at::Tensor xgmi_handle(int64_t id) {
+  auto t = at::zeros({64}, at::TensorOptions().dtype(at::kByte));
+  int rc = st_xgmi_handle(id, t.data_ptr());
+  TORCH_CHECK(rc == 0, "hipIpcGetMemHandle failed (", rc, ")");
+  return t;
+}
+void xgmi_open(int64_t id, int64_t r, const at::Tensor& h) {
+  TORCH_CHECK(!h.is_cuda() && h.numel() == 64 && h.scalar_type() == at::kByte, "xgmi_open: uint8[64] CPU handle");
+  auto hc = h.contiguous();
+  int rc = st_xgmi_open(id, (int)r, hc.data_ptr());
+  TORCH_CHECK(rc == 0, "hipIpcOpenMemHandle for peer ", r, " failed (", rc, ")");
+}
+void xgmi_set_peer(int64_t id, int64_t r, int64_t peer) {
+  TORCH_CHECK(st_xgmi_set_peer(id, (int)r, peer) == 0, "xgmi_set_peer");
+}
+void xgmi_all_reduce(int64_t id, const at::Tensor& inp, at::Tensor out, int64_t mode, int64_t blocks) {
+  TORCH_CHECK(inp.is_cuda() && out.is_cuda() && inp.device() == out.device(), "xgmi: GPU tensors");
+  TORCH_CHECK(inp.is_contiguous() && out.is_contiguous() && inp.numel() == out.numel() &&
+                  inp.scalar_type() == out.scalar_type(), "xgmi: contiguous, same shape/dtype");
+  TORCH_CHECK(inp.scalar_type() == at::kBFloat16 || inp.scalar_type() == at::kFloat, "xgmi: bf16 or fp32");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(inp.device());
+  int rc = st_xgmi_all_reduce(id, inp.data_ptr(), out.data_ptr(), inp.numel(),
+                              inp.scalar_type() == at::kBFloat16 ? 0 : 1, (int)mode, (int)blocks, cur_stream());
+  TORCH_CHECK(rc == 0, "xgmi_all_reduce failed (", rc, "): size must be a multiple of 8 and fit the buffer");
+}
+void xgmi_all_reduce_sim(std::vector<int64_t> ids, std::vector<at::Tensor> ins, std::vector<at::Tensor> outs,
+                         int64_t mode, int64_t blocks) {
+  const size_t w = ids.size();
+  TORCH_CHECK(w >= 1 && ins.size() == w && outs.size() == w, "xgmi_all_reduce_sim: one in/out per rank");
+  std::vector<const void*> ip(w);
+  std::vector<void*> op(w);
+  for (size_t r = 0; r < w; ++r) {
+    TORCH_CHECK(ins[r].is_cuda() && outs[r].is_cuda() && ins[r].is_contiguous() && outs[r].is_contiguous() &&
+                    ins[r].numel() == ins[0].numel() && outs[r].numel() == ins[0].numel() &&
+                    ins[r].scalar_type() == ins[0].scalar_type() && outs[r].scalar_type() == ins[0].scalar_type() &&
+                    ins[r].device() == ins[0].device() && outs[r].device() == ins[0].device(),
+                "xgmi_all_reduce_sim: matching contiguous GPU tensors");
+    ip[r] = ins[r].data_ptr();
+    op[r] = outs[r].data_ptr();
+  }
+  TORCH_CHECK(ins[0].scalar_type() == at::kBFloat16 || ins[0].scalar_type() == at::kFloat, "xgmi: bf16 or fp32");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(ins[0].device());
+  int rc = st_xgmi_all_reduce_sim(ids.data(), ip.data(), op.data(), (int)w, ins[0].numel(),
+                                  ins[0].scalar_type() == at::kBFloat16 ? 0 : 1, (int)mode, (int)blocks,
+                                  cur_stream());
+  TORCH_CHECK(rc == 0, "xgmi_all_reduce_sim failed (", rc, ")");
+}
+int64_t xgmi_error(int64_t id) { return st_xgmi_error(id); }
+void xgmi_destroy(int64_t id) { st_xgmi_destroy(id); }
+
 // ---------------------------------------------------------------- cross-entropy
 std::vector<at::Tensor> xent_fwd(const at::Tensor& logits, const at::Tensor& tgt,
                                  int64_t vocab_start) {
@@ -444,6 +513,15 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("flash_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int q_offset, int k_offset) -> Tensor[]");
   m.def("flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, int q_offset, int k_offset, Tensor(a!)? dq_out=None, Tensor(b!)? dk_out=None, Tensor(c!)? dv_out=None) -> Tensor[]");
   m.def("wgrad_gemm_(Tensor(a!) out, Tensor dy, Tensor x, int beta) -> bool");
+  m.def("xgmi_create(int rank, int world, int cap, int epoch_base) -> int", &xgmi_create);
+  m.def("xgmi_handle(int id) -> Tensor", &xgmi_handle);
+  m.def("xgmi_open(int id, int r, Tensor handle) -> ()", &xgmi_open);
+  m.def("xgmi_set_peer(int id, int r, int peer) -> ()", &xgmi_set_peer);
+  m.def("xgmi_all_reduce(int id, Tensor inp, Tensor(a!) out, int mode, int blocks) -> ()", &xgmi_all_reduce);
+  m.def("xgmi_all_reduce_sim(int[] ids, Tensor[] ins, Tensor(a!)[] outs, int mode, int blocks) -> ()",
+        &xgmi_all_reduce_sim);
+  m.def("xgmi_error(int id) -> int", &xgmi_error);
+  m.def("xgmi_destroy(int id) -> ()", &xgmi_destroy);
   m.def("lse_merge_(Tensor(a!) out, Tensor(b!) lse, Tensor block_out, Tensor block_lse) -> ()");
 }
 

@@ -1,0 +1,434 @@
+// Custom intra-node all-reduce over xGMI peer memory (one-shot / two-shot).
+//
+// Reference: the TP all-reduces of scaletorch (ReduceFromModelParallelRegion,
+// RowParallelLinear and the async grad-input all-reduce,
+// scaletorch/parallel/tensor_parallel/tp_comms.py:117-166, :229-320) which go
+// through NCCL/HCCL for every message size.  SURVEY.md §2.2 "custom transport".
+//
+// Why: a TP all-reduce of one activation ([b, S, h] bf16, 1-32 MiB) is
+// latency/launch bound on RCCL's ring at small sizes and per-link bound at
+// large ones.  An MI355X node is fully connected (every GPU has a direct xGMI
+// link to each of the 7 others), so a rank can READ all peers' buffers at once:
+//   * one-shot: every rank copies its input into its IPC-shared buffer, signals,
+//     then reads the same slice from all W buffers and sums (fp32) -- one
+//     round trip, W-1 links busy in parallel; best for small messages.
+//   * two-shot: reduce-scatter (rank p sums partition p from all buffers into
+//     its result area), signal, all-gather (every rank copies partition p from
+//     rank p's result area) -- 2 (W-1)/W of the bytes per rank, for large ones.
+// Buffers are plain device allocations; coherence is explicit: every load and
+// store of a shared area carries the system-coherence bits (sc0 sc1: written
+// through / re-fetched past the non-coherent XCD L2s), flags are system-scope
+// atomics, the writer retires its stores (vmcnt(0)) before the release flag
+// store and the reader acquires before loading.  (An "uncached" allocation
+// alone was not enough: order-dependent stale slices were observed with it.)
+//
+// Synchronisation is per BLOCK, not per grid: block b of every rank owns the
+// same slice of the message, so block b only waits for block b of its peers
+// (flags[phase][b][rank], written into the PEER's buffer).  Each call has an
+// epoch (host counter, identical on every rank); data areas are double-buffered
+// by epoch parity, which with the per-call handshake guarantees no rank
+// overwrites a slice a slower peer may still be reading.  Every spin is
+// bounded (s_memrealtime, 100 MHz): a dead peer sets the error word and the
+// kernel exits instead of hanging the GPU.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+
+using namespace st;
+
+namespace {
+
+constexpr int kMaxRanks = 8;
+constexpr int kMaxBlocks = 64;
+constexpr int kThreads = 512;
+constexpr int64_t kFlagBytes = 2 * kMaxBlocks * kMaxRanks * 4;  // [phase][block][rank] uint32
+constexpr int64_t kHeader = 4096;                               // flags padded to 4 KiB
+
+struct Peers {
+  char* buf[kMaxRanks];
+};
+
+// What one rank contributes; a launch normally carries one job (gridDim.y = 1).
+// The in-process simulation launches every rank's job as blockIdx.y of ONE grid,
+// so all simulated ranks are co-resident by construction.
+struct Job {
+  const void* in;
+  void* out;
+  int rank;
+  int* err;
+};
+struct Jobs {
+  Job j[kMaxRanks];
+};
+
+ST_DEVICE uint32_t* flag_ptr(char* base, int phase, int block, int rank) {
+  return reinterpret_cast<uint32_t*>(base) + ((phase * kMaxBlocks + block) * kMaxRanks + rank);
+}
+
+// Per-block cross-rank barrier: tell every peer "my block b reached phase p of
+// epoch e", then wait until every peer told me the same.  Returns false on timeout.
+ST_DEVICE bool block_barrier(const Peers& P, int rank, int world, int phase, uint32_t epoch, int* err) {
+  // Every wave retires its own data stores first: __syncthreads() is only a
+  // workgroup-scope fence and does NOT wait for global stores to complete, and the
+  // flag thread's system release below only covers its own wave's stores.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  bool ok = true;
+  if (threadIdx.x < (unsigned)world) {
+    __threadfence_system();
+    __hip_atomic_store(flag_ptr(P.buf[threadIdx.x], phase, blockIdx.x, rank), epoch, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* mine = flag_ptr(P.buf[rank], phase, blockIdx.x, threadIdx.x);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
+        atomicExch(err, 1);
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  // every wave acquires (invalidates its CU's vector L1 / non-coherent L2 lines)
+  // before reading what the peers published
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  return ok;
+}
+
+// ---- shared-area access: 16 B per lane through a buffer descriptor with the
+// system-coherence bits (sc0 sc1) on EVERY load and store, so no XCD's L2 (and
+// no CU's L1) serves or keeps a stale copy of another rank's bytes -- neither
+// within one GPU (XCD L2s are not coherent with each other) nor across xGMI.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr int kSys = 1 | 16;  // cache policy: sc0 | sc1
+
+ST_DEVICE rsrc_t buf_rsrc(const char* base, int64_t cap) {
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)(uint32_t)(kHeader + 4 * cap), 0x00020000);
+}
+ST_DEVICE u32x4 sh_load(rsrc_t rs, uint32_t off) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kSys));
+}
+ST_DEVICE void sh_store(rsrc_t rs, uint32_t off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, off, 0, kSys);
+}
+// byte offset of 8-element vector v of area (which, parity)
+template <typename T>
+ST_DEVICE uint32_t area_off(int which, int parity, int64_t cap, int64_t v) {
+  return (uint32_t)(kHeader + (int64_t)(which * 2 + parity) * cap + v * 8 * (int64_t)sizeof(T));
+}
+
+// 8 elements <-> fp32 (T = bf16: one 16-B vector; T = fp32: two)
+template <typename T>
+ST_DEVICE void sh_load8(rsrc_t rs, uint32_t off, float (&f)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const u32x4 v = sh_load(rs, off);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[2 * i] = __uint_as_float(v[i] << 16);
+      f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+    }
+  } else {
+    const u32x4 a = sh_load(rs, off), b = sh_load(rs, off + 16);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[i] = __uint_as_float(a[i]);
+      f[4 + i] = __uint_as_float(b[i]);
+    }
+  }
+}
+template <typename T>
+ST_DEVICE void sh_store8(rsrc_t rs, uint32_t off, const float (&f)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    u32x4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = pack_bf16x2(f[2 * i], f[2 * i + 1]);
+    sh_store(rs, off, v);
+  } else {
+    u32x4 a, b;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[i] = __float_as_uint(f[i]);
+      b[i] = __float_as_uint(f[4 + i]);
+    }
+    sh_store(rs, off, a);
+    sh_store(rs, off + 16, b);
+  }
+}
+// plain local tensor -> shared area (raw bytes)
+template <typename T>
+ST_DEVICE void put8(rsrc_t rs, uint32_t off, const T* src) {
+  const u32x4* p = reinterpret_cast<const u32x4*>(src);
+  sh_store(rs, off, p[0]);
+  if constexpr (sizeof(T) == 4) sh_store(rs, off + 16, p[1]);
+}
+// shared area -> plain local tensor (raw bytes)
+template <typename T>
+ST_DEVICE void get8(rsrc_t rs, uint32_t off, T* dst) {
+  u32x4* p = reinterpret_cast<u32x4*>(dst);
+  p[0] = sh_load(rs, off);
+  if constexpr (sizeof(T) == 4) p[1] = sh_load(rs, off + 16);
+}
+template <typename T>
+ST_DEVICE void store_local8(T* p, const float (&f)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    *reinterpret_cast<BF8*>(p) = pack8(f);
+  } else {
+    reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+  }
+}
+
+// n8: number of 8-element vectors.  One-shot: block b owns vectors [lo, hi).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void oneshot_kernel(Peers P, Jobs J, int world, int64_t n8, int64_t cap,
+                                                           uint32_t epoch) {
+  const Job& jb = J.j[blockIdx.y];
+  const int rank = jb.rank;
+  const T* __restrict__ in = (const T*)jb.in;
+  T* __restrict__ out = (T*)jb.out;
+  int* err = jb.err;
+  const int parity = epoch & 1;
+  const int64_t per = (n8 + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = blockIdx.x * per, hi = min(n8, lo + per);
+  const rsrc_t mine = buf_rsrc(P.buf[rank], cap);
+  for (int64_t v = lo + threadIdx.x; v < hi; v += blockDim.x) put8<T>(mine, area_off<T>(0, parity, cap, v), in + v * 8);
+  if (!block_barrier(P, rank, world, 0, epoch, err)) return;
+  for (int64_t v = lo + threadIdx.x; v < hi; v += blockDim.x) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < world; ++r) {  // fixed rank order: bitwise identical on every rank
+      float f[8];
+      sh_load8<T>(buf_rsrc(P.buf[r], cap), area_off<T>(0, parity, cap, v), f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += f[i];
+    }
+    store_local8<T>(out + v * 8, acc);
+  }
+}
+
+// Two-shot: partition p = vectors [p*P8, (p+1)*P8); block b owns slice b of every partition.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void twoshot_kernel(Peers P, Jobs J, int world, int64_t n8, int64_t cap,
+                                                           uint32_t epoch) {
+  const Job& jb = J.j[blockIdx.y];
+  const int rank = jb.rank;
+  const T* __restrict__ in = (const T*)jb.in;
+  T* __restrict__ out = (T*)jb.out;
+  int* err = jb.err;
+  const int parity = epoch & 1;
+  const int64_t P8 = (n8 + world - 1) / world;
+  const int64_t per = (P8 + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = blockIdx.x * per, hi = min(P8, lo + per);
+  const rsrc_t mine = buf_rsrc(P.buf[rank], cap);
+  for (int p = 0; p < world; ++p) {
+    const int64_t e = min(n8, (p + 1) * P8);
+    for (int64_t v = p * P8 + lo + threadIdx.x; v < min(e, p * P8 + hi); v += blockDim.x)
+      put8<T>(mine, area_off<T>(0, parity, cap, v), in + v * 8);
+  }
+  if (!block_barrier(P, rank, world, 0, epoch, err)) return;
+  // reduce-scatter: my partition, my slice
+  const int64_t pe = min(n8, (rank + 1) * P8);
+  for (int64_t v = rank * P8 + lo + threadIdx.x; v < min(pe, rank * P8 + hi); v += blockDim.x) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < world; ++r) {
+      float f[8];
+      sh_load8<T>(buf_rsrc(P.buf[r], cap), area_off<T>(0, parity, cap, v), f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += f[i];
+    }
+    sh_store8<T>(mine, area_off<T>(1, parity, cap, v), acc);
+  }
+  if (!block_barrier(P, rank, world, 1, epoch, err)) return;
+  // all-gather: partition p from rank p's result area
+  for (int p = 0; p < world; ++p) {
+    const rsrc_t src = buf_rsrc(P.buf[p], cap);
+    const int64_t e = min(n8, (p + 1) * P8);
+    for (int64_t v = p * P8 + lo + threadIdx.x; v < min(e, p * P8 + hi); v += blockDim.x)
+      get8<T>(src, area_off<T>(1, parity, cap, v), out + v * 8);
+  }
+}
+
+struct Comm {
+  int rank = 0, world = 1;
+  int64_t cap = 0;  // bytes per data area
+  char* local = nullptr;
+  Peers peers{};
+  bool opened[kMaxRanks] = {};
+  int* err = nullptr;
+  uint32_t epoch = 0;
+  int device = 0;
+};
+
+std::mutex g_mu;
+std::vector<Comm*> g_comms;
+
+Comm* get(int64_t id) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (id < 0 || id >= (int64_t)g_comms.size()) return nullptr;
+  return g_comms[id];
+}
+
+}  // namespace
+
+extern "C" {
+
+int st_xgmi_header_bytes() { return (int)kHeader; }
+int st_xgmi_max_ranks() { return kMaxRanks; }
+
+// Allocate this rank's shared buffer (header + 4 data areas of `cap` bytes) on
+// the current device; returns an id >= 0 or a negative hip error.
+// `epoch_base`: first epoch - 1.  Must be identical on every rank of the group and
+// larger than any epoch an earlier communicator reached, so a flag word left over
+// at a reused address (or seen through a stale cache line) can never satisfy a
+// new communicator's wait (dist/xgmi.py passes (creation serial) << 24).
+int64_t st_xgmi_create(int rank, int world, int64_t cap, int64_t epoch_base) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || cap <= 0 || cap % 256) return -2;
+  if (kHeader + 4 * cap >= ((int64_t)1 << 32)) return -2;  // 32-bit buffer offsets
+  Comm* c = new Comm();
+  c->rank = rank;
+  c->world = world;
+  c->cap = cap;
+  c->epoch = (uint32_t)epoch_base;
+  (void)hipGetDevice(&c->device);
+  const int64_t bytes = kHeader + 4 * cap;
+  hipError_t e = hipMalloc((void**)&c->local, bytes);
+  if (e != hipSuccess) {
+    delete c;
+    return -(int64_t)e;
+  }
+  (void)hipMemset(c->local, 0xff, kHeader + 4 * cap);  // data areas poisoned (NaN): a stale read cannot pass
+  (void)hipMemset(c->local, 0, kHeader);
+  (void)hipDeviceSynchronize();
+  hipMalloc((void**)&c->err, sizeof(int));
+  hipMemset(c->err, 0, sizeof(int));
+  hipDeviceSynchronize();
+  c->peers.buf[rank] = c->local;
+  c->opened[rank] = false;
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_comms.push_back(c);
+  return (int64_t)g_comms.size() - 1;
+}
+
+// 64-byte IPC handle of this rank's buffer.
+int st_xgmi_handle(int64_t id, void* out64) {
+  Comm* c = get(id);
+  if (!c) return -2;
+  hipIpcMemHandle_t h;
+  hipError_t e = hipIpcGetMemHandle(&h, c->local);
+  if (e != hipSuccess) return (int)e;
+  static_assert(sizeof(h) <= 64, "ipc handle size");
+  std::memset(out64, 0, 64);
+  std::memcpy(out64, &h, sizeof(h));
+  return 0;
+}
+
+// Map peer r's buffer from its IPC handle (not for r == own rank).
+int st_xgmi_open(int64_t id, int r, const void* handle64) {
+  Comm* c = get(id);
+  if (!c || r < 0 || r >= c->world || r == c->rank) return -2;
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle64, sizeof(h));
+  void* p = nullptr;
+  hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+  if (e != hipSuccess) return (int)e;
+  c->peers.buf[r] = (char*)p;
+  c->opened[r] = true;
+  return 0;
+}
+
+// Same-process wiring (tests / single-process multi-stream simulation): peer r's
+// buffer is comm `peer_id`'s local buffer.
+int st_xgmi_set_peer(int64_t id, int r, int64_t peer_id) {
+  Comm* c = get(id);
+  Comm* p = get(peer_id);
+  if (!c || !p || r < 0 || r >= c->world) return -2;
+  c->peers.buf[r] = p->local;
+  return 0;
+}
+
+static int launch(const Peers& P, const Jobs& J, int njobs, int world, int64_t n, int64_t cap, int dtype,
+                  int mode, int blocks, uint32_t epoch, hipStream_t st) {
+  const int64_t n8 = n / 8;
+  const dim3 grid(blocks, njobs);
+  if (dtype == 0) {
+    if (mode == 0) oneshot_kernel<bf16_t><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch);
+    else twoshot_kernel<bf16_t><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch);
+  } else {
+    if (mode == 0) oneshot_kernel<float><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch);
+    else twoshot_kernel<float><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch);
+  }
+  return (int)hipGetLastError();
+}
+
+// In-place-or-not all-reduce of n elements (dtype 0 = bf16, 1 = fp32); mode 0 =
+// one-shot, 1 = two-shot.  n must be a multiple of 8 and n * elt <= cap.
+int st_xgmi_all_reduce(int64_t id, const void* in, void* out, int64_t n, int dtype, int mode, int blocks,
+                       hipStream_t st) {
+  Comm* c = get(id);
+  if (!c) return -2;
+  const int64_t elt = dtype == 0 ? 2 : 4;
+  if (n % 8 || n * elt > c->cap || ((uintptr_t)in | (uintptr_t)out) % 16) return -2;
+  for (int r = 0; r < c->world; ++r)
+    if (!c->peers.buf[r]) return -3;
+  if (n == 0) return 0;
+  if (blocks <= 0 || blocks > kMaxBlocks) blocks = kMaxBlocks;
+  Jobs J{};
+  J.j[0] = Job{in, out, c->rank, c->err};
+  return launch(c->peers, J, 1, c->world, n, c->cap, dtype, mode, blocks, ++c->epoch, st);
+}
+
+// Simulation: comms ids[0..world) (wired with st_xgmi_set_peer, one process)
+// all-reduce ins[r] -> outs[r] in ONE launch (rank r = blockIdx.y).
+int st_xgmi_all_reduce_sim(const int64_t* ids, const void* const* ins, void* const* outs, int world, int64_t n,
+                           int dtype, int mode, int blocks, hipStream_t st) {
+  if (world < 1 || world > kMaxRanks) return -2;
+  Jobs J{};
+  Comm* c0 = get(ids[0]);
+  if (!c0 || c0->world != world) return -2;
+  const int64_t elt = dtype == 0 ? 2 : 4;
+  if (n % 8 || n * elt > c0->cap) return -2;
+  if (blocks <= 0 || blocks > kMaxBlocks) blocks = kMaxBlocks;
+  uint32_t epoch = 0;
+  for (int r = 0; r < world; ++r) {
+    Comm* c = get(ids[r]);
+    if (!c || c->rank != r || c->world != world || c->cap != c0->cap) return -2;
+    if (((uintptr_t)ins[r] | (uintptr_t)outs[r]) % 16) return -2;
+    J.j[r] = Job{ins[r], outs[r], r, c->err};
+    epoch = ++c->epoch;  // every comm advances together
+  }
+  if (n == 0) return 0;
+  return launch(c0->peers, J, world, world, n, c0->cap, dtype, mode, blocks, epoch, st);
+}
+
+// 1 if any kernel of this comm timed out waiting for a peer (host sync).
+int st_xgmi_error(int64_t id) {
+  Comm* c = get(id);
+  if (!c) return -2;
+  int v = 0;
+  hipMemcpy(&v, c->err, sizeof(int), hipMemcpyDeviceToHost);
+  return v;
+}
+
+int st_xgmi_destroy(int64_t id) {
+  Comm* c = get(id);
+  if (!c) return -2;
+  hipDeviceSynchronize();
+  for (int r = 0; r < c->world; ++r)
+    if (c->opened[r]) hipIpcCloseMemHandle(c->peers.buf[r]);
+  hipFree(c->local);
+  hipFree(c->err);
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_comms[id] = nullptr;
+  delete c;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,129 @@
+"""Intra-node custom all-reduce over xGMI peer memory (csrc/xgmi_allreduce.hip).
+
+The reference sends every tensor-parallel all-reduce through NCCL/HCCL
+(scaletorch/parallel/tensor_parallel/tp_comms.py:117-166, :229-320; SURVEY.md
+§2.2 "custom transport").  On one MI355X node every GPU has a direct xGMI link to
+each of the others, so a TP group can all-reduce by READING its peers' buffers:
+
+* each rank allocates one IPC-shareable buffer (accessed with system-coherent
+  loads/stores only); the 64-byte IPC
+  handles are exchanged once over the process group and every rank maps the
+  others (``hipIpcOpenMemHandle``);
+* ``all_reduce(t)``: one-shot (copy in, per-block cross-rank flag handshake, sum
+  the slice from all W buffers) for messages up to ``oneshot_max`` bytes,
+  two-shot (reduce-scatter into a result area, handshake, all-gather) above it;
+  fp32 accumulation in a fixed rank order, so every rank gets bitwise the same
+  result; anything that does not fit (size, dtype, alignment) goes to RCCL;
+* every wait is bounded: a peer that never arrives sets an error word
+  (``check()``) instead of hanging the GPU.
+
+Use: ``XgmiAllReduce(group)`` collectively on every rank of ``group`` (all ranks
+on ONE node, one GPU each), then ``comm.all_reduce(t)`` in the same order on all
+ranks.  ``tensor_parallel.set_tp_comm("xgmi")`` routes the TP all-reduces here.
+"""
+from __future__ import annotations
+
+import socket
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _lib
+
+
+def _ops():
+    if not _lib.load():
+        raise RuntimeError(f"xgmi all-reduce needs the HIP kernel library: {_lib.load_error()}")
+    return _lib.ops()
+
+
+def _blocks_for(nbytes: int) -> int:
+    """Workgroups per rank: ~64 KiB of message per block, 8..64 blocks."""
+    return int(min(64, max(8, nbytes // (64 << 10))))
+
+
+class XgmiAllReduce:
+    """Custom all-reduce for one process group whose ranks share a node."""
+
+    # communicators created so far in this process; creation is collective, so the
+    # count (-> epoch base) is identical on every rank of a group
+    _serial = 0
+
+    @classmethod
+    def _next_base(cls) -> int:
+        cls._serial += 1
+        return (cls._serial % 255) << 24
+
+    def __init__(self, group=None, max_bytes: int = 64 << 20, oneshot_max: int = 512 << 10, _sim=None):
+        self.group = group
+        self.oneshot_max = oneshot_max
+        self.cap = (max_bytes + 255) // 256 * 256
+        if _sim is not None:  # in-process simulation (tests): (rank, world, epoch base)
+            self.rank, self.world, base = _sim
+            self.id = int(_ops().xgmi_create(self.rank, self.world, self.cap, base))
+            return
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if self.world > 8:
+            raise ValueError("xgmi all-reduce spans at most the 8 GPUs of one node")
+        where = [None] * self.world
+        dist.all_gather_object(where, (socket.gethostname(), torch.cuda.current_device()), group=group)
+        if len({h for h, _ in where}) != 1 or len({d for _, d in where}) != self.world:
+            raise ValueError(f"xgmi all-reduce needs one GPU per rank on one node, got {where}")
+        self.id = int(_ops().xgmi_create(self.rank, self.world, self.cap, self._next_base()))
+        mine = _ops().xgmi_handle(self.id).tolist()
+        handles = [None] * self.world
+        dist.all_gather_object(handles, mine, group=group)
+        for r, h in enumerate(handles):
+            if r != self.rank:
+                _ops().xgmi_open(self.id, r, torch.tensor(h, dtype=torch.uint8))
+        dist.barrier(group=group)
+
+    @classmethod
+    def simulate(cls, world: int, max_bytes: int = 8 << 20, oneshot_max: int = 512 << 10):
+        """``world`` communicators in THIS process wired to each other's buffers
+        (one GPU), for tests: ``all_reduce_sim`` runs every rank's job in ONE launch
+        (rank = blockIdx.y), exercising the kernels and the cross-rank flag protocol
+        without IPC.  (Separate streams per simulated rank are not enough: HIP maps
+        a process's streams onto a few shared hardware queues, and two spinning
+        kernels on one queue serialise.)"""
+        base = cls._next_base()
+        comms = [cls(max_bytes=max_bytes, oneshot_max=oneshot_max, _sim=(r, world, base)) for r in range(world)]
+        for c in comms:
+            for r, p in enumerate(comms):
+                _ops().xgmi_set_peer(c.id, r, p.id)
+        return comms
+
+    def supports(self, t: torch.Tensor) -> bool:
+        return (t.is_cuda and t.dtype in (torch.bfloat16, torch.float32) and t.is_contiguous()
+                and t.numel() % 8 == 0 and t.numel() * t.element_size() <= self.cap
+                and t.data_ptr() % 16 == 0)
+
+    def all_reduce(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Sum of ``t`` over the group into ``out`` (default: in place)."""
+        out = t if out is None else out
+        if not self.supports(t):
+            if out is not t:
+                out.copy_(t)
+            dist.all_reduce(out, group=self.group)
+            return out
+        nbytes = t.numel() * t.element_size()
+        mode = 0 if nbytes <= self.oneshot_max else 1
+        _ops().xgmi_all_reduce(self.id, t, out, mode, _blocks_for(nbytes))
+        return out
+
+    @staticmethod
+    def all_reduce_sim(comms, ins, outs) -> None:
+        nbytes = ins[0].numel() * ins[0].element_size()
+        mode = 0 if nbytes <= comms[0].oneshot_max else 1
+        _ops().xgmi_all_reduce_sim([c.id for c in comms], ins, outs, mode, _blocks_for(nbytes))
+
+    def check(self) -> None:
+        """Raise if any all-reduce of this communicator timed out (host sync)."""
+        if int(_ops().xgmi_error(self.id)):
+            raise RuntimeError("xgmi all-reduce: a peer did not arrive within 2 s (rank died or call order differs)")
+
+    def close(self) -> None:
+        if getattr(self, "id", None) is not None:
+            _ops().xgmi_destroy(self.id)
+            self.id = None

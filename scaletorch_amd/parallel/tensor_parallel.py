@@ -39,6 +39,56 @@ def _ws(group) -> int:
     return C.get_world_size(group)
 
 
+# TP all-reduce transport: "rccl" (default) or "xgmi" (dist/xgmi.py: one-shot /
+# two-shot over IPC-mapped peer buffers; falls back to RCCL for messages it
+# does not take).  One communicator per TP group, created on first use.
+_TP_COMM = "rccl"
+_XGMI: dict = {}
+_XGMI_STREAM: dict = {}
+
+
+def set_tp_comm(kind: str) -> None:
+    global _TP_COMM
+    if kind not in ("rccl", "xgmi"):
+        raise ValueError(f"tp_comm must be rccl or xgmi, got {kind!r}")
+    _TP_COMM = kind
+
+
+class _StreamWork:
+    """Async handle for an all-reduce issued on a side stream."""
+
+    def __init__(self, stream):
+        self.ev = torch.cuda.Event()
+        self.ev.record(stream)
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
+def _tp_all_reduce(x: torch.Tensor, group, async_op: bool = False):
+    """Sum over the TP group; returns a handle with ``wait()`` when ``async_op``."""
+    if _TP_COMM == "xgmi" and x.is_cuda and group is not None:
+        from ..dist.xgmi import XgmiAllReduce
+
+        key = id(group)
+        comm = _XGMI.get(key)
+        if comm is None:
+            comm = _XGMI[key] = XgmiAllReduce(group)
+        if comm.supports(x):
+            if not async_op:
+                comm.all_reduce(x)
+                return None
+            st = _XGMI_STREAM.get(x.device.index)
+            if st is None:
+                st = _XGMI_STREAM[x.device.index] = torch.cuda.Stream(device=x.device)
+            st.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(st):
+                comm.all_reduce(x)
+            x.record_stream(st)
+            return _StreamWork(st)
+    return C.all_reduce(x, group=group, async_op=async_op)
+
+
 class CopyToTensorParallelRegion(torch.autograd.Function):
     """Megatron ``f``: identity forward, all-reduce backward."""
 
@@ -51,7 +101,7 @@ class CopyToTensorParallelRegion(torch.autograd.Function):
     def backward(ctx, g):
         if _ws(ctx.group) > 1:
             g = g.contiguous()
-            C.all_reduce(g, group=ctx.group)
+            _tp_all_reduce(g, ctx.group)
         return g, None
 
 
@@ -63,7 +113,7 @@ class ReduceFromTensorParallelRegion(torch.autograd.Function):
         if _ws(group) == 1:
             return x
         x = x.contiguous()
-        C.all_reduce(x, group=group)
+        _tp_all_reduce(x, group)
         return x
 
     @staticmethod
@@ -202,7 +252,7 @@ class _ColumnParallelFn(torch.autograd.Function):
         dx = dy.matmul(weight)
         handle = None
         if _ws(ctx.group) > 1:
-            handle = C.all_reduce(dx, group=ctx.group, async_op=True)
+            handle = _tp_all_reduce(dx, ctx.group, async_op=True)
         dy2 = dy.reshape(-1, dy.shape[-1])
         dw = accumulate_linear_wgrad(weight, dy2, x.reshape(-1, x.shape[-1])) if ctx.needs_input_grad[1] else None
         db = None

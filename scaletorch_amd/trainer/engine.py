@@ -53,6 +53,10 @@ class Trainer:
                 from ..dist import debug
 
                 debug.enable(timeout_s=a.timeout_s)
+        if a.tensor_parallel_size > 1:
+            from ..parallel.tensor_parallel import set_tp_comm
+
+            set_tp_comm(a.tp_comm)
         if a.context_parallel_size > 1:
             from ..parallel.context_parallel import set_cp_comm, set_cp_zigzag
 
