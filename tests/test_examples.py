@@ -100,3 +100,29 @@ def test_arena_dp_without_mesh_reduces_over_world():
     got = run_workers(_arena_vs_local, 2, "arena")
     for a, b in zip(ref, got):
         torch.testing.assert_close(b, a)
+
+
+def test_verify_model_tool_tiny_families():
+    """tools/verify_model.py: params == analytic count, loss ~ ln V, finite grads,
+    reference-layout state dict round trip, for every tiny family (CPU)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("verify_model", os.path.join(ROOT, "tools", "verify_model.py"))
+    vm = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(vm)
+    for m in ("tiny-llama", "tiny-qwen3", "tiny-moe", "tiny-mixtral"):
+        r = vm.verify(m, None, "cpu", seq=32)
+        assert r["ok"], r
+
+
+def test_profile_mfu_tool_breakdown():
+    import json
+    import subprocess
+    import sys
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "profile_mfu.py"), "--model", "llama3-8b",
+                        "--json", "--step-ms", "400"], capture_output=True, text=True, timeout=120)
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    # 3 GEMM passes of 2*T*N_matmul each (T = 8192 tokens, 7.5e9 matmul params)
+    assert abs(d["components"]["gemm_fwd"]["tflop"] - 122.96) < 0.5
+    assert 40 < d["mfu_pct"] < 50

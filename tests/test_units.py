@@ -304,3 +304,22 @@ def test_dist_wrappers_world1():
     with pytest.raises(ValueError):
         D.reduce_op("median")
     assert D.get_world_size(D.SINGLE) == 1
+
+
+def test_group_nodes_and_env_helpers():
+    import importlib.util
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("group_nodes", os.path.join(root, "scripts", "group_nodes.py"))
+    gn = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gn)
+    g = gn.group_nodes(["mi-r1-n1", "mi-r1-n2", "mi-r2-n1", "mi-r2-n10"])
+    assert dict(g) == {"mi-r1-n": ["mi-r1-n1", "mi-r1-n2"], "mi-r2-n": ["mi-r2-n1", "mi-r2-n10"]}
+    assert list(gn.group_nodes(list("abc"), size=2).values()) == [["a", "b"], ["c"]]
+    from scaletorch_amd import env
+
+    info = env.get_system_info()
+    assert info["torch"] and "hostname" in info
+    os.environ["ST_TEST_FLAG"] = "yes"
+    assert env.env_flag("ST_TEST_FLAG") and not env.env_flag("ST_TEST_FLAG_UNSET")
