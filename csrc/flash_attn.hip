@@ -182,15 +182,53 @@ ST_DEVICE bfx8 bload_frag(rsrc_t rs, uint32_t off) {
 // instruction writes 1 KiB of LDS lane-linearly, so the XOR swizzle is applied
 // on the SOURCE side -- lane l of a wave fetches the global chunk that belongs
 // at LDS byte (base + 16 l) of the swizzled image.  No staging registers, no
-// ds_write; rows past the descriptor's range land as zeros.  The loads are
-// issued at the top of a step and retired by the end-of-step barrier
-// (__syncthreads waits vmcnt(0)), so they overlap the step's MFMAs.
+// ds_write; rows past the descriptor's range land as zeros.
+// Issued from inline asm (M0 = the wave's LDS base): hipcc cannot prove that
+// the builtin form's LDS write misses the tile being read, so it drained every
+// DMA with `s_waitcnt vmcnt(0)` before the step's first ds_read -- the next
+// tile's load was never overlapped with this step's MFMAs.  Hidden from hipcc,
+// the DMA is retired by hand at the end of the step (dma_barrier).
 ST_DEVICE void lds_dma16(rsrc_t rs, lds_t* dst, uint32_t voff) {
-  // device pass only: in the host pass this target builtin poisons the enclosing
-  // kernel templates and hipcc silently drops their host launch stubs
-#if defined(__HIP_DEVICE_COMPILE__)
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, voff, 0, 0, 0);
-#endif
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved: nothing else in these kernels uses it
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(m0), "v"(voff), "s"(rs)
+               : "memory", "m0");
+#pragma clang diagnostic pop
+}
+
+// 4 bytes per lane (64 floats per wave-instruction): the per-query softmax
+// statistics (lse, delta) of a 64-query block go through the same DMA path, so
+// the loop carries no ordinary global load (hipcc would drain every DMA with
+// vmcnt(0) to wait for it).
+ST_DEVICE void lds_dma4(rsrc_t rs, lds_t* dst, uint32_t voff) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds"
+               :
+               : "s"(m0), "v"(voff), "s"(rs)
+               : "memory", "m0");
+#pragma clang diagnostic pop
+}
+
+ST_DEVICE rsrc_t make_rsrc_f32(const float* base, int n) {
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane((uint32_t)(n > 0 ? n * 4 : 0)),
+                                           0x00020000);
+}
+
+// End of a pipeline step: this wave's LDS-DMA has landed (hipcc does not count
+// the asm DMA, so the wait is explicit), then the workgroup barrier publishes
+// every wave's tile and retires this step's LDS reads.
+ST_DEVICE void dma_barrier() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 }
 
 template <int D, int ROWS>
@@ -286,6 +324,10 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(AttnParams p, bf16_t*
   for (int kk = 0; kk < NKK; ++kk)
     qf[kk] = bload_frag(rq, (uint32_t)my_q * (uint32_t)(p.sqs * 2) + (2 * kk + h) * 16);
 
+  // register fragments resident before the DMA pipeline starts: hipcc's own
+  // vmcnt bookkeeping for these loads otherwise lands inside the loop, where
+  // (the asm DMAs being invisible to it) a small vmcnt would wait for them
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   int nkb, kb_mask;
   key_blocks<BM, BN>(p, q0, true, nkb, kb_mask);
 
@@ -306,7 +348,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(AttnParams p, bf16_t*
     sk.load(rk, smem, 0);
     sv.load(rv, smem + 2 * TB, 0);
   }
-  __syncthreads();
+  dma_barrier();
 
   auto step = [&](auto bufc, int kb) {
     constexpr int BUF = decltype(bufc)::value;
@@ -374,7 +416,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(AttnParams p, bf16_t*
       oacc[dt] = mfma(la.trf(vt, 32, 0, dt), p10, oacc[dt]);
       oacc[dt] = mfma(la.trf(vt, 32, 1, dt), p11, oacc[dt]);
     }
-    __syncthreads();  // also retires this step's LDS-DMA (vmcnt(0))
+    dma_barrier();
   };
   for (int kb = 0; kb < nkb; kb += 2) {
     step(Buf<0>(), kb);
@@ -468,6 +510,10 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
   const int64_t li = ((int64_t)b * p.H + hq) * p.Sq + my_q;
   const float lse2 = my_q < p.Sq ? lse[li] * kLog2e : 0.f;
   const float dlt = my_q < p.Sq ? delta[li] : 0.f;
+  // register fragments resident before the DMA pipeline starts: hipcc's own
+  // vmcnt bookkeeping for these loads otherwise lands inside the loop, where
+  // (the asm DMAs being invisible to it) a small vmcnt would wait for them
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   const float c2 = p.scale * kLog2e;
   const int64_t qg = p.q_offset + my_q;
 
@@ -488,7 +534,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
     sk.load(rk, smem, 0);
     sv.load(rv, smem + 2 * TB, 0);
   }
-  __syncthreads();
+  dma_barrier();
 
   auto step = [&](auto bufc, int kb) {
     constexpr int BUF = decltype(bufc)::value;
@@ -551,7 +597,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
       mfma_acc(dqacc[dt], tk[dt][2], g10);
       mfma_acc(dqacc[dt], tk[dt][3], g11);
     }
-    __syncthreads();  // also retires this step's LDS-DMA (vmcnt(0))
+    dma_barrier();
   };
   for (int kb = 0; kb < nkb; kb += 2) {
     step(Buf<0>(), kb);
@@ -604,6 +650,10 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
     kf[kk] = bload_frag(rk, (uint32_t)my_k * (uint32_t)(p.sks * 2) + (2 * kk + h) * 16);
     vf[kk] = bload_frag(rv, (uint32_t)my_k * (uint32_t)(p.svs * 2) + (2 * kk + h) * 16);
   }
+  // register fragments resident before the DMA pipeline starts: hipcc's own
+  // vmcnt bookkeeping for these loads otherwise lands inside the loop, where
+  // (the asm DMAs being invisible to it) a small vmcnt would wait for them
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   const int64_t kg = p.k_offset + my_k;
   const float c2 = p.scale * kLog2e;
 
@@ -629,27 +679,21 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) dkacc[dt] = dvacc[dt] = zero16();
 
-  float st_v = 0.f;
-  // Q / dO tiles of step (g, qb) DMA'd straight into LDS buffer `buf`; lse / delta into a register
+  // Q / dO tiles of step (g, qb) and the block's lse / delta rows DMA'd straight
+  // into LDS buffer `buf` (rows past Sq land as zeros: their Q / dO rows are zero
+  // too, so P * (dP - delta) vanishes there and they contribute nothing)
   auto issue = [&](int g, int qb, int buf) {
     const int hq = hk * G + g;
     sq.load(make_rsrc(p.q + (int64_t)b * p.sqb + (int64_t)hq * p.sqh, p.Sq, p.sqs, D), smem + buf * TB, qb * BQ);
     sd.load(make_rsrc(dout + (int64_t)b * sdb + (int64_t)hq * sdh, p.Sq, sds, D), smem + (2 + buf) * TB, qb * BQ);
     if (wid < 2) {
-      const int qi = qb * BQ + lane;
       const int64_t row = ((int64_t)b * p.H + hq) * p.Sq;
-      if (wid == 0) st_v = qi < p.Sq ? lse[row + qi] * kLog2e : INFINITY;
-      else st_v = qi < p.Sq ? delta[row + qi] : 0.f;
+      lds_dma4(make_rsrc_f32((wid == 0 ? lse : delta) + row, p.Sq),
+               (lds_t*)(stats + buf * 2 * BQ + wid * BQ), (uint32_t)((qb * BQ + lane) * 4));
     }
   };
-  auto commit = [&](int buf) {
-    if (wid < 2) stats[buf * 2 * BQ + wid * BQ + lane] = st_v;
-  };
-  if (total > 0) {
-    issue(0, qb0, 0);
-    commit(0);
-  }
-  __syncthreads();
+  if (total > 0) issue(0, qb0, 0);
+  dma_barrier();
 
   int g_c = 0, qb_c = qb0;
   auto step = [&](auto bufc, int it) {
@@ -702,7 +746,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
           const int rowo = 32 * u + 8 * gq + 4 * h;
-          const f32x4 L = *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * rowo);
+          const f32x4 L = *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * rowo) * kLog2e;
           const f32x4 Dl =
               *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * (BQ + rowo));
 #pragma unroll
@@ -742,8 +786,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
         mfma_acc(dkacc[dt], tk[gi][1], gf[u][1]);
       }
     }
-    if (more) commit(BUF ^ 1);
-    __syncthreads();
+    dma_barrier();
     g_c = g_n;
     qb_c = qb_n;
   };

@@ -19,10 +19,11 @@ run() {  # name timeout cmd...
 }
 has() { [[ " $STAGES " == *" $1 "* ]]; }
 rc_ok() { [ "$1" -eq 0 ]; }
-if has kernels; then run pytest_kernels 600 python -m pytest tests/test_kernels_gpu.py -x -q -m gpu; rc=$?; rc_ok $rc || exit $rc; fi
+if has kernels; then run pytest_kernels 600 python -m pytest tests/test_kernels_gpu.py tests/test_xgmi_gpu.py -x -q -m gpu; rc=$?; rc_ok $rc || exit $rc; fi
 if has train; then HIP_LAUNCH_BLOCKING=1 run pytest_train 400 python -m pytest tests/test_train_gpu.py -x -q -m gpu; rc=$?; rc_ok $rc || exit $rc; fi
 if has smoke; then run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; [ $rc -eq 0 ] || exit $rc; fi
 if has bench; then run bench 900 python bench.py --gpus 1 --steps "$STEPS" --warmup "$WARMUP" ${BENCH_ARGS:-}; rc=$?; [ $rc -eq 0 ] || exit $rc; fi
+if has opt; then run optimize_mfu 900 python tools/optimize_mfu.py --rounds 3 --steps 3; rc=$?; [ $rc -eq 0 ] || exit $rc; fi
 if has prof; then
   export TMPDIR=/tmp
   run rocprof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
