@@ -66,6 +66,13 @@ int st_xgmi_all_reduce_sim(const int64_t* ids, const void* const* ins, void* con
                            int dtype, int mode, int blocks, hipStream_t st);
 int st_xgmi_error(int64_t id);
 int st_xgmi_destroy(int64_t id);
+int st_qknorm_rope_bwd_blocks();
+int st_qknorm_rope_fwd(void* qkv, void* xsave, float* rstd, const void* wq, const void* wk, const float* cos_t,
+                       const float* sin_t, const int64_t* pos, int64_t N, int S, int H, int Hkv, int D, float eps,
+                       int64_t max_pos, hipStream_t st);
+int st_qknorm_rope_bwd(void* dqkv, const void* xsave, const float* rstd, const void* wq, const void* wk,
+                       const float* cos_t, const float* sin_t, const int64_t* pos, int64_t N, int S, int H, int Hkv,
+                       int D, int64_t max_pos, float* partial, float* dw_out, hipStream_t st);
 int st_lse_merge(float* out, float* lse, const void* bout, const float* blse, int B, int S, int H,
                  int D, int64_t sbb, int64_t sbs, int64_t sbh, hipStream_t st);
 }
@@ -345,6 +352,71 @@ void xgmi_all_reduce_sim(std::vector<int64_t> ids, std::vector<at::Tensor> ins, 
 int64_t xgmi_error(int64_t id) { return st_xgmi_error(id); }
 void xgmi_destroy(int64_t id) { st_xgmi_destroy(id); }
 
+// ---------------------------------------------------------------- fused QK-norm + RoPE
+// qkv [B, S, H + 2 Hkv, D] contiguous bf16, modified in place (q, k heads).
+static void check_qknorm_args(const at::Tensor& qkv, const at::Tensor& wq, const at::Tensor& wk,
+                              const at::Tensor& cos, const at::Tensor& sin, const c10::optional<at::Tensor>& pos,
+                              int64_t H, int64_t Hkv) {
+  check_bf16_cuda(qkv, "qkv");
+  check_bf16_cuda(wq, "q_norm.weight");
+  check_bf16_cuda(wk, "k_norm.weight");
+  TORCH_CHECK(qkv.dim() == 4 && qkv.is_contiguous() && qkv.size(2) == H + 2 * Hkv, "qknorm_rope: qkv [B,S,H+2Hkv,D]");
+  const int64_t D = qkv.size(3);
+  TORCH_CHECK(D == 64 || D == 128, "qknorm_rope: head_dim 64 or 128");
+  TORCH_CHECK(wq.numel() == D && wk.numel() == D && wq.is_contiguous() && wk.is_contiguous(), "qknorm_rope: weights [D]");
+  TORCH_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat && cos.is_contiguous() &&
+                  sin.is_contiguous() && cos.dim() == 2 && cos.size(1) == D / 2 && sin.sizes() == cos.sizes(),
+              "qknorm_rope: fp32 cos/sin [max_pos, D/2]");
+  check_same_gpu(wq, qkv, "q_norm.weight");
+  check_same_gpu(wk, qkv, "k_norm.weight");
+  check_same_gpu(cos, qkv, "cos");
+  check_same_gpu(sin, qkv, "sin");
+  if (pos.has_value() && pos->defined()) {
+    TORCH_CHECK(pos->scalar_type() == at::kLong && pos->is_contiguous() &&
+                    pos->numel() == qkv.size(0) * qkv.size(1), "qknorm_rope: position ids int64 [B,S]");
+    check_same_gpu(*pos, qkv, "position_ids");
+  }
+}
+
+std::vector<at::Tensor> qknorm_rope_fwd_(at::Tensor qkv, const at::Tensor& wq, const at::Tensor& wk,
+                                         const at::Tensor& cos, const at::Tensor& sin,
+                                         const c10::optional<at::Tensor>& pos, int64_t H, int64_t Hkv, double eps) {
+  check_qknorm_args(qkv, wq, wk, cos, sin, pos, H, Hkv);
+  const int64_t B = qkv.size(0), S = qkv.size(1), D = qkv.size(3);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  auto xsave = at::empty({B * S, H + Hkv, D}, qkv.options());
+  auto rstd = at::empty({B * S, H + Hkv}, qkv.options().dtype(at::kFloat));
+  const int64_t* pp = (pos.has_value() && pos->defined()) ? pos->data_ptr<int64_t>() : nullptr;
+  int rc = st_qknorm_rope_fwd(qkv.data_ptr(), xsave.data_ptr(), rstd.data_ptr<float>(), wq.data_ptr(), wk.data_ptr(),
+                              cos.data_ptr<float>(), sin.data_ptr<float>(), pp, B * S, (int)S, (int)H, (int)Hkv,
+                              (int)D, (float)eps, cos.size(0), cur_stream());
+  ST_CHECK_RC(rc, "qknorm_rope_fwd_");
+  return {xsave, rstd};
+}
+
+// returns dw [2, D] fp32 (q-norm, k-norm weight gradients); dqkv modified in place
+at::Tensor qknorm_rope_bwd_(at::Tensor dqkv, const at::Tensor& xsave, const at::Tensor& rstd, const at::Tensor& wq,
+                            const at::Tensor& wk, const at::Tensor& cos, const at::Tensor& sin,
+                            const c10::optional<at::Tensor>& pos, int64_t H, int64_t Hkv) {
+  check_qknorm_args(dqkv, wq, wk, cos, sin, pos, H, Hkv);
+  const int64_t B = dqkv.size(0), S = dqkv.size(1), D = dqkv.size(3);
+  check_bf16_cuda(xsave, "xsave");
+  check_same_gpu(xsave, dqkv, "xsave");
+  check_same_gpu(rstd, dqkv, "rstd");
+  TORCH_CHECK(xsave.is_contiguous() && xsave.numel() == B * S * (H + Hkv) * D, "qknorm_rope_bwd: xsave shape");
+  TORCH_CHECK(rstd.is_contiguous() && rstd.scalar_type() == at::kFloat && rstd.numel() == B * S * (H + Hkv),
+              "qknorm_rope_bwd: rstd shape");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dqkv.device());
+  auto dw = at::zeros({2, D}, dqkv.options().dtype(at::kFloat));
+  auto partial = at::empty({(int64_t)st_qknorm_rope_bwd_blocks() * 2 * D}, dqkv.options().dtype(at::kFloat));
+  const int64_t* pp = (pos.has_value() && pos->defined()) ? pos->data_ptr<int64_t>() : nullptr;
+  int rc = st_qknorm_rope_bwd(dqkv.data_ptr(), xsave.data_ptr(), rstd.data_ptr<float>(), wq.data_ptr(), wk.data_ptr(),
+                              cos.data_ptr<float>(), sin.data_ptr<float>(), pp, B * S, (int)S, (int)H, (int)Hkv,
+                              (int)D, cos.size(0), partial.data_ptr<float>(), dw.data_ptr<float>(), cur_stream());
+  ST_CHECK_RC(rc, "qknorm_rope_bwd_");
+  return dw;
+}
+
 // ---------------------------------------------------------------- cross-entropy
 std::vector<at::Tensor> xent_fwd(const at::Tensor& logits, const at::Tensor& tgt,
                                  int64_t vocab_start) {
@@ -522,6 +594,8 @@ TORCH_LIBRARY(st_amd, m) {
         &xgmi_all_reduce_sim);
   m.def("xgmi_error(int id) -> int", &xgmi_error);
   m.def("xgmi_destroy(int id) -> ()", &xgmi_destroy);
+  m.def("qknorm_rope_fwd_(Tensor(a!) qkv, Tensor wq, Tensor wk, Tensor cos, Tensor sin, Tensor? pos, int H, int Hkv, float eps) -> Tensor[]");
+  m.def("qknorm_rope_bwd_(Tensor(a!) dqkv, Tensor xsave, Tensor rstd, Tensor wq, Tensor wk, Tensor cos, Tensor sin, Tensor? pos, int H, int Hkv) -> Tensor");
   m.def("lse_merge_(Tensor(a!) out, Tensor(b!) lse, Tensor block_out, Tensor block_lse) -> ()");
 }
 
@@ -539,4 +613,6 @@ TORCH_LIBRARY_IMPL(st_amd, CUDA, m) {
   m.impl("flash_bwd", &flash_bwd);
   m.impl("lse_merge_", &lse_merge_);
   m.impl("wgrad_gemm_", &wgrad_gemm_);
+  m.impl("qknorm_rope_fwd_", &qknorm_rope_fwd_);
+  m.impl("qknorm_rope_bwd_", &qknorm_rope_bwd_);
 }

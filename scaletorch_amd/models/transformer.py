@@ -18,6 +18,7 @@ pass ``(x, residual)`` pairs, so no standalone elementwise add kernel runs.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -65,6 +66,12 @@ class Attention(nn.Module):
         qkv = self.qkv_proj(x)
         B, S = qkv.shape[0], qkv.shape[1]
         H, Hkv, D = self.H, self.Hkv, self.D
+        if self.qk_norm and mesh.cp_size() == 1 and os.environ.get("ST_FUSED_QKNORM", "1") == "1":
+            # Qwen3: per-head QK-norm + RoPE fused in place on the QKV buffer (csrc/qknorm_rope.hip)
+            out = ops.qknorm_rope_attention(qkv, self.q_norm.weight, self.k_norm.weight, self.q_norm.eps, cos, sin,
+                                            position_ids, H, Hkv, D, causal=True, scale=self.scale)
+            if out is not None:
+                return self.out_proj(out)
         if self.qk_norm:
             q, k, v = qkv.view(B, S, H + 2 * Hkv, D).split([H, Hkv, Hkv], dim=2)
             q = self.q_norm(q.contiguous())

@@ -23,6 +23,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
+from .grad import accumulate_grad
 
 
 # ---------------------------------------------------------------- RoPE tables
@@ -247,6 +248,57 @@ class _RopeAttnFn(torch.autograd.Function):
                       dqkv[:, :, :H], dqkv[:, :, H: H + Hkv], dqkv[:, :, H + Hkv:])
         ops.rope_(dqkv[:, :, : H + Hkv], cos, sin, pos if has_pos else None, 0, True)
         return dqkv.view(B, S, -1), None, None, None, None, None, None, None, None
+
+
+class _QKNormRopeAttnFn(torch.autograd.Function):
+    """Qwen3 attention core: per-head q/k RMSNorm + RoPE fused in place on the QKV
+    buffer (csrc/qknorm_rope.hip), then flash attention; backward: flash backward,
+    then the fused inverse-RoPE + RMSNorm backward on dQ / dK with the two weight
+    gradients reduced on device."""
+
+    @staticmethod
+    def forward(ctx, qkv, wq, wk, cos, sin, pos, H, Hkv, D, causal, scale, eps):
+        B, S = qkv.shape[0], qkv.shape[1]
+        qkv4 = qkv.view(B, S, H + 2 * Hkv, D)
+        ops = _lib.ops()
+        xsave, rstd = ops.qknorm_rope_fwd_(qkv4, wq, wk, cos, sin, pos, H, Hkv, eps)
+        q, k, v = qkv4[:, :, :H], qkv4[:, :, H: H + Hkv], qkv4[:, :, H + Hkv:]
+        out, lse = ops.flash_fwd(q, k, v, scale, causal, 0, 0)
+        ctx.save_for_backward(qkv4, out, lse, xsave, rstd, cos, sin, pos if pos is not None else torch.empty(0))
+        ctx.wq, ctx.wk = wq, wk
+        ctx.meta = (H, Hkv, D, causal, scale, pos is not None)
+        return out.view(B, S, H * D)
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv4, out, lse, xsave, rstd, cos, sin, pos = ctx.saved_tensors
+        H, Hkv, D, causal, scale, has_pos = ctx.meta
+        B, S = qkv4.shape[0], qkv4.shape[1]
+        ops = _lib.ops()
+        dqkv = torch.empty_like(qkv4)
+        q, k, v = qkv4[:, :, :H], qkv4[:, :, H: H + Hkv], qkv4[:, :, H + Hkv:]
+        ops.flash_bwd(dout.view(B, S, H, D).contiguous(), q, k, v, out, lse, scale, causal, 0, 0,
+                      dqkv[:, :, :H], dqkv[:, :, H: H + Hkv], dqkv[:, :, H + Hkv:])
+        dw = ops.qknorm_rope_bwd_(dqkv, xsave, rstd, ctx.wq, ctx.wk, cos, sin, pos if has_pos else None, H, Hkv)
+        gq = accumulate_grad(ctx.wq, dw[0]) if ctx.needs_input_grad[1] else None
+        gk = accumulate_grad(ctx.wk, dw[1]) if ctx.needs_input_grad[2] else None
+        return dqkv.view(B, S, -1), gq, gk, None, None, None, None, None, None, None, None, None
+
+
+def qknorm_rope_attention(qkv: torch.Tensor, q_weight: torch.Tensor, k_weight: torch.Tensor, eps: float,
+                          cos: torch.Tensor, sin: torch.Tensor, pos: torch.Tensor | None, n_heads: int,
+                          n_kv_heads: int, head_dim: int, causal: bool = True,
+                          scale: float | None = None) -> torch.Tensor | None:
+    """Fused Qwen3 QK-norm + RoPE + attention on qkv [B, S, (H + 2 Hkv) D]; None when
+    the HIP path does not apply (caller runs the unfused modules)."""
+    if not (_lib.use_native(qkv) and qkv.dtype == torch.bfloat16 and head_dim in (64, 128)
+            and q_weight.dtype == torch.bfloat16 and k_weight.dtype == torch.bfloat16):
+        return None
+    scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
+    if pos is not None:
+        pos = pos.contiguous()
+    return _QKNormRopeAttnFn.apply(qkv.contiguous(), q_weight, k_weight, cos, sin, pos, n_heads, n_kv_heads,
+                                   head_dim, causal, scale, eps)
 
 
 def rope_attention(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos: torch.Tensor | None,

@@ -198,7 +198,8 @@ class GradArena:
         b.launched = True
         self.zero_fresh(b.params)
         if self.world == 1:
-            self._bucket_sumsq(b)
+            if not dist.is_initialized() or dist.get_world_size() == 1:
+                self._bucket_sumsq(b)  # only consumed when no TP/PP/EP peer shares the norm
             return
         g = self.grad_flat[b.start: b.end]
         nccl = dist.get_backend(self.group) == "nccl"

@@ -329,3 +329,37 @@ def test_wgrad_gemm_unsupported_shape_declines():
     out = torch.zeros(200, 192, device="cuda")
     assert not _lib.ops().wgrad_gemm_(out, dy, x, 0)
     assert out.abs().sum().item() == 0
+
+
+@pytest.mark.parametrize("D,with_pos", [(128, False), (128, True), (64, True)])
+def test_qknorm_rope_attention_matches_unfused(D, with_pos):
+    """Fused per-head QK-norm + RoPE + flash attention (csrc/qknorm_rope.hip) vs the
+    fp32 reference chain (RMSNorm per head -> RoPE -> SDPA): output, dQKV and both
+    norm-weight gradients."""
+    from scaletorch_amd.ops.attention import apply_rope_ref, rope_tables, sdpa_ref
+    from scaletorch_amd.ops.norm import rms_norm_ref
+
+    torch.manual_seed(0)
+    B, S, H, Hkv = 2, 192, 4, 2
+    qkv = torch.randn(B, S, (H + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16) * 2
+    wq = torch.nn.Parameter(1 + 0.3 * torch.randn(D, device="cuda", dtype=torch.bfloat16))
+    wk = torch.nn.Parameter(1 + 0.3 * torch.randn(D, device="cuda", dtype=torch.bfloat16))
+    cos, sin = rope_tables(1024, D, 10000.0, device="cuda")
+    pos = (torch.randperm(1024, device="cuda")[:S].sort().values.expand(B, S).contiguous() if with_pos else None)
+    x = qkv.clone().requires_grad_(True)
+    out = ops.qknorm_rope_attention(x, wq, wk, 1e-6, cos, sin, pos, H, Hkv, D)
+    g = torch.randn_like(out)
+    out.backward(g)
+    # fp32 reference
+    xr = qkv.float().clone().requires_grad_(True)
+    wqr, wkr = wq.detach().float().requires_grad_(True), wk.detach().float().requires_grad_(True)
+    x4 = xr.view(B, S, H + 2 * Hkv, D)
+    q = rms_norm_ref(x4[:, :, :H], wqr, 1e-6)
+    k = rms_norm_ref(x4[:, :, H: H + Hkv], wkr, 1e-6)
+    q = apply_rope_ref(q, cos, sin, pos)
+    k = apply_rope_ref(k, cos, sin, pos)
+    ref = sdpa_ref(q, k, x4[:, :, H + Hkv:], True, 1.0 / math.sqrt(D))[0].reshape(B, S, H * D)
+    ref.backward(g.float())
+    assert rel(out, ref) < 2e-2
+    assert rel(x.grad, xr.grad) < 3e-2
+    assert rel(wq.grad, wqr.grad) < 3e-2 and rel(wk.grad, wkr.grad) < 3e-2
