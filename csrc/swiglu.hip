@@ -11,69 +11,109 @@ using namespace st;
 
 namespace {
 
+// 2-D mapping: blockIdx.y walks rows (no 64-bit division per element), each lane
+// owns U 16-byte column vectors 256 apart so U loads per operand are in flight
+// before the first use (the grid-stride one-vector loop held only one).
+template <int U>
 __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16_t* __restrict__ gu,
                                                           bf16_t* __restrict__ out, int64_t I8,
-                                                          int64_t total) {
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t row = t / I8, c = t - row * I8;
-    const bf16_t* gp = gu + row * (I8 * 16) + c * 8;
-    float g[8], u[8], o[8];
-    unpack8(ld8(gp), g);
-    unpack8(ld8(gp + I8 * 8), u);
+                                                          int64_t N) {
+  const int64_t c0 = (int64_t)blockIdx.x * (256 * U) + threadIdx.x;
+  for (int64_t row = blockIdx.y; row < N; row += gridDim.y) {
+    const bf16_t* gp = gu + row * (I8 * 16);
+    BF8 rg[U], ru[U];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = silu(g[i]) * u[i];
-    st8(out + row * (I8 * 8) + c * 8, pack8(o));
+    for (int u = 0; u < U; ++u) {
+      const int64_t c = c0 + u * 256;
+      if (c < I8) {
+        rg[u] = ld8(gp + c * 8);
+        ru[u] = ld8(gp + I8 * 8 + c * 8);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t c = c0 + u * 256;
+      if (c < I8) {
+        float g[8], v[8], o[8];
+        unpack8(rg[u], g);
+        unpack8(ru[u], v);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = silu(g[i]) * v[i];
+        st8(out + row * (I8 * 8) + c * 8, pack8(o));
+      }
+    }
   }
 }
 
+template <int U>
 __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restrict__ dout,
                                                           const bf16_t* __restrict__ gu,
                                                           bf16_t* __restrict__ dgu, int64_t I8,
-                                                          int64_t total) {
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t row = t / I8, c = t - row * I8;
-    const int64_t off = row * (I8 * 16) + c * 8;
-    float g[8], u[8], d[8], dg[8], du[8];
-    unpack8(ld8(gu + off), g);
-    unpack8(ld8(gu + off + I8 * 8), u);
-    unpack8(ld8(dout + row * (I8 * 8) + c * 8), d);
+                                                          int64_t N) {
+  const int64_t c0 = (int64_t)blockIdx.x * (256 * U) + threadIdx.x;
+  for (int64_t row = blockIdx.y; row < N; row += gridDim.y) {
+    const int64_t base = row * (I8 * 16);
+    BF8 rg[U], ru[U], rd[U];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float sg = 1.f / (1.f + __expf(-g[i]));
-      const float sl = g[i] * sg;
-      du[i] = d[i] * sl;
-      dg[i] = d[i] * u[i] * (sg + sl * (1.f - sg));
+    for (int u = 0; u < U; ++u) {
+      const int64_t c = c0 + u * 256;
+      if (c < I8) {
+        rg[u] = ld8(gu + base + c * 8);
+        ru[u] = ld8(gu + base + I8 * 8 + c * 8);
+        rd[u] = ld8(dout + row * (I8 * 8) + c * 8);
+      }
     }
-    st8(dgu + off, pack8(dg));
-    st8(dgu + off + I8 * 8, pack8(du));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t c = c0 + u * 256;
+      if (c < I8) {
+        float g[8], v[8], d[8], dg[8], du[8];
+        unpack8(rg[u], g);
+        unpack8(ru[u], v);
+        unpack8(rd[u], d);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float sg = 1.f / (1.f + __expf(-g[i]));
+          const float sl = g[i] * sg;
+          du[i] = d[i] * sl;
+          dg[i] = d[i] * v[i] * (sg + sl * (1.f - sg));
+        }
+        st8(dgu + base + c * 8, pack8(dg));
+        st8(dgu + base + I8 * 8 + c * 8, pack8(du));
+      }
+    }
   }
 }
 
-inline unsigned grid_for(int64_t total) {
-  int64_t b = (total + 255) / 256;
-  if (b > 8192) b = 8192;
-  if (b < 1) b = 1;
-  return (unsigned)b;
+inline dim3 grid_for(int64_t I8, int64_t N, int U) {
+  const int64_t gx = (I8 + 256 * U - 1) / (256 * U);
+  const int64_t gy = N < 65535 ? N : 65535;
+  return dim3((unsigned)gx, (unsigned)gy);
 }
 
 }  // namespace
 
 extern "C" int st_swiglu_fwd(const void* gu, void* out, int64_t N, int64_t I, hipStream_t st) {
   if (I % 8 != 0) return -2;
-  const int64_t total = N * (I / 8);
-  if (total == 0) return 0;
-  swiglu_fwd_kernel<<<grid_for(total), 256, 0, st>>>((const bf16_t*)gu, (bf16_t*)out, I / 8, total);
+  const int64_t I8 = I / 8;
+  if (N == 0 || I8 == 0) return 0;
+  if (I8 >= 1024)
+    swiglu_fwd_kernel<2><<<grid_for(I8, N, 2), 256, 0, st>>>((const bf16_t*)gu, (bf16_t*)out, I8, N);
+  else
+    swiglu_fwd_kernel<1><<<grid_for(I8, N, 1), 256, 0, st>>>((const bf16_t*)gu, (bf16_t*)out, I8, N);
   return (int)hipGetLastError();
 }
 
 extern "C" int st_swiglu_bwd(const void* dout, const void* gu, void* dgu, int64_t N, int64_t I,
                              hipStream_t st) {
   if (I % 8 != 0) return -2;
-  const int64_t total = N * (I / 8);
-  if (total == 0) return 0;
-  swiglu_bwd_kernel<<<grid_for(total), 256, 0, st>>>((const bf16_t*)dout, (const bf16_t*)gu,
-                                                     (bf16_t*)dgu, I / 8, total);
+  const int64_t I8 = I / 8;
+  if (N == 0 || I8 == 0) return 0;
+  if (I8 >= 1024)
+    swiglu_bwd_kernel<2><<<grid_for(I8, N, 2), 256, 0, st>>>((const bf16_t*)dout, (const bf16_t*)gu,
+                                                              (bf16_t*)dgu, I8, N);
+  else
+    swiglu_bwd_kernel<1><<<grid_for(I8, N, 1), 256, 0, st>>>((const bf16_t*)dout, (const bf16_t*)gu,
+                                                              (bf16_t*)dgu, I8, N);
   return (int)hipGetLastError();
 }

@@ -81,9 +81,10 @@ def test_host_pointer_rejected_before_launch():
         _lib.ops().xent_fwd(torch.randn(4, 64, device="cuda", dtype=torch.bfloat16), torch.zeros(4, dtype=torch.long), 0)
 
 
-def test_swiglu():
+@pytest.mark.parametrize("I", [384, 8 * 1100])  # one-vector and two-vector-per-lane paths, ragged tail
+def test_swiglu(I):
     torch.manual_seed(0)
-    gu = torch.randn(5, 33, 2 * 384, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    gu = torch.randn(5, 33, 2 * I, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     y = ops.swiglu(gu)
     g = torch.randn_like(y)
     (y.float() * g.float()).sum().backward()
