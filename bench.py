@@ -8,6 +8,11 @@ fwd+bwd).  Weak scaling: every GPU processes
 ``--micro_batch_size x --seq_len`` tokens per micro-batch; N GPUs = DP=N
 (override the layout with --tp/--pp/--cp/--ep).
 
+Default micro-batch is 4 x 4096 tokens: the step is sized for 288 GB of HBM3E
+(226.5 GB peak at DP=1, less under ZeRO-1).  Measured on one MI355X
+(profiles/micro_batch_sweep_1gpu.log): mbs 2 -> 20.9k tok/s, mbs 4 -> 22.5k,
+mbs 6 -> 23.1k at 267 GB (too close to capacity to be the default).
+
 Usage:
   python bench.py --gpus 1 --steps 10 --warmup 3
   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8 --steps 10 --warmup 3
@@ -34,7 +39,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="llama3-8b")
-    ap.add_argument("--micro_batch_size", type=int, default=2)
+    ap.add_argument("--micro_batch_size", type=int, default=4)
     ap.add_argument("--seq_len", type=int, default=4096)
     ap.add_argument("--grad_acc", type=int, default=1)
     ap.add_argument("--tp", type=int, default=1)
