@@ -12,8 +12,10 @@
 //     the new residual stream and normalised from the rounded value, so the
 //     fused path is bit-compatible with the unfused bf16 graph;
 //   * backward recomputes xhat from s and rstd (fp32, saved by forward), emits
-//     ds (+ an optional incoming residual-stream gradient) and per-wave fp32
+//     ds (+ an optional incoming residual-stream gradient) and per-block fp32
 //     partial sums of dy*xhat that a second pass reduces into dweight.
+#include <cstdlib>
+
 #include "common.h"
 
 using namespace st;
@@ -70,8 +72,10 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
 }
 
 // grid-stride over rows; each wave accumulates its dweight partial in
-// registers and writes it once to partial[wave_global, h].  The row operands
-// are kept packed (bf16) in registers to bound VGPR use at h = 8192.
+// registers; the 4 waves of a block fold them through LDS in a fixed order
+// (3->1, 2->0, then 1->0: deterministic) and wave 0 writes one row of
+// partial[block, h].  The row operands are kept packed (bf16) in registers to
+// bound VGPR use at h = 8192.  Dynamic LDS: 2 * h fp32.
 template <int NCH, bool DRES>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s, const bf16_t* __restrict__ w,
@@ -93,17 +97,21 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
   for (int row = gw; row < rows; row += nw) {
     const size_t base = (size_t)row * h;
     const float rs = rstd[row];
-    BF8 sp[NCH], dp[NCH];
+    BF8 sp[NCH], dp[NCH], rp[DRES ? NCH : 1];
     float dot = 0.f;
+    // every operand of the row (incl. the residual-stream gradient) is issued
+    // before the reduction, so a wave has 2-3 x NCH 16-byte loads in flight
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = c * 512 + lane * 8;
       if (col < h) {
         sp[c] = ld8(s + base + col);
         dp[c] = ld8(dy + base + col);
+        if (DRES) rp[DRES ? c : 0] = ld8(dres + base + col);
       } else {
         sp[c] = BF8{{0u, 0u, 0u, 0u}};
         dp[c] = BF8{{0u, 0u, 0u, 0u}};
+        if (DRES) rp[DRES ? c : 0] = BF8{{0u, 0u, 0u, 0u}};
       }
     }
 #pragma unroll
@@ -132,7 +140,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
         for (int i = 0; i < 8; ++i) o[i] = rs * (dv[i] * wf[i] - sv[i] * rs * dot);
         if (DRES) {
           float r[8];
-          unpack8(ld8(dres + base + col), r);
+          unpack8(rp[DRES ? c : 0], r);
 #pragma unroll
           for (int i = 0; i < 8; ++i) o[i] += r[i];
         }
@@ -140,13 +148,56 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
       }
     }
   }
-  float* pr = partial + (size_t)gw * h;
+  extern __shared__ float red_lds[];  // [2][h]
+  const int wid = threadIdx.x >> 6;
+  // step 1: waves 2,3 park their partials; waves 0,1 add them
+  if (wid >= 2) {
+    float* dst = red_lds + (size_t)(wid - 2) * h;
 #pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int col = c * 512 + lane * 8;
-    if (col < h) {
-      st4f(pr + col, make_float4(dwp[c][0], dwp[c][1], dwp[c][2], dwp[c][3]));
-      st4f(pr + col + 4, make_float4(dwp[c][4], dwp[c][5], dwp[c][6], dwp[c][7]));
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < h) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dst[col + i] = dwp[c][i];
+      }
+    }
+  }
+  __syncthreads();
+  if (wid < 2) {
+    const float* src = red_lds + (size_t)wid * h;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < h) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dwp[c][i] += src[col + i];
+      }
+    }
+  }
+  __syncthreads();
+  // step 2: wave 1 parks, wave 0 adds and writes the block's partial row
+  if (wid == 1) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < h) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) red_lds[col + i] = dwp[c][i];
+      }
+    }
+  }
+  __syncthreads();
+  if (wid == 0) {
+    float* pr = partial + (size_t)blockIdx.x * h;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < h) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dwp[c][i] += red_lds[col + i];
+        st4f(pr + col, make_float4(dwp[c][0], dwp[c][1], dwp[c][2], dwp[c][3]));
+        st4f(pr + col + 4, make_float4(dwp[c][4], dwp[c][5], dwp[c][6], dwp[c][7]));
+      }
     }
   }
 }
@@ -207,11 +258,12 @@ int launch_fwd(const void* x, const void* res, const void* w, void* y, void* sum
 
 template <bool DRES>
 int launch_bwd(const void* dy, const void* s, const void* w, const float* rstd, const void* dres,
-               void* ds, float* partial, int nwaves, int rows, int h, hipStream_t st) {
+               void* ds, float* partial, int nblocks, int rows, int h, hipStream_t st) {
   const int nch = (h + 511) / 512;
-  dim3 grid(nwaves / kRowsPerBlock), block(256);
+  dim3 grid(nblocks), block(256);
+  const size_t lds = 2 * (size_t)h * sizeof(float);
 #define ST_RMS_BWD(N)                                                                       \
-  rmsnorm_bwd_kernel<N, DRES><<<grid, block, 0, st>>>(                                      \
+  rmsnorm_bwd_kernel<N, DRES><<<grid, block, lds, st>>>(                                    \
       (const bf16_t*)dy, (const bf16_t*)s, (const bf16_t*)w, rstd, (const bf16_t*)dres,     \
       (bf16_t*)ds, partial, rows, h)
   if (nch <= 1) ST_RMS_BWD(1);
@@ -229,12 +281,25 @@ int launch_bwd(const void* dy, const void* s, const void* w, const float* rstd, 
 
 extern "C" {
 
-// Number of waves the backward uses (the partial buffer must hold nwaves*h fp32).
+// Number of dweight partial rows the backward writes (one per block; the
+// partial buffer must hold nwaves*h fp32).  Name kept for the binding.
+// Block cap: enough waves per SIMD across 256 CUs to hide HBM latency; the
+// fp32 partial buffer (blocks x h) that colsum re-reads grows with it.
+// ST_RMSNORM_BWD_BLOCKS overrides it (A/B only).
+static int rmsnorm_bwd_block_cap() {
+  static int cap = [] {
+    const char* e = getenv("ST_RMSNORM_BWD_BLOCKS");
+    int v = e ? atoi(e) : 0;
+    return (v >= 64 && v <= 4096) ? v : 256;
+  }();
+  return cap;
+}
+
 int st_rmsnorm_bwd_nwaves(int rows) {
   int blocks = (rows + kRowsPerBlock - 1) / kRowsPerBlock;
-  if (blocks > 256) blocks = 256;
+  if (blocks > rmsnorm_bwd_block_cap()) blocks = rmsnorm_bwd_block_cap();
   if (blocks < 1) blocks = 1;
-  return blocks * kRowsPerBlock;
+  return blocks;
 }
 
 int st_rmsnorm_fwd(const void* x, const void* res, const void* w, void* y, void* sum_out,
@@ -254,7 +319,10 @@ int st_rmsnorm_bwd(const void* dy, const void* s, const void* w, const float* rs
   int rc = dres ? launch_bwd<true>(dy, s, w, rstd, dres, ds, partial, nw, rows, h, st)
                 : launch_bwd<false>(dy, s, w, rstd, nullptr, ds, partial, nw, rows, h, st);
   if (rc) return rc;
-  const int splits = nw >= 256 ? 16 : 1;
+  // enough (column-group x row-split) blocks to fill the chip: the partial
+  // rows are reduced with 4-wave strided loads, at most 16 rows per wave
+  int splits = 1;
+  while (splits < 64 && nw / splits > 64) splits *= 2;
   dim3 grid((h + 255) / 256, splits);
   colsum_kernel<<<grid, 256, 0, st>>>(partial, dw_out, nw, h, splits);
   return (int)hipGetLastError();
