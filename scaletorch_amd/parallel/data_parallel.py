@@ -383,7 +383,10 @@ class DataParallel(nn.Module):
         dev = params[0].device if params else torch.device("cpu")
         self.side_stream = None
         if dev.type == "cuda" and os.environ.get("ST_OVERLAP_OPT", "1") == "1":
-            self.side_stream = torch.cuda.Stream(device=dev)
+            # ST_SIDE_STREAM_PRIORITY: HIP stream priority of the side stream (0 = default,
+            # -1 = high: its AdamW buckets are dispatched ahead of the forward's kernels)
+            prio = int(os.environ.get("ST_SIDE_STREAM_PRIORITY", "0"))
+            self.side_stream = torch.cuda.Stream(device=dev, priority=prio)
             for a in self.arenas:
                 a.side_stream = self.side_stream
         if self.zero1 or self.side_stream is not None:
