@@ -75,7 +75,8 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
 // registers; the 4 waves of a block fold them through LDS in a fixed order
 // (3->1, 2->0, then 1->0: deterministic) and wave 0 writes one row of
 // partial[block, h].  The row operands are kept packed (bf16) in registers to
-// bound VGPR use at h = 8192.  Dynamic LDS: 2 * h fp32.
+// bound VGPR use at h = 8192.  Dynamic LDS: 2 * NCH * 512 fp32, lane-major
+// (element i of lane L in chunk c at c*512 + i*64 + L: bank-conflict free).
 template <int NCH, bool DRES>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s, const bf16_t* __restrict__ w,
@@ -148,29 +149,30 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
       }
     }
   }
-  extern __shared__ float red_lds[];  // [2][h]
+  extern __shared__ float red_lds[];  // [2][NCH * 512]
+  constexpr int kSlab = NCH * 512;
   const int wid = threadIdx.x >> 6;
   // step 1: waves 2,3 park their partials; waves 0,1 add them
   if (wid >= 2) {
-    float* dst = red_lds + (size_t)(wid - 2) * h;
+    float* dst = red_lds + (wid - 2) * kSlab;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = c * 512 + lane * 8;
       if (col < h) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) dst[col + i] = dwp[c][i];
+        for (int i = 0; i < 8; ++i) dst[c * 512 + i * 64 + lane] = dwp[c][i];
       }
     }
   }
   __syncthreads();
   if (wid < 2) {
-    const float* src = red_lds + (size_t)wid * h;
+    const float* src = red_lds + wid * kSlab;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = c * 512 + lane * 8;
       if (col < h) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) dwp[c][i] += src[col + i];
+        for (int i = 0; i < 8; ++i) dwp[c][i] += src[c * 512 + i * 64 + lane];
       }
     }
   }
@@ -182,7 +184,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
       const int col = c * 512 + lane * 8;
       if (col < h) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) red_lds[col + i] = dwp[c][i];
+        for (int i = 0; i < 8; ++i) red_lds[c * 512 + i * 64 + lane] = dwp[c][i];
       }
     }
   }
@@ -194,7 +196,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
       const int col = c * 512 + lane * 8;
       if (col < h) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) dwp[c][i] += red_lds[col + i];
+        for (int i = 0; i < 8; ++i) dwp[c][i] += red_lds[c * 512 + i * 64 + lane];
         st4f(pr + col, make_float4(dwp[c][0], dwp[c][1], dwp[c][2], dwp[c][3]));
         st4f(pr + col + 4, make_float4(dwp[c][4], dwp[c][5], dwp[c][6], dwp[c][7]));
       }
@@ -261,9 +263,8 @@ int launch_bwd(const void* dy, const void* s, const void* w, const float* rstd, 
                void* ds, float* partial, int nblocks, int rows, int h, hipStream_t st) {
   const int nch = (h + 511) / 512;
   dim3 grid(nblocks), block(256);
-  const size_t lds = 2 * (size_t)h * sizeof(float);
 #define ST_RMS_BWD(N)                                                                       \
-  rmsnorm_bwd_kernel<N, DRES><<<grid, block, lds, st>>>(                                    \
+  rmsnorm_bwd_kernel<N, DRES><<<grid, block, 2 * (N) * 512 * sizeof(float), st>>>(        \
       (const bf16_t*)dy, (const bf16_t*)s, (const bf16_t*)w, rstd, (const bf16_t*)dres,     \
       (bf16_t*)ds, partial, rows, h)
   if (nch <= 1) ST_RMS_BWD(1);
