@@ -1,0 +1,29 @@
+"""bench.py driver contract on CPU: one JSON line from rank 0 with the required keys,
+whole-job tokens/s, world_size 2 over gloo (the same torchrun launch the driver uses)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+            "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def test_bench_json_line_dp2_gloo():
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", "29731", "bench.py", "--gpus", "2",
+           "--steps", "1", "--warmup", "1", "--model", "tiny-llama", "--layers", "2", "--seq_len", "64",
+           "--micro_batch_size", "2", "--backend", "gloo"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 only
+    d = json.loads(lines[0])
+    assert REQUIRED <= set(d)
+    assert d["n_gpus"] == 2 and d["steps"] == 1 and d["warmup"] == 1 and d["scaling"] == "weak"
+    cfg = d["config"]
+    assert cfg["parallelism"] == "dp2" and cfg["global_batch"] == 4 and cfg["seq_len"] == 64
+    # value is the whole-job aggregate: global tokens per step / step time
+    assert abs(d["value"] - 4 * 64 / (d["ms_per_step"] / 1e3)) / d["value"] < 0.02
