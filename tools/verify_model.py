@@ -69,7 +69,7 @@ def verify(name: str, layers: int | None, device: str, seq: int = 128, batch: in
     res = {
         "model": name, "layers": cfg.num_hidden_layers, "device": device, "dtype": str(dtype).split(".")[-1],
         "params_built": n_built, "params_config": n_cfg, "params_match": n_built == n_cfg,
-        "loss": round(float(loss), 4), "ln_vocab": round(lnv, 4), "loss_near_ln_vocab": abs(float(loss) - lnv) < 0.15 * lnv,
+        "loss": round(float(loss.detach()), 4), "ln_vocab": round(lnv, 4), "loss_near_ln_vocab": abs(float(loss.detach()) - lnv) < 0.15 * lnv,
         "aux_loss": None if aux is None else round(float(aux), 5),
         "params_without_grad": no_grad, "non_finite_grads": bad_grad, "zero_grads": zero_grad[:5],
         "reference_names": has_ref_names, "reference_roundtrip": roundtrip,
