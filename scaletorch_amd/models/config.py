@@ -162,7 +162,7 @@ _REGISTRY: dict[str, dict] = {
     "tiny-mixtral": dict(model_type="mixtral", vocab_size=512, hidden_size=256, intermediate_size=256,
                          num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2,
                          max_position_embeddings=1024, rms_norm_eps=1e-5, rope_theta=1000000.0,
-                         num_experts=4, num_experts_per_tok=2),
+                         num_experts=8, num_experts_per_tok=2),
 }
 
 _ALIASES = {

@@ -163,7 +163,7 @@ class MoEExperts(nn.Module):
                 counts = torch.tensor(counts, dtype=torch.int32)
             offs = torch.cumsum(counts.to(device=x.device, dtype=torch.int32), 0, dtype=torch.int32)
             if x.shape[0] == 0:
-                return x.new_zeros(0, self.hidden)
+                return self._empty(x)
             gu = torch._grouped_mm(x.contiguous(), self.w_gate_up.transpose(-2, -1), offs=offs)
             return torch._grouped_mm(ops.swiglu(gu), self.w_down.transpose(-2, -1), offs=offs)
         if isinstance(counts, torch.Tensor):
@@ -178,8 +178,15 @@ class MoEExperts(nn.Module):
             outs.append(torch.matmul(ops.swiglu(gu), self.w_down[e].t()))
             off += n
         if not outs:
-            return x.new_zeros(0, self.hidden)
+            return self._empty(x)
         return torch.cat(outs, 0)
+
+    def _empty(self, x: torch.Tensor) -> torch.Tensor:
+        """No rows routed here: an empty result that stays CONNECTED to the graph
+        (x and the expert weights), so backward still reaches the dispatch
+        all-to-all on this rank -- every EP peer must issue the same collectives."""
+        z = (x.sum() + self.w_gate_up.sum() + self.w_down.sum()) * 0
+        return z.to(x.dtype).expand(0, self.hidden)
 
 
 class MoELayer(nn.Module):

@@ -67,6 +67,12 @@ class Bucket:
         self.opt_event = None  # side-stream optimizer update of this bucket (optim.py overlap)
 
 
+def _is_rccl(group) -> bool:
+    """RCCL (backend "nccl") process group: AVG reductions and in-place
+    reduce-scatter (recv = send + rank * count) are used; gloo gets SUM + divide."""
+    return dist.get_backend(group) == "nccl"
+
+
 def _aligned(n: int) -> int:
     return math.ceil(n / ALIGN) * ALIGN
 
@@ -202,7 +208,7 @@ class GradArena:
                 self._bucket_sumsq(b)  # only consumed when no TP/PP/EP peer shares the norm
             return
         g = self.grad_flat[b.start: b.end]
-        nccl = dist.get_backend(self.group) == "nccl"
+        nccl = _is_rccl(self.group)
         if self.reduce_dtype != g.dtype:
             if b.comm_buf is None or b.comm_buf.numel() != g.numel():
                 b.comm_buf = torch.empty(g.numel(), dtype=self.reduce_dtype, device=g.device)

@@ -82,12 +82,17 @@ class ProcessGroupManager:
         idx = tuple(slice(None) if a in varying else self.coords[a] for a in AXES)
         return self.grid[idx].flatten().tolist()
 
-    def _family(self, varying: tuple[str, ...]):
+    def _family(self, varying: tuple[str, ...], channel: str = "model"):
         """Create (collectively, same order on every rank) the groups of one family.
 
         Trivial families (size 1) get the ``SINGLE`` sentinel instead of a
         communicator -- every collective wrapper treats it as a no-op -- and a
-        family with the same rank lists as an earlier one reuses its groups.
+        family with the same rank lists as an earlier one OF THE SAME CHANNEL
+        reuses its groups.  Channels keep communicators apart whose collectives
+        are issued from different places: the gradient buckets ("grad") fire
+        from post-accumulate hooks whose timing relative to the autograd-driven
+        model collectives (EP all-to-all, TP/CP) may differ across ranks, so
+        they must never share an RCCL communicator (one ordered queue) with them.
         """
         mine = self.my_ranks(varying)
         if len(mine) == 1:
@@ -95,7 +100,7 @@ class ProcessGroupManager:
         if not self._create_groups:
             return None, mine
         lists = self.group_ranks(varying)
-        key = tuple(tuple(x) for x in lists)
+        key = (channel,) + tuple(tuple(x) for x in lists)
         cache = self.__dict__.setdefault("_family_cache", {})
         if key not in cache:
             groups = []
@@ -115,8 +120,8 @@ class ProcessGroupManager:
         self.cp_dp_group, self.cp_dp_group_ids = self._family(("dp", "cp"))
         self.pp_dp_group, self.pp_dp_group_ids = self._family(("dp", "pp"))
         # gradient-reduction groups (EP carved out of DP)
-        self.dense_dp_group, self.dense_dp_group_ids = self._family(("dp", "cp", "ep"))
-        self.expert_dp_group, self.expert_dp_group_ids = self.cp_dp_group, self.cp_dp_group_ids
+        self.dense_dp_group, self.dense_dp_group_ids = self._family(("dp", "cp", "ep"), channel="grad")
+        self.expert_dp_group, self.expert_dp_group_ids = self._family(("dp", "cp"), channel="grad")
         # model-parallel group for global grad-norm (everything but data replicas)
         self.mp_group, self.mp_group_ids = self._family(("pp", "tp", "ep"))
 

@@ -46,17 +46,34 @@ def run_workers(fn, world: int, *args, timeout: float = 240.0) -> list:
     procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q)) for r in range(world)]
     for p in procs:
         p.start()
-    results = {}
+    results, errors = {}, {}
     try:
+        import io
+        import queue
+
+        import torch
+
         for _ in range(world):
-            rank, status, val = q.get(timeout=timeout)
+            try:
+                rank, status, val = q.get(timeout=timeout if not errors else 20)
+            except queue.Empty:
+                if errors:
+                    break
+                raise
             if status == "err":
-                raise RuntimeError(f"rank {rank} failed:\n{val}")
-            import io
-
-            import torch
-
+                errors[rank] = val
+                continue
             results[rank] = torch.load(io.BytesIO(val), weights_only=True)
+        if errors:
+            # the root cause first: peers of a failed rank only see "Connection reset"
+            first = sorted(errors, key=lambda r: ("Connection reset" in errors[r] or "Connection closed" in errors[r], r))
+            dead = [r for r, p in enumerate(procs) if p.exitcode not in (None, 0)]
+            raise RuntimeError(f"rank {first[0]} failed (errors from ranks {sorted(errors)}, "
+                               f"abnormal exits {dead}):\n{errors[first[0]]}")
+        missing = [r for r in range(world) if r not in results]
+        if missing:
+            codes = {r: procs[r].exitcode for r in missing}
+            raise RuntimeError(f"ranks {missing} returned nothing (exit codes {codes})")
     finally:
         for p in procs:
             p.join(timeout=30)
