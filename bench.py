@@ -16,6 +16,11 @@ mbs 6 -> 23.1k at 267 GB (too close to capacity to be the default).
 Usage:
   python bench.py --gpus 1 --steps 10 --warmup 3
   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8 --steps 10 --warmup 3
+  torchrun --nproc-per-node 8 ... bench.py --gpus 8 --layout tp2pp2dp2   # BASELINE.json 8-GPU configs:
+      dp (default) | tp2pp2dp2 | cp8_32k | mixtral_ep8  (explicit flags override a preset)
+
+Every run prints its per-rank HBM estimate (utils/memory.py) to stderr before
+building anything and refuses a layout that would not fit in 288 GB.
 
 Rank 0 prints ONE JSON line; ``value`` = whole-job tokens/s (all GPUs).
 """
@@ -32,21 +37,35 @@ import time
 # real DP/TP work.  vs_baseline compares per-GPU throughput against it.
 BASELINE_TOK_S_PER_GPU = 1391.0
 
+# BASELINE.json's 8-GPU configurations (reference scripts/benchmark_comprehensive.py:54-173
+# layouts).  Sizes are per GPU; the data-parallel width absorbs the rest of the job.
+LAYOUTS = {
+    "dp": dict(),
+    # 3-D: TP inside an xGMI pair, 2 pipeline stages, DP over the rest; 8 micro-batches keep
+    # the 1F1B bubble at (pp-1)/(M+pp-1) = 11 %; sequence parallel shards norm/residual activations
+    "tp2pp2dp2": dict(tp=2, pp=2, sp=True, micro_batch_size=4, grad_acc=8),
+    # long context: 32K tokens over 8 CP ranks (4K local), zig-zag chunks, GQA-sized K/V
+    "cp8_32k": dict(cp=-1, seq_len=32768, micro_batch_size=1),
+    # Mixtral 8x7B: one expert per GPU (EP carved out of DP), dense weights ZeRO-1 over DP x EP
+    "mixtral_ep8": dict(model="mixtral-8x7b", ep=-1, micro_batch_size=2),
+}
+
 
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--model", default="llama3-8b")
-    ap.add_argument("--micro_batch_size", type=int, default=4)
-    ap.add_argument("--seq_len", type=int, default=4096)
-    ap.add_argument("--grad_acc", type=int, default=1)
-    ap.add_argument("--tp", type=int, default=1)
-    ap.add_argument("--pp", type=int, default=1)
-    ap.add_argument("--cp", type=int, default=1)
-    ap.add_argument("--ep", type=int, default=1)
-    ap.add_argument("--sp", action="store_true")
+    ap.add_argument("--layout", default="dp", choices=sorted(LAYOUTS))
+    ap.add_argument("--model", default=None, help="default llama3-8b")
+    ap.add_argument("--micro_batch_size", type=int, default=None, help="default 4")
+    ap.add_argument("--seq_len", type=int, default=None, help="default 4096")
+    ap.add_argument("--grad_acc", type=int, default=None, help="default 1")
+    ap.add_argument("--tp", type=int, default=None)
+    ap.add_argument("--pp", type=int, default=None)
+    ap.add_argument("--cp", type=int, default=None)
+    ap.add_argument("--ep", type=int, default=None)
+    ap.add_argument("--sp", action="store_true", default=None)
     ap.add_argument("--cp_comm", default="allgather", help="allgather | ring | ulysses")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) | gloo (debug rehearsals only)")
     ap.add_argument("--gc", action="store_true", help="activation checkpointing")
@@ -56,6 +75,12 @@ def main() -> int:
                                                          "1: sharded optimizer / reduce-scatter + all-gather)")
     ap.add_argument("--layers", type=int, default=None, help="(debug only; result marked invalid)")
     args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    preset = dict(model="llama3-8b", micro_batch_size=4, seq_len=4096, grad_acc=1, tp=1, pp=1, cp=1, ep=1, sp=False)
+    preset.update({k: (world if v == -1 else v) for k, v in LAYOUTS[args.layout].items()})
+    for k, v in preset.items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
 
     import torch
     import torch.distributed as dist
@@ -65,7 +90,6 @@ def main() -> int:
     from scaletorch_amd.utils.device import get_theoretical_flops
     from scaletorch_amd.utils.misc import flops_per_token
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     mp = args.tp * args.pp * args.cp * args.ep
@@ -73,6 +97,20 @@ def main() -> int:
         raise SystemExit(f"world {world} not divisible by tp*pp*cp*ep={mp}")
     dp = world // mp
     ga = args.grad_acc if args.pp == 1 else max(args.grad_acc, 4 * args.pp)
+    from scaletorch_amd.models import get_model_config
+    from scaletorch_amd.utils.memory import estimate_rank_memory
+
+    mcfg = get_model_config(args.model, num_hidden_layers=args.layers)
+    est = estimate_rank_memory(mcfg, tp=args.tp, pp=args.pp, cp=args.cp, ep=args.ep, dp=dp,
+                               micro_batch=args.micro_batch_size, seq_len=args.seq_len, grad_acc=ga,
+                               zero1=args.zero >= 1 and dp * args.cp * args.ep > 1, sequence_parallel=args.sp,
+                               gradient_checkpointing=args.gc, grad_reduce_dtype=args.grad_reduce_dtype)
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench] layout {args.layout}: {args.model} tp{args.tp} pp{args.pp} cp{args.cp} ep{args.ep} dp{dp} "
+              f"mbs{args.micro_batch_size} ga{ga} seq{args.seq_len}; HBM estimate {est.summary()}",
+              file=sys.stderr, flush=True)
+    if not est.fits():
+        raise SystemExit(f"layout {args.layout} would not fit: {est.summary()}")
     a = ScaleTorchArguments(
         model_name_or_path=args.model, synthetic_data=True, micro_batch_size=args.micro_batch_size,
         sequence_length=args.seq_len, gradient_accumulation_steps=ga, total_train_steps=args.warmup + args.steps,
@@ -121,9 +159,10 @@ def main() -> int:
     mfu = per_gpu * fpt / peak * 100
     par = "".join(f"{k}{v}" for k, v in (("dp", dp), ("tp", args.tp), ("pp", args.pp), ("cp", args.cp),
                                          ("ep", args.ep)) if v > 1 or k == "dp")
-    valid = args.layers is None and args.model == "llama3-8b"
+    valid = args.layers is None
+    names = {"llama3-8b": "Llama-3-8B", "mixtral-8x7b": "Mixtral-8x7B"}
     out = {
-        "metric": "tokens/sec (Llama-3-8B training, full step)",
+        "metric": f"tokens/sec ({names.get(args.model, args.model)} training, full step)",
         "value": round(tok_s, 1),
         "unit": "tokens/s",
         "n_gpus": world,
@@ -137,7 +176,7 @@ def main() -> int:
         "data": "synthetic (random tokens), random-init weights",
         "config": {"model": args.model, "global_batch": dp * args.ep * args.micro_batch_size * ga,
                    "micro_batch": args.micro_batch_size, "grad_accum": ga, "seq_len": args.seq_len,
-                   "parallelism": par, "sequence_parallel": args.sp, "activation_checkpointing": args.gc,
+                   "parallelism": par, "layout": args.layout, "sequence_parallel": args.sp, "activation_checkpointing": args.gc,
                    "grad_reduce_dtype": args.grad_reduce_dtype, "zero_stage": args.zero if dp > 1 else 0},
         "tokens_per_s_per_gpu": round(per_gpu, 1),
         "mfu_pct": round(mfu, 2),

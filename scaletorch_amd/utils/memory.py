@@ -1,0 +1,88 @@
+"""Per-rank HBM estimate for a (model, layout) pair, sized against 288 GB of HBM3E.
+
+Used by ``bench.py --layout`` and ``tools/train.py`` to print what a rank will
+hold before anything is allocated, so an 8-GPU layout that would not fit is
+caught on the host.  The terms follow this framework's storage layout
+(parallel/data_parallel.py, optim.py): bf16 parameters, fp32 ``main_grad``
+arena, fp32 master + Adam m/v (sharded over the reduction group under ZeRO-1),
+and activations calibrated on one MI355X: Llama-3-8B at micro-batch 4 x 4096
+peaked at 226.5 GB (profiles/micro_batch_sweep_1gpu.log), i.e. ~34 bytes per
+hidden element per token per layer once the 144.5 GB of model state and the
+bf16 logits (+ grad) are taken out.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+HBM_GB = 288.0
+_ACT_ATTN = 14  # bytes per (token, layer, hidden element): norms, QKV, attention out, residual
+_ACT_MLP = 20   # gate|up output, SwiGLU output, down input (dense MLP with I = 3.5 h)
+
+
+@dataclass
+class MemoryEstimate:
+    params_gb: float
+    grads_gb: float
+    optimizer_gb: float
+    activations_gb: float
+    logits_gb: float
+    comm_gb: float
+
+    @property
+    def total_gb(self) -> float:
+        return (self.params_gb + self.grads_gb + self.optimizer_gb + self.activations_gb + self.logits_gb
+                + self.comm_gb)
+
+    def fits(self, capacity_gb: float = HBM_GB, headroom_gb: float = 16.0) -> bool:
+        return self.total_gb + headroom_gb <= capacity_gb
+
+    def summary(self) -> str:
+        return (f"{self.total_gb:.1f} GB/rank (params {self.params_gb:.1f}, grads {self.grads_gb:.1f}, "
+                f"optimizer {self.optimizer_gb:.1f}, activations {self.activations_gb:.1f}, "
+                f"logits {self.logits_gb:.1f}, comm buffers {self.comm_gb:.1f}) of {HBM_GB:.0f} GB")
+
+
+def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1, dp: int = 1,
+                         micro_batch: int = 1, seq_len: int = 4096, grad_acc: int = 1, zero1: bool = False,
+                         sequence_parallel: bool = False, gradient_checkpointing: bool = False,
+                         pp_engine: str = "1f1b", grad_reduce_dtype: str = "bf16") -> MemoryEstimate:
+    """Worst-rank estimate (first pipeline stage for activations, largest stage for weights)."""
+    h, d = cfg.hidden_size, cfg.head_dim
+    H, Hkv = cfg.num_attention_heads, cfg.num_key_value_heads
+    L = cfg.num_hidden_layers
+    layers = -(-L // pp)
+    attn = (h * d * (H + 2 * Hkv) + H * d * h) / tp + 2 * h
+    dense, expert = 0.0, 0.0
+    for i in range(layers):
+        dense += attn
+        if cfg.layer_is_moe(i):
+            expert += (cfg.num_experts // ep) * 3 * h * cfg.moe_intermediate_size / tp
+            dense += h * cfg.num_experts
+        else:
+            dense += 3 * h * cfg.intermediate_size / tp
+    emb = cfg.vocab_size * h / tp
+    dense += emb * (1 if pp > 1 or cfg.tie_word_embeddings else 2)  # embedding (+ untied LM head)
+    n = dense + expert
+    dense_dp = dp * cp * ep
+    expert_dp = dp * cp
+    opt = 12 * (dense / (dense_dp if zero1 else 1) + expert / (expert_dp if zero1 else 1))
+    # activations of the micro-batches a rank holds at once
+    tokens = micro_batch * seq_len / cp
+    if pp > 1:
+        tokens *= grad_acc if pp_engine == "afab" else min(pp, grad_acc)
+    if cfg.is_moe:
+        k_eff = cfg.num_experts_per_tok * cfg.moe_intermediate_size / max(1, cfg.intermediate_size)
+    else:
+        k_eff = 1.0
+    per_layer = _ACT_ATTN * h + _ACT_MLP * h * k_eff * cfg.intermediate_size / (3.5 * h)
+    if tp > 1:
+        per_layer = per_layer / tp if sequence_parallel else 8 * h + (per_layer - 8 * h) / tp
+    if gradient_checkpointing:
+        act = tokens * (2 * h * layers) + tokens * per_layer
+    else:
+        act = tokens * per_layer * layers
+    logits = micro_batch * seq_len / cp * cfg.vocab_size / tp * 2 * 2  # bf16 logits + grad (last stage)
+    comm = n * 2 if grad_reduce_dtype in ("bf16", "bfloat16") and dense_dp > 1 else 0.0
+    g = 1e9
+    return MemoryEstimate(params_gb=2 * n / g, grads_gb=4 * n / g, optimizer_gb=opt / g, activations_gb=act / g,
+                          logits_gb=logits / g, comm_gb=comm / g)

@@ -27,3 +27,29 @@ def test_bench_json_line_dp2_gloo():
     assert cfg["parallelism"] == "dp2" and cfg["global_batch"] == 4 and cfg["seq_len"] == 64
     # value is the whole-job aggregate: global tokens per step / step time
     assert abs(d["value"] - 4 * 64 / (d["ms_per_step"] / 1e3)) / d["value"] < 0.02
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("layout,model,extra,par", [
+    ("tp2pp2dp2", "tiny-llama", ["--seq_len", "64", "--micro_batch_size", "1"], "dp2tp2pp2"),
+    ("cp8_32k", "tiny-llama", ["--seq_len", "256"], "dp1cp8"),
+    ("mixtral_ep8", "tiny-mixtral", ["--seq_len", "64", "--micro_batch_size", "1"], "dp1ep8"),
+])
+def test_bench_layout_presets_world8_gloo(layout, model, extra, par):
+    """The 8-GPU layout presets run end to end under an 8-rank torchrun (tiny models on
+    CPU/gloo) and report the whole-job line with the layout's parallelism."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+           "--master-addr", "127.0.0.1", "--master-port", str(29741 + len(layout)), "bench.py", "--gpus", "8",
+           "--steps", "1", "--warmup", "1", "--layout", layout, "--model", model, "--layers", "2",
+           "--backend", "gloo"] + extra
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["config"]["parallelism"] == par and d["config"]["layout"] == layout and d["n_gpus"] == 8
+    assert "HBM estimate" in out.stderr
