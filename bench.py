@@ -177,7 +177,7 @@ def main() -> int:
         "config": {"model": args.model, "global_batch": dp * args.ep * args.micro_batch_size * ga,
                    "micro_batch": args.micro_batch_size, "grad_accum": ga, "seq_len": args.seq_len,
                    "parallelism": par, "layout": args.layout, "sequence_parallel": args.sp, "activation_checkpointing": args.gc,
-                   "grad_reduce_dtype": args.grad_reduce_dtype, "zero_stage": args.zero if dp > 1 else 0},
+                   "grad_reduce_dtype": args.grad_reduce_dtype, "zero_stage": args.zero if dp * args.cp * args.ep > 1 else 0},
         "tokens_per_s_per_gpu": round(per_gpu, 1),
         "mfu_pct": round(mfu, 2),
         "mfu_pct_causal_flops": round(per_gpu * fpt_causal / peak * 100, 2),
