@@ -62,6 +62,27 @@ class Collator:
                 "position_ids": pos, "hidden_states": None}
 
 
+class _ResumableSampler(torch.utils.data.Sampler):
+    """DistributedSampler whose next iteration starts ``skip`` samples into the epoch
+    (resume from a checkpoint mid-epoch without replaying the consumed samples)."""
+
+    def __init__(self, inner: DistributedSampler):
+        self.inner, self.skip = inner, 0
+
+    def __iter__(self):
+        it = iter(self.inner)
+        for _ in range(self.skip):
+            next(it, None)
+        self.skip = 0
+        return it
+
+    def __len__(self) -> int:
+        return len(self.inner)
+
+    def set_epoch(self, epoch: int) -> None:
+        self.inner.set_epoch(epoch)
+
+
 class MicroBatchDataLoader(DataLoader):
     def __init__(self, dataset: Dataset, micro_batch_size: int, seq_len: int, grad_acc_steps: int = 1,
                  data_rank: int = 0, data_world_size: int = 1, cp_rank: int = 0, cp_size: int = 1,
@@ -70,8 +91,8 @@ class MicroBatchDataLoader(DataLoader):
         self.micro_batch_size, self.seq_len = micro_batch_size, seq_len
         self.gradient_accumulation_steps = grad_acc_steps
         self.global_batch_size = micro_batch_size * grad_acc_steps * data_world_size
-        self.sampler_ = DistributedSampler(dataset, num_replicas=data_world_size, rank=data_rank,
-                                           shuffle=shuffle, seed=seed, drop_last=drop_last)
+        self.sampler_ = _ResumableSampler(DistributedSampler(dataset, num_replicas=data_world_size, rank=data_rank,
+                                                             shuffle=shuffle, seed=seed, drop_last=drop_last))
         self.collator = Collator(seq_len, cp_size, cp_rank, zigzag)
         super().__init__(dataset, batch_size=micro_batch_size, sampler=self.sampler_, collate_fn=self.collator,
                          num_workers=num_workers, pin_memory=pin_memory, drop_last=drop_last,
@@ -95,6 +116,12 @@ class MicroBatchDataLoader(DataLoader):
         self.sampler_.set_epoch(epoch)
         self._it = None
 
+    def skip_batches(self, n: int) -> None:
+        """Position the loader after ``n`` consumed micro-batches (checkpoint resume)."""
+        per_epoch = max(1, len(self.sampler_) // self.micro_batch_size)
+        self.set_epoch(n // per_epoch)
+        self.sampler_.skip = (n % per_epoch) * self.micro_batch_size
+
 
 class DeviceSyntheticLoader:
     """Synthetic batches generated directly on the device (benchmarks): no host
@@ -113,6 +140,10 @@ class DeviceSyntheticLoader:
 
     def __iter__(self):
         return self
+
+    def skip_batches(self, n: int) -> None:
+        for _ in range(n):
+            torch.randint(0, self.vocab_size, (self.mbs, self.seq_len + 1), device=self.device, generator=self.gen)
 
     def __next__(self) -> dict:
         ids = torch.randint(0, self.vocab_size, (self.mbs, self.seq_len + 1), device=self.device, generator=self.gen)

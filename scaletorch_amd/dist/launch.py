@@ -125,6 +125,13 @@ def init_dist(launcher: str | None = None, backend: str | None = None, use_cpu: 
                   timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kw["device_id"] = torch.device("cuda", gpu)
+        attempt = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
+        if attempt > 0:
+            # torchrun restart: the agent's store still holds the previous attempt's
+            # rendezvous keys (peer addresses of dead ranks) -> namespace this attempt
+            store, _, _ = next(dist.rendezvous("env://", rank=rank, world_size=world, timeout=kw["timeout"]))
+            kw.pop("init_method")
+            kw["store"] = dist.PrefixStore(f"/scaletorch_amd/attempt_{attempt}/", store)
         dist.init_process_group(**kw)
     return rank, local_rank, world
 

@@ -90,6 +90,7 @@ class MoERouter(nn.Module):
         self.norm_topk_prob, self.aux_coef = norm_topk_prob, aux_coef
         self.init_std = init_std
         self.gate = nn.Linear(hidden, num_experts, bias=False)
+        self._st_reads = (self.gate,)  # forward reads gate.weight directly (DataParallel bucket waits)
         self.reset_parameters()
 
     def reset_parameters(self) -> None:

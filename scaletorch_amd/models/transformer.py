@@ -27,8 +27,7 @@ from torch.utils.checkpoint import checkpoint as torch_checkpoint
 from .. import ops
 from ..parallel import mesh
 from ..parallel.tensor_parallel import (ColumnParallelLinear, FusedColumnParallelLinear, RowParallelLinear,
-                                        ScatterToSequenceParallelRegion, VocabParallelEmbedding,
-                                        AllGatherFromSequenceParallelRegion)
+                                        VocabParallelEmbedding)
 from .config import ModelConfig
 
 
@@ -53,6 +52,9 @@ class Attention(nn.Module):
             self.q_norm = ops.RMSNorm(D, eps=cfg.rms_norm_eps)
             self.k_norm = ops.RMSNorm(D, eps=cfg.rms_norm_eps)
             self.q_norm._per_head = self.k_norm._per_head = True  # grads summed over this rank's heads only
+            # the fused QK-norm+RoPE kernel reads these weights without calling the modules:
+            # DataParallel makes this module's forward wait for their optimizer buckets too
+            self._st_reads = (self.q_norm, self.k_norm)
 
     def reset_parameters(self) -> None:
         self.qkv_proj.reset_parameters()
@@ -245,10 +247,8 @@ class TransformerLM(nn.Module):
         if not self.last_stage:
             return x if residual is None else x + residual
         x = self.final_norm(x) if residual is None else self.final_norm(x, residual)[0]
-        if self.sequence_parallel:
-            x = AllGatherFromSequenceParallelRegion.apply(x, mesh.tp_group())
-            from ..ops.mlp import linear
-            return linear(x, self.final_proj.weight)
+        # a module call (SP: gather along seq inside the column-parallel fn), so the head's
+        # forward pre-hook orders it after the weight's optimizer update / ZeRO-1 gather
         return self.final_proj(x)
 
     # ------------------------------------------------------------------ checkpoints in reference layout

@@ -67,6 +67,18 @@ class _ArenaOptimizer(torch.optim.Optimizer):
             master = a.master[so: so + n] if a.master is not None else a.param_flat[lo:hi]
             yield (a.param_flat[lo:hi], a.grad_flat[lo:hi], master) + tuple(s[so: so + n] for s in states)
 
+    @torch.no_grad()
+    def reload_masters(self) -> None:
+        """Re-read the fp32 master copy from the (externally overwritten) bf16 params,
+        e.g. after an HF weight import into a model whose optimizer already exists."""
+        self.sync()
+        for a in self.arenas:
+            if a.master is None:
+                continue
+            a.wait_params()
+            for lo, hi, so in a.segments():
+                a.master[so: so + hi - lo].copy_(a.param_flat[lo:hi])
+
     def _finish_step(self) -> None:
         for a in self.arenas:
             a.gather_params()

@@ -428,15 +428,38 @@ class DataParallel(nn.Module):
                     a.wait_bucket(i)
             return hook
 
+        self.wait_cover = {}
         for m in self.module.modules():
-            needs = sorted({where[id(p)] for p in m.parameters(recurse=False) if id(p) in where},
+            params = list(m.parameters(recurse=False))
+            # weights a module's forward reads without calling their owner (fused kernels)
+            for sub in getattr(m, "_st_reads", ()):
+                params += list(sub.parameters())
+            needs = sorted({where[id(p)] for p in params if id(p) in where},
                            key=lambda t: (id(t[0]), t[1]))
             if needs:
                 m.register_forward_pre_hook(make_hook(needs))
+                self.wait_cover[m] = {id(p) for p in params}
 
     def gather_params(self) -> None:
         for a in self.arenas:
             a.gather_params()
+
+    def uncovered_params(self, run_forward) -> list[str]:
+        """Debug check: names of trainable parameters NOT covered by the bucket wait of
+        any module whose forward actually ran in ``run_forward()`` -- such a weight
+        could be read before its (side-stream / ZeRO-1) update lands."""
+        if not hasattr(self, "wait_cover"):
+            self._install_param_waits()
+        called = []
+        hook = nn.modules.module.register_module_forward_pre_hook(lambda m, _i: called.append(m))
+        try:
+            run_forward()
+        finally:
+            hook.remove()
+        covered = set()
+        for m in called:
+            covered |= self.wait_cover.get(m, set())
+        return [n for n, p in self.module.named_parameters() if p.requires_grad and id(p) not in covered]
 
     def wait_params(self) -> None:
         for a in self.arenas:

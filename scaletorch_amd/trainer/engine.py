@@ -190,6 +190,26 @@ class Trainer:
         self.trained_tokens += self.tokens_per_step
         return loss
 
+    def resume(self, ckpt_manager, path: str) -> None:
+        """Load a checkpoint on EVERY rank or fail on every rank: a rank that could not
+        load (missing shard, bad file) must not continue from step 0 while its peers
+        resume at step N (different LR schedule / step counts -> hang or divergence).
+        The data loaders are advanced past the consumed micro-batches."""
+        ok, err = 1, None
+        try:
+            self.step, self.trained_tokens = ckpt_manager.load_checkpoint(self.model, self.optimizer, path,
+                                                                          self.lr_scheduler)
+        except (FileNotFoundError, KeyError, ValueError, RuntimeError) as e:
+            ok, err = 0, e
+        flag = torch.tensor([ok], dtype=torch.int32, device=self.device if C.get_world_size() > 1 else "cpu")
+        if C.get_world_size() > 1:
+            C.all_reduce(flag, op="min")
+        if int(flag.item()) != 1:
+            raise RuntimeError(f"resume from {path} failed on at least one rank"
+                               + (f" (this rank: {err})" if err is not None else ""))
+        if self.data is not None and hasattr(self.data, "skip_batches"):
+            self.data.skip_batches(self.step * self.args.gradient_accumulation_steps)
+
     def reduced_loss(self, loss: torch.Tensor) -> float:
         """Mean loss over data-parallel replicas (last PP stage holds it); host sync."""
         pg = mesh.pgm

@@ -59,11 +59,28 @@ def _to_cpu(obj):
     return obj
 
 
+_DONE = "complete_rank_world_size={}_{}"
+
+
+def is_complete(step_dir: str) -> bool:
+    """Every rank of the job that wrote ``step_dir`` finished its files: each rank
+    drops ``complete_rank_world_size={r}_{W}`` after its own writes (incl. ZeRO-1
+    optimizer shards); a directory from a crash mid-save lacks some markers."""
+    marks = glob.glob(os.path.join(step_dir, "complete_rank_world_size=*"))
+    if not marks:
+        return False
+    worlds = {m.rsplit("_", 1)[-1] for m in marks}
+    if len(worlds) != 1:
+        return False
+    return len(marks) == int(worlds.pop())
+
+
 def latest_checkpoint(work_dir: str) -> str | None:
+    """Newest COMPLETE step directory under ``work_dir`` (auto-resume)."""
     steps = []
     for d in glob.glob(os.path.join(work_dir, "*")):
         b = os.path.basename(d)
-        if b.isdigit() and glob.glob(os.path.join(d, "weights_*.pth")):
+        if b.isdigit() and glob.glob(os.path.join(d, "weights_*.pth")) and is_complete(d):
             steps.append(int(b))
     return os.path.join(work_dir, str(max(steps))) if steps else None
 
@@ -98,24 +115,26 @@ class CheckpointManager:
             writes.append((path, payload))
         if sharded:  # ZeRO-1: every rank owns a distinct optimizer shard
             writes.append((os.path.join(out_dir, _shard_filename()), _to_cpu(optimizer.state_dict())))
-        if writes:
-            os.makedirs(out_dir, exist_ok=True)
-            sched = _to_cpu(lr_scheduler.state_dict()) if (lr_scheduler is not None and writer) else None
-            self.wait()
+        os.makedirs(out_dir, exist_ok=True)
+        sched = _to_cpu(lr_scheduler.state_dict()) if (lr_scheduler is not None and writer) else None
+        self.wait()
+        done = os.path.join(out_dir, _DONE.format(C.get_rank(), C.get_world_size()))
 
-            def _write():
-                for pth, obj in writes:
-                    tmp = pth + ".tmp"
-                    torch.save(obj, tmp, _use_new_zipfile_serialization=True)
-                    os.replace(tmp, pth)
-                if sched is not None and tp == 0 and pp == 0 and ep == 0:
-                    torch.save(sched, os.path.join(out_dir, "scheduler.pt"))
+        def _write():
+            for pth, obj in writes:
+                tmp = pth + ".tmp"
+                torch.save(obj, tmp, _use_new_zipfile_serialization=True)
+                os.replace(tmp, pth)
+            if sched is not None and tp == 0 and pp == 0 and ep == 0:
+                torch.save(sched, os.path.join(out_dir, "scheduler.pt"))
+            with open(done, "w") as f:  # last: this rank's part of the step directory is on disk
+                f.write("ok\n")
 
-            if self.async_save:
-                self._thread = threading.Thread(target=_write, daemon=False)
-                self._thread.start()
-            else:
-                _write()
+        if self.async_save:
+            self._thread = threading.Thread(target=_write, daemon=False)
+            self._thread.start()
+        else:
+            _write()
         return path
 
     def load_checkpoint(self, model, optimizer, resume_path: str, lr_scheduler=None, strict: bool = True):
@@ -185,10 +204,13 @@ def _tp_slice(name: str, t: torch.Tensor, tp: int, rank: int) -> torch.Tensor:
     return t
 
 
-def load_hf_safetensors(model, path: str, strict: bool = False) -> list[str]:
+def load_hf_safetensors(model, path: str, strict: bool = False, optimizer=None) -> list[str]:
     """Load this rank's shard of an HF checkpoint dir (single file or sharded index) into ``model``.
 
     Only the tensors of this PP stage / EP shard are read (safetensors memory-maps the files).
+    The bf16 parameters are views into the arena, so the copy lands there; when an
+    arena optimizer already exists pass it as ``optimizer`` so its fp32 master copy
+    is refreshed (otherwise its first step would write the stale masters back).
     Returns the list of internal names loaded.
     """
     from safetensors import safe_open
@@ -223,5 +245,6 @@ def load_hf_safetensors(model, path: str, strict: bool = False) -> list[str]:
         sd["final_proj.weight"] = sd["embedding.weight"]
     with torch.no_grad():
         raw.load_reference_state_dict({k: v.to(next(raw.parameters()).dtype) for k, v in sd.items()}, strict=strict)
-    # arenas: params are views into the flat buffer, so the copy landed there; refresh fp32 masters
+    if optimizer is not None and hasattr(optimizer, "reload_masters"):
+        optimizer.reload_masters()
     return sorted(sd)

@@ -1,0 +1,62 @@
+"""Failure detection / elastic recovery: a rank is killed mid-run (ST_FAULT_STEP fault
+injection), torchrun restarts the job (--max-restarts), and --auto_resume continues
+from the newest COMPLETE checkpoint, data position included -- the resumed run ends
+on the same loss as an uninterrupted one (CPU / gloo, 2 ranks, ZeRO-1 AdamW).
+Reference: scripts/torch_dist/launch_single_node.sh:60-100 (restart launcher),
+SURVEY.md §5.3 (no fault injection / resume test in the reference)."""
+from __future__ import annotations
+
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.slow
+
+
+def _train(work_dir: str, port: int, env_extra: dict, restarts: int = 0):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1", **env_extra)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           f"--max-restarts={restarts}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           "tools/train.py", "--model_name_or_path", "tiny-llama", "--synthetic_data", "True", "--use_cpu", "True",
+           "--backend", "gloo", "--dtype", "float32", "--data_parallel_size", "2", "--micro_batch_size", "2",
+           "--sequence_length", "32", "--total_train_steps", "6", "--save_frequency", "2", "--learning_rate",
+           "1e-2", "--zero_stage", "1", "--auto_resume", "True", "--work_dir", work_dir]
+    return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+
+
+def _losses(text: str) -> dict:
+    return {int(m.group(1)): float(m.group(2)) for m in re.finditer(r"Step: (\d+)\s*\| Loss: ([0-9.]+)", text)}
+
+
+def test_kill_restart_auto_resume(tmp_path):
+    clean = _train(str(tmp_path / "clean"), 29761, {})
+    assert clean.returncode == 0, clean.stderr[-3000:]
+    faulted = _train(str(tmp_path / "faulted"), 29763, {"ST_FAULT_STEP": "3", "ST_FAULT_RANK": "1"}, restarts=1)
+    out = faulted.stdout + faulted.stderr
+    assert faulted.returncode == 0, out[-3000:]
+    assert "fault injection: rank 1 exits at step 3" in out
+    assert "resumed from" in out and "at step 2" in out
+    ref, got = _losses(clean.stdout + clean.stderr), _losses(out)
+    assert 6 in ref and 6 in got, (ref, got)
+    assert got[6] == ref[6], (got, ref)
+    # every saved step directory carries both ranks' completion markers
+    from scaletorch_amd.utils.checkpoint import is_complete, latest_checkpoint
+
+    assert is_complete(str(tmp_path / "faulted" / "6"))
+    assert latest_checkpoint(str(tmp_path / "faulted")).endswith("/6")
+
+
+def test_incomplete_checkpoint_is_skipped(tmp_path):
+    from scaletorch_amd.utils.checkpoint import latest_checkpoint
+
+    for step, ranks in ((2, (0, 1)), (4, (0,))):  # step 4: rank 1 died mid-save
+        d = tmp_path / str(step)
+        d.mkdir()
+        (d / "weights_tp_rank_world_size=0_1_pp_rank_world_size=0_1.pth").write_bytes(b"x")
+        for r in ranks:
+            (d / f"complete_rank_world_size={r}_2").write_text("ok\n")
+    assert latest_checkpoint(str(tmp_path)).endswith("/2")

@@ -306,3 +306,27 @@ def test_rccl_only_branches(kw, expect):
         assert r[3][expect] > 0, r[3]
     tol = dict(atol=5e-5, rtol=5e-3) if opt else dict(atol=2e-3, rtol=2e-2, loss_rtol=1e-3)
     _compare(ref, [r[:3] for r in res], **tol)
+
+
+def _cover_worker(rank, world, model, kw):
+    from scaletorch_amd.trainer.engine import Trainer
+
+    tr = Trainer(_make_args(model, **kw), build_data=False)
+    X = _global_batch(tr.model_config.vocab_size)
+    b = _batches_for(tr, X)[0]
+    return tr.model.uncovered_params(lambda: tr.model(input_ids=b["input_ids"], position_ids=b["position_ids"]))
+
+
+@pytest.mark.parametrize("model,world,kw", [
+    ("tiny-llama", 1, dict(micro_batch_size=4)),
+    ("tiny-qwen3", 1, dict(micro_batch_size=4)),
+    ("tiny-moe", 1, dict(micro_batch_size=4)),
+    ("tiny-llama", 2, dict(tensor_parallel_size=2, sequence_parallel=True, micro_batch_size=4)),
+    ("tiny-qwen3", 2, dict(tensor_parallel_size=2, sequence_parallel=True, micro_batch_size=4)),
+], ids=["llama", "qwen3", "moe", "llama_tp2_sp", "qwen3_tied_tp2_sp"])
+def test_every_weight_read_waits_for_its_bucket(model, world, kw):
+    """Every trainable weight is covered by the forward pre-hook bucket wait of a module
+    that actually runs (the SP LM head and the fused QK-norm read weights
+    without calling their owning module, racing the side-stream optimizer update)."""
+    for missing in run_workers(_cover_worker, world, model, kw):
+        assert missing == [], missing

@@ -140,3 +140,38 @@ def test_overlapped_optimizer_matches_serial(ga):
         assert abs(a - b) <= 1e-5 * abs(a), (n0, n1)
     assert l0 == l1, (l0, l1)
     assert torch.equal(p0, p1)
+
+
+@pytest.mark.parametrize("model", ["tiny-qwen3", "tiny-moe"])
+def test_delayed_side_stream_update_is_waited_for(model, monkeypatch):
+    """The side-stream optimizer update is artificially delayed (a ~50 ms spin on the
+    side stream before every step's AdamW): weights read by fused kernels without a
+    module call (Qwen3 QK-norm, MoE router gate) must still wait for it -- losses
+    equal the serial optimizer's bitwise.  Also: no trainable weight escapes the
+    forward pre-hook bucket waits on the GPU path."""
+    from scaletorch_amd import optim
+
+    orig = optim.ArenaAdamW._step_overlapped
+
+    def delayed(self, t):
+        with torch.cuda.stream(self.side_stream):
+            torch.cuda._sleep(100_000_000)
+        return orig(self, t)
+
+    def run(overlap):
+        os.environ["ST_OVERLAP_OPT"] = "1" if overlap else "0"
+        try:
+            tr = _tiny_trainer(model_name_or_path=model, bucket_size_mb=0.25, max_grad_norm=0.0)
+        finally:
+            os.environ["ST_OVERLAP_OPT"] = "1"
+        b = next(tr.data)  # (both runs consume this batch)
+        with torch.no_grad():
+            missing = tr.model.uncovered_params(
+                lambda: tr.model(input_ids=b["input_ids"], position_ids=b["position_ids"]))
+        assert missing == [], missing
+        return [tr.reduced_loss(tr.train_step()) for _ in range(4)]
+
+    ref = run(False)
+    monkeypatch.setattr(optim.ArenaAdamW, "_step_overlapped", delayed)
+    got = run(True)
+    assert got == ref, (got, ref)

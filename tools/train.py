@@ -57,12 +57,11 @@ def main(argv=None) -> int:
 
     ckpt = CheckpointManager(args.work_dir, async_save=args.async_save)
     resume = args.resume_path or (latest_checkpoint(args.work_dir) if args.auto_resume else None)
+    if args.auto_resume and not args.resume_path and world > 1:
+        resume = C.broadcast_object_list([resume], src=0)[0]  # one decision for every rank
     if resume:
-        try:
-            tr.step, tr.trained_tokens = ckpt.load_checkpoint(tr.model, tr.optimizer, resume, tr.lr_scheduler)
-            log.info("resumed from %s at step %d", resume, tr.step)
-        except FileNotFoundError as e:
-            log.warning("resume failed: %s", e)
+        tr.resume(ckpt, resume)  # fatal on every rank if any rank cannot load
+        log.info("resumed from %s at step %d", resume, tr.step)
 
     wandb = None
     if args.use_wandb and _is_log_rank():
@@ -75,7 +74,10 @@ def main(argv=None) -> int:
             log.warning("wandb unavailable: %s", e)
 
     total = args.total_train_steps or 1000
+    # fault injection (tests): on the first launch only, so a torchrun restart can resume
     fault_step = int(os.environ.get("ST_FAULT_STEP", "-1"))
+    if int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")) > 0:
+        fault_step = -1
     fault_rank = int(os.environ.get("ST_FAULT_RANK", "0"))
     monitor = PerformanceMonitor(warmup_steps=2, rank=tr.rank)
     n_active = cfg.active_params()
