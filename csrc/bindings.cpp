@@ -73,6 +73,7 @@ int st_qknorm_rope_fwd(void* qkv, void* xsave, float* rstd, const void* wq, cons
 int st_qknorm_rope_bwd(void* dqkv, const void* xsave, const float* rstd, const void* wq, const void* wk,
                        const float* cos_t, const float* sin_t, const int64_t* pos, int64_t N, int S, int H, int Hkv,
                        int D, int64_t max_pos, float* partial, float* dw_out, hipStream_t st);
+int st_transpose_bf16(const void* src, void* dst, int R, int C, int64_t lds_src, int64_t lds_dst, hipStream_t st);
 int st_lse_merge(float* out, float* lse, const void* bout, const float* blse, int B, int S, int H,
                  int D, int64_t sbb, int64_t sbs, int64_t sbh, hipStream_t st);
 }
@@ -258,6 +259,26 @@ void adamw_step_(at::Tensor master, at::Tensor exp_avg, at::Tensor exp_avg_sq,
                          (float)beta1, (float)beta2, (float)eps, (float)weight_decay, (float)bc1,
                          (float)std::sqrt(bc2), cur_stream());
   ST_CHECK_RC(rc, "adamw_step_");
+}
+
+void transpose_(const at::Tensor& src, at::Tensor dst) {
+  check_bf16_cuda(src, "src");
+  check_bf16_cuda(dst, "dst");
+  check_same_gpu(dst, src, "dst");
+  TORCH_CHECK(src.dim() == 2 && dst.dim() == 2, "transpose_: 2-D tensors");
+  const int64_t R = src.size(0), C = src.size(1);
+  TORCH_CHECK(dst.size(0) == C && dst.size(1) == R, "transpose_: dst must be [C, R]");
+  TORCH_CHECK(R % 64 == 0 && C % 64 == 0, "transpose_: both dims must be multiples of 64");
+  TORCH_CHECK(src.stride(1) == 1 && dst.stride(1) == 1 && src.stride(0) % 8 == 0 && dst.stride(0) % 8 == 0 &&
+                  src.stride(0) >= C && dst.stride(0) >= R,
+              "transpose_: row-major with 16-B aligned rows");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(src.data_ptr()) % 16) == 0 &&
+                  (reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16) == 0, "transpose_: 16-B aligned");
+  TORCH_CHECK(R < (1LL << 31) && C < (1LL << 31), "transpose_: dims");
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(src.device());
+  int rc = st_transpose_bf16(src.data_ptr(), dst.data_ptr(), (int)R, (int)C, src.stride(0), dst.stride(0),
+                             cur_stream());
+  ST_CHECK_RC(rc, "transpose_");
 }
 
 void sumsq_(const at::Tensor& g, at::Tensor out) {
@@ -580,6 +601,7 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("swiglu_bwd(Tensor dout, Tensor gate_up) -> Tensor");
   m.def("adamw_step_(Tensor(a!) master, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor grad, Tensor(d!)? param, Tensor? clip_coef, float lr, float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
   m.def("sumsq_(Tensor g, Tensor(a!) out) -> ()");
+  m.def("transpose_(Tensor src, Tensor(a!) dst) -> ()");
   m.def("xent_fwd(Tensor logits, Tensor target, int vocab_start) -> Tensor[]");
   m.def("xent_bwd_(Tensor logits, Tensor target, int vocab_start, Tensor lse, Tensor dloss, Tensor(a!) dlogits) -> ()");
   m.def("flash_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int q_offset, int k_offset) -> Tensor[]");
@@ -607,6 +629,7 @@ TORCH_LIBRARY_IMPL(st_amd, CUDA, m) {
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("adamw_step_", &adamw_step_);
   m.impl("sumsq_", &sumsq_);
+  m.impl("transpose_", &transpose_);
   m.impl("xent_fwd", &xent_fwd);
   m.impl("xent_bwd_", &xent_bwd_);
   m.impl("flash_fwd", &flash_fwd);

@@ -13,7 +13,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
-from .grad import accumulate_grad, accumulate_linear_wgrad
+from .grad import accumulate_grad, accumulate_linear_wgrad, dgrad, prepare_dgrad_weight
 
 
 class _SwiGLUFn(torch.autograd.Function):
@@ -46,13 +46,15 @@ class _LinearFn(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         ctx.bias = bias
+        if x.requires_grad:
+            prepare_dgrad_weight(weight)
         return F.linear(x, weight, bias)
 
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1])
-        dx = dy.matmul(weight) if ctx.needs_input_grad[0] else None
+        dx = dgrad(dy, weight) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
             dw = accumulate_linear_wgrad(weight, dy2, x.reshape(-1, x.shape[-1]))

@@ -541,6 +541,9 @@ class DataParallel(nn.Module):
             self.require_backward_grad_sync = prev
 
     def zero_grad(self, set_to_none: bool = False) -> None:  # noqa: ARG002 - arenas are persistent
+        from ..ops.grad import bump_weight_epoch
+
+        bump_weight_epoch()  # a new step: the weights' W^T copies (dgrad layout) are stale
         for a in self.arenas:
             a.mark_fresh()
             a.reset_counts()

@@ -8,6 +8,12 @@ Differences:
   norm + LM head on the last;
 * every exchange is non-blocking (``batch_isend_irecv``); the paired
   send-forward/recv-backward of the 1F1B steady state is ONE grouped RCCL call;
+  a received tensor is waited for right before its first use, and a pure send
+  is never waited on the compute path: its work handle (and the tensor) is kept
+  until the end of the step, so the next micro-batch's compute does not stall
+  until the peer has posted its receive (the reference blocked on every
+  send/recv, pp_comms.py:181-186).  The RCCL issue order is unchanged, so this
+  cannot introduce a p2p deadlock;
 * the schedule owns the loss (the reference stored it on the DP wrapper and
   crashed with PP+DP), losses stay on device (one host sync
   per step, at logging), and the DP gradient sync is enabled only for the last
@@ -36,9 +42,24 @@ def reset_communication_stats() -> None:
         _STATS[k] = 0
 
 
+# sends in flight: (work handles, tensors kept alive) -- joined by ``wait_sends`` at step end
+_INFLIGHT: list = []
+
+
+def wait_sends() -> None:
+    """Join every un-waited send (stream-ordered on RCCL, host wait on gloo)."""
+    while _INFLIGHT:
+        works, _keep = _INFLIGHT.pop()
+        for w in works:
+            w.wait()
+
+
 def _p2p(send_fwd=None, send_bwd=None, recv_fwd_shape=None, recv_bwd_shape=None, dtype=torch.bfloat16,
          device=None):
-    """One grouped exchange with the neighbouring stages; returns (recv_fwd, recv_bwd)."""
+    """One grouped exchange with the neighbouring stages; returns (recv_fwd, recv_bwd).
+
+    Groups with a receive are joined before returning (the caller consumes the data
+    next); send-only groups are left in flight (``wait_sends``)."""
     pg = mesh.pgm
     group = pg.pp_group
     ops, rf, rb = [], None, None
@@ -57,8 +78,12 @@ def _p2p(send_fwd=None, send_bwd=None, recv_fwd_shape=None, recv_bwd_shape=None,
         ops.append(dist.P2POp(dist.irecv, rb, pg.pp_next_rank, group))
         _STATS["recv_backward"] += 1
     if ops:
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
+        works = dist.batch_isend_irecv(ops)
+        if rf is None and rb is None:
+            _INFLIGHT.append((works, [op.tensor for op in ops]))
+        else:
+            for w in works:
+                w.wait()
     if rf is not None:
         rf.requires_grad_(True)
     return rf, rb
@@ -150,6 +175,7 @@ class PipelineEngine:
             x, y = ins.popleft(), outs.popleft()
             dx = self._backward(x, y, dy, last_backward=(i == num_micro - 1))
             _p2p(send_bwd=dx)
+        wait_sends()
         return loss_sum
 
     def train_step_1f1b(self, data_iter, num_micro: int) -> torch.Tensor:
@@ -194,6 +220,7 @@ class PipelineEngine:
             n_bwd += 1
             dx = self._backward(xo, yo, dy, last_backward=(n_bwd == num_micro))
             _p2p(send_bwd=dx)
+        wait_sends()
         return loss_sum
 
 

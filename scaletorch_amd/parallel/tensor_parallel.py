@@ -30,7 +30,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..dist import collectives as C
-from ..ops.grad import accumulate_grad, accumulate_linear_wgrad
+from ..ops.grad import accumulate_grad, accumulate_linear_wgrad, dgrad, prepare_dgrad_weight
 from . import mesh
 
 
@@ -185,6 +185,36 @@ def _reduce_scatter_seq(x: torch.Tensor, group) -> torch.Tensor:
     return out.transpose(0, 1).contiguous()
 
 
+def _gather_seq_async(x: torch.Tensor, group):
+    """Issue the sequence all-gather; returns ``finish() -> [B, S, ...]`` (waits on first call)."""
+    ws = _ws(group)
+    if ws == 1:
+        return lambda: x
+    B = x.shape[0]
+    xt = x[0].contiguous() if B == 1 else x.transpose(0, 1).contiguous()
+    out, work = C.all_gather(xt, group=group, async_op=True)
+
+    def finish():
+        work.wait()
+        return out.unsqueeze(0) if B == 1 else out.transpose(0, 1).contiguous()
+    return finish
+
+
+def _reduce_scatter_seq_async(x: torch.Tensor, group):
+    """Issue the sequence reduce-scatter; returns ``finish() -> [B, S/tp, ...]``."""
+    ws = _ws(group)
+    if ws == 1:
+        return lambda: x
+    B = x.shape[0]
+    xt = x[0].contiguous() if B == 1 else x.transpose(0, 1).contiguous()
+    out, work = C.reduce_scatter(xt, group=group, async_op=True)
+
+    def finish():
+        work.wait()
+        return out.unsqueeze(0) if B == 1 else out.transpose(0, 1).contiguous()
+    return finish
+
+
 def _split_seq(x: torch.Tensor, group) -> torch.Tensor:
     ws = _ws(group)
     if ws == 1:
@@ -244,12 +274,14 @@ class _ColumnParallelFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, group):
         ctx.save_for_backward(x, weight)
         ctx.group, ctx.bias = group, bias
+        if x.requires_grad:
+            prepare_dgrad_weight(weight)
         return F.linear(x, weight, bias)
 
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
-        dx = dy.matmul(weight)
+        dx = dgrad(dy, weight)
         handle = None
         if _ws(ctx.group) > 1:
             handle = _tp_all_reduce(dx, ctx.group, async_op=True)
@@ -266,9 +298,12 @@ class _ColumnParallelFn(torch.autograd.Function):
 class _SPColumnParallelFn(torch.autograd.Function):
     """Sequence-parallel column linear: all-gather x along seq, GEMM.
 
-    Backward: reduce-scatter of dX (async) overlapped with the dW GEMM.  The
-    gathered input is NOT saved; it is re-gathered in backward (Megatron's
-    memory/traffic trade-off: an all-gather of [B,S,h] instead of keeping it).
+    Backward (every collective async, each hidden behind a GEMM): the re-gather
+    of x is issued first and runs under the dX = dY W GEMM; the reduce-scatter
+    of dX is issued next and runs under the dW GEMM (accumulated into
+    main_grad).  The gathered input is NOT saved (Megatron's memory/traffic
+    trade-off: an all-gather of [B,S,h] in backward instead of keeping it).
+    Reference: sp_comms.py:31-61 + tp_comms.py:288-311 (which serialised them).
     """
 
     @staticmethod
@@ -276,20 +311,76 @@ class _SPColumnParallelFn(torch.autograd.Function):
         xg = _gather_seq(x_shard, group)
         ctx.save_for_backward(x_shard, weight)
         ctx.group, ctx.bias = group, bias
+        if x_shard.requires_grad:
+            prepare_dgrad_weight(weight)
         return F.linear(xg, weight, bias)
 
     @staticmethod
     def backward(ctx, dy):
         x_shard, weight = ctx.saved_tensors
-        xg = _gather_seq(x_shard, ctx.group)
-        dx_full = dy.matmul(weight)
+        gather = _gather_seq_async(x_shard, ctx.group) if ctx.needs_input_grad[1] else None
+        dx_full = dgrad(dy, weight)                           # overlaps the all-gather
+        scatter = _reduce_scatter_seq_async(dx_full, ctx.group)
         dy2 = dy.reshape(-1, dy.shape[-1])
-        dw = accumulate_linear_wgrad(weight, dy2, xg.reshape(-1, xg.shape[-1])) if ctx.needs_input_grad[1] else None
+        dw = None
+        if gather is not None:
+            xg = gather()
+            dw = accumulate_linear_wgrad(weight, dy2, xg.reshape(-1, xg.shape[-1]))  # overlaps the RS
         db = None
         if ctx.bias is not None and ctx.needs_input_grad[2]:
             db = accumulate_grad(ctx.bias, dy2.float().sum(0))
-        dx = _reduce_scatter_seq(dx_full, ctx.group)
-        return dx, dw, db, None
+        return scatter(), dw, db, None
+
+
+def _ar_chunks(tokens: int) -> int:
+    """Token chunks of the row-parallel forward (ST_TP_AR_CHUNKS overrides)."""
+    import os
+
+    env = os.environ.get("ST_TP_AR_CHUNKS")
+    if env:
+        return max(1, int(env))
+    return 4 if tokens >= 8192 else (2 if tokens >= 2048 else 1)
+
+
+class _RowParallelFn(torch.autograd.Function):
+    """y = all_reduce(x W^T) over TP with the all-reduce PIPELINED against the GEMM:
+    the tokens are split into chunks, and chunk i's all-reduce (async, RCCL
+    stream / xGMI side stream) runs while chunk i+1's GEMM computes, so only the
+    last chunk's all-reduce is exposed.  Backward needs no communication (dY is
+    replicated): dX = dY W and dW = dY^T X into main_grad.
+    Reference: RowParallelLinear + ReduceFromModelParallelRegion
+    (tensor_parallel.py:352-362, tp_comms.py:140-153), a blocking all-reduce."""
+
+    @staticmethod
+    def forward(ctx, x, weight, group):
+        ctx.save_for_backward(x, weight)
+        if x.requires_grad:
+            prepare_dgrad_weight(weight)
+        x2 = x.reshape(-1, x.shape[-1])
+        T = x2.shape[0]
+        n = _ar_chunks(T)
+        y = torch.empty(T, weight.shape[0], dtype=x.dtype, device=x.device)
+        works = []
+        bounds = [T * i // n for i in range(n + 1)]
+        for lo, hi in zip(bounds[:-1], bounds[1:]):
+            if hi > lo:
+                yc = y[lo:hi]
+                torch.matmul(x2[lo:hi], weight.t(), out=yc)
+                works.append(_tp_all_reduce(yc, group, async_op=True))
+        for w in works:
+            if w is not None:
+                w.wait()
+        return y.view(*x.shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx = dgrad(dy, weight) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = accumulate_linear_wgrad(weight, dy2, x.reshape(-1, x.shape[-1]))
+        return dx, dw, None
 
 
 def _init_shard_(weight: torch.Tensor, init: str, std: float, fan_in: int) -> None:
@@ -390,12 +481,12 @@ class RowParallelLinear(nn.Module):
 
         if not self.input_is_parallel and self.tp > 1:
             x = ScatterToTensorParallelRegion.apply(x, self.group)
-        y = linear(x, self.weight, None)
-        if self.tp > 1:
-            if self.sequence_parallel:
+        if self.tp > 1 and not self.sequence_parallel:
+            y = _RowParallelFn.apply(x, self.weight, self.group)  # GEMM / all-reduce pipelined
+        else:
+            y = linear(x, self.weight, None)
+            if self.tp > 1:
                 y = ReduceScatterToSequenceParallelRegion.apply(y, self.group)
-            else:
-                y = ReduceFromTensorParallelRegion.apply(y, self.group)
         if self.bias is not None:
             y = y + self.bias
         return y

@@ -364,3 +364,14 @@ def test_qknorm_rope_attention_matches_unfused(D, with_pos):
     assert rel(out, ref) < 2e-2
     assert rel(x.grad, xr.grad) < 3e-2
     assert rel(wq.grad, wqr.grad) < 3e-2 and rel(wk.grad, wkr.grad) < 3e-2
+
+
+@pytest.mark.parametrize("shape", [(64, 64), (128, 192), (4096, 1024), (6144, 4096)])
+def test_transpose_bf16(shape):
+    from scaletorch_amd.ops import _lib
+
+    R, C = shape
+    src = torch.randn(R, C, device="cuda", dtype=torch.bfloat16)
+    dst = torch.empty(C, R, device="cuda", dtype=torch.bfloat16)
+    _lib.ops().transpose_(src, dst)
+    assert torch.equal(dst, src.t().contiguous())

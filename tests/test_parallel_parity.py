@@ -62,6 +62,9 @@ def _run_one_step(model: str, **kw):
 
     steps = kw.pop("steps", 1)
     global_b = kw.pop("global_b", GLOBAL_B)
+    import os
+
+    os.environ.update(kw.pop("env", {}))
     tr = Trainer(_make_args(model, **kw), build_data=False)
     X = _global_batch(tr.model_config.vocab_size, global_b)
     batches = _batches_for(tr, X)
@@ -120,6 +123,7 @@ def _compare(ref, results, atol=2e-5, rtol=2e-3, loss_rtol=1e-4):
     dict(data_parallel_size=2, micro_batch_size=1, gradient_accumulation_steps=2),
     dict(tensor_parallel_size=2, micro_batch_size=4),
     dict(tensor_parallel_size=2, micro_batch_size=4, sequence_parallel=True),
+    dict(tensor_parallel_size=2, micro_batch_size=4, env={"ST_TP_AR_CHUNKS": "3"}),
     dict(context_parallel_size=2, micro_batch_size=4),
     dict(context_parallel_size=2, micro_batch_size=4, cp_comm="ring"),
     dict(context_parallel_size=2, micro_batch_size=4, cp_comm="ring", cp_zigzag=False),
@@ -127,7 +131,7 @@ def _compare(ref, results, atol=2e-5, rtol=2e-3, loss_rtol=1e-4):
     dict(context_parallel_size=2, micro_batch_size=4, cp_comm="ulysses", cp_zigzag=False),
     dict(pipeline_parallel_size=2, micro_batch_size=2, gradient_accumulation_steps=2),
     dict(pipeline_parallel_size=2, micro_batch_size=2, gradient_accumulation_steps=2, pipeline_parallel_engine="afab"),
-], ids=["dp2", "dp2_ga2", "tp2", "tp2_sp", "cp2", "cp2_ring", "cp2_ring_contig", "cp2_ulysses",
+], ids=["dp2", "dp2_ga2", "tp2", "tp2_sp", "tp2_chunked_ar", "cp2", "cp2_ring", "cp2_ring_contig", "cp2_ulysses",
         "cp2_ulysses_contig", "pp2_1f1b", "pp2_afab"])
 def test_dense_parity_world2(kw):
     ref = _reference("tiny-llama")
