@@ -66,7 +66,7 @@ def main() -> int:
     ap.add_argument("--cp", type=int, default=None)
     ap.add_argument("--ep", type=int, default=None)
     ap.add_argument("--sp", action="store_true", default=None)
-    ap.add_argument("--cp_comm", default="allgather", help="allgather | ring | ulysses")
+    ap.add_argument("--cp_comm", default="auto", help="auto | allgather | ring | ulysses")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) | gloo (debug rehearsals only)")
     ap.add_argument("--gc", action="store_true", help="activation checkpointing")
     ap.add_argument("--grad_reduce_dtype", default="bf16")

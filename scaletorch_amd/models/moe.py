@@ -80,6 +80,24 @@ def _grouped_mm_available() -> bool:
     return _GMM_OK
 
 
+def expert_major_order(recv_mat: torch.Tensor, total: int) -> torch.Tensor:
+    """Row permutation taking received rows from [src rank][local expert] order to
+    [local expert][src rank] order (each expert's rows contiguous for the grouped
+    GEMM), derived on the device from the received count matrix ``recv_mat``
+    [ep, E_local] -- no host loop, no sync (``total`` = rows received, known on the
+    host from the all-to-all splits).  ``order[i]`` = received row placed at i."""
+    ep, el = recv_mat.shape
+    dev = recv_mat.device
+    counts_se = recv_mat.reshape(-1).long()                  # blocks in arrival order (s, e)
+    start_se = torch.cumsum(counts_se, 0) - counts_se        # arrival offset of block (s, e)
+    counts_es = recv_mat.t().reshape(-1).long()              # blocks in expert-major order (e, s)
+    block_es = torch.arange(ep * el, device=dev).view(ep, el).t().reshape(-1)  # (e, s) -> flat (s, e) id
+    start_es = torch.cumsum(counts_es, 0) - counts_es
+    blk = torch.repeat_interleave(torch.arange(ep * el, device=dev), counts_es, output_size=total)
+    within = torch.arange(total, device=dev) - start_es[blk]
+    return start_se[block_es[blk]] + within
+
+
 class MoERouter(nn.Module):
     """Top-k softmax router (reference model_qwen3_moe.py:30-92)."""
 
@@ -251,26 +269,13 @@ class MoELayer(nn.Module):
             # counts per (dest rank, local expert); exchange the full matrix once
             send_mat = counts.view(self.ep, self.num_local)
             recv_mat = C.all_to_all(send_mat.contiguous(), group=group)  # [src, local expert]
-            mats = torch.stack([send_mat, recv_mat]).cpu()  # one host sync per layer
-            send_splits = mats[0].sum(1).tolist()
-            recv_mat_h = mats[1]
-            recv_splits = recv_mat_h.sum(1).tolist()
-            xr = all_to_all_rows(xs, recv_splits, send_splits, group)  # grouped [src][expert]
-            # regroup received rows expert-major: [expert][src]
-            idx = []
-            starts = torch.zeros_like(recv_mat_h)
-            flat = recv_mat_h.reshape(-1)
-            starts.view(-1)[1:] = torch.cumsum(flat, 0)[:-1]
-            for e in range(self.num_local):
-                for s in range(self.ep):
-                    n = int(recv_mat_h[s, e])
-                    if n:
-                        b = int(starts[s, e])
-                        idx.append(torch.arange(b, b + n))
-            regroup = torch.cat(idx).to(x.device) if idx else torch.zeros(0, dtype=torch.long, device=x.device)
-            ye = self.experts(xr.index_select(0, regroup), recv_mat_h.sum(0))
-            yr = torch.empty_like(ye)
-            yr = yr.index_copy(0, regroup, ye) if regroup.numel() else ye
+            mats = torch.stack([send_mat.sum(1), recv_mat.sum(1)]).cpu()  # the ONE host sync per layer
+            send_splits, recv_splits = mats[0].tolist(), mats[1].tolist()
+            xr = all_to_all_rows(xs, recv_splits, send_splits, group)  # rows grouped [src][expert]
+            # src-major -> expert-major order, computed on device from the count matrix
+            order = expert_major_order(recv_mat, sum(recv_splits))
+            ye = self.experts(xr.index_select(0, order), recv_mat.sum(0))
+            yr = ye.index_select(0, torch.argsort(order))  # back to [src][expert] for the return trip
             y = all_to_all_rows(yr, send_splits, recv_splits, group)
         out = ops.moe.combine(y, topw, perm).view(shape)
         # expert down-projections are TP partial sums: reduce once, after the combine

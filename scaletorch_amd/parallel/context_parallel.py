@@ -68,28 +68,42 @@ def _reduce_scatter_seq_dim1(x: torch.Tensor, group) -> torch.Tensor:
 
 
 class _CPAttnFn(torch.autograd.Function):
+    """K/V all-gather transport with the gather OVERLAPPED: the packed local [K|V]
+    all-gather is issued async, and while it is in flight every local query chunk
+    attends to its OWN chunk (the causal diagonal block, all local data); after
+    the gather lands, each chunk attends to the keys before it ([0, g0), no mask)
+    and the two partial results are combined by the LSE-merge kernel.  Backward:
+    one flash backward per chunk over its visible prefix, writing dQ and dK/dV
+    straight into their output buffers (the widest prefix first, the next one
+    added in place: the same single bf16 rounding per partial as an fp32
+    accumulator, without a full-S fp32 buffer), then ONE reduce-scatter."""
+
     @staticmethod
     def forward(ctx, q, kv, H, Hkv, D, scale, zigzag):
         """q [B, s, H, D] (roped), kv [B, s, 2*Hkv, D] (k roped | v) local shards."""
         group, cp, rank = _cp()
         B, s = q.shape[0], q.shape[1]
         S = s * cp
-        kv_g = _gather_seq_dim1(kv, group)  # [B, S, 2Hkv, D] rank order
-        if zigzag:
-            idx = _global_order_index(S, cp, q.device)
-            kv_g = kv_g.index_select(1, idx)
-            starts = zigzag_chunk_starts(S, cp, rank)[:2]
-            c = s // 2
-            chunks = [(0, c, starts[0]), (c, c, starts[1])]
-        else:
-            kv_g = kv_g.contiguous()
-            chunks = [(0, s, rank * s)]
+        xt = kv.transpose(0, 1).contiguous()
+        gathered, work = C.all_gather(xt, group=group, async_op=True)
+        chunks = _chunks_of(rank, S, cp, s, zigzag)
+        parts = []
+        for off, n, g0 in chunks:  # diagonal blocks: local keys only, under the gather
+            o, l = ops.flash_attn_fwd(q[:, off: off + n], kv[:, off: off + n, :Hkv], kv[:, off: off + n, Hkv:],
+                                      scale, True, g0, g0)
+            parts.append((o, l))
+        if work is not None:
+            work.wait()
+        kv_g = gathered.transpose(0, 1)  # [B, S, 2Hkv, D] rank order
+        kv_g = kv_g.index_select(1, _global_order_index(S, cp, q.device)) if zigzag else kv_g.contiguous()
         k_full, v_full = kv_g[:, :, :Hkv], kv_g[:, :, Hkv:]
         outs, lses = [], []
-        for off, n, g0 in chunks:
-            qc = q[:, off: off + n]
-            kend = g0 + n
-            o, l = ops.flash_attn_fwd(qc, k_full[:, :kend], v_full[:, :kend], scale, True, g0, 0)
+        for (off, n, g0), (o, l) in zip(chunks, parts):
+            if g0 > 0:  # every key of [0, g0) precedes every query of the chunk
+                bo, bl = ops.flash_attn_fwd(q[:, off: off + n], k_full[:, :g0], v_full[:, :g0], scale, True, g0, 0)
+                acc = o.float()
+                _merge(acc, l, bo, bl)
+                o = acc.to(q.dtype)
             outs.append(o)
             lses.append(l)
         out = torch.cat(outs, dim=1) if len(outs) > 1 else outs[0]
@@ -105,22 +119,25 @@ class _CPAttnFn(torch.autograd.Function):
         group, cp, rank = _cp()
         k_full, v_full = kv_g[:, :, :Hkv], kv_g[:, :, Hkv:]
         dq = torch.empty_like(q)
-        dkv = torch.zeros(kv_g.shape, dtype=torch.float32, device=q.device)
+        dkv = torch.empty(kv_g.shape, dtype=q.dtype, device=q.device)
         dout = dout.contiguous()
-        for (off, n, g0), lse in zip(chunks, lses):
+        order = sorted(range(len(chunks)), key=lambda i: -(chunks[i][2] + chunks[i][1]))  # widest prefix first
+        covered = 0
+        for i in order:
+            off, n, g0 = chunks[i]
             kend = g0 + n
-            dq_c, dk_c, dv_c = ops.flash_attn_bwd(dout[:, off: off + n], q[:, off: off + n], k_full[:, :kend],
-                                                 v_full[:, :kend], out[:, off: off + n].contiguous(), lse, scale,
-                                                 True, g0, 0)
-            dq[:, off: off + n] = dq_c
-            dkv[:, :kend, :Hkv] += dk_c.float()
-            dkv[:, :kend, Hkv:] += dv_c.float()
-        dkv = dkv.to(q.dtype)
+            args = (dout[:, off: off + n], q[:, off: off + n], k_full[:, :kend], v_full[:, :kend],
+                    out[:, off: off + n].contiguous(), lses[i], scale, True, g0, 0)
+            if covered == 0:
+                dkv[:, kend:].zero_()
+                ops.flash_attn_bwd(*args, dq=dq[:, off: off + n], dk=dkv[:, :kend, :Hkv], dv=dkv[:, :kend, Hkv:])
+                covered = kend
+            else:
+                dq_c, dk_c, dv_c = ops.flash_attn_bwd(*args, dq=dq[:, off: off + n])
+                dkv[:, :kend, :Hkv] += dk_c
+                dkv[:, :kend, Hkv:] += dv_c
         if zigzag:
-            idx = _global_order_index(S, cp, q.device)
-            inv = torch.empty_like(idx)
-            inv[idx] = torch.arange(S, device=q.device)
-            dkv = dkv.index_select(1, inv)  # back to rank order
+            dkv = dkv.index_select(1, _inverse(_global_order_index(S, cp, q.device)))  # back to rank order
         dkv_local = _reduce_scatter_seq_dim1(dkv.contiguous(), group)
         return dq, dkv_local.contiguous(), None, None, None, None, None
 
@@ -337,15 +354,24 @@ def _inverse(idx: torch.Tensor) -> torch.Tensor:
     return inv
 
 
-_CP_COMM = "allgather"
+_CP_COMM = "auto"
 _CP_FNS = {"allgather": "_CPAttnFn", "ring": "_RingAttnFn", "ulysses": "_UlyssesAttnFn"}
 
 
 def set_cp_comm(mode: str) -> None:
     global _CP_COMM
-    if mode not in _CP_FNS:
-        raise ValueError(f"cp_comm must be one of {sorted(_CP_FNS)}, got {mode!r}")
+    if mode not in _CP_FNS and mode != "auto":
+        raise ValueError(f"cp_comm must be auto or one of {sorted(_CP_FNS)}, got {mode!r}")
     _CP_COMM = mode
+
+
+def resolve_cp_comm(cp: int) -> str:
+    """``auto``: the overlapped K/V all-gather at cp <= 2 (one exchange, the local
+    diagonal hides it), the ring above (per-step p2p hidden behind each block's
+    flash compute; the gathered K/V and its exposed tail grow with cp)."""
+    if _CP_COMM != "auto":
+        return _CP_COMM
+    return "allgather" if cp <= 2 else "ring"
 
 
 def context_parallel_attention(qkv: torch.Tensor, cos, sin, position_ids, H: int, Hkv: int, D: int,
@@ -358,7 +384,7 @@ def context_parallel_attention(qkv: torch.Tensor, cos, sin, position_ids, H: int
     q = ops.apply_rope(qkv4[:, :, :H], cos, sin, position_ids)
     k = ops.apply_rope(qkv4[:, :, H: H + Hkv], cos, sin, position_ids)
     kv = torch.cat([k, qkv4[:, :, H + Hkv:]], dim=2)
-    fn = globals()[_CP_FNS[_CP_COMM]]
+    fn = globals()[_CP_FNS[resolve_cp_comm(mesh.cp_size())]]
     out = fn.apply(q.contiguous(), kv.contiguous(), H, Hkv, D, scale, zigzag)
     return out.reshape(B, s, H * D)
 
