@@ -175,3 +175,21 @@ def test_delayed_side_stream_update_is_waited_for(model, monkeypatch):
     monkeypatch.setattr(optim.ArenaAdamW, "_step_overlapped", delayed)
     got = run(True)
     assert got == ref, (got, ref)
+
+
+def test_performance_monitor_events_no_device_sync():
+    """Event-timed monitor: non-logging steps do not block the host on the device,
+    logged steps resolve exactly; telemetry present."""
+    from scaletorch_amd.utils.logger import PerformanceMonitor
+
+    m = PerformanceMonitor(warmup_steps=0, telemetry_interval=1)
+    x = torch.randn(4096, 4096, device="cuda")
+    for i in range(3):
+        m.start_iteration()
+        for _ in range(20):
+            x = x @ x
+            x = x / x.norm()
+        rec = m.end_iteration(1000, sync=(i == 2))
+    assert rec["step_time_s"] > 0
+    s = m.summary()
+    assert s["steps_measured"] == 3 and "avg_mem_fragmentation" in s

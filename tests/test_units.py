@@ -323,3 +323,19 @@ def test_group_nodes_and_env_helpers():
     assert info["torch"] and "hostname" in info
     os.environ["ST_TEST_FLAG"] = "yes"
     assert env.env_flag("ST_TEST_FLAG") and not env.env_flag("ST_TEST_FLAG_UNSET")
+
+
+def test_performance_monitor_cpu_ring_buffers_and_telemetry():
+    import time as _t
+
+    from scaletorch_amd.utils.logger import PerformanceMonitor
+
+    m = PerformanceMonitor(warmup_steps=1, window=3, telemetry_interval=2)
+    for _ in range(5):
+        m.start_iteration()
+        _t.sleep(0.002)
+        rec = m.end_iteration(100)
+        assert rec["tokens_per_s"] > 0
+    s = m.summary()
+    assert s["steps_measured"] == 3  # ring buffer of 3, warm-up excluded
+    assert "avg_host_rss_gb" in s and s["tokens_per_s"] > 0

@@ -111,12 +111,13 @@ def main(argv=None) -> int:
                 os._exit(17)
             monitor.start_iteration()
             loss_t = tr.train_step()
-            rec = monitor.end_iteration(tr.tokens_per_step)
+            log_now = tr.step % max(1, args.log_interval) == 0 or tr.step == total
+            rec = monitor.end_iteration(tr.tokens_per_step, sync=log_now)  # events only: no device-wide sync
             if watchdog is not None:
                 watchdog.kick(tr.step)
             if prof is not None:
                 prof.step()
-            if tr.step % max(1, args.log_interval) == 0 or tr.step == total:
+            if log_now:
                 loss = tr.reduced_loss(loss_t)
                 if args.nan_check and loss != loss:
                     raise FloatingPointError(f"non-finite loss at step {tr.step}")
