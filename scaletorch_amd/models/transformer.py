@@ -65,10 +65,13 @@ class Attention(nn.Module):
 
     def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor,
                 position_ids: torch.Tensor | None) -> torch.Tensor:
+        from .attention_backends import attention, resolve_attention_backend_name
+
         qkv = self.qkv_proj(x)
         B, S = qkv.shape[0], qkv.shape[1]
         H, Hkv, D = self.H, self.Hkv, self.D
-        if self.qk_norm and mesh.cp_size() == 1 and os.environ.get("ST_FUSED_QKNORM", "1") == "1":
+        backend = resolve_attention_backend_name(mesh.cp_size() > 1)
+        if self.qk_norm and backend == "flash" and os.environ.get("ST_FUSED_QKNORM", "1") == "1":
             # Qwen3: per-head QK-norm + RoPE fused in place on the QKV buffer (csrc/qknorm_rope.hip)
             out = ops.qknorm_rope_attention(qkv, self.q_norm.weight, self.k_norm.weight, self.q_norm.eps, cos, sin,
                                             position_ids, H, Hkv, D, causal=True, scale=self.scale)
@@ -79,12 +82,7 @@ class Attention(nn.Module):
             q = self.q_norm(q.contiguous())
             k = self.k_norm(k.contiguous())
             qkv = torch.cat([q, k, v], dim=2).view(B, S, -1)
-        if mesh.cp_size() > 1:
-            from ..parallel.context_parallel import context_parallel_attention
-
-            out = context_parallel_attention(qkv, cos, sin, position_ids, H, Hkv, D, self.scale)
-        else:
-            out = ops.rope_attention(qkv, cos, sin, position_ids, H, Hkv, D, causal=True, scale=self.scale)
+        out = attention(qkv, cos, sin, position_ids, H, Hkv, D, self.scale, backend)  # registry dispatch
         return self.out_proj(out)
 
 

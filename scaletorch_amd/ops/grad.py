@@ -84,6 +84,62 @@ def dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return dy.matmul(w)
 
 
+# ---------------------------------------------------------------- weight-gradient GEMM layout
+# dW = dY^T X with both operands token-major is an "NT" GEMM (neither operand
+# K-contiguous); hipBLASLt's TN kernels on token-contiguous copies dY^T [out, T]
+# and X^T [in, T] run 1.25-1.38 PF/s vs 1.0-1.17 for the NT path and for the
+# hand-written csrc/wgrad_gemm.hip (profiles/gemm_microbench.json "wgradT").
+# The two transposes (csrc/transpose.hip, ~5.5 TB/s) are issued on a side
+# stream BEFORE the layer's data-gradient GEMM.  Measured in-step on MI355X it LOSES
+# (735 vs 713 ms/step, profiles/r02/wgrad_tn_ab.log): off by default (ST_WGRAD_TN=1 on).
+_WG_STREAMS: dict = {}
+
+
+def _wgrad_tn_ok(dy2d: torch.Tensor, x2d: torch.Tensor) -> bool:
+    return (dy2d.is_cuda and dy2d.dtype == torch.bfloat16 and x2d.dtype == torch.bfloat16
+            and dy2d.shape[0] % 64 == 0 and dy2d.shape[1] % 64 == 0 and x2d.shape[1] % 64 == 0
+            and dy2d.stride(1) == 1 and x2d.stride(1) == 1 and dy2d.stride(0) % 8 == 0 and x2d.stride(0) % 8 == 0
+            and dy2d.data_ptr() % 16 == 0 and x2d.data_ptr() % 16 == 0
+            and os.environ.get("ST_WGRAD_TN", "0") == "1")
+
+
+class WgradOperands:
+    """Token-contiguous copies of (dY, X) being produced on a side stream."""
+
+    __slots__ = ("dyt", "xt", "done")
+
+    def __init__(self, dyt, xt, done):
+        self.dyt, self.xt, self.done = dyt, xt, done
+
+
+def prefetch_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor):
+    """Start the dY^T / X^T transposes for ``param``'s weight gradient on a side
+    stream (call before the data-gradient GEMM so they overlap it); None when the
+    TN path does not apply."""
+    mg = getattr(param, "main_grad", None)
+    if mg is None or mg.dtype != torch.float32 or not _wgrad_tn_ok(dy2d, x2d):
+        return None
+    from . import _lib
+
+    if not _lib.use_native(dy2d):
+        return None
+    T = dy2d.shape[0]
+    dyt = torch.empty(dy2d.shape[1], T, dtype=dy2d.dtype, device=dy2d.device)
+    xt = torch.empty(x2d.shape[1], T, dtype=x2d.dtype, device=x2d.device)
+    st = _WG_STREAMS.get(dy2d.device.index)
+    if st is None:
+        st = _WG_STREAMS[dy2d.device.index] = torch.cuda.Stream(device=dy2d.device)
+    ready = torch.cuda.Event()
+    ready.record()
+    with torch.cuda.stream(st):
+        st.wait_event(ready)
+        _lib.ops().transpose_(dy2d, dyt)
+        _lib.ops().transpose_(x2d, xt)
+        done = torch.cuda.Event()
+        done.record(st)
+    return WgradOperands(dyt, xt, done)
+
+
 def _grad_ready(param: torch.Tensor) -> None:
     hook = getattr(param, "_st_grad_ready", None)
     if hook is not None:
@@ -163,20 +219,29 @@ def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> bool:
     return choice
 
 
-def accumulate_linear_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor):
+def accumulate_linear_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, pre=None):
     """dW = dy^T x, accumulated into ``param.main_grad`` in fp32 when present.
 
     On GPU the product runs on the hand-written gfx950 weight-gradient GEMM
     (csrc/wgrad_gemm.hip: both operands token-major, read with LDS transpose
     reads, fp32 epilogue accumulating into main_grad); shapes it does not tile
     go to ``aten::addmm.dtype_out`` (hipBLASLt, bf16 operands, fp32 C/D).
-    ``ST_WGRAD_KERNEL=0`` forces the hipBLASLt path (A/B).
+    ``ST_WGRAD_KERNEL=0`` forces the hipBLASLt path (A/B).  Preferred on GPU: the
+    TN GEMM on token-contiguous copies (``prefetch_wgrad``; opt-in ``ST_WGRAD_TN=1``).
     """
     global _ADDMM_DTYPE_OK
     mg = getattr(param, "main_grad", None)
     if mg is None:
         return dy2d.t().mm(x2d)
+    if pre is None and mg.dtype == torch.float32:
+        pre = prefetch_wgrad(param, dy2d, x2d)
     beta = 0 if take_fresh(param) else 1
+    if pre is not None:
+        torch.cuda.current_stream().wait_event(pre.done)
+        m2 = mg.view(mg.shape[0], -1)
+        torch.ops.aten.addmm.dtype_out(m2, pre.dyt, pre.xt.t(), torch.float32, beta=beta, alpha=1, out=m2)
+        _grad_ready(param)
+        return None
     if mg.dtype == dy2d.dtype:
         mg.addmm_(dy2d.t(), x2d, beta=beta)
     else:

@@ -13,7 +13,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
-from .grad import accumulate_grad, accumulate_linear_wgrad, dgrad, prepare_dgrad_weight
+from .grad import accumulate_grad, accumulate_linear_wgrad, dgrad, prefetch_wgrad, prepare_dgrad_weight
 
 
 class _SwiGLUFn(torch.autograd.Function):
@@ -54,10 +54,12 @@ class _LinearFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1])
+        x2 = x.reshape(-1, x.shape[-1])
+        pre = prefetch_wgrad(weight, dy2, x2) if ctx.needs_input_grad[1] else None  # overlaps the dgrad GEMM
         dx = dgrad(dy, weight) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
-            dw = accumulate_linear_wgrad(weight, dy2, x.reshape(-1, x.shape[-1]))
+            dw = accumulate_linear_wgrad(weight, dy2, x2, pre)
         db = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = accumulate_grad(ctx.bias, dy2.float().sum(0))

@@ -30,7 +30,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..dist import collectives as C
-from ..ops.grad import accumulate_grad, accumulate_linear_wgrad, dgrad, prepare_dgrad_weight
+from ..ops.grad import accumulate_grad, accumulate_linear_wgrad, dgrad, prefetch_wgrad, prepare_dgrad_weight
 from . import mesh
 
 
@@ -281,12 +281,14 @@ class _ColumnParallelFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        x2 = x.reshape(-1, x.shape[-1])
+        pre = prefetch_wgrad(weight, dy2, x2) if ctx.needs_input_grad[1] else None  # overlaps the dgrad GEMM
         dx = dgrad(dy, weight)
         handle = None
         if _ws(ctx.group) > 1:
             handle = _tp_all_reduce(dx, ctx.group, async_op=True)
-        dy2 = dy.reshape(-1, dy.shape[-1])
-        dw = accumulate_linear_wgrad(weight, dy2, x.reshape(-1, x.shape[-1])) if ctx.needs_input_grad[1] else None
+        dw = accumulate_linear_wgrad(weight, dy2, x2, pre) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.bias is not None and ctx.needs_input_grad[2]:
             db = accumulate_grad(ctx.bias, dy2.float().sum(0))
@@ -376,10 +378,12 @@ class _RowParallelFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1])
+        x2 = x.reshape(-1, x.shape[-1])
+        pre = prefetch_wgrad(weight, dy2, x2) if ctx.needs_input_grad[1] else None  # overlaps the dgrad GEMM
         dx = dgrad(dy, weight) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
-            dw = accumulate_linear_wgrad(weight, dy2, x.reshape(-1, x.shape[-1]))
+            dw = accumulate_linear_wgrad(weight, dy2, x2, pre)
         return dx, dw, None
 
 

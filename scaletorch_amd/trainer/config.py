@@ -3,9 +3,13 @@
 Same flag names and defaults as the reference ``ScaleTorchArguments``
 (scaletorch/trainer/config.py:31-461) so existing launch scripts work; the
 reference's env toggles (FLASH_ATTEN, CONTEXT_PARALLEL, SEQUENCE_PARALLEL, DTYPE)
-are CLI flags here, read once, and every parsed flag is honoured (the reference
-parsed but ignored several).  Extra MI355X-side flags are
-grouped in ``SystemArguments``.
+are CLI flags here, read once.  Flags the reference parsed but ignored
+ are wired up: ``use_flash_attention`` selects the flash or sdpa
+attention backend (models/attention_backends.py), ``epochs`` bounds training by
+data passes, ``test_batch_size`` is the number of held-out sequences per
+evaluation (``eval_interval``), ``dtype``/``backend``/``pin_memory``/
+``log_interval``/``save_model_checkpoint`` are read by the trainer and
+tools/train.py.  Extra MI355X-side flags are grouped in ``SystemArguments``.
 """
 from __future__ import annotations
 
@@ -123,18 +127,19 @@ class OptimizerArguments:
 @dataclass
 class TrainingArguments:
     batch_size: int = field(default=64)
-    test_batch_size: int = field(default=1000)
+    test_batch_size: int = field(default=1000, metadata={"help": "held-out sequences per evaluation"})
     micro_batch_size: int | None = field(default=None)
     gradient_accumulation_steps: int = field(default=1)
     gradient_checkpointing: bool = field(default=False)
     max_grad_norm: float | None = field(default=1.0)
-    epochs: int = field(default=5)
+    epochs: int = field(default=5, metadata={"help": "stop after this many passes over the dataset"})
     seed: int = field(default=1)
     sequence_length: int | None = field(default=1024)
     log_interval: int = field(default=1)
     max_tokens: int | None = field(default=None)
     total_train_steps: int | None = field(default=None)
     use_cpu: bool = field(default=False)
+    eval_interval: int = field(default=0, metadata={"help": "evaluate held-out loss every N steps (0 = off)"})
 
     def __post_init__(self) -> None:
         if self.gradient_accumulation_steps < 1:

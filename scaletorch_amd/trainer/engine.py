@@ -57,6 +57,9 @@ class Trainer:
             from ..parallel.tensor_parallel import set_tp_comm
 
             set_tp_comm(a.tp_comm)
+        from ..models.attention_backends import set_use_flash_attention
+
+        set_use_flash_attention(a.use_flash_attention)
         if a.context_parallel_size > 1:
             from ..parallel.context_parallel import set_cp_comm, set_cp_zigzag
 
@@ -189,6 +192,52 @@ class Trainer:
         self.step += 1
         self.trained_tokens += self.tokens_per_step
         return loss
+
+    @torch.no_grad()
+    def evaluate(self, num_sequences: int | None = None) -> float:
+        """Mean held-out loss over ``num_sequences`` (default ``--test_batch_size``)
+        sequences, sharded over the data-parallel replicas, forward only, in
+        micro-batches of ``--micro_batch_size``.  The held-out stream is a separate
+        synthetic stream (seed + 1) or the dataset's ``validation`` split."""
+        a = self.args
+        if self.pp > 1:
+            raise NotImplementedError("evaluation with pipeline parallelism is not supported; use pp = 1")
+        n = num_sequences or a.test_batch_size
+        pg = mesh.pgm
+        data_world = pg.data_world_size if pg else 1
+        per_rank = max(1, n // data_world)
+        steps = max(1, per_rank // a.micro_batch_size)
+        loader = getattr(self, "_eval_data", None)
+        if loader is None:
+            loader = self._eval_data = self._build_eval_data()
+        was_training = self.raw_model.training
+        self.raw_model.eval()
+        total = torch.zeros((), dtype=torch.float32, device=self.device)
+        try:
+            for _ in range(steps):
+                batch = self._to_device(next(loader))
+                logits = self.model(input_ids=batch["input_ids"], position_ids=batch["position_ids"])
+                total += self._loss(logits, batch).float()
+        finally:
+            self.raw_model.train(was_training)
+        return self.reduced_loss(total / steps)
+
+    def _build_eval_data(self):
+        a, pg = self.args, mesh.pgm
+        data_rank = pg.data_rank if pg else 0
+        data_world = pg.data_world_size if pg else 1
+        if a.synthetic_data or a.use_cpu and not a.dataset_name:
+            ds = SyntheticTokenDataset(self.model_config.vocab_size, a.sequence_length, seed=a.seed + 1)
+        else:
+            from ..data.dataset import build_dataset
+
+            import copy
+
+            b = copy.copy(a)
+            b.split = "validation"
+            ds = build_dataset(b, a.sequence_length)
+        return MicroBatchDataLoader(ds, a.micro_batch_size, a.sequence_length, 1, data_rank, data_world,
+                                    self.cp_rank, self.cp, a.cp_zigzag, shuffle=False, seed=a.seed)
 
     def resume(self, ckpt_manager, path: str) -> None:
         """Load a checkpoint on EVERY rank or fail on every rank: a rank that could not

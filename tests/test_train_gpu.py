@@ -193,3 +193,26 @@ def test_performance_monitor_events_no_device_sync():
     assert rec["step_time_s"] > 0
     s = m.summary()
     assert s["steps_measured"] == 3 and "avg_mem_fragmentation" in s
+
+
+@pytest.mark.parametrize("tn", ["1", "0"])
+def test_wgrad_tn_path_accumulates_fp32(tn, monkeypatch):
+    """TN weight-gradient GEMM (side-stream dY^T / X^T transposes + hipBLASLt, fp32
+    beta epilogue into main_grad) == fp32 reference, first write (beta 0) and
+    accumulate (beta 1); ST_WGRAD_TN=0 keeps the previous path."""
+    from scaletorch_amd.ops.grad import accumulate_linear_wgrad
+
+    monkeypatch.setenv("ST_WGRAD_TN", tn)  # 1 = TN path, 0 = default path
+    torch.manual_seed(0)
+    w = torch.nn.Parameter(torch.randn(384, 256, device="cuda", dtype=torch.bfloat16))
+    w.main_grad = torch.full((384, 256), 7.0, device="cuda")
+    dy = torch.randn(1024, 384, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(1024, 256, device="cuda", dtype=torch.bfloat16)
+    ref = dy.float().t() @ x.float()
+    w._st_fresh = True
+    accumulate_linear_wgrad(w, dy, x)
+    torch.cuda.synchronize()
+    assert rel(w.main_grad, ref) < 1e-3
+    accumulate_linear_wgrad(w, dy, x)
+    torch.cuda.synchronize()
+    assert rel(w.main_grad, 2 * ref) < 1e-3

@@ -339,3 +339,57 @@ def test_performance_monitor_cpu_ring_buffers_and_telemetry():
     s = m.summary()
     assert s["steps_measured"] == 3  # ring buffer of 3, warm-up excluded
     assert "avg_host_rss_gb" in s and s["tokens_per_s"] > 0
+
+
+def test_attention_backend_registry_flash_vs_sdpa():
+    import math
+
+    import torch
+
+    from scaletorch_amd import ops
+    from scaletorch_amd.models import attention_backends as ab
+
+    assert {"flash", "sdpa", "ring", "context_parallel"} <= set(ab.registered_attention_backends())
+    assert ab.resolve_attention_backend_name(True, True) == "ring"
+    assert ab.resolve_attention_backend_name(False, True) == "flash"
+    assert ab.resolve_attention_backend_name(False, False) == "sdpa"
+    torch.manual_seed(0)
+    B, S, H, Hkv, D = 2, 16, 4, 2, 32
+    qkv = torch.randn(B, S, (H + 2 * Hkv) * D)
+    cos, sin = ops.rope_tables(64, D, 10000.0)
+    outs = [ab.get_attention_backend(n)(qkv, cos, sin, None, H, Hkv, D, 1 / math.sqrt(D)) for n in ("flash", "sdpa")]
+    torch.testing.assert_close(outs[0], outs[1], atol=1e-5, rtol=1e-4)
+
+
+def test_use_flash_attention_flag_and_evaluate():
+    from scaletorch_amd.models import attention_backends as ab
+    from scaletorch_amd.trainer.config import ScaleTorchArguments
+    from scaletorch_amd.trainer.engine import Trainer
+
+    a = ScaleTorchArguments(model_name_or_path="tiny-llama", synthetic_data=True, micro_batch_size=2,
+                            sequence_length=32, use_cpu=True, dtype="float32", use_flash_attention=False,
+                            test_batch_size=6, total_train_steps=2)
+    tr = Trainer(a)
+    try:
+        assert ab.resolve_attention_backend_name(False) == "sdpa"
+        tr.train_step()
+        v = tr.evaluate()
+        assert v == v and v > 0
+        assert tr.raw_model.training
+    finally:
+        ab.set_use_flash_attention(True)
+
+
+def test_loader_skip_batches_resumes_position():
+    import torch
+
+    from scaletorch_amd.data.loader import MicroBatchDataLoader, SyntheticTokenDataset
+
+    ds = SyntheticTokenDataset(100, 8, num_samples=10)
+    full = MicroBatchDataLoader(ds, 2, 8, seed=3)
+    seq = [next(full)["input_ids"] for _ in range(7)]  # crosses an epoch (5 batches / epoch)
+    assert full.epoch == 1
+    again = MicroBatchDataLoader(ds, 2, 8, seed=3)
+    again.skip_batches(4)
+    assert torch.equal(next(again)["input_ids"], seq[4])
+    assert torch.equal(next(again)["input_ids"], seq[5]) and again.epoch == 1

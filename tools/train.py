@@ -106,6 +106,9 @@ def main(argv=None) -> int:
         while tr.step < total and not stop["flag"]:
             if args.max_tokens and tr.trained_tokens >= args.max_tokens:
                 break
+            if getattr(tr.data, "epoch", 0) >= args.epochs:  # --epochs: data passes
+                log.info("completed %d epochs", args.epochs)
+                break
             if tr.step == fault_step and tr.rank == fault_rank:
                 log.error("fault injection: rank %d exits at step %d", tr.rank, tr.step)
                 os._exit(17)
@@ -145,6 +148,11 @@ def main(argv=None) -> int:
                     if wandb is not None:
                         wandb.log({"loss": loss, "tokens_per_second": tok_s, "tokens_per_second_per_gpu": per_gpu,
                                    "mfu": mfu, "grad_norm": gn, "trained_tokens": tr.trained_tokens}, step=tr.step)
+            if args.eval_interval > 0 and tr.step % args.eval_interval == 0:
+                vloss = tr.evaluate()
+                if _is_log_rank():
+                    rank_print(f"[rank {tr.rank}] Step: {tr.step:<5d} | Eval loss: {vloss:6.4f} | "
+                               f"Eval sequences: {args.test_batch_size}")
             if args.save_model_checkpoint and args.save_frequency > 0 and tr.step % args.save_frequency == 0:
                 ckpt.save_checkpoint(tr.model, tr.optimizer, tr.step, tr.trained_tokens, lr_scheduler=tr.lr_scheduler)
     except KeyboardInterrupt:
