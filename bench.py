@@ -69,6 +69,7 @@ def main() -> int:
     ap.add_argument("--cp_comm", default="auto", help="auto | allgather | ring | ulysses")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) | gloo (debug rehearsals only)")
     ap.add_argument("--gc", action="store_true", help="activation checkpointing")
+    ap.add_argument("--recompute", default="selective", help="with --gc: full | selective (norm+MLP only)")
     ap.add_argument("--grad_reduce_dtype", default="bf16")
     ap.add_argument("--bucket_mb", type=float, default=256)
     ap.add_argument("--zero", type=int, default=1, help="ZeRO stage when DP > 1 (0: replicated optimizer, "
@@ -104,7 +105,8 @@ def main() -> int:
     est = estimate_rank_memory(mcfg, tp=args.tp, pp=args.pp, cp=args.cp, ep=args.ep, dp=dp,
                                micro_batch=args.micro_batch_size, seq_len=args.seq_len, grad_acc=ga,
                                zero1=args.zero >= 1 and dp * args.cp * args.ep > 1, sequence_parallel=args.sp,
-                               gradient_checkpointing=args.gc, grad_reduce_dtype=args.grad_reduce_dtype)
+                               gradient_checkpointing=(args.recompute if args.gc else False),
+                               grad_reduce_dtype=args.grad_reduce_dtype)
     if int(os.environ.get("RANK", "0")) == 0:
         print(f"[bench] layout {args.layout}: {args.model} tp{args.tp} pp{args.pp} cp{args.cp} ep{args.ep} dp{dp} "
               f"mbs{args.micro_batch_size} ga{ga} seq{args.seq_len}; HBM estimate {est.summary()}",
@@ -117,7 +119,7 @@ def main() -> int:
         tensor_parallel_size=args.tp, pipeline_parallel_size=args.pp, context_parallel_size=args.cp,
         expert_parallel_size=args.ep, data_parallel_size=dp, sequence_parallel=args.sp,
         cp_comm=args.cp_comm, backend=args.backend,
-        gradient_checkpointing=args.gc, learning_rate=3e-4, lr_scheduler_type="cosine", warmup_steps=0,
+        gradient_checkpointing=args.gc, recompute_granularity=args.recompute, learning_rate=3e-4, lr_scheduler_type="cosine", warmup_steps=0,
         max_grad_norm=1.0, grad_reduce_dtype=args.grad_reduce_dtype, bucket_size_mb=args.bucket_mb,
         num_hidden_layers=args.layers, dtype="bfloat16", weight_decay=0.1, betas=(0.9, 0.95),
         zero_stage=args.zero,

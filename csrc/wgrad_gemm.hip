@@ -26,6 +26,10 @@
 //   * K loop over 32-token tiles through a ring of 4 LDS stages with 3 tiles in
 //     flight: the DMA is issued from inline asm (so hipcc does not drain it
 //     before the transposed reads) and retired by a counted vmcnt + s_barrier.
+//   * tried and dropped (profiles/r02/wgrad_v3_pipelined_ab.log): a schedule that
+//     reads the next step's fragments into a second register set under the
+//     current step's MFMAs (one barrier per step after the MFMAs) ran 4-15 %
+//     SLOWER at T = 16384 -- the exposed cost here is not LDS read latency.
 //   * XCD-aware tile order: the dispatcher deals workgroups round-robin to the
 //     8 XCDs; the bijective remap gives each XCD a contiguous range of tiles,
 //     grouped 4 M-blocks x N so the ~32 tiles an XCD runs at once share their

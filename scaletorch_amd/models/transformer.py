@@ -125,14 +125,25 @@ class DecoderLayer(nn.Module):
                   self.moe if self.is_moe else self.mlp):
             m.reset_parameters()
 
-    def forward(self, x, residual, cos, sin, position_ids):
-        """(x, residual) -> (block output, residual stream).  ``residual`` None = first layer."""
+    def forward(self, x, residual, cos, sin, position_ids, selective_recompute: bool = False):
+        """(x, residual) -> (block output, residual stream).  ``residual`` None = first layer.
+
+        ``selective_recompute``: the attention sub-block keeps its activations (QKV,
+        flash output + lse -- the expensive S^2 part is never recomputed) and only the
+        norm + MLP sub-block is checkpointed: it holds most of a layer's activation
+        bytes (gate|up output 2I, SwiGLU output I per token) and costs only GEMMs to
+        recompute.  (Reference: full-layer torch.utils.checkpoint, llama.py:535-545.)"""
         if residual is None:
             h = self.input_layernorm(x)
             residual = x
         else:
             h, residual = self.input_layernorm(x, residual)
         a = self.attention(h, cos, sin, position_ids)
+        if selective_recompute and self.training and torch.is_grad_enabled():
+            return torch_checkpoint(self._mlp_block, a, residual, use_reentrant=False)
+        return self._mlp_block(a, residual)
+
+    def _mlp_block(self, a, residual):
         h, residual = self.post_attention_layernorm(a, residual)
         out = self.moe(h) if self.is_moe else self.mlp(h)
         return out, residual
@@ -236,12 +247,14 @@ class TransformerLM(nn.Module):
                 raise ValueError("hidden_states required on non-first pipeline stages")
             x = hidden_states
         residual = None
+        full = gradient_checkpointing in (True, "full") and self.training
+        selective = gradient_checkpointing == "selective"
         for layer in self.decoder_layers.values():
-            if gradient_checkpointing and self.training:
+            if full:
                 x, residual = torch_checkpoint(layer, x, residual, self.cos, self.sin, position_ids,
                                                use_reentrant=False)
             else:
-                x, residual = layer(x, residual, self.cos, self.sin, position_ids)
+                x, residual = layer(x, residual, self.cos, self.sin, position_ids, selective_recompute=selective)
         if not self.last_stage:
             return x if residual is None else x + residual
         x = self.final_norm(x) if residual is None else self.final_norm(x, residual)[0]

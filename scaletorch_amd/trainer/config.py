@@ -131,6 +131,9 @@ class TrainingArguments:
     micro_batch_size: int | None = field(default=None)
     gradient_accumulation_steps: int = field(default=1)
     gradient_checkpointing: bool = field(default=False)
+    recompute_granularity: str = field(default="full", metadata={"help": "with --gradient_checkpointing: full "
+                                                                      "(whole layer) | selective (norm+MLP "
+                                                                      "only; attention activations kept)"})
     max_grad_norm: float | None = field(default=1.0)
     epochs: int = field(default=5, metadata={"help": "stop after this many passes over the dataset"})
     seed: int = field(default=1)

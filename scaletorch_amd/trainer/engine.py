@@ -108,6 +108,9 @@ class Trainer:
         self.cp = pg.cp_world_size if pg else 1
         self.cp_rank = pg.cp_rank if pg else 0
         self.tokens_per_step = a.global_batch_size * (a.sequence_length or 0)
+        # activation checkpointing mode handed to the model: False | "full" | "selective"
+        self.gc_mode = (a.recompute_granularity if a.recompute_granularity in ("full", "selective") else "full") \
+            if a.gradient_checkpointing else False
         self.step = 0
         self.trained_tokens = 0
         self.data = None
@@ -119,7 +122,7 @@ class Trainer:
                 S //= mesh.tp_size()
             self.pipeline = PipelineEngine(self.model, self._loss, (a.micro_batch_size, S, cfg.hidden_size),
                                            dtype=self.dtype, device=self.device,
-                                           gradient_checkpointing=a.gradient_checkpointing,
+                                           gradient_checkpointing=self.gc_mode,
                                            aux_loss_fn=model.aux_loss if cfg.is_moe else None)
 
     # ---------------------------------------------------------------- data
@@ -175,7 +178,7 @@ class Trainer:
                 with ctx:
                     with profiling.range("forward"):
                         logits = self.model(input_ids=batch["input_ids"], position_ids=batch["position_ids"],
-                                            gradient_checkpointing=a.gradient_checkpointing)
+                                            gradient_checkpointing=self.gc_mode)
                         l = self._loss(logits, batch) / ga
                         del logits
                         if self.model_config.is_moe:

@@ -3,7 +3,7 @@
 Used by ``bench.py --layout`` and ``tools/train.py`` to print what a rank will
 hold before anything is allocated, so an 8-GPU layout that would not fit is
 caught on the host.  The terms follow this framework's storage layout
-(parallel/data_parallel.py, optim.py): bf16 parameters, fp32 ``main_grad``
+(parallel/data_parallel.py, optim.py): bf16 parameters (+ their bf16 W^T copies), fp32 ``main_grad``
 arena, fp32 master + Adam m/v (sharded over the reduction group under ZeRO-1),
 and activations calibrated on one MI355X: Llama-3-8B at micro-batch 4 x 4096
 peaked at 226.5 GB (profiles/micro_batch_sweep_1gpu.log), i.e. ~34 bytes per
@@ -77,12 +77,18 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
     per_layer = _ACT_ATTN * h + _ACT_MLP * h * k_eff * cfg.intermediate_size / (3.5 * h)
     if tp > 1:
         per_layer = per_layer / tp if sequence_parallel else 8 * h + (per_layer - 8 * h) / tp
-    if gradient_checkpointing:
+    if gradient_checkpointing == "selective":  # attention activations kept, norm + MLP recomputed
+        mlp = _ACT_MLP * h * k_eff * cfg.intermediate_size / (3.5 * h) / tp
+        kept = max(per_layer - mlp, 2 * h)
+        act = tokens * kept * layers + tokens * per_layer
+    elif gradient_checkpointing:
         act = tokens * (2 * h * layers) + tokens * per_layer
     else:
         act = tokens * per_layer * layers
     logits = micro_batch * seq_len / cp * cfg.vocab_size / tp * 2 * 2  # bf16 logits + grad (last stage)
     comm = n * 2 if grad_reduce_dtype in ("bf16", "bfloat16") and dense_dp > 1 else 0.0
+    # bf16 W^T copies of the dense projection weights (TN data-gradient GEMMs, ops/grad.py)
+    wt = 2 * (dense - 2 * h * layers - (h * cfg.num_experts if cfg.is_moe else 0) * layers)
     g = 1e9
-    return MemoryEstimate(params_gb=2 * n / g, grads_gb=4 * n / g, optimizer_gb=opt / g, activations_gb=act / g,
+    return MemoryEstimate(params_gb=(2 * n + wt) / g, grads_gb=4 * n / g, optimizer_gb=opt / g, activations_gb=act / g,
                           logits_gb=logits / g, comm_gb=comm / g)
