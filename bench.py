@@ -148,6 +148,7 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     final_loss = tr.reduced_loss(loss)
+    tr.health_check()
 
     tokens_per_step = tr.tokens_per_step  # global: dp*ep*mbs*ga*seq
     tok_s = tokens_per_step * args.steps / elapsed

@@ -65,6 +65,8 @@ int st_xgmi_all_reduce(int64_t id, const void* in, void* out, int64_t n, int dty
 int st_xgmi_all_reduce_sim(const int64_t* ids, const void* const* ins, void* const* outs, int world, int64_t n,
                            int dtype, int mode, int blocks, hipStream_t st);
 int st_xgmi_error(int64_t id);
+int st_xgmi_set_timeout(int64_t id, double seconds);
+int st_xgmi_world(int64_t id);
 int st_xgmi_destroy(int64_t id);
 int st_qknorm_rope_bwd_blocks();
 int st_qknorm_rope_fwd(void* qkv, void* xsave, float* rstd, const void* wq, const void* wk, const float* cos_t,
@@ -338,15 +340,38 @@ void xgmi_open(int64_t id, int64_t r, const at::Tensor& h) {
 void xgmi_set_peer(int64_t id, int64_t r, int64_t peer) {
   TORCH_CHECK(st_xgmi_set_peer(id, (int)r, peer) == 0, "xgmi_set_peer");
 }
+// elements n the kernels are told about: the tensor (all-reduce), the per-rank
+// contribution (all-gather: out = world x in) or the output (reduce-scatter: in = world x out)
+static int64_t xgmi_count(int64_t mode, int64_t world, const at::Tensor& inp, const at::Tensor& out) {
+  if (mode == 2) {
+    TORCH_CHECK(out.numel() == world * inp.numel(), "xgmi all_gather: out must hold world x input elements");
+    return inp.numel();
+  }
+  if (mode == 3) {
+    TORCH_CHECK(inp.numel() == world * out.numel(), "xgmi reduce_scatter: input must hold world x out elements");
+    return out.numel();
+  }
+  TORCH_CHECK(mode == 0 || mode == 1, "xgmi: mode 0..3");
+  TORCH_CHECK(inp.numel() == out.numel(), "xgmi all_reduce: same size");
+  return inp.numel();
+}
+
 void xgmi_all_reduce(int64_t id, const at::Tensor& inp, at::Tensor out, int64_t mode, int64_t blocks) {
   TORCH_CHECK(inp.is_cuda() && out.is_cuda() && inp.device() == out.device(), "xgmi: GPU tensors");
-  TORCH_CHECK(inp.is_contiguous() && out.is_contiguous() && inp.numel() == out.numel() &&
-                  inp.scalar_type() == out.scalar_type(), "xgmi: contiguous, same shape/dtype");
+  TORCH_CHECK(inp.is_contiguous() && out.is_contiguous() && inp.scalar_type() == out.scalar_type(),
+              "xgmi: contiguous, same dtype");
   TORCH_CHECK(inp.scalar_type() == at::kBFloat16 || inp.scalar_type() == at::kFloat, "xgmi: bf16 or fp32");
+  const int world = st_xgmi_world(id);
+  TORCH_CHECK(world > 0, "xgmi: unknown communicator");
+  const int64_t n = xgmi_count(mode, world, inp, out);
+  TORCH_CHECK(mode < 2 || inp.data_ptr() != out.data_ptr(), "xgmi all_gather/reduce_scatter: out-of-place only");
   c10::hip::HIPGuardMasqueradingAsCUDA g(inp.device());
-  int rc = st_xgmi_all_reduce(id, inp.data_ptr(), out.data_ptr(), inp.numel(),
-                              inp.scalar_type() == at::kBFloat16 ? 0 : 1, (int)mode, (int)blocks, cur_stream());
-  TORCH_CHECK(rc == 0, "xgmi_all_reduce failed (", rc, "): size must be a multiple of 8 and fit the buffer");
+  int rc = st_xgmi_all_reduce(id, inp.data_ptr(), out.data_ptr(), n, inp.scalar_type() == at::kBFloat16 ? 0 : 1,
+                              (int)mode, (int)blocks, cur_stream());
+  TORCH_CHECK(rc == 0, "xgmi collective failed (", rc, "): size must be a multiple of 8 and fit the buffer");
+}
+void xgmi_set_timeout(int64_t id, double seconds) {
+  TORCH_CHECK(st_xgmi_set_timeout(id, seconds) == 0, "xgmi_set_timeout: bad id or value");
 }
 void xgmi_all_reduce_sim(std::vector<int64_t> ids, std::vector<at::Tensor> ins, std::vector<at::Tensor> outs,
                          int64_t mode, int64_t blocks) {
@@ -354,9 +379,10 @@ void xgmi_all_reduce_sim(std::vector<int64_t> ids, std::vector<at::Tensor> ins, 
   TORCH_CHECK(w >= 1 && ins.size() == w && outs.size() == w, "xgmi_all_reduce_sim: one in/out per rank");
   std::vector<const void*> ip(w);
   std::vector<void*> op(w);
+  const int64_t n = xgmi_count(mode, (int64_t)w, ins[0], outs[0]);
   for (size_t r = 0; r < w; ++r) {
     TORCH_CHECK(ins[r].is_cuda() && outs[r].is_cuda() && ins[r].is_contiguous() && outs[r].is_contiguous() &&
-                    ins[r].numel() == ins[0].numel() && outs[r].numel() == ins[0].numel() &&
+                    ins[r].numel() == ins[0].numel() && outs[r].numel() == outs[0].numel() &&
                     ins[r].scalar_type() == ins[0].scalar_type() && outs[r].scalar_type() == ins[0].scalar_type() &&
                     ins[r].device() == ins[0].device() && outs[r].device() == ins[0].device(),
                 "xgmi_all_reduce_sim: matching contiguous GPU tensors");
@@ -365,7 +391,7 @@ void xgmi_all_reduce_sim(std::vector<int64_t> ids, std::vector<at::Tensor> ins, 
   }
   TORCH_CHECK(ins[0].scalar_type() == at::kBFloat16 || ins[0].scalar_type() == at::kFloat, "xgmi: bf16 or fp32");
   c10::hip::HIPGuardMasqueradingAsCUDA g(ins[0].device());
-  int rc = st_xgmi_all_reduce_sim(ids.data(), ip.data(), op.data(), (int)w, ins[0].numel(),
+  int rc = st_xgmi_all_reduce_sim(ids.data(), ip.data(), op.data(), (int)w, n,
                                   ins[0].scalar_type() == at::kBFloat16 ? 0 : 1, (int)mode, (int)blocks,
                                   cur_stream());
   TORCH_CHECK(rc == 0, "xgmi_all_reduce_sim failed (", rc, ")");
@@ -615,6 +641,7 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("xgmi_all_reduce_sim(int[] ids, Tensor[] ins, Tensor(a!)[] outs, int mode, int blocks) -> ()",
         &xgmi_all_reduce_sim);
   m.def("xgmi_error(int id) -> int", &xgmi_error);
+  m.def("xgmi_set_timeout(int id, float seconds) -> ()", &xgmi_set_timeout);
   m.def("xgmi_destroy(int id) -> ()", &xgmi_destroy);
   m.def("qknorm_rope_fwd_(Tensor(a!) qkv, Tensor wq, Tensor wk, Tensor cos, Tensor sin, Tensor? pos, int H, int Hkv, float eps) -> Tensor[]");
   m.def("qknorm_rope_bwd_(Tensor(a!) dqkv, Tensor xsave, Tensor rstd, Tensor wq, Tensor wk, Tensor cos, Tensor sin, Tensor? pos, int H, int Hkv) -> Tensor");

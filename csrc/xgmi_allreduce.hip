@@ -1,4 +1,6 @@
-// Custom intra-node all-reduce over xGMI peer memory (one-shot / two-shot).
+// Custom intra-node collectives over xGMI peer memory: all-reduce (one-shot /
+// two-shot), all-gather and reduce-scatter (the sequence-parallel / CP K/V
+// collectives), on one flag protocol.
 //
 // Reference: the TP all-reduces of scaletorch (ReduceFromModelParallelRegion,
 // RowParallelLinear and the async grad-input all-reduce,
@@ -43,10 +45,11 @@ using namespace st;
 namespace {
 
 constexpr int kMaxRanks = 8;
-constexpr int kMaxBlocks = 64;
+constexpr int kMaxBlocks = 256;  // one 512-thread block per CU at most: every block co-resident
 constexpr int kThreads = 512;
 constexpr int64_t kFlagBytes = 2 * kMaxBlocks * kMaxRanks * 4;  // [phase][block][rank] uint32
-constexpr int64_t kHeader = 4096;                               // flags padded to 4 KiB
+constexpr int64_t kHeader = 16384;                              // flags padded to 16 KiB
+static_assert(kFlagBytes <= kHeader, "flag area");
 
 struct Peers {
   char* buf[kMaxRanks];
@@ -60,6 +63,7 @@ struct Job {
   void* out;
   int rank;
   int* err;
+  uint64_t timeout;  // spin bound in s_memrealtime ticks (100 MHz)
 };
 struct Jobs {
   Job j[kMaxRanks];
@@ -71,7 +75,8 @@ ST_DEVICE uint32_t* flag_ptr(char* base, int phase, int block, int rank) {
 
 // Per-block cross-rank barrier: tell every peer "my block b reached phase p of
 // epoch e", then wait until every peer told me the same.  Returns false on timeout.
-ST_DEVICE bool block_barrier(const Peers& P, int rank, int world, int phase, uint32_t epoch, int* err) {
+ST_DEVICE bool block_barrier(const Peers& P, int rank, int world, int phase, uint32_t epoch, int* err,
+                             uint64_t timeout) {
   // Every wave retires its own data stores first: __syncthreads() is only a
   // workgroup-scope fence and does NOT wait for global stores to complete, and the
   // flag thread's system release below only covers its own wave's stores.
@@ -85,7 +90,7 @@ ST_DEVICE bool block_barrier(const Peers& P, int rank, int world, int phase, uin
     uint32_t* mine = flag_ptr(P.buf[rank], phase, blockIdx.x, threadIdx.x);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
+      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {  // default 2 s at 100 MHz
         atomicExch(err, 1);
         ok = false;
         break;
@@ -201,7 +206,7 @@ __global__ __launch_bounds__(kThreads) void oneshot_kernel(Peers P, Jobs J, int 
   const int64_t lo = blockIdx.x * per, hi = min(n8, lo + per);
   const rsrc_t mine = buf_rsrc(P.buf[rank], cap);
   for (int64_t v = lo + threadIdx.x; v < hi; v += blockDim.x) put8<T>(mine, area_off<T>(0, parity, cap, v), in + v * 8);
-  if (!block_barrier(P, rank, world, 0, epoch, err)) return;
+  if (!block_barrier(P, rank, world, 0, epoch, err, jb.timeout)) return;
   for (int64_t v = lo + threadIdx.x; v < hi; v += blockDim.x) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int r = 0; r < world; ++r) {  // fixed rank order: bitwise identical on every rank
@@ -233,7 +238,7 @@ __global__ __launch_bounds__(kThreads) void twoshot_kernel(Peers P, Jobs J, int 
     for (int64_t v = p * P8 + lo + threadIdx.x; v < min(e, p * P8 + hi); v += blockDim.x)
       put8<T>(mine, area_off<T>(0, parity, cap, v), in + v * 8);
   }
-  if (!block_barrier(P, rank, world, 0, epoch, err)) return;
+  if (!block_barrier(P, rank, world, 0, epoch, err, jb.timeout)) return;
   // reduce-scatter: my partition, my slice
   const int64_t pe = min(n8, (rank + 1) * P8);
   for (int64_t v = rank * P8 + lo + threadIdx.x; v < min(pe, rank * P8 + hi); v += blockDim.x) {
@@ -246,13 +251,65 @@ __global__ __launch_bounds__(kThreads) void twoshot_kernel(Peers P, Jobs J, int 
     }
     sh_store8<T>(mine, area_off<T>(1, parity, cap, v), acc);
   }
-  if (!block_barrier(P, rank, world, 1, epoch, err)) return;
+  if (!block_barrier(P, rank, world, 1, epoch, err, jb.timeout)) return;
   // all-gather: partition p from rank p's result area
   for (int p = 0; p < world; ++p) {
     const rsrc_t src = buf_rsrc(P.buf[p], cap);
     const int64_t e = min(n8, (p + 1) * P8);
     for (int64_t v = p * P8 + lo + threadIdx.x; v < min(e, p * P8 + hi); v += blockDim.x)
       get8<T>(src, area_off<T>(1, parity, cap, v), out + v * 8);
+  }
+}
+
+// All-gather: every rank contributes n8 vectors; out = [rank 0 | rank 1 | ...] (n8 each).
+// Block b owns slice b of the contribution; after the handshake it copies slice b
+// of every peer's contribution over xGMI (all W-1 links busy at once).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void allgather_kernel(Peers P, Jobs J, int world, int64_t n8, int64_t cap,
+                                                             uint32_t epoch) {
+  const Job& jb = J.j[blockIdx.y];
+  const int rank = jb.rank;
+  const T* __restrict__ in = (const T*)jb.in;
+  T* __restrict__ out = (T*)jb.out;
+  const int parity = epoch & 1;
+  const int64_t per = (n8 + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = blockIdx.x * per, hi = min(n8, lo + per);
+  const rsrc_t mine = buf_rsrc(P.buf[rank], cap);
+  for (int64_t v = lo + threadIdx.x; v < hi; v += blockDim.x) put8<T>(mine, area_off<T>(0, parity, cap, v), in + v * 8);
+  if (!block_barrier(P, rank, world, 0, epoch, jb.err, jb.timeout)) return;
+  for (int r = 0; r < world; ++r) {
+    const rsrc_t src = buf_rsrc(P.buf[r], cap);
+    for (int64_t v = lo + threadIdx.x; v < hi; v += blockDim.x)
+      get8<T>(src, area_off<T>(0, parity, cap, v), out + ((int64_t)r * n8 + v) * 8);
+  }
+}
+
+// Reduce-scatter: every rank contributes W * n8 vectors; rank r keeps the fp32 sum
+// (fixed rank order) of partition r = vectors [r n8, (r+1) n8) -> out (n8 vectors).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void reducescatter_kernel(Peers P, Jobs J, int world, int64_t n8,
+                                                                 int64_t cap, uint32_t epoch) {
+  const Job& jb = J.j[blockIdx.y];
+  const int rank = jb.rank;
+  const T* __restrict__ in = (const T*)jb.in;
+  T* __restrict__ out = (T*)jb.out;
+  const int parity = epoch & 1;
+  const int64_t per = (n8 + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = blockIdx.x * per, hi = min(n8, lo + per);
+  const rsrc_t mine = buf_rsrc(P.buf[rank], cap);
+  for (int p = 0; p < world; ++p)
+    for (int64_t v = lo + threadIdx.x; v < hi; v += blockDim.x)
+      put8<T>(mine, area_off<T>(0, parity, cap, (int64_t)p * n8 + v), in + ((int64_t)p * n8 + v) * 8);
+  if (!block_barrier(P, rank, world, 0, epoch, jb.err, jb.timeout)) return;
+  for (int64_t v = lo + threadIdx.x; v < hi; v += blockDim.x) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < world; ++r) {
+      float f[8];
+      sh_load8<T>(buf_rsrc(P.buf[r], cap), area_off<T>(0, parity, cap, (int64_t)rank * n8 + v), f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += f[i];
+    }
+    store_local8<T>(out + v * 8, acc);
   }
 }
 
@@ -265,7 +322,23 @@ struct Comm {
   int* err = nullptr;
   uint32_t epoch = 0;
   int device = 0;
+  uint64_t timeout = 200000000ull;  // 2 s of s_memrealtime ticks
 };
+
+// mode: 0 one-shot all-reduce, 1 two-shot all-reduce, 2 all-gather, 3 reduce-scatter.
+// n = elements of the per-rank CONTRIBUTION (all-gather) / of the OUTPUT (reduce-scatter) /
+// of the tensor (all-reduce).
+template <typename T>
+static void launch_t(const Peers& P, const Jobs& J, dim3 grid, int world, int64_t n8, int64_t cap, int mode,
+                     uint32_t epoch, hipStream_t st) {
+  switch (mode) {
+    case 0: oneshot_kernel<T><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch); break;
+    case 1: twoshot_kernel<T><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch); break;
+    case 2: allgather_kernel<T><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch); break;
+    default: reducescatter_kernel<T><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch); break;
+  }
+}
+
 
 std::mutex g_mu;
 std::vector<Comm*> g_comms;
@@ -356,33 +429,47 @@ int st_xgmi_set_peer(int64_t id, int r, int64_t peer_id) {
 
 static int launch(const Peers& P, const Jobs& J, int njobs, int world, int64_t n, int64_t cap, int dtype,
                   int mode, int blocks, uint32_t epoch, hipStream_t st) {
-  const int64_t n8 = n / 8;
   const dim3 grid(blocks, njobs);
-  if (dtype == 0) {
-    if (mode == 0) oneshot_kernel<bf16_t><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch);
-    else twoshot_kernel<bf16_t><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch);
-  } else {
-    if (mode == 0) oneshot_kernel<float><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch);
-    else twoshot_kernel<float><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch);
-  }
+  if (dtype == 0) launch_t<bf16_t>(P, J, grid, world, n / 8, cap, mode, epoch, st);
+  else launch_t<float>(P, J, grid, world, n / 8, cap, mode, epoch, st);
   return (int)hipGetLastError();
 }
 
-// In-place-or-not all-reduce of n elements (dtype 0 = bf16, 1 = fp32); mode 0 =
-// one-shot, 1 = two-shot.  n must be a multiple of 8 and n * elt <= cap.
+// bytes of one data area a collective of n elements needs on each rank
+static int64_t area_bytes(int mode, int world, int64_t n, int64_t elt) {
+  return mode == 3 ? (int64_t)world * n * elt : n * elt;
+}
+
+// Collective of n elements (dtype 0 = bf16, 1 = fp32); mode 0 = one-shot all-reduce,
+// 1 = two-shot all-reduce (in place allowed), 2 = all-gather (n per rank, out holds
+// world * n), 3 = reduce-scatter (in holds world * n, out n).  n must be a multiple
+// of 8 and fit the data area (cap bytes).
 int st_xgmi_all_reduce(int64_t id, const void* in, void* out, int64_t n, int dtype, int mode, int blocks,
                        hipStream_t st) {
   Comm* c = get(id);
-  if (!c) return -2;
+  if (!c || mode < 0 || mode > 3) return -2;
   const int64_t elt = dtype == 0 ? 2 : 4;
-  if (n % 8 || n * elt > c->cap || ((uintptr_t)in | (uintptr_t)out) % 16) return -2;
+  if (n % 8 || area_bytes(mode, c->world, n, elt) > c->cap || ((uintptr_t)in | (uintptr_t)out) % 16) return -2;
   for (int r = 0; r < c->world; ++r)
     if (!c->peers.buf[r]) return -3;
   if (n == 0) return 0;
   if (blocks <= 0 || blocks > kMaxBlocks) blocks = kMaxBlocks;
   Jobs J{};
-  J.j[0] = Job{in, out, c->rank, c->err};
+  J.j[0] = Job{in, out, c->rank, c->err, c->timeout};
   return launch(c->peers, J, 1, c->world, n, c->cap, dtype, mode, blocks, ++c->epoch, st);
+}
+
+int st_xgmi_world(int64_t id) {
+  Comm* c = get(id);
+  return c ? c->world : -2;
+}
+
+// Bound (seconds) on every cross-rank wait of this communicator's kernels.
+int st_xgmi_set_timeout(int64_t id, double seconds) {
+  Comm* c = get(id);
+  if (!c || !(seconds > 0)) return -2;
+  c->timeout = (uint64_t)(seconds * 1e8);
+  return 0;
 }
 
 // Simulation: comms ids[0..world) (wired with st_xgmi_set_peer, one process)
@@ -394,14 +481,14 @@ int st_xgmi_all_reduce_sim(const int64_t* ids, const void* const* ins, void* con
   Comm* c0 = get(ids[0]);
   if (!c0 || c0->world != world) return -2;
   const int64_t elt = dtype == 0 ? 2 : 4;
-  if (n % 8 || n * elt > c0->cap) return -2;
+  if (mode < 0 || mode > 3 || n % 8 || area_bytes(mode, world, n, elt) > c0->cap) return -2;
   if (blocks <= 0 || blocks > kMaxBlocks) blocks = kMaxBlocks;
   uint32_t epoch = 0;
   for (int r = 0; r < world; ++r) {
     Comm* c = get(ids[r]);
     if (!c || c->rank != r || c->world != world || c->cap != c0->cap) return -2;
     if (((uintptr_t)ins[r] | (uintptr_t)outs[r]) % 16) return -2;
-    J.j[r] = Job{ins[r], outs[r], r, c->err};
+    J.j[r] = Job{ins[r], outs[r], r, c->err, c->timeout};
     epoch = ++c->epoch;  // every comm advances together
   }
   if (n == 0) return 0;

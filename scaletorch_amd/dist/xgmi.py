@@ -1,4 +1,5 @@
-"""Intra-node custom all-reduce over xGMI peer memory (csrc/xgmi_allreduce.hip).
+"""Intra-node custom collectives over xGMI peer memory (csrc/xgmi_allreduce.hip):
+all-reduce, all-gather and reduce-scatter on one IPC buffer + flag protocol.
 
 The reference sends every tensor-parallel all-reduce through NCCL/HCCL
 (scaletorch/parallel/tensor_parallel/tp_comms.py:117-166, :229-320; SURVEY.md
@@ -14,8 +15,14 @@ each of the others, so a TP group can all-reduce by READING its peers' buffers:
   two-shot (reduce-scatter into a result area, handshake, all-gather) above it;
   fp32 accumulation in a fixed rank order, so every rank gets bitwise the same
   result; anything that does not fit (size, dtype, alignment) goes to RCCL;
-* every wait is bounded: a peer that never arrives sets an error word
-  (``check()``) instead of hanging the GPU.
+* ``all_gather(t)`` / ``reduce_scatter(t)``: every rank publishes its input once,
+  then block b of every rank pulls slice b of ALL peers' data at once (all 7
+  links busy) -- the sequence-parallel activation gather / gradient scatter;
+* up to 256 workgroups (one per CU) pull at once, sized by message;
+* every wait is bounded (``ST_XGMI_TIMEOUT_S``, default 2 s): a peer that never
+  arrives sets an error word instead of hanging the GPU; ``check()`` (polled by the
+  trainer at every logging step, tensor_parallel.check_xgmi) turns it into an
+  exception so the job exits non-zero and a torchrun restart can resume.
 
 Use: ``XgmiAllReduce(group)`` collectively on every rank of ``group`` (all ranks
 on ONE node, one GPU each), then ``comm.all_reduce(t)`` in the same order on all
@@ -38,8 +45,12 @@ def _ops():
 
 
 def _blocks_for(nbytes: int) -> int:
-    """Workgroups per rank: ~64 KiB of message per block, 8..64 blocks."""
-    return int(min(64, max(8, nbytes // (64 << 10))))
+    """Workgroups per rank: ~64 KiB of message per block, 8..256 blocks (one per CU
+    at most, so every block of the grid is co-resident)."""
+    return int(min(256, max(8, nbytes // (64 << 10))))
+
+
+_MODES = {"oneshot": 0, "twoshot": 1, "all_gather": 2, "reduce_scatter": 3}
 
 
 class XgmiAllReduce:
@@ -54,13 +65,18 @@ class XgmiAllReduce:
         cls._serial += 1
         return (cls._serial % 255) << 24
 
-    def __init__(self, group=None, max_bytes: int = 64 << 20, oneshot_max: int = 512 << 10, _sim=None):
+    def __init__(self, group=None, max_bytes: int = 64 << 20, oneshot_max: int = 512 << 10, _sim=None,
+                 timeout_s: float | None = None):
+        import os
+
         self.group = group
         self.oneshot_max = oneshot_max
         self.cap = (max_bytes + 255) // 256 * 256
+        self.timeout_s = float(timeout_s if timeout_s is not None else os.environ.get("ST_XGMI_TIMEOUT_S", "2.0"))
         if _sim is not None:  # in-process simulation (tests): (rank, world, epoch base)
             self.rank, self.world, base = _sim
             self.id = int(_ops().xgmi_create(self.rank, self.world, self.cap, base))
+            _ops().xgmi_set_timeout(self.id, self.timeout_s)
             return
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -71,6 +87,7 @@ class XgmiAllReduce:
         if len({h for h, _ in where}) != 1 or len({d for _, d in where}) != self.world:
             raise ValueError(f"xgmi all-reduce needs one GPU per rank on one node, got {where}")
         self.id = int(_ops().xgmi_create(self.rank, self.world, self.cap, self._next_base()))
+        _ops().xgmi_set_timeout(self.id, self.timeout_s)
         mine = _ops().xgmi_handle(self.id).tolist()
         handles = [None] * self.world
         dist.all_gather_object(handles, mine, group=group)
@@ -80,7 +97,8 @@ class XgmiAllReduce:
         dist.barrier(group=group)
 
     @classmethod
-    def simulate(cls, world: int, max_bytes: int = 8 << 20, oneshot_max: int = 512 << 10):
+    def simulate(cls, world: int, max_bytes: int = 8 << 20, oneshot_max: int = 512 << 10,
+                 timeout_s: float | None = None):
         """``world`` communicators in THIS process wired to each other's buffers
         (one GPU), for tests: ``all_reduce_sim`` runs every rank's job in ONE launch
         (rank = blockIdx.y), exercising the kernels and the cross-rank flag protocol
@@ -88,16 +106,46 @@ class XgmiAllReduce:
         a process's streams onto a few shared hardware queues, and two spinning
         kernels on one queue serialise.)"""
         base = cls._next_base()
-        comms = [cls(max_bytes=max_bytes, oneshot_max=oneshot_max, _sim=(r, world, base)) for r in range(world)]
+        comms = [cls(max_bytes=max_bytes, oneshot_max=oneshot_max, _sim=(r, world, base), timeout_s=timeout_s)
+                 for r in range(world)]
         for c in comms:
             for r, p in enumerate(comms):
                 _ops().xgmi_set_peer(c.id, r, p.id)
         return comms
 
-    def supports(self, t: torch.Tensor) -> bool:
+    def supports(self, t: torch.Tensor, scale: int = 1) -> bool:
+        """``t`` can go through the kernels; ``scale`` = data-area multiple the op needs
+        (reduce-scatter publishes world x its output)."""
         return (t.is_cuda and t.dtype in (torch.bfloat16, torch.float32) and t.is_contiguous()
-                and t.numel() % 8 == 0 and t.numel() * t.element_size() <= self.cap
+                and t.numel() % 8 == 0 and t.numel() * t.element_size() * scale <= self.cap
                 and t.data_ptr() % 16 == 0)
+
+    def all_gather(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """[n] per rank -> [world * n] in rank order (RCCL when the kernels do not apply)."""
+        if out is None:
+            out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        if not self.supports(t) or out.data_ptr() % 16:
+            dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+            return out
+        _ops().xgmi_all_reduce(self.id, t, out, _MODES["all_gather"], _blocks_for(t.numel() * t.element_size()))
+        return out
+
+    def reduce_scatter(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """[world * n] per rank -> this rank's [n] of the sum (fp32 accumulation, fixed order)."""
+        if out is None:
+            out = torch.empty((t.shape[0] // self.world,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        if not self.supports(out, scale=self.world) or not self.supports(t) or out.data_ptr() % 16:
+            dist.reduce_scatter_tensor(out, t.contiguous(), group=self.group)
+            return out
+        _ops().xgmi_all_reduce(self.id, t, out, _MODES["reduce_scatter"],
+                               _blocks_for(out.numel() * out.element_size()))
+        return out
+
+    @staticmethod
+    def collective_sim(comms, ins, outs, op: str) -> None:
+        """Simulation of ``op`` (all_gather | reduce_scatter) across ``comms`` in ONE launch."""
+        nbytes = (ins[0] if op == "all_gather" else outs[0]).numel() * ins[0].element_size()
+        _ops().xgmi_all_reduce_sim([c.id for c in comms], ins, outs, _MODES[op], _blocks_for(nbytes))
 
     def all_reduce(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         """Sum of ``t`` over the group into ``out`` (default: in place)."""
@@ -119,11 +167,15 @@ class XgmiAllReduce:
         _ops().xgmi_all_reduce_sim([c.id for c in comms], ins, outs, mode, _blocks_for(nbytes))
 
     def check(self) -> None:
-        """Raise if any all-reduce of this communicator timed out (host sync)."""
+        """Raise if any collective of this communicator timed out (host sync)."""
         if int(_ops().xgmi_error(self.id)):
-            raise RuntimeError("xgmi all-reduce: a peer did not arrive within 2 s (rank died or call order differs)")
+            raise RuntimeError(f"xgmi collective: a peer did not arrive within {self.timeout_s:g} s (rank died or "
+                               "call order differs); outputs since then are invalid")
 
     def close(self) -> None:
         if getattr(self, "id", None) is not None:
             _ops().xgmi_destroy(self.id)
             self.id = None
+
+
+XgmiComm = XgmiAllReduce  # the communicator carries all three collectives

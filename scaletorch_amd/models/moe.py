@@ -28,6 +28,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..dist import collectives as C
+from ..dist import trace
 from ..parallel import mesh
 from ..parallel.tensor_parallel import (AllGatherFromSequenceParallelRegion, ReduceFromTensorParallelRegion,
                                         ReduceScatterToSequenceParallelRegion)
@@ -39,6 +40,7 @@ class _AllToAll(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, out_splits, in_splits, group):
+        trace.record("ep.all_to_all", x, group_size=C.get_world_size(group), send=list(in_splits), recv=list(out_splits))
         ctx.splits = (out_splits, in_splits)
         ctx.group = group
         return C.all_to_all(x.contiguous(), group=group, output_split_sizes=out_splits, input_split_sizes=in_splits)
@@ -46,6 +48,7 @@ class _AllToAll(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         out_splits, in_splits = ctx.splits
+        trace.record("ep.all_to_all_bwd", g, group_size=C.get_world_size(ctx.group))
         return (C.all_to_all(g.contiguous(), group=ctx.group, output_split_sizes=in_splits,
                              input_split_sizes=out_splits), None, None, None)
 

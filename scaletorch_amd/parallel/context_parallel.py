@@ -27,6 +27,7 @@ import torch
 
 from .. import ops
 from ..dist import collectives as C
+from ..dist import trace
 from ..ops import _lib
 from . import mesh
 
@@ -63,6 +64,7 @@ def _gather_seq_dim1(x: torch.Tensor, group) -> torch.Tensor:
 
 def _reduce_scatter_seq_dim1(x: torch.Tensor, group) -> torch.Tensor:
     xt = x.transpose(0, 1).contiguous()
+    trace.record("cp.dkv_reduce_scatter", xt, group_size=C.get_world_size(group))
     out = C.reduce_scatter(xt, group=group)
     return out.transpose(0, 1)
 
@@ -85,6 +87,7 @@ class _CPAttnFn(torch.autograd.Function):
         B, s = q.shape[0], q.shape[1]
         S = s * cp
         xt = kv.transpose(0, 1).contiguous()
+        trace.record("cp.kv_all_gather", xt, group_size=cp)
         gathered, work = C.all_gather(xt, group=group, async_op=True)
         chunks = _chunks_of(rank, S, cp, s, zigzag)
         parts = []
@@ -158,6 +161,8 @@ def _ring_exchange(tensors: list[torch.Tensor], group, cp: int, rank: int):
     prv = C.global_rank_of(group, (rank - 1) % cp)
     recv = [torch.empty_like(t) for t in tensors]
     ops = []
+    for t in tensors:
+        trace.record("cp.ring_send_recv", t, peer=f"{nxt}<-{prv}", group_size=cp)
     for t, r in zip(tensors, recv):
         ops.append(dist.P2POp(dist.isend, t, nxt, group))
         ops.append(dist.P2POp(dist.irecv, r, prv, group))
@@ -257,6 +262,7 @@ def _merge(acc: torch.Tensor, lse: torch.Tensor, bo: torch.Tensor, bl: torch.Ten
 # ---------------------------------------------------------------- Ulysses (all-to-all) transport
 def _a2a(x: torch.Tensor, group) -> torch.Tensor:
     """all_to_all_single over dim 0 (= destination rank on input, source rank on output)."""
+    trace.record("cp.ulysses_all_to_all", x, group_size=C.get_world_size(group))
     return C.all_to_all(x.contiguous(), group=group)
 
 

@@ -28,6 +28,7 @@ import torch
 import torch.distributed as dist
 
 from ..dist import collectives as C
+from ..dist import trace
 from . import mesh
 
 _STATS = {"send_forward": 0, "recv_forward": 0, "send_backward": 0, "recv_backward": 0}
@@ -66,17 +67,21 @@ def _p2p(send_fwd=None, send_bwd=None, recv_fwd_shape=None, recv_bwd_shape=None,
     if send_fwd is not None and pg.pp_next_rank is not None:
         ops.append(dist.P2POp(dist.isend, send_fwd.contiguous(), pg.pp_next_rank, group))
         _STATS["send_forward"] += 1
+        trace.record("pp.send_forward", send_fwd, peer=pg.pp_next_rank)
     if send_bwd is not None and pg.pp_prev_rank is not None:
         ops.append(dist.P2POp(dist.isend, send_bwd.contiguous(), pg.pp_prev_rank, group))
         _STATS["send_backward"] += 1
+        trace.record("pp.send_backward", send_bwd, peer=pg.pp_prev_rank)
     if recv_fwd_shape is not None and pg.pp_prev_rank is not None:
         rf = torch.empty(recv_fwd_shape, dtype=dtype, device=device)
         ops.append(dist.P2POp(dist.irecv, rf, pg.pp_prev_rank, group))
         _STATS["recv_forward"] += 1
+        trace.record("pp.recv_forward", rf, peer=pg.pp_prev_rank)
     if recv_bwd_shape is not None and pg.pp_next_rank is not None:
         rb = torch.empty(recv_bwd_shape, dtype=dtype, device=device)
         ops.append(dist.P2POp(dist.irecv, rb, pg.pp_next_rank, group))
         _STATS["recv_backward"] += 1
+        trace.record("pp.recv_backward", rb, peer=pg.pp_next_rank)
     if ops:
         works = dist.batch_isend_irecv(ops)
         if rf is None and rb is None:

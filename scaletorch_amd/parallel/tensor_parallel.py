@@ -67,6 +67,9 @@ class _StreamWork:
 
 def _tp_all_reduce(x: torch.Tensor, group, async_op: bool = False):
     """Sum over the TP group; returns a handle with ``wait()`` when ``async_op``."""
+    from ..dist import trace
+
+    trace.record("tp.all_reduce", x, group_size=_ws(group), transport=_TP_COMM, overlapped=async_op)
     if _TP_COMM == "xgmi" and x.is_cuda and group is not None:
         from ..dist.xgmi import XgmiAllReduce
 
@@ -87,6 +90,25 @@ def _tp_all_reduce(x: torch.Tensor, group, async_op: bool = False):
             x.record_stream(st)
             return _StreamWork(st)
     return C.all_reduce(x, group=group, async_op=async_op)
+
+
+def _xgmi_comm(group):
+    """The xGMI communicator of ``group`` when --tp_comm xgmi is active (else None)."""
+    if _TP_COMM != "xgmi" or group is None or _ws(group) == 1:
+        return None
+    from ..dist.xgmi import XgmiAllReduce
+
+    comm = _XGMI.get(id(group))
+    if comm is None:
+        comm = _XGMI[id(group)] = XgmiAllReduce(group)
+    return comm
+
+
+def check_xgmi() -> None:
+    """Raise if any xGMI collective of this process timed out (one host sync per
+    communicator; the trainer polls it at logging steps -- ADVICE r1)."""
+    for comm in list(_XGMI.values()):
+        comm.check()
 
 
 class CopyToTensorParallelRegion(torch.autograd.Function):
@@ -165,12 +187,12 @@ def _gather_seq(x: torch.Tensor, group) -> torch.Tensor:
     ws = _ws(group)
     if ws == 1:
         return x
+    xg = _xgmi_comm(group) if x.is_cuda else None
+    gather = xg.all_gather if xg is not None else (lambda t: C.all_gather(t, group=group))
     if x.shape[0] == 1:
-        out = C.all_gather(x[0].contiguous(), group=group)
-        return out.unsqueeze(0)
+        return gather(x[0].contiguous()).unsqueeze(0)
     xt = x.transpose(0, 1).contiguous()  # [S/tp, B, ...]
-    out = C.all_gather(xt, group=group)
-    return out.transpose(0, 1).contiguous()
+    return gather(xt).transpose(0, 1).contiguous()
 
 
 def _reduce_scatter_seq(x: torch.Tensor, group) -> torch.Tensor:
@@ -178,11 +200,12 @@ def _reduce_scatter_seq(x: torch.Tensor, group) -> torch.Tensor:
     ws = _ws(group)
     if ws == 1:
         return x
+    xg = _xgmi_comm(group) if x.is_cuda else None
+    scatter = xg.reduce_scatter if xg is not None else (lambda t: C.reduce_scatter(t, group=group))
     if x.shape[0] == 1:
-        return C.reduce_scatter(x[0].contiguous(), group=group).unsqueeze(0)
+        return scatter(x[0].contiguous()).unsqueeze(0)
     xt = x.transpose(0, 1).contiguous()
-    out = C.reduce_scatter(xt, group=group)
-    return out.transpose(0, 1).contiguous()
+    return scatter(xt).transpose(0, 1).contiguous()
 
 
 def _gather_seq_async(x: torch.Tensor, group):

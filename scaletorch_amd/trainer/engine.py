@@ -262,6 +262,15 @@ class Trainer:
         if self.data is not None and hasattr(self.data, "skip_batches"):
             self.data.skip_batches(self.step * self.args.gradient_accumulation_steps)
 
+    def health_check(self) -> None:
+        """Raise if a custom xGMI collective timed out since the last check (its
+        outputs are invalid); called at logging steps by tools/train.py and at the
+        end of bench.py so the job exits non-zero instead of training on garbage."""
+        if self.args.tp_comm == "xgmi":
+            from ..parallel.tensor_parallel import check_xgmi
+
+            check_xgmi()
+
     def reduced_loss(self, loss: torch.Tensor) -> float:
         """Mean loss over data-parallel replicas (last PP stage holds it); host sync."""
         pg = mesh.pgm

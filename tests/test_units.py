@@ -393,3 +393,23 @@ def test_loader_skip_batches_resumes_position():
     again.skip_batches(4)
     assert torch.equal(next(again)["input_ids"], seq[4])
     assert torch.equal(next(again)["input_ids"], seq[5]) and again.epoch == 1
+
+
+def _trace_worker(rank, world):
+    from scaletorch_amd.dist import trace
+    from tests.test_parallel_parity import _run_one_step
+
+    trace.set_verbose(True)
+    trace.reset()
+    _run_one_step("tiny-llama", pipeline_parallel_size=2, micro_batch_size=2, gradient_accumulation_steps=2)
+    return trace.stats()
+
+
+def test_verbose_comm_tracing_counts_pp_ops():
+    """VERBOSE tracing: every PP p2p call is recorded with its bytes (reference
+    cp_comms.py:60-70 / pp_comms.py:18-26 log lines + get_communication_stats)."""
+    from tests.dist_harness import run_workers
+
+    s0, s1 = run_workers(_trace_worker, 2)
+    assert s0["pp.send_forward"]["calls"] == 2 and s1["pp.recv_forward"]["calls"] == 2
+    assert s1["pp.send_backward"]["calls"] == 2 and s0["pp.send_forward"]["bytes"] > 0

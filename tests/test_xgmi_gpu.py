@@ -111,3 +111,55 @@ def test_xgmi_ipc_processes_same_gpu(world):
     assert kinds == {"ok"}, got
     sums = [v for _, _, v in sorted(got)]
     assert all(s == sums[0] for s in sums)  # identical reduced tensors on every rank
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("n", [8, 4096 + 8, 200_000])
+def test_xgmi_allgather_reducescatter_simulated(world, dtype, n):
+    """all-gather: rank order concatenation, bitwise; reduce-scatter: rank r's slice of
+    the fp32-accumulated sum, bitwise identical to the all-reduce's slice."""
+    assert _lib.load(), _lib.load_error()
+    comms = XgmiAllReduce.simulate(world, max_bytes=8 << 20)
+    try:
+        torch.manual_seed(1)
+        xs = [torch.randn(n, device="cuda", dtype=dtype) for _ in range(world)]
+        outs = [torch.empty(world * n, device="cuda", dtype=dtype) for _ in range(world)]
+        for _ in range(2):
+            XgmiAllReduce.collective_sim(comms, xs, outs, "all_gather")
+            torch.cuda.synchronize()
+            ref = torch.cat(xs)
+            for o in outs:
+                assert torch.equal(o, ref)
+        big = [torch.randn(world * n, device="cuda", dtype=dtype) for _ in range(world)]
+        rs = [torch.empty(n, device="cuda", dtype=dtype) for _ in range(world)]
+        ar = [torch.empty(world * n, device="cuda", dtype=dtype) for _ in range(world)]
+        for _ in range(2):
+            XgmiAllReduce.collective_sim(comms, big, rs, "reduce_scatter")
+            XgmiAllReduce.all_reduce_sim(comms, big, ar)
+            torch.cuda.synchronize()
+            for c in comms:
+                c.check()
+            tot = sum(b.float() for b in big)
+            for r in range(world):
+                assert torch.equal(rs[r], ar[0][r * n:(r + 1) * n])
+                assert ((rs[r].float() - tot[r * n:(r + 1) * n]).norm() / tot[r * n:(r + 1) * n].norm()) < 1e-2
+    finally:
+        for c in comms:
+            c.close()
+
+
+def test_xgmi_absent_peer_times_out_and_check_raises():
+    """A peer that never joins: the kernel gives up after the configured timeout (no
+    GPU hang), the output is not produced, and check() raises."""
+    comms = XgmiAllReduce.simulate(2, max_bytes=1 << 20, timeout_s=0.05)
+    try:
+        x = torch.randn(4096, device="cuda", dtype=torch.bfloat16)
+        comms[0].all_reduce(x)  # rank 1 never calls
+        torch.cuda.synchronize()
+        with pytest.raises(RuntimeError, match="did not arrive"):
+            comms[0].check()
+        comms[1].check()  # the absent rank itself saw no error
+    finally:
+        for c in comms:
+            c.close()

@@ -121,6 +121,7 @@ def main(argv=None) -> int:
             if prof is not None:
                 prof.step()
             if log_now:
+                tr.health_check()  # xGMI collective timeouts -> non-zero exit (restart + --auto_resume)
                 loss = tr.reduced_loss(loss_t)
                 if args.nan_check and loss != loss:
                     raise FloatingPointError(f"non-finite loss at step {tr.step}")
