@@ -12,6 +12,11 @@ MNIST.  Launch modes:
   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/mnist/mnist_ddp.py --mode ddp
   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/mnist/mnist_ddp.py --mode arena
   python examples/mnist/mnist_ddp.py --mode spawn --nproc 2 --cpu   # mp.spawn launcher
+  torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/mnist/mnist_ddp.py --mode fsdp  # FSDP1
+
+Reference file -> mode: basic_mnist.py -> single, multigpu_mnist.py -> spawn,
+torchrun_mnist.py -> ddp, fsdp_mnist.py -> fsdp (FullyShardedDataParallel with a
+size-based auto-wrap policy and a full-state-dict checkpoint of the sharded model).
 """
 from __future__ import annotations
 
@@ -50,7 +55,8 @@ def load_data(path: str | None, n: int):
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", default="ddp", choices=["single", "ddp", "arena", "spawn"])
+    ap.add_argument("--mode", default="ddp", choices=["single", "ddp", "arena", "spawn", "fsdp"])
+    ap.add_argument("--save-model", default="", help="fsdp: write the full (gathered) state dict here")
     ap.add_argument("--nproc", type=int, default=2)
     ap.add_argument("--epochs", type=int, default=2)
     ap.add_argument("--batch-size", type=int, default=64)
@@ -68,7 +74,7 @@ def train(args) -> dict:
     from scaletorch_amd.models.attention_variants import LeNet
     from scaletorch_amd.parallel.data_parallel import DataParallel
 
-    distributed = args.mode in ("ddp", "arena")
+    distributed = args.mode in ("ddp", "arena", "fsdp")
     if distributed:
         rank, local_rank, world = init_dist(backend="gloo" if args.cpu else None, use_cpu=args.cpu)
     else:
@@ -80,6 +86,14 @@ def train(args) -> dict:
         model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local_rank] if dev.type == "cuda" else None)
     elif args.mode == "arena":
         model = DataParallel(model, bucket_size=1 << 20, expose_grads=True)  # flat fp32 grad arena + RCCL buckets
+    elif args.mode == "fsdp":
+        import functools
+
+        from torch.distributed.fsdp import FullyShardedDataParallel as FSDP
+        from torch.distributed.fsdp.wrap import size_based_auto_wrap_policy
+
+        policy = functools.partial(size_based_auto_wrap_policy, min_num_params=20000)  # fc1 gets its own unit
+        model = FSDP(model, auto_wrap_policy=policy, device_id=dev, use_orig_params=True)
     opt = torch.optim.Adadelta(model.parameters(), lr=args.lr)
     sched = torch.optim.lr_scheduler.StepLR(opt, step_size=1, gamma=args.gamma)
     x, y = load_data(args.data, args.samples)
@@ -107,6 +121,12 @@ def train(args) -> dict:
     with torch.no_grad():
         pred = model(xt.to(dev)).argmax(1).cpu()
     acc = (pred == yt).float().mean().item()
+    if args.mode == "fsdp" and args.save_model:
+        from torch.distributed.checkpoint.state_dict import StateDictOptions, get_model_state_dict
+
+        sd = get_model_state_dict(model, options=StateDictOptions(full_state_dict=True, cpu_offload=dev.type == "cuda"))
+        if rank == 0:
+            torch.save(sd, args.save_model)
     if rank == 0:
         print(f"mnist[{args.mode}] world {world}: test accuracy {acc:.3f} after {steps} steps", flush=True)
     return {"acc": acc, "steps": steps, "world": world}

@@ -23,8 +23,8 @@ def test_mingpt_dp2_cpu_gloo(tmp_path):
     assert float(m.group(1)) < 2.5  # char vocab ~ 20: ln(20)=3.0 at init
 
 
-def _torchrun(script, args, port, timeout=600):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+def _torchrun(script, args, port, timeout=600, n=2):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, script), *args]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
@@ -126,3 +126,45 @@ def test_profile_mfu_tool_breakdown():
     # 3 GEMM passes of 2*T*N_matmul each (T = 8192 tokens, 7.5e9 matmul params)
     assert abs(d["components"]["gemm_fwd"]["tflop"] - 122.96) < 0.5
     assert 40 < d["mfu_pct"] < 50
+
+
+@pytest.mark.slow
+def test_fsdp2_tp_llama_loss_parallel_dcp_resume_offload(tmp_path):
+    """2-D FSDP2 x TP (DTensor SP plan + loss_parallel) on 4 gloo ranks: step-0 loss
+    equals the TP=1 run's (same replica batch), a DCP resume continues the exact
+    trajectory, and the CPU-offload mode trains."""
+    def losses(out):
+        return {int(a): float(b) for a, b in re.findall(r"step (\d+) loss ([0-9.]+)", out)}
+
+    ck = str(tmp_path / "ck")
+    full = losses(_torchrun("examples/fsdp2/fsdp2_tp_llama.py", ["--cpu", "--tp", "2", "--steps", "3",
+                                                                  "--ckpt-dir", str(tmp_path / "full")], 29651, n=4))
+    tp1 = losses(_torchrun("examples/fsdp2/fsdp2_tp_llama.py", ["--cpu", "--tp", "1", "--steps", "1",
+                                                                 "--ckpt-dir", str(tmp_path / "tp1")], 29652, n=4))
+    assert abs(full[0] - tp1[0]) < 1e-4, (full, tp1)
+    _torchrun("examples/fsdp2/fsdp2_tp_llama.py", ["--cpu", "--tp", "2", "--steps", "2", "--ckpt-dir", ck], 29653, n=4)
+    res = losses(_torchrun("examples/fsdp2/fsdp2_tp_llama.py", ["--cpu", "--tp", "2", "--steps", "1", "--resume",
+                                                                 "--ckpt-dir", ck], 29654, n=4))
+    assert abs(res[2] - full[2]) < 1e-4, (res, full)
+    off = _torchrun("examples/fsdp2/fsdp2_tp_llama.py", ["--cpu", "--tp", "2", "--steps", "1", "--cpu-offload",
+                                                          "--ckpt-dir", str(tmp_path / "off")], 29655, n=4)
+    assert "fsdp2xtp done" in off
+
+
+@pytest.mark.slow
+def test_mnist_fsdp1_and_basic_modes(tmp_path):
+    """Reference fsdp_mnist.py (FSDP1, auto-wrap, full state dict) and basic_mnist.py
+    (single process) equivalents learn the synthetic digits."""
+    ck = str(tmp_path / "lenet.pt")
+    out = _torchrun("examples/mnist/mnist_ddp.py", ["--mode", "fsdp", "--cpu", "--epochs", "1", "--max-steps", "30",
+                                                    "--save-model", ck], 29656)
+    acc = float(re.search(r"test accuracy ([0-9.]+)", out).group(1))
+    assert acc > 0.3, out
+    import torch
+
+    sd = torch.load(ck, weights_only=True)
+    assert any(k.endswith("weight") for k in sd)
+    from examples.mnist.mnist_ddp import main
+
+    r = main(["--mode", "single", "--cpu", "--epochs", "1", "--max-steps", "30"])
+    assert r["acc"] > 0.3
