@@ -40,6 +40,7 @@
 //     registers) -- no atomics, no partial buffers, bitwise deterministic.
 //   * causal: workgroups are numbered heaviest-first so the dispatcher's
 //     greedy fill is a longest-job-first schedule.
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -422,6 +423,205 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(AttnParams p, bf16_t*
     step(Buf<0>(), kb);
     if (kb + 1 < nkb) step(Buf<1>(), kb + 1);
   }
+
+  if (my_q < p.Sq) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    bf16_t* orow = o + (int64_t)b * sob + (int64_t)my_q * sos + (int64_t)hq * soh;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * h;
+        uint2 w;
+        w.x = pack_bf16x2(oacc[dt][4 * g + 0] * inv, oacc[dt][4 * g + 1] * inv);
+        w.y = pack_bf16x2(oacc[dt][4 * g + 2] * inv, oacc[dt][4 * g + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + d) = w;
+      }
+    }
+    if (h == 0)
+      lse[((int64_t)b * p.H + hq) * p.Sq + my_q] = l > 0.f ? (m * kLn2 + __logf(l)) : -INFINITY;
+  }
+}
+
+// ============================================================== forward, 8-wave ping-pong
+// 256 queries per workgroup in two groups of 4 waves (A = waves 0-3, queries
+// 0-127; B = waves 4-7, queries 128-255); wave w and w+4 share a SIMD.  Every key
+// block k is split into two phases separated by workgroup barriers:
+//   X(k): PV(k-1) MFMAs (P of the previous block against V(k-1)) + S(k) = K(k) Q^T MFMAs
+//   Y(k): the softmax of S(k) (VALU / transcendental), P(k) fragments, running max/sum
+// Group B starts one barrier late, so on every SIMD one wave runs its MFMA phase
+// while its partner runs the softmax phase (MI355X_MICROARCH.md "Two waves per
+// SIMD"): the matrix pipe no longer idles during the exp/convert work.  K(k+1)
+// and V(k) are DMA'd (LDS-DMA, XOR-swizzled images as in the 4-wave kernel) by
+// group B during its softmax phase, into double-buffered slots whose previous
+// contents were last read one barrier earlier; they are retired by B's
+// vmcnt(0) before the next odd barrier.  Interval i: k = i/2; even i: A X(k), B
+// Y(k-1) + DMA; odd i: A Y(k), B X(k).  2*nkb+2 intervals, same barrier count in
+// both groups.
+template <int D>
+__global__ __launch_bounds__(512, 1) void flash_fwd_pp_kernel(AttnParams p, bf16_t* __restrict__ o,
+                                                              int64_t sob, int64_t sos, int64_t soh,
+                                                              float* __restrict__ lse) {
+  constexpr int BM = 256, BG = 128, BN = 64, NKK = D / 16, NDT = D / 32;
+  constexpr int TB = BN * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];  // K0 K1 V0 V1
+  lds_t* smem = (lds_t*)smem_raw;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wid >> 2, wg = wid & 3;
+  const int BH = p.B * p.H, nqt = (p.Sq + BM - 1) / BM, id = blockIdx.x;
+  const int qt = p.causal ? nqt - 1 - id / BH : id / BH;
+  const int bh = id % BH, b = bh / p.H, hq = bh % p.H, hk = hq / (p.H / p.Hkv);
+  const int q0 = qt * BM, g0 = q0 + grp * BG, my_q = g0 + wg * 32 + r;
+
+  const rsrc_t rq = make_rsrc(p.q + (int64_t)b * p.sqb + (int64_t)hq * p.sqh, p.Sq, p.sqs, D);
+  const rsrc_t rk = make_rsrc(p.k + (int64_t)b * p.skb + (int64_t)hk * p.skh, p.Sk, p.sks, D);
+  const rsrc_t rv = make_rsrc(p.v + (int64_t)b * p.svb + (int64_t)hk * p.svh, p.Sk, p.svs, D);
+  bfx8 qf[NKK];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk)
+    qf[kk] = bload_frag(rq, (uint32_t)my_q * (uint32_t)(p.sqs * 2) + (2 * kk + h) * 16);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): fragments resident before the DMA pipeline
+  int nkb, kbm_unused, my_nkb, kb_mask;
+  key_blocks<BM, BN>(p, q0, true, nkb, kbm_unused);  // blocks any query of the workgroup sees
+  key_blocks<BG, BN>(p, g0, true, my_nkb, kb_mask);   // blocks this group's queries see
+
+  LdsAddr<D> la;
+  la.init(lane);
+  DmaStager<D, BN> sk, sv;  // group B (4 waves) moves every tile
+  sk.init(wg, lane, p.sks);
+  sv.init(wg, lane, p.svs);
+
+  f32x16 oacc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) oacc[dt] = zero16();
+  f32x16 s0 = zero16(), s1 = zero16();
+  bfx8 p00 = {}, p01 = {}, p10 = {}, p11 = {};
+  float m = -INFINITY, l = 0.f;
+  const float c2 = p.scale * kLog2e;
+  const int64_t qg = p.q_offset + my_q;
+
+  if (grp == 1 && nkb > 0) sk.load(rk, smem, 0);
+  dma_barrier();
+  if (grp == 1) __builtin_amdgcn_s_setprio(1);  // the younger half wins arbitration (item 4)
+
+  auto xphase = [&](auto kpar, int k) {
+    constexpr int KP = decltype(kpar)::value;
+    if (k >= 1 && k - 1 < my_nkb) {  // PV(k-1)
+      const lds_t* vt = smem + (2 + (KP ^ 1)) * TB;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        oacc[dt] = mfma(la.trf(vt, 0, 0, dt), p00, oacc[dt]);
+        oacc[dt] = mfma(la.trf(vt, 0, 1, dt), p01, oacc[dt]);
+        oacc[dt] = mfma(la.trf(vt, 32, 0, dt), p10, oacc[dt]);
+        oacc[dt] = mfma(la.trf(vt, 32, 1, dt), p11, oacc[dt]);
+      }
+    }
+    if (k < my_nkb) {  // S(k)
+      const lds_t* kt = smem + KP * TB;
+      s0 = zero16();
+      s1 = zero16();
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        s0 = mfma(la.rowf(kt, 0, kk), qf[kk], s0);
+        s1 = mfma(la.rowf(kt, 1, kk), qf[kk], s1);
+      }
+    }
+  };
+  auto yphase = [&](int k) {
+    if (k < 0 || k >= my_nkb) return;
+    if (k >= kb_mask) {
+      const int lim = key_limit(p, k, BN, qg, h, true);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (acc_row0(i) > lim) s0[i] = -INFINITY;
+        if (acc_row0(i) + 32 > lim) s1[i] = -INFINITY;
+      }
+    }
+    float mx0 = fmaxf(s0[0], s1[0]), mx1 = fmaxf(s0[1], s1[1]);
+#pragma unroll
+    for (int i = 2; i < 16; i += 2) {
+      mx0 = fmaxf(mx0, fmaxf(s0[i], s1[i]));
+      mx1 = fmaxf(mx1, fmaxf(s0[i + 1], s1[i + 1]));
+    }
+    float mx = fmaxf(mx0, mx1);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mxs = mx * c2;
+    if (__any(mxs > m + kRescaleThr)) {  // T13
+      const float m_new = fmaxf(m, mxs);
+      const float alpha = (m == m_new) ? 1.f : fast_exp2(m - m_new);
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+      m = m_new;
+    }
+    const float mu = (m == -INFINITY) ? 0.f : m;
+    float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+      s0[i] = fast_exp2(fmaf(s0[i], c2, -mu));
+      s1[i] = fast_exp2(fmaf(s1[i], c2, -mu));
+      s0[i + 1] = fast_exp2(fmaf(s0[i + 1], c2, -mu));
+      s1[i + 1] = fast_exp2(fmaf(s1[i + 1], c2, -mu));
+      r0 += s0[i];
+      r1 += s1[i];
+      r2 += s0[i + 1];
+      r3 += s1[i + 1];
+    }
+    float rs = (r0 + r1) + (r2 + r3);
+    rs += __shfl_xor(rs, 32, 64);
+    l += rs;
+    p00 = acc_frag(s0, 0);
+    p01 = acc_frag(s0, 1);
+    p10 = acc_frag(s1, 0);
+    p11 = acc_frag(s1, 1);
+  };
+  auto bar = [] {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // One key block = two intervals (even, odd); the slot parity of k is a template
+  // constant.  Each group runs its own straight-line loop (same barrier count).
+  // No lambda captures another lambda: a captured closure object keeps pointers
+  // to the accumulators alive and pins them in scratch.
+  // A: even X(k) | odd Y(k).   B: even Y(k-1) + DMA K(k+1), V(k) | odd X(k).
+  if (grp == 0) {
+    for (int k = 0; k <= nkb; k += 2) {
+      xphase(Buf<0>(), k);
+      bar();
+      yphase(k);
+      bar();
+      if (k + 1 <= nkb) {
+        xphase(Buf<1>(), k + 1);
+        bar();
+        yphase(k + 1);
+        bar();
+      }
+    }
+  } else {
+    for (int k = 0; k <= nkb; k += 2) {
+      if (k + 1 < nkb) sk.load(rk, smem + TB, (k + 1) * BN);
+      if (k < nkb) sv.load(rv, smem + 2 * TB, k * BN);
+      yphase(k - 1);
+      bar();
+      xphase(Buf<0>(), k);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // DMAs retired before the odd barrier
+      bar();
+      if (k + 1 <= nkb) {
+        if (k + 2 < nkb) sk.load(rk, smem, (k + 2) * BN);
+        if (k + 1 < nkb) sv.load(rv, smem + 3 * TB, (k + 1) * BN);
+        yphase(k);
+        bar();
+        xphase(Buf<1>(), k + 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();
+      }
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
 
   if (my_q < p.Sq) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
@@ -893,7 +1093,15 @@ int st_flash_fwd(const void* q, const void* k, const void* v, void* o, float* ls
   AttnParams p = make_params(q, k, v, B, Sq, Sk, H, Hkv, sqb, sqs, sqh, skb, sks, skh, svb, svs, svh,
                              scale, causal, q_offset, k_offset);
   const unsigned grid = (unsigned)(((Sq + 127) / 128) * B * H);
-  if (D == 128)
+  // ST_FLASH_PP=1 selects the 8-wave ping-pong kernel; it measured equal to the
+  // 4-wave kernel (0.345 ms both, B2 S4096 H32/8 causal), so the 4-wave one stays default
+  // (read per call so tests can switch it; one getenv per launch)
+  const char* ppe = std::getenv("ST_FLASH_PP");
+  const int pp = ppe ? std::atoi(ppe) : 0;
+  if (D == 128 && pp) {
+    const unsigned grid2 = (unsigned)(((Sq + 255) / 256) * B * H);
+    flash_fwd_pp_kernel<128><<<grid2, 512, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
+  } else if (D == 128)
     flash_fwd_kernel<128><<<grid, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
   else if (D == 64)
     flash_fwd_kernel<64><<<grid, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);

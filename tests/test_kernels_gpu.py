@@ -375,3 +375,63 @@ def test_transpose_bf16(shape):
     dst = torch.empty(C, R, device="cuda", dtype=torch.bfloat16)
     _lib.ops().transpose_(src, dst)
     assert torch.equal(dst, src.t().contiguous())
+
+
+def _attn_rows_ref(q, k, v, rows, scale, q_offset=0):
+    """fp32 causal attention for the query rows ``rows`` (global position q_offset + row)
+    against keys [0, position]; GQA by head groups.  Returns (out [B,n,H,D], lse [B,H,n])."""
+    B, _, H, D = q.shape
+    g = H // k.shape[2]
+    qs = q[:, rows].float()  # [B, n, H, D]
+    kf = k.float().repeat_interleave(g, dim=2)
+    vf = v.float().repeat_interleave(g, dim=2)
+    s = torch.einsum("bnhd,bkhd->bhnk", qs, kf) * scale
+    pos = torch.as_tensor(rows, device=q.device) + q_offset
+    mask = torch.arange(k.shape[1], device=q.device)[None, :] > pos[:, None]
+    s = s.masked_fill(mask[None, None], float("-inf"))
+    lse = torch.logsumexp(s, dim=-1)
+    out = torch.einsum("bhnk,bkhd->bnhd", torch.softmax(s, dim=-1), vf)
+    return out, lse
+
+
+@pytest.mark.parametrize("S", [4096, 8192, 32768])
+@pytest.mark.parametrize("pp", ["1", "0"])
+def test_flash_long_sequence_sampled_rows(S, pp, monkeypatch):
+    """Long causal sequences (the bench's 4K, 8K and the CP8@32K global length):
+    the kernel's output and lse on sampled query rows (start, middle, end) against
+    an fp32 reference over every visible key; both forward kernels (8-wave
+    ping-pong, opt-in via ST_FLASH_PP=1, and the default 4-wave one)."""
+    monkeypatch.setenv("ST_FLASH_PP", pp)
+    torch.manual_seed(0)
+    B, H, Hkv, D = 1, 4, 2, 128
+    q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    out, lse = ops.flash_attn_fwd(q, k, v, scale, True, 0, 0)
+    for start in (0, S // 2 - 100, S - 256):
+        rows = list(range(start, start + 256))
+        ro, rl = _attn_rows_ref(q, k, v, rows, scale)
+        assert rel(out[:, rows], ro) < 1e-2, start
+        assert (lse[:, :, rows] - rl).abs().max().item() < 1e-2, start
+
+
+@pytest.mark.parametrize("q_off", [0, 12288, 28672])
+def test_flash_cp_chunk_at_global_offset(q_off):
+    """The CP8@32K building block: a 4096-query chunk at global offset q_off against
+    every key before it (Sk = q_off + 4096), forward AND backward, vs fp32."""
+    torch.manual_seed(1)
+    B, H, Hkv, D, n = 1, 4, 2, 128, 4096
+    Sk = q_off + n
+    q = torch.randn(B, n, H, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, Sk, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, Sk, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    out, lse = ops.flash_attn_fwd(q, k, v, scale, True, q_off, 0)
+    ref_out, ref_lse = ops.sdpa_ref(q, k, v, True, scale, q_off, 0)
+    assert rel(out, ref_out) < 1e-2
+    assert (lse - ref_lse).abs().max().item() < 1e-2
+    dout = torch.randn_like(out)
+    dq, dk, dv = ops.flash_attn_bwd(dout, q, k, v, out, lse, scale, True, q_off, 0)
+    rq, rk, rv = ops.attention.flash_bwd_ref(dout, q, k, v, out, lse, scale, True, q_off, 0)
+    assert rel(dq, rq) < 2e-2 and rel(dk, rk) < 2e-2 and rel(dv, rv) < 2e-2
