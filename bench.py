@@ -74,6 +74,10 @@ def main() -> int:
     ap.add_argument("--bucket_mb", type=float, default=256)
     ap.add_argument("--zero", type=int, default=1, help="ZeRO stage when DP > 1 (0: replicated optimizer, "
                                                          "1: sharded optimizer / reduce-scatter + all-gather)")
+    ap.add_argument("--fused_head", type=int, default=0,
+                    help="1: fused chunked LM head + CE (no logits tensor; -5.1 GB, +6 ms at mbs 4, "
+                         "profiles/r02/fused_head_ab.log)")
+    ap.add_argument("--head_chunk", type=int, default=4096, help="tokens per fused LM-head chunk")
     ap.add_argument("--layers", type=int, default=None, help="(debug only; result marked invalid)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -106,7 +110,8 @@ def main() -> int:
                                micro_batch=args.micro_batch_size, seq_len=args.seq_len, grad_acc=ga,
                                zero1=args.zero >= 1 and dp * args.cp * args.ep > 1, sequence_parallel=args.sp,
                                gradient_checkpointing=(args.recompute if args.gc else False),
-                               grad_reduce_dtype=args.grad_reduce_dtype)
+                               grad_reduce_dtype=args.grad_reduce_dtype,
+                               fused_head_chunk=args.head_chunk if args.fused_head else 0)
     if int(os.environ.get("RANK", "0")) == 0:
         print(f"[bench] layout {args.layout}: {args.model} tp{args.tp} pp{args.pp} cp{args.cp} ep{args.ep} dp{dp} "
               f"mbs{args.micro_batch_size} ga{ga} seq{args.seq_len}; HBM estimate {est.summary()}",
@@ -122,7 +127,7 @@ def main() -> int:
         gradient_checkpointing=args.gc, recompute_granularity=args.recompute, learning_rate=3e-4, lr_scheduler_type="cosine", warmup_steps=0,
         max_grad_norm=1.0, grad_reduce_dtype=args.grad_reduce_dtype, bucket_size_mb=args.bucket_mb,
         num_hidden_layers=args.layers, dtype="bfloat16", weight_decay=0.1, betas=(0.9, 0.95),
-        zero_stage=args.zero,
+        zero_stage=args.zero, fused_lm_head=bool(args.fused_head), lm_head_chunk_tokens=args.head_chunk,
     )
     tr = Trainer(a)
     rank = tr.rank
@@ -180,6 +185,7 @@ def main() -> int:
         "config": {"model": args.model, "global_batch": dp * args.ep * args.micro_batch_size * ga,
                    "micro_batch": args.micro_batch_size, "grad_accum": ga, "seq_len": args.seq_len,
                    "parallelism": par, "layout": args.layout, "sequence_parallel": args.sp, "activation_checkpointing": args.gc,
+                   "lm_head": f"fused, {args.head_chunk}-token chunks" if args.fused_head else "logits + CE",
                    "grad_reduce_dtype": args.grad_reduce_dtype, "zero_stage": args.zero if dp * args.cp * args.ep > 1 else 0},
         "tokens_per_s_per_gpu": round(per_gpu, 1),
         "mfu_pct": round(mfu, 2),

@@ -239,7 +239,11 @@ class TransformerLM(nn.Module):
     # ------------------------------------------------------------------ forward
     def forward(self, input_ids: torch.Tensor | None = None, position_ids: torch.Tensor | None = None,
                 hidden_states: torch.Tensor | None = None, gradient_checkpointing: bool = False,
-                attention_mask: torch.Tensor | None = None) -> torch.Tensor:
+                attention_mask: torch.Tensor | None = None, labels: torch.Tensor | None = None,
+                lm_head_chunk: int | None = None) -> torch.Tensor:
+        """Logits shard (last stage), or -- with ``labels`` (global target ids) on
+        the last stage -- the mean cross-entropy from the fused chunked LM head
+        (ops/fused_head.py), which never materialises the logits."""
         if self.first_stage:
             x = self.embedding(input_ids)
         else:
@@ -260,6 +264,8 @@ class TransformerLM(nn.Module):
         x = self.final_norm(x) if residual is None else self.final_norm(x, residual)[0]
         # a module call (SP: gather along seq inside the column-parallel fn), so the head's
         # forward pre-hook orders it after the weight's optimizer update / ZeRO-1 gather
+        if labels is not None:
+            return self.final_proj(x, labels=labels, chunk=lm_head_chunk)
         return self.final_proj(x)
 
     # ------------------------------------------------------------------ checkpoints in reference layout

@@ -229,7 +229,6 @@ def accumulate_linear_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
     ``ST_WGRAD_KERNEL=0`` forces the hipBLASLt path (A/B).  Preferred on GPU: the
     TN GEMM on token-contiguous copies (``prefetch_wgrad``; opt-in ``ST_WGRAD_TN=1``).
     """
-    global _ADDMM_DTYPE_OK
     mg = getattr(param, "main_grad", None)
     if mg is None:
         return dy2d.t().mm(x2d)
@@ -242,27 +241,34 @@ def accumulate_linear_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
         torch.ops.aten.addmm.dtype_out(m2, pre.dyt, pre.xt.t(), torch.float32, beta=beta, alpha=1, out=m2)
         _grad_ready(param)
         return None
-    if mg.dtype == dy2d.dtype:
-        mg.addmm_(dy2d.t(), x2d, beta=beta)
-    else:
-        done = False
-        if (mg.dtype == torch.float32 and dy2d.is_cuda and dy2d.dtype == torch.bfloat16
-                and x2d.dtype == torch.bfloat16 and os.environ.get("ST_WGRAD_KERNEL", "1") == "1"):
-            from . import _lib
-
-            if _lib.use_native(dy2d) and _wgrad_pick(dy2d, x2d):
-                done = bool(_lib.ops().wgrad_gemm_(mg.view(mg.shape[0], -1), dy2d, x2d, beta))
-        if not done and _ADDMM_DTYPE_OK is not False and dy2d.is_cuda and os.environ.get("ST_WGRAD_FP32_GEMM", "1") == "1":
-            try:
-                torch.ops.aten.addmm.dtype_out(mg, dy2d.t(), x2d, mg.dtype, beta=beta, alpha=1, out=mg)
-                _ADDMM_DTYPE_OK = True
-                done = True
-            except (RuntimeError, NotImplementedError):
-                _ADDMM_DTYPE_OK = False
-        if not done:
-            if beta == 0:
-                mg.copy_(dy2d.t().mm(x2d))
-            else:
-                mg.add_(dy2d.t().mm(x2d))
+    wgrad_into(mg.view(mg.shape[0], -1), dy2d, x2d, beta)
     _grad_ready(param)
     return None
+
+
+def wgrad_into(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, beta: int) -> None:
+    """``out = beta * out + dy2d^T x2d`` for a 2-D ``out`` (fp32 accumulator or the
+    operands' dtype), on the per-shape faster of csrc/wgrad_gemm.hip and hipBLASLt."""
+    global _ADDMM_DTYPE_OK
+    if out.dtype == dy2d.dtype:
+        out.addmm_(dy2d.t(), x2d, beta=beta)
+        return
+    if (out.dtype == torch.float32 and dy2d.is_cuda and dy2d.dtype == torch.bfloat16
+            and x2d.dtype == torch.bfloat16 and os.environ.get("ST_WGRAD_KERNEL", "1") == "1"):
+        from . import _lib
+
+        if _lib.use_native(dy2d) and _wgrad_pick(dy2d, x2d):
+            if _lib.ops().wgrad_gemm_(out, dy2d, x2d, beta):
+                return
+    if _ADDMM_DTYPE_OK is not False and dy2d.is_cuda and os.environ.get("ST_WGRAD_FP32_GEMM", "1") == "1":
+        try:
+            torch.ops.aten.addmm.dtype_out(out, dy2d.t(), x2d, out.dtype, beta=beta, alpha=1, out=out)
+            _ADDMM_DTYPE_OK = True
+            return
+        except (RuntimeError, NotImplementedError):
+            _ADDMM_DTYPE_OK = False
+    prod = dy2d.t().mm(x2d)
+    if beta == 0:
+        out.copy_(prod)
+    else:
+        out.add_(prod)

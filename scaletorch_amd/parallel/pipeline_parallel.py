@@ -121,9 +121,10 @@ class PipelineEngine:
     """Runs one optimizer step's worth of micro-batches through this stage."""
 
     def __init__(self, model, loss_fn, tensor_shape, dtype=torch.bfloat16, device=None,
-                 gradient_checkpointing: bool = False, aux_loss_fn=None):
+                 gradient_checkpointing: bool = False, aux_loss_fn=None, head_kwargs_fn=None):
         self.model = model  # DataParallel-wrapped stage
-        self.loss_fn = loss_fn  # (logits, batch) -> scalar loss
+        self.loss_fn = loss_fn  # (logits or the fused head's loss, batch) -> scalar loss
+        self.head_kwargs_fn = head_kwargs_fn  # batch -> extra model kwargs on the last stage (fused LM head)
         self.tensor_shape = tuple(tensor_shape)
         self.dtype, self.device = dtype, device
         self.gc = gradient_checkpointing
@@ -138,8 +139,10 @@ class PipelineEngine:
         return mesh.pgm.pp_is_last_stage
 
     def _forward(self, batch, x, num_micro):
+        extra = self.head_kwargs_fn(batch) if (self._last and self.head_kwargs_fn is not None) else {}
         out = self.model(input_ids=batch["input_ids"] if self._first else None,
-                         position_ids=batch["position_ids"], hidden_states=x, gradient_checkpointing=self.gc)
+                         position_ids=batch["position_ids"], hidden_states=x, gradient_checkpointing=self.gc,
+                         **extra)
         if self._last:
             loss = self.loss_fn(out, batch) / num_micro
             if self.aux_loss_fn is not None:

@@ -457,7 +457,23 @@ class ColumnParallelLinear(nn.Module):
         if self.bias is not None:
             nn.init.zeros_(self.bias)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, labels: torch.Tensor | None = None, chunk: int | None = None) -> torch.Tensor:
+        """Logits shard ``[..., out/tp]``; with ``labels`` (LM head use) the mean
+        vocab-parallel cross-entropy instead, fused and chunked so the logits are
+        never materialised (ops/fused_head.py).  Both run as a module call so the
+        forward pre-hook (optimizer-bucket wait) precedes every read of the weight."""
+        if labels is not None:
+            from ..ops.fused_head import fused_linear_cross_entropy
+
+            if self.bias is not None:
+                raise ValueError("fused LM head + cross-entropy takes a bias-free projection")
+            if self.sequence_parallel and self.tp > 1:
+                x = AllGatherFromSequenceParallelRegion.apply(x, self.group)
+            elif self.tp > 1:
+                x = CopyToTensorParallelRegion.apply(x, self.group)
+            vocab_start = C.get_rank(self.group) * self.out_per_rank if self.tp > 1 else 0
+            return fused_linear_cross_entropy(x, self.weight, labels, vocab_start,
+                                              group=self.group if self.tp > 1 else None, chunk=chunk)
         if self.sequence_parallel and self.tp > 1:
             y = _SPColumnParallelFn.apply(x, self.weight, self.bias, self.group)
         elif self.tp > 1 or getattr(self.weight, "main_grad", None) is not None:

@@ -134,6 +134,10 @@ class TrainingArguments:
     recompute_granularity: str = field(default="full", metadata={"help": "with --gradient_checkpointing: full "
                                                                       "(whole layer) | selective (norm+MLP "
                                                                       "only; attention activations kept)"})
+    fused_lm_head: bool = field(default=True, metadata={"help": "LM head + cross-entropy fused and chunked "
+                                                                "(ops/fused_head.py): the [tokens, vocab] logits "
+                                                                "are never materialised"})
+    lm_head_chunk_tokens: int = field(default=4096, metadata={"help": "tokens per fused LM-head chunk"})
     max_grad_norm: float | None = field(default=1.0)
     epochs: int = field(default=5, metadata={"help": "stop after this many passes over the dataset"})
     seed: int = field(default=1)

@@ -123,7 +123,8 @@ class Trainer:
             self.pipeline = PipelineEngine(self.model, self._loss, (a.micro_batch_size, S, cfg.hidden_size),
                                            dtype=self.dtype, device=self.device,
                                            gradient_checkpointing=self.gc_mode,
-                                           aux_loss_fn=model.aux_loss if cfg.is_moe else None)
+                                           aux_loss_fn=model.aux_loss if cfg.is_moe else None,
+                                           head_kwargs_fn=self._head_kwargs)
 
     # ---------------------------------------------------------------- data
     def _build_data(self, synthetic: bool):
@@ -152,7 +153,16 @@ class Trainer:
         return out
 
     # ---------------------------------------------------------------- loss
+    def _head_kwargs(self, batch: dict) -> dict:
+        """Model kwargs that make the last stage return the fused head's loss."""
+        a = self.args
+        if not getattr(a, "fused_lm_head", False):
+            return {}
+        return {"labels": batch["target_ids"], "lm_head_chunk": a.lm_head_chunk_tokens}
+
     def _loss(self, logits: torch.Tensor, batch: dict) -> torch.Tensor:
+        if logits.dim() == 0:  # the fused LM head already produced the loss
+            return logits
         tgt = batch["target_ids"].to(logits.device)
         group = self.tp_group if mesh.tp_size() > 1 else None
         return ops.cross_entropy(logits, tgt, vocab_start=self.raw_model.vocab_start, group=group)
@@ -178,7 +188,7 @@ class Trainer:
                 with ctx:
                     with profiling.range("forward"):
                         logits = self.model(input_ids=batch["input_ids"], position_ids=batch["position_ids"],
-                                            gradient_checkpointing=self.gc_mode)
+                                            gradient_checkpointing=self.gc_mode, **self._head_kwargs(batch))
                         l = self._loss(logits, batch) / ga
                         del logits
                         if self.model_config.is_moe:
@@ -219,7 +229,8 @@ class Trainer:
         try:
             for _ in range(steps):
                 batch = self._to_device(next(loader))
-                logits = self.model(input_ids=batch["input_ids"], position_ids=batch["position_ids"])
+                logits = self.model(input_ids=batch["input_ids"], position_ids=batch["position_ids"],
+                                    **self._head_kwargs(batch))
                 total += self._loss(logits, batch).float()
         finally:
             self.raw_model.train(was_training)

@@ -45,8 +45,13 @@ class MemoryEstimate:
 def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1, dp: int = 1,
                          micro_batch: int = 1, seq_len: int = 4096, grad_acc: int = 1, zero1: bool = False,
                          sequence_parallel: bool = False, gradient_checkpointing: bool = False,
-                         pp_engine: str = "1f1b", grad_reduce_dtype: str = "bf16") -> MemoryEstimate:
-    """Worst-rank estimate (first pipeline stage for activations, largest stage for weights)."""
+                         pp_engine: str = "1f1b", grad_reduce_dtype: str = "bf16",
+                         fused_head_chunk: int = 0) -> MemoryEstimate:
+    """Worst-rank estimate (first pipeline stage for activations, largest stage for weights).
+
+    ``fused_head_chunk`` > 0: the fused chunked LM head (ops/fused_head.py) -- one
+    chunk of logits, dX and the fp32 head-gradient buffer instead of the logits
+    and their gradient."""
     h, d = cfg.hidden_size, cfg.head_dim
     H, Hkv = cfg.num_attention_heads, cfg.num_key_value_heads
     L = cfg.num_hidden_layers
@@ -85,7 +90,12 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
         act = tokens * (2 * h * layers) + tokens * per_layer
     else:
         act = tokens * per_layer * layers
-    logits = micro_batch * seq_len / cp * cfg.vocab_size / tp * 2 * 2  # bf16 logits + grad (last stage)
+    head_tokens = micro_batch * seq_len / cp
+    if fused_head_chunk:
+        logits = min(fused_head_chunk, head_tokens) * cfg.vocab_size / tp * 2 + head_tokens * h * 2 \
+            + cfg.vocab_size / tp * h * 4
+    else:
+        logits = head_tokens * cfg.vocab_size / tp * 2 * 2  # bf16 logits + grad (last stage)
     comm = n * 2 if grad_reduce_dtype in ("bf16", "bfloat16") and dense_dp > 1 else 0.0
     # bf16 W^T copies of the dense projection weights (TN data-gradient GEMMs, ops/grad.py)
     wt = 2 * (dense - 2 * h * layers - (h * cfg.num_experts if cfg.is_moe else 0) * layers)
