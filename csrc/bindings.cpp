@@ -53,7 +53,7 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
                  int64_t sdks, int64_t sdkh, float scale, int causal, int64_t q_offset,
                  int64_t k_offset, hipStream_t st);
 int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int M,
-                  int N, int T, int beta, hipStream_t st);
+                  int N, int T, int beta, int variant, hipStream_t st);
 int st_xgmi_header_bytes();
 int st_xgmi_max_ranks();
 int64_t st_xgmi_create(int rank, int world, int64_t cap, int64_t epoch_base);
@@ -298,7 +298,7 @@ void sumsq_(const at::Tensor& g, at::Tensor out) {
 // ---------------------------------------------------------------- weight-gradient GEMM
 // out[M,N] fp32 (+)= dy[T,M]^T @ x[T,N]; returns false when the shape is not one the
 // kernel tiles (caller falls back to hipBLASLt).
-bool wgrad_gemm_(at::Tensor out, const at::Tensor& dy, const at::Tensor& x, int64_t beta) {
+bool wgrad_gemm_(at::Tensor out, const at::Tensor& dy, const at::Tensor& x, int64_t beta, int64_t variant) {
   check_bf16_cuda(dy, "dy");
   check_bf16_cuda(x, "x");
   check_same_gpu(x, dy, "x");
@@ -312,7 +312,7 @@ bool wgrad_gemm_(at::Tensor out, const at::Tensor& dy, const at::Tensor& x, int6
   if (T > INT32_MAX || M > INT32_MAX || N > INT32_MAX) return false;
   c10::hip::HIPGuardMasqueradingAsCUDA g(out.device());
   int rc = st_wgrad_gemm(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr<float>(),
-                         out.stride(0), (int)M, (int)N, (int)T, beta ? 1 : 0, cur_stream());
+                         out.stride(0), (int)M, (int)N, (int)T, beta ? 1 : 0, (int)variant, cur_stream());
   if (rc == -2) return false;
   ST_CHECK_RC(rc, "wgrad_gemm_");
   return true;
@@ -632,7 +632,7 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("xent_bwd_(Tensor logits, Tensor target, int vocab_start, Tensor lse, Tensor dloss, Tensor(a!) dlogits) -> ()");
   m.def("flash_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int q_offset, int k_offset) -> Tensor[]");
   m.def("flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, int q_offset, int k_offset, Tensor(a!)? dq_out=None, Tensor(b!)? dk_out=None, Tensor(c!)? dv_out=None) -> Tensor[]");
-  m.def("wgrad_gemm_(Tensor(a!) out, Tensor dy, Tensor x, int beta) -> bool");
+  m.def("wgrad_gemm_(Tensor(a!) out, Tensor dy, Tensor x, int beta, int variant=0) -> bool");
   m.def("xgmi_create(int rank, int world, int cap, int epoch_base) -> int", &xgmi_create);
   m.def("xgmi_handle(int id) -> Tensor", &xgmi_handle);
   m.def("xgmi_open(int id, int r, Tensor handle) -> ()", &xgmi_open);

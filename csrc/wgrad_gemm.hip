@@ -232,6 +232,216 @@ __global__ __launch_bounds__(NT, 2) void wgrad_gemm_kernel(const bf16_t* __restr
       }
 }
 
+// ============================================================ 8-phase variant
+// 256x256 tile, BK = 64 tokens, 8 waves as 2 (M) x 4 (N), wave (wr, wc) owning
+// the four 64x32 quadrants (mq, nq) at rows mq*128 + wr*64, columns nq*128 + wc*32:
+// quadrant (mq, nq) reads ONLY the A half-image mq and the B half-image nq
+// ([64 tokens][128 features], 16 KiB each), so a K-tile is consumed half-image by
+// half-image and the next tile's half-images stream in behind it.  Four phases
+// per K-tile, quadrants (0,0) (0,1) (1,1) (1,0):
+//   reads (p0: A0+B0, p1: B1, p2: A1, p3: none -- B0/B1 stay in registers)
+//   + counted vmcnt retiring what the NEXT phase reads     | barrier |
+//   16 MFMAs (quadrant x 64 tokens), with one half-image of tile t+1 issued
+//   by LDS-DMA between them (p0 A0, p1 B0, p2 B1, p3 A1)  | barrier |
+// (DMA issued from the reading section instead measured 3-7 % slower: the
+// read section, not the MFMA section, was the longer one.)
+// Waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave issues
+// its LDS reads and DMA while its partner runs MFMAs (cdna_hip_programming.md
+// "The 256² 8-phase template"; counted waits + raw barriers only: a DMA stays
+// in flight across every barrier).  Every read of a half-image is ordered after
+// the issuing waves' vmcnt AND one extra barrier (the stagger), since the wait
+// for phase p+1's data sits before phase p's first barrier.
+namespace p8 {
+constexpr int BK = 64;
+constexpr int IMGB = BK * RB;    // [64 tokens][128 features]: 16 KiB
+constexpr int BUFB = 4 * IMGB;   // A0 A1 B0 B1: 64 KiB per K-tile
+
+// half-image X of K-tile kt -> buffer buf.  X: 0 = A0, 1 = B0, 2 = B1, 3 = A1.  A plain
+// function, not a lambda: a closure captured by the phase lambda would pin the
+// operand arrays in scratch.
+template <int X>
+ST_DEVICE void p8_dma(const i32x4& rsA, const i32x4& rsB, uint32_t ldsw, const uint32_t (&vA)[2],
+                      const uint32_t (&vB)[2], uint32_t sA, uint32_t sB, int buf, int kt, int piece) {
+  constexpr bool isA = (X == 0 || X == 3);
+  constexpr int img = X == 0 ? 0 : X == 3 ? 1 : X == 1 ? 2 : 3;
+  constexpr uint32_t col = (X == 2 || X == 3) ? 256u : 0u;  // byte offset of feature 128
+  const uint32_t koff = (uint32_t)(kt * BK) * (isA ? sA : sB) + col;
+  const uint32_t v = piece ? (isA ? vA[1] : vB[1]) : (isA ? vA[0] : vB[0]);
+  lds_dma16(isA ? rsA : rsB, ldsw + (uint32_t)(buf * BUFB + img * IMGB + piece * 1024), v + koff);
+}
+}  // namespace p8
+
+template <int PROBE>  // timing probes (wrong results): 1 = no K-loop DMA, 2 = no K-loop LDS reads
+__global__ __launch_bounds__(NT, 1) void wgrad8_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                       const bf16_t* __restrict__ B, int64_t ldb,
+                                                       float* __restrict__ C, int64_t ldc, int M, int N, int T,
+                                                       int beta) {
+  using namespace p8;
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * BUFB];  // 128 KiB: two K-tiles
+  lds_t* smem = (lds_t*)smem_raw;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = wid >> 2, wr = grp, wc = wid & 3;
+  const int nbm = M / BM, nbn = N / 256, nwg = nbm * nbn;
+  const int logical = xcd_remap((int)blockIdx.x, nwg);
+  const int per_group = GROUP_M * nbn;
+  const int first_bm = (logical / per_group) * GROUP_M;
+  const int gsz = min(nbm - first_bm, GROUP_M);
+  const int in_group = logical % per_group;
+  const int m0 = (first_bm + in_group % gsz) * BM, n0 = (in_group / gsz) * 256;
+
+  // ---- DMA plan: a half-image is 16 pieces of 1 KiB (4 token rows each); wave w
+  // fills pieces 2w and 2w+1 of every half-image (source address pre-swizzled).
+  const i32x4 rsA = make_rsrc(A + m0, (uint32_t)(((int64_t)(T - 1) * lda + BM) * 2));
+  const i32x4 rsB = make_rsrc(B + n0, (uint32_t)(((int64_t)(T - 1) * ldb + 256) * 2));
+  const uint32_t sA = (uint32_t)(lda * 2), sB = (uint32_t)(ldb * 2);
+  uint32_t vA[2], vB[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 4 * (2 * wid + i) + (lane >> 4), pos = lane & 15;
+    const uint32_t c = (uint32_t)(16 * (pos ^ swz(row)));
+    vA[i] = (uint32_t)row * sA + c;
+    vB[i] = (uint32_t)row * sB + c;
+  }
+  const uint32_t ldsw = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem + (uint32_t)(wid * 2048));
+  // half-image X of K-tile kt into buffer buf (p8_dma); X: 0 = A0, 1 = B0, 2 = B1, 3 = A1 (the issue order)
+  // ---- fragment read plan (T10 image (b), as the 4-stage kernel): lane group G
+  // reads token rows 8G..8G+7 (+32 for the second 32-token half of the tile)
+  const int G = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  int aoff[4][2], boff[2][2];
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      aoff[i][hf] = lds_off(8 * G + 4 * hf + q, ((wr * 64 + 16 * i) / 8) + (pp >> 1)) + 8 * (pp & 1);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      boff[j][hf] = lds_off(8 * G + 4 * hf + q, ((wc * 32 + 16 * j) / 8) + (pp >> 1)) + 8 * (pp & 1);
+  }
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
+  bfx8 af[4][2] = {}, b0[2][2] = {}, b1[2][2] = {};
+
+  auto bar = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  const int KT = T / p8::BK;
+  // prologue: tile 0's four half-images; A0 + B0 retired for phase 0
+#pragma unroll
+  for (int pc = 0; pc < 2; ++pc) p8_dma<0>(rsA, rsB, ldsw, vA, vB, sA, sB, 0, 0, pc);  // half-image by half-image:
+#pragma unroll
+  for (int pc = 0; pc < 2; ++pc) p8_dma<1>(rsA, rsB, ldsw, vA, vB, sA, sB, 0, 0, pc);  // the counted waits retire
+#pragma unroll
+  for (int pc = 0; pc < 2; ++pc) p8_dma<2>(rsA, rsB, ldsw, vA, vB, sA, sB, 0, 0, pc);  // whole half-images in
+#pragma unroll
+  for (int pc = 0; pc < 2; ++pc) p8_dma<3>(rsA, rsB, ldsw, vA, vB, sA, sB, 0, 0, pc);  // issue order
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  bar();
+  if (grp == 1) bar();  // the stagger: waves 4-7 run one barrier behind
+
+  auto phase = [&](auto bufc, auto pc, int kt) {
+    constexpr int BUF = decltype(bufc)::value, P = decltype(pc)::value;
+    constexpr int MQ = (P == 0 || P == 1) ? 0 : 1, NQ = (P == 0 || P == 3) ? 0 : 1;
+    const bool more = kt + 1 < KT;
+    const lds_t* st = smem + BUF * BUFB;
+    const lds_t* ai = st + (MQ ? IMGB : 0);
+    // A fragments 0-1 before the barrier, 2-3 after it under the first MFMAs (balances
+    // the read sections: p0 would otherwise carry 24 of a tile's 48 reads)
+    if constexpr (PROBE != 2 && (P == 0 || P == 2)) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) af[i][ks] = lds_tr(ai + aoff[i][0] + ks * 32 * RB, ai + aoff[i][1] + ks * 32 * RB);
+    }
+    if constexpr (PROBE != 2 && (P == 0 || P == 1)) {
+      const lds_t* bi = st + (2 + NQ) * IMGB;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bfx8 v = lds_tr(bi + boff[j][0] + ks * 32 * RB, bi + boff[j][1] + ks * 32 * RB);
+          if constexpr (NQ == 0) b0[j][ks] = v;
+          else b1[j][ks] = v;
+        }
+    }
+    // retire what the NEXT phase reads: this phase's DMA is issued after the wait
+    // (under the MFMAs), so only the previous phase's half-image may stay in flight
+    if (more) {
+      if constexpr (P == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();
+    if constexpr (PROBE != 2 && (P == 0 || P == 2)) {
+#pragma unroll
+      for (int i = 2; i < 4; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) af[i][ks] = lds_tr(ai + aoff[i][0] + ks * 32 * RB, ai + aoff[i][1] + ks * 32 * RB);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const bfx8 bv = NQ == 0 ? b0[j][ks] : b1[j][ks];
+          acc[MQ * 4 + i][NQ * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bv,
+                                                                                 acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
+        }
+      // the next tile's half-image, one 1-KiB piece after the 4th and the 8th MFMA
+      if ((i == 0 || i == 1) && more && PROBE != 1) {
+        __builtin_amdgcn_sched_barrier(0);
+        p8_dma<P>(rsA, rsB, ldsw, vA, vB, sA, sB, BUF ^ 1, kt + 1, i);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  for (int kt = 0; kt < KT; kt += 2) {
+    phase(I0(), I0(), kt);
+    phase(I0(), I1(), kt);
+    phase(I0(), I2(), kt);
+    phase(I0(), I3(), kt);
+    if (kt + 1 < KT) {
+      phase(I1(), I0(), kt + 1);
+      phase(I1(), I1(), kt + 1);
+      phase(I1(), I2(), kt + 1);
+      phase(I1(), I3(), kt + 1);
+    }
+  }
+  if (grp == 0) bar();  // same barrier count in both groups
+
+  // ---- epilogue: 16x16 C/D row = 4 (lane>>4) + reg, column = lane & 15
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + (i >> 2) * 128 + wr * 64 + 16 * (i & 3) + 4 * G + r;
+        float* p = C + (int64_t)m * ldc + n0 + (j >> 1) * 128 + wc * 32 + 16 * (j & 1) + (lane & 15);
+        *p = beta ? *p + acc[i][j][r] : acc[i][j][r];
+      }
+}
+
 }  // namespace
 
 extern "C" {
@@ -240,8 +450,10 @@ extern "C" {
 // Tile width: 256 unless only 128 divides N or the 256-wide grid would end in a
 // partial wave of workgroups that the 128-wide one avoids (qkv 6144x4096: 384
 // vs 768 tiles; down 4096x14336: 896 vs 1792 on 256 CUs).
+// variant: 0 = default (the 4-stage kernel, or the 8-phase one when ST_WGRAD_P8=1),
+// 1 = the 4-stage kernel, 2 = the 8-phase kernel (ops/grad.py times them per shape).
 int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int M,
-                  int N, int T, int beta, hipStream_t st) {
+                  int N, int T, int beta, int variant, hipStream_t st) {
   if (M <= 0 || N <= 0 || T <= 0) return -2;
   if (M % BM || N % 128 || T % BK) return -2;
   if (lda % 8 || ldb % 8 || lda < M || ldb < N || ldc < N) return -2;
@@ -264,6 +476,18 @@ int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float*
   if (bn == 256 && N % 256) return -2;
   const bf16_t *a = (const bf16_t*)A, *b = (const bf16_t*)B;
   const int bt = beta ? 1 : 0;
+  if (variant == 0) {
+    const char* ve = std::getenv("ST_WGRAD_P8");
+    variant = (ve && std::atoi(ve) == 1) ? 2 : 1;
+  }
+  if (variant == 2) {
+    if (N % 256 || T % p8::BK) return -2;
+    const int g8 = (M / BM) * (N / 256);
+    if (probe == 1) wgrad8_kernel<1><<<g8, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
+    else if (probe == 2) wgrad8_kernel<2><<<g8, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
+    else wgrad8_kernel<0><<<g8, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
+    return (int)hipGetLastError();
+  }
   const int nwg = (M / BM) * (N / bn);
   if (bn == 256) {
     if (probe == 1) wgrad_gemm_kernel<1, 256><<<nwg, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);

@@ -19,7 +19,7 @@ import os
 import torch
 
 _ADDMM_DTYPE_OK: bool | None = None
-# per-shape winner of the weight-gradient GEMM: True = csrc/wgrad_gemm.hip, False = hipBLASLt
+# per-shape winner of the weight-gradient GEMM: 1 / 2 = csrc/wgrad_gemm.hip 4-stage / 8-phase, 0 = hipBLASLt
 _WGRAD_CHOICE: dict = {}
 _WGRAD_TIMES: dict = {}  # tuning measurements (ms for two calls), for tools/ab_step.py
 _TUNE_MAX_BYTES = 512 << 20
@@ -173,10 +173,13 @@ def accumulate_grad(param: torch.Tensor, grad: torch.Tensor):
     return None
 
 
-def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> bool:
-    """First call per (shape, strides): time the HIP kernel against the hipBLASLt
-    fp32-epilogue GEMM on a scratch output (5 x 2 runs, same stream) and keep the
-    faster one -- on gfx950 neither wins every projection shape."""
+def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> int:
+    """First call per (shape, strides): time the two HIP kernels (1: 4-stage ring,
+    2: 8-phase ping-pong, csrc/wgrad_gemm.hip) against the hipBLASLt fp32-epilogue
+    GEMM on a scratch output (5 rounds x 2 calls, same stream, interleaved) and keep
+    the fastest -- 0 = hipBLASLt.  On gfx950 none wins every projection shape
+    (tools/probe_wgrad.py: the 8-phase kernel +3-13 % on out/down, -1-2 % on
+    gate_up/qkv)."""
     from . import _lib
 
     key = (tuple(dy2d.shape), dy2d.stride(0), tuple(x2d.shape), x2d.stride(0), dy2d.device.index)
@@ -185,24 +188,24 @@ def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> bool:
         return got
     M, N = dy2d.shape[1], x2d.shape[1]
     if M * N * 4 > _TUNE_MAX_BYTES or os.environ.get("ST_WGRAD_TUNE", "1") != "1":
-        _WGRAD_CHOICE[key] = True
-        return True
+        _WGRAD_CHOICE[key] = 1
+        return 1
     scratch = torch.zeros(M, N, dtype=torch.float32, device=dy2d.device)
-    if not _lib.ops().wgrad_gemm_(scratch, dy2d, x2d, 0):
-        _WGRAD_CHOICE[key] = False
-        return False
-
-    def ours():
-        _lib.ops().wgrad_gemm_(scratch, dy2d, x2d, 1)
+    arms = {v: (lambda v=v: _lib.ops().wgrad_gemm_(scratch, dy2d, x2d, 1, v)) for v in (1, 2)
+            if _lib.ops().wgrad_gemm_(scratch, dy2d, x2d, 0, v)}
+    if not arms:
+        _WGRAD_CHOICE[key] = 0
+        return 0
 
     def blas():
         torch.ops.aten.addmm.dtype_out(scratch, dy2d.t(), x2d, torch.float32, beta=1, alpha=1, out=scratch)
 
+    arms[0] = blas
     best = {}
     try:
         blas()
         for _ in range(5):
-            for name, fn in (("ours", ours), ("blas", blas)):
+            for name, fn in arms.items():
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
                 fn()
@@ -210,9 +213,9 @@ def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> bool:
                 e.record()
                 e.synchronize()
                 best[name] = min(best.get(name, 1e30), s.elapsed_time(e))
-        choice = best["ours"] <= best["blas"]
+        choice = min(best, key=best.get)
     except (RuntimeError, NotImplementedError):
-        choice = True
+        choice = 1
     del scratch
     _WGRAD_CHOICE[key] = choice
     _WGRAD_TIMES[key] = best
@@ -257,8 +260,10 @@ def wgrad_into(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, beta: i
             and x2d.dtype == torch.bfloat16 and os.environ.get("ST_WGRAD_KERNEL", "1") == "1"):
         from . import _lib
 
-        if _lib.use_native(dy2d) and _wgrad_pick(dy2d, x2d):
-            if _lib.ops().wgrad_gemm_(out, dy2d, x2d, beta):
+        if _lib.use_native(dy2d):
+            forced = os.environ.get("ST_WGRAD_VARIANT", "")  # 0 / 1 / 2 overrides the per-shape pick (A/B)
+            variant = int(forced) if forced in ("0", "1", "2") else _wgrad_pick(dy2d, x2d)
+            if variant and _lib.ops().wgrad_gemm_(out, dy2d, x2d, beta, variant):
                 return
     if _ADDMM_DTYPE_OK is not False and dy2d.is_cuda and os.environ.get("ST_WGRAD_FP32_GEMM", "1") == "1":
         try:

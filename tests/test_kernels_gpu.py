@@ -324,6 +324,23 @@ def test_wgrad_gemm(T, M, N, beta, bn, monkeypatch):
     assert rel(out, ref) < 1e-5
 
 
+@pytest.mark.parametrize("T,M,N,beta", [(64, 256, 256, 0), (192, 512, 768, 1), (4096, 512, 1024, 1), (1024, 768, 512, 0)])
+def test_wgrad_gemm_8phase(T, M, N, beta, monkeypatch):
+    """The 8-phase 256x256 kernel (ST_WGRAD_P8=1): single, odd (tail) and long K-tile
+    counts, strided operands, beta = 0/1, vs the fp32 reference."""
+    monkeypatch.setenv("ST_WGRAD_P8", "1")
+    torch.manual_seed(1)
+    dy_full = torch.randn(T, M + 64, device="cuda", dtype=torch.bfloat16)
+    x_full = torch.randn(T, N + 128, device="cuda", dtype=torch.bfloat16)
+    dy, x = dy_full[:, 32: 32 + M], x_full[:, 64: 64 + N]
+    ramp = torch.arange(N, device="cuda", dtype=torch.float32)[None, :] * 1e-3
+    out = torch.randn(M, N, device="cuda") + ramp
+    ref = dy.float().t() @ x.float() + (out if beta else 0)
+    assert _lib.ops().wgrad_gemm_(out, dy, x, beta)
+    torch.cuda.synchronize()
+    assert rel(out, ref) < 1e-5
+
+
 def test_wgrad_gemm_unsupported_shape_declines():
     dy = torch.randn(64, 200, device="cuda", dtype=torch.bfloat16)
     x = torch.randn(64, 192, device="cuda", dtype=torch.bfloat16)

@@ -44,7 +44,7 @@ def main() -> int:
     ap.add_argument("--variants", default="overlap,serial")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--micro_batch_size", type=int, default=2)
+    ap.add_argument("--micro_batch_size", type=int, default=4)
     ap.add_argument("--seq_len", type=int, default=4096)
     ap.add_argument("--layers", type=int, default=None)
     args = ap.parse_args()
@@ -56,7 +56,8 @@ def main() -> int:
     a = ScaleTorchArguments(model_name_or_path=args.model, synthetic_data=True, micro_batch_size=args.micro_batch_size,
                             sequence_length=args.seq_len, total_train_steps=10_000, learning_rate=3e-4,
                             lr_scheduler_type="constant", warmup_steps=0, max_grad_norm=1.0, dtype="bfloat16",
-                            num_hidden_layers=args.layers, weight_decay=0.1, betas=(0.9, 0.95))
+                            num_hidden_layers=args.layers, weight_decay=0.1, betas=(0.9, 0.95),
+                            fused_lm_head=False)  # the bench.py configuration
     tr = Trainer(a)
     side = tr.model.side_stream
     variants = args.variants.split(",")
@@ -80,7 +81,7 @@ def main() -> int:
 
     for k, v in G._WGRAD_TIMES.items():
         print("wgrad tune", k[0], k[2], {a: round(b, 3) for a, b in v.items()}, "->",
-              "hip" if G._WGRAD_CHOICE.get(k) else "hipblaslt")
+              {0: "hipblaslt", 1: "hip 4-stage", 2: "hip 8-phase"}.get(G._WGRAD_CHOICE.get(k), "?"))
     print(json.dumps({v: round(statistics.median(t), 2) for v, t in times.items()}))
     return 0
 

@@ -44,13 +44,25 @@ def main() -> int:
         def t_ours():
             _lib.ops().wgrad_gemm_(out0, dy, x, 1)
 
+        def t_p8():
+            os.environ["ST_WGRAD_P8"] = "1"
+            _lib.ops().wgrad_gemm_(out0, dy, x, 1)
+            os.environ["ST_WGRAD_P8"] = "0"
+
+        os.environ["ST_WGRAD_P8"] = "1"
+        out2 = torch.zeros(M, N, device="cuda")
+        ok8 = _lib.ops().wgrad_gemm_(out2, dy, x, 0)
+        os.environ["ST_WGRAD_P8"] = "0"
+        err8 = ((out2 - out1).norm() / out1.norm()).item() if ok8 else None
+        del out2
+
         def t_blas():
             torch.ops.aten.addmm.dtype_out(out1, dy.t(), x, torch.float32, beta=1, alpha=1, out=out1)
 
         fl = 2.0 * T * M * N
-        times = {"ours": [], "hipblaslt": []}
+        times = {"ours": [], "p8": [], "hipblaslt": []}
         for _ in range(3):
-            for k, fn in (("ours", t_ours), ("hipblaslt", t_blas)):
+            for k, fn in (("ours", t_ours), ("p8", t_p8), ("hipblaslt", t_blas)):
                 if k == "ours" and not ok:
                     continue
                 fn()
@@ -62,7 +74,7 @@ def main() -> int:
                 e.record()
                 torch.cuda.synchronize()
                 times[k].append(s.elapsed_time(e) / args.iters)
-        row = {"M": M, "N": N, "T": T, "rel_err": err}
+        row = {"M": M, "N": N, "T": T, "rel_err": err, "rel_err_p8": err8}
         for k, v in times.items():
             if v:
                 ms = min(v)
