@@ -679,7 +679,7 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
 // per lane; dQ^T += K^T dS^T feeds dS^T back as the B operand.  Keys past Sk
 // read as zero (K = V = 0 => dS^T K^T contributes nothing), so only the causal
 // diagonal is masked.
-template <int D>
+template <int D, int PROBE = 0>  // PROBE 1: softmax / dS VALU skipped (timing probe, wrong results)
 __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
                                                               const bf16_t* __restrict__ dout,
                                                               int64_t sdb, int64_t sds, int64_t sdh,
@@ -765,7 +765,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
       d1 = mfma(fv[kk][1], df[kk], d1);
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < (PROBE ? 0 : 16); ++i) {
       const float pa = fast_exp2(fmaf(s0[i], c2, -lse2));
       const float pb = fast_exp2(fmaf(s1[i], c2, -lse2));
       s0[i] = pa * (d0[i] - dlt);
@@ -826,7 +826,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
 // query head of the GQA group x query blocks of 64 rows staged in LDS (Q, dO,
 // lse, delta), so dK/dV of the kv head are summed in registers and written
 // once as bf16.  Rows past Sq read as zero with lse = +inf => P = dS = 0.
-template <int D>
+template <int D, int PROBE = 0>  // PROBE 1: softmax / dS VALU skipped (timing probe, wrong results)
 __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
     AttnParams p, const bf16_t* __restrict__ dout, int64_t sdb, int64_t sds, int64_t sdh,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dk,
@@ -944,7 +944,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
           thr = t > 64 ? 64 : (int)t;
         }
 #pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
+        for (int gq = 0; gq < (PROBE ? 0 : 4); ++gq) {
           const int rowo = 32 * u + 8 * gq + 4 * h;
           const f32x4 L = *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * rowo) * kLog2e;
           const f32x4 Dl =
@@ -1149,9 +1149,16 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
   const unsigned gk = (unsigned)(((Sk + 127) / 128) * B * Hkv);
   const bf16_t* dop = (const bf16_t*)dout;
   if (D == 128) {
-    flash_bwd_dq_kernel<128><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq);
-    flash_bwd_dkdv_kernel<128><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
+    const char* pe = std::getenv("ST_FLASH_PROBE");  // diagnostics only (tools/probe_flash.py)
+    if (pe && std::atoi(pe) == 1) {
+      flash_bwd_dq_kernel<128, 1><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq);
+      flash_bwd_dkdv_kernel<128, 1><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
                                                    (bf16_t*)dv);
+    } else {
+      flash_bwd_dq_kernel<128><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq);
+      flash_bwd_dkdv_kernel<128><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
+                                                   (bf16_t*)dv);
+    }
   } else if (D == 64) {
     flash_bwd_dq_kernel<64><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq);
     flash_bwd_dkdv_kernel<64><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,

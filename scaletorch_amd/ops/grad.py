@@ -62,6 +62,13 @@ def prepare_dgrad_weight(w: torch.Tensor) -> None:
     if buf is None or buf.shape != (w.shape[1], w.shape[0]):
         buf = torch.empty(w.shape[1], w.shape[0], dtype=w.dtype, device=w.device)
         w._st_wt = buf
+    if os.environ.get("ST_DGRAD_WT_STREAM", "side") == "main":  # serialised into the forward (A/B)
+        _lib.ops().transpose_(w.detach(), buf)
+        done = torch.cuda.Event()
+        done.record()
+        w._st_wt_done = done
+        w._st_wt_epoch = _WT_EPOCH[0]
+        return
     st = _WT_STREAMS.get(w.device.index)
     if st is None:
         st = _WT_STREAMS[w.device.index] = torch.cuda.Stream(device=w.device)

@@ -161,6 +161,7 @@ def test_flash_fwd_bwd(B, Sq, Sk, H, Hkv, D, causal):
     _flash_case(B, Sq, Sk, H, Hkv, D, causal, 1.0)
 
 
+
 @pytest.mark.parametrize("qscale", [6.0, 30.0])
 def test_flash_large_logits(qscale):
     """Peaked softmax: exercises the deferred (thresholded) O rescale."""
