@@ -40,6 +40,9 @@ _DTYPES = {"bfloat16": torch.bfloat16, "bf16": torch.bfloat16, "float16": torch.
            "float32": torch.float32, "fp32": torch.float32}
 
 
+_COMPUTE_STREAMS: dict = {}
+
+
 class Trainer:
     def __init__(self, args, device_data: bool | None = None, build_data: bool = True):
         self.args = args
@@ -169,7 +172,27 @@ class Trainer:
 
     # ---------------------------------------------------------------- step
     def train_step(self) -> torch.Tensor:
-        """One optimizer step; returns the mean loss as a DEVICE tensor."""
+        """One optimizer step; returns the mean loss as a DEVICE tensor.
+
+        ``ST_COMPUTE_STREAM_PRIORITY`` < 0 runs the step on a high-priority HIP
+        stream, so the side streams (optimizer update, W^T copies) -- default
+        priority -- are dispatched behind the forward/backward kernels they
+        overlap.  The caller's stream waits for it before the loss is returned."""
+        prio = int(os.environ.get("ST_COMPUTE_STREAM_PRIORITY", "0")) if self.device.type == "cuda" else 0
+        if prio == 0:
+            return self._train_step()
+        key = (self.device.index, prio)
+        st = _COMPUTE_STREAMS.get(key)
+        if st is None:
+            st = _COMPUTE_STREAMS[key] = torch.cuda.Stream(device=self.device, priority=prio)
+        caller = torch.cuda.current_stream(self.device)
+        st.wait_stream(caller)
+        with torch.cuda.stream(st):
+            loss = self._train_step()
+        caller.wait_stream(st)
+        return loss
+
+    def _train_step(self) -> torch.Tensor:
         a = self.args
         ga = a.gradient_accumulation_steps
         self.optimizer.zero_grad()
