@@ -129,6 +129,10 @@ def main() -> int:
         num_hidden_layers=args.layers, dtype="bfloat16", weight_decay=0.1, betas=(0.9, 0.95),
         zero_stage=args.zero, fused_lm_head=bool(args.fused_head), lm_head_chunk_tokens=args.head_chunk,
     )
+    if args.backend == "gloo" and torch.cuda.is_available():  # 1-GPU multi-rank rehearsal
+        from scaletorch_amd.dist.gloo_staging import stage_gloo_cuda_p2p
+
+        stage_gloo_cuda_p2p()
     tr = Trainer(a)
     rank = tr.rank
     dev = tr.device

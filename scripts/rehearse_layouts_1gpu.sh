@@ -10,6 +10,10 @@ mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0 ST_GPU_OVERSUBSCRIBE=1 OMP_NUM_THREADS=2
 LAYOUTS=${LAYOUTS:-"tp2pp2dp2 cp8_32k mixtral_ep8 dp"}
 port=29810
+# heartbeat: a layout can run minutes without printing (gpurun kills silent commands)
+( while true; do sleep 50; echo "[rehearse] alive $(date +%T)"; done ) &
+hb=$!
+trap 'kill $hb 2>/dev/null' EXIT
 for lay in $LAYOUTS; do
   port=$((port + 1))
   echo "=== layout $lay"

@@ -83,45 +83,7 @@ def run_workers(fn, world: int, *args, timeout: float = 240.0) -> list:
 
 
 def stage_gloo_cuda_p2p() -> None:
-    """Test-only: let gloo groups carry CUDA tensors through point-to-point and
-    all-to-all by staging them through host memory (gloo has no device path for
-    those; RCCL refuses two ranks on one GPU, so multi-rank GPU tests on a
-    1-GPU box run gloo).  Blocking semantics; every op is completed in place."""
-    import torch
-    import torch.distributed as dist
+    """Test-only alias of scaletorch_amd.dist.gloo_staging.stage_gloo_cuda_p2p."""
+    from scaletorch_amd.dist.gloo_staging import stage_gloo_cuda_p2p as _stage
 
-    real_batch, real_a2a = dist.batch_isend_irecv, dist.all_to_all_single
-
-    class _Done:
-        def wait(self):
-            return True
-
-        def is_completed(self):
-            return True
-
-    def batch_isend_irecv(ops):
-        if not any(op.tensor.is_cuda for op in ops):
-            return real_batch(ops)
-        host, back = [], []
-        for op in ops:
-            t = op.tensor.detach().to("cpu", copy=True)
-            host.append(dist.P2POp(op.op, t, op.peer, op.group, op.tag))
-            if op.op in (dist.irecv, dist.recv):
-                back.append((op.tensor, t))
-        for w in real_batch(host):
-            w.wait()
-        for dst, t in back:
-            dst.copy_(t)
-        return [_Done()]
-
-    def all_to_all_single(output, input, output_split_sizes=None, input_split_sizes=None, group=None,
-                          async_op=False):
-        if not input.is_cuda:
-            return real_a2a(output, input, output_split_sizes, input_split_sizes, group=group, async_op=async_op)
-        out_h = torch.empty(output.shape, dtype=output.dtype)
-        real_a2a(out_h, input.cpu(), output_split_sizes, input_split_sizes, group=group)
-        output.copy_(out_h)
-        return _Done() if async_op else None
-
-    dist.batch_isend_irecv = batch_isend_irecv
-    dist.all_to_all_single = all_to_all_single
+    _stage()
