@@ -76,6 +76,8 @@ int st_qknorm_rope_bwd(void* dqkv, const void* xsave, const float* rstd, const v
                        const float* cos_t, const float* sin_t, const int64_t* pos, int64_t N, int S, int H, int Hkv,
                        int D, int64_t max_pos, float* partial, float* dw_out, hipStream_t st);
 int st_transpose_bf16(const void* src, void* dst, int R, int C, int64_t lds_src, int64_t lds_dst, hipStream_t st);
+int st_embedding_bwd(const int64_t* sorted_ids, const int64_t* order, const void* dy, int64_t ldd, float* grad,
+                     int64_t ldg, int T, int H, int64_t V, hipStream_t st);
 int st_lse_merge(float* out, float* lse, const void* bout, const float* blse, int B, int S, int H,
                  int D, int64_t sbb, int64_t sbs, int64_t sbh, hipStream_t st);
 }
@@ -261,6 +263,27 @@ void adamw_step_(at::Tensor master, at::Tensor exp_avg, at::Tensor exp_avg_sq,
                          (float)beta1, (float)beta2, (float)eps, (float)weight_decay, (float)bc1,
                          (float)std::sqrt(bc2), cur_stream());
   ST_CHECK_RC(rc, "adamw_step_");
+}
+
+// grad[V, H] fp32 += rows of dy[T, H] bf16 grouped by token id; sorted_ids / order from a
+// STABLE sort of the ids (deterministic: fixed summation order, no atomics)
+void embedding_bwd_(at::Tensor grad, const at::Tensor& dy, const at::Tensor& sorted_ids, const at::Tensor& order) {
+  check_bf16_cuda(dy, "dy");
+  check_same_gpu(grad, dy, "grad");
+  check_same_gpu(sorted_ids, dy, "sorted_ids");
+  check_same_gpu(order, dy, "order");
+  TORCH_CHECK(grad.scalar_type() == at::kFloat && grad.dim() == 2 && grad.stride(1) == 1, "embedding_bwd_: grad fp32 [V, H]");
+  TORCH_CHECK(dy.dim() == 2 && dy.stride(1) == 1 && dy.size(1) == grad.size(1), "embedding_bwd_: dy [T, H]");
+  TORCH_CHECK(sorted_ids.scalar_type() == at::kLong && order.scalar_type() == at::kLong && sorted_ids.is_contiguous() &&
+                  order.is_contiguous() && sorted_ids.numel() == dy.size(0) && order.numel() == dy.size(0),
+              "embedding_bwd_: int64 sorted_ids / order of length T");
+  TORCH_CHECK(dy.size(1) % 4 == 0 && dy.stride(0) % 4 == 0 && grad.stride(0) % 4 == 0, "embedding_bwd_: H % 4");
+  TORCH_CHECK(dy.size(0) < (1LL << 31) && dy.size(1) < (1LL << 31), "embedding_bwd_: dims");
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(dy.device());
+  int rc = st_embedding_bwd(sorted_ids.data_ptr<int64_t>(), order.data_ptr<int64_t>(), dy.data_ptr(), dy.stride(0),
+                            grad.data_ptr<float>(), grad.stride(0), (int)dy.size(0), (int)dy.size(1), grad.size(0),
+                            cur_stream());
+  ST_CHECK_RC(rc, "embedding_bwd_");
 }
 
 void transpose_(const at::Tensor& src, at::Tensor dst) {
@@ -628,6 +651,7 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("adamw_step_(Tensor(a!) master, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor grad, Tensor(d!)? param, Tensor? clip_coef, float lr, float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
   m.def("sumsq_(Tensor g, Tensor(a!) out) -> ()");
   m.def("transpose_(Tensor src, Tensor(a!) dst) -> ()");
+  m.def("embedding_bwd_(Tensor(a!) grad, Tensor dy, Tensor sorted_ids, Tensor order) -> ()");
   m.def("xent_fwd(Tensor logits, Tensor target, int vocab_start) -> Tensor[]");
   m.def("xent_bwd_(Tensor logits, Tensor target, int vocab_start, Tensor lse, Tensor dloss, Tensor(a!) dlogits) -> ()");
   m.def("flash_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int q_offset, int k_offset) -> Tensor[]");
@@ -657,6 +681,7 @@ TORCH_LIBRARY_IMPL(st_amd, CUDA, m) {
   m.impl("adamw_step_", &adamw_step_);
   m.impl("sumsq_", &sumsq_);
   m.impl("transpose_", &transpose_);
+  m.impl("embedding_bwd_", &embedding_bwd_);
   m.impl("xent_fwd", &xent_fwd);
   m.impl("xent_bwd_", &xent_bwd_);
   m.impl("flash_fwd", &flash_fwd);

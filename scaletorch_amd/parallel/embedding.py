@@ -1,7 +1,11 @@
 """Embedding lookup whose weight gradient is scattered straight into the fp32
-``main_grad`` arena (one index_add over the N looked-up rows) instead of
-materialising a dense [V, h] bf16 gradient (reference: F.embedding in
-scaletorch/models/llama.py:382-420 / tensor_parallel.py:479-507)."""
+``main_grad`` arena instead of materialising a dense [V, h] bf16 gradient
+(reference: F.embedding in scaletorch/models/llama.py:382-420 /
+tensor_parallel.py:479-507, whose backward sums with atomics).
+
+On GPU the scatter is deterministic (csrc/embedding.hip): token ids are sorted
+stably on device and one workgroup per distinct id sums its rows in token order,
+so the step is bitwise reproducible run to run.  CPU: ``index_add_`` (sequential)."""
 from __future__ import annotations
 
 import torch
@@ -24,7 +28,17 @@ class _EmbeddingFn(torch.autograd.Function):
         mg = w.main_grad
         if take_fresh(w):
             mg.zero_()
-        mg.index_add_(0, ids.reshape(-1), dy.reshape(-1, dy.shape[-1]).to(mg.dtype))
+        flat = ids.reshape(-1)
+        rows = dy.reshape(-1, dy.shape[-1])
+        from ..ops import _lib
+
+        if (_lib.use_native(rows) and rows.dtype == torch.bfloat16 and mg.dtype == torch.float32
+                and rows.shape[-1] % 4 == 0):
+            sorted_ids, order = torch.sort(flat.to(torch.int64), stable=True)
+            _lib.ops().embedding_bwd_(mg.view(mg.shape[0], -1), rows.contiguous(), sorted_ids.contiguous(),
+                                      order.contiguous())
+        else:
+            mg.index_add_(0, flat, rows.to(mg.dtype))
         _grad_ready(w)
         return None, None
 

@@ -453,3 +453,28 @@ def test_flash_cp_chunk_at_global_offset(q_off):
     dq, dk, dv = ops.flash_attn_bwd(dout, q, k, v, out, lse, scale, True, q_off, 0)
     rq, rk, rv = ops.attention.flash_bwd_ref(dout, q, k, v, out, lse, scale, True, q_off, 0)
     assert rel(dq, rq) < 2e-2 and rel(dk, rk) < 2e-2 and rel(dv, rv) < 2e-2
+
+
+def test_embedding_bwd_deterministic():
+    """Sorted-segment embedding backward (csrc/embedding.hip): equals the fp64
+    index_add reference, accumulates into existing rows, and is bitwise identical
+    run to run (the atomics path it replaces is not)."""
+    from scaletorch_amd.parallel.embedding import embedding
+
+    torch.manual_seed(3)
+    V, H, T = 300, 256, 5000
+    w = torch.nn.Parameter(torch.randn(V, H, device="cuda").bfloat16())
+    ids = torch.randint(0, V, (2, T // 2), device="cuda")
+    ids[0, :400] = 7  # one long run
+    dy = torch.randn(2, T // 2, H, device="cuda", dtype=torch.bfloat16)
+    ref = torch.zeros(V, H, dtype=torch.float64, device="cuda").index_add_(0, ids.reshape(-1),
+                                                                          dy.reshape(-1, H).double())
+    outs = []
+    for _ in range(2):
+        w.main_grad = torch.full((V, H), 0.5, device="cuda")
+        w._st_fresh = False  # accumulate into the existing 0.5
+        embedding(ids, w).backward(dy)
+        outs.append(w.main_grad.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    assert ((outs[0].double() - 0.5) - ref).abs().max().item() < 1e-3

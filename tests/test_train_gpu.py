@@ -216,3 +216,30 @@ def test_wgrad_tn_path_accumulates_fp32(tn, monkeypatch):
     accumulate_linear_wgrad(w, dy, x)
     torch.cuda.synchronize()
     assert rel(w.main_grad, 2 * ref) < 1e-3
+
+
+@pytest.mark.gpu
+def test_training_step_bitwise_deterministic():
+    """Two identical runs (same seed, synthetic data) end on bitwise-identical
+    losses and weights: no atomics anywhere in the step (embedding backward by
+    sorted segments, deterministic norms / dweight reductions, split-free GEMMs)."""
+    import torch
+
+    from scaletorch_amd.trainer.config import ScaleTorchArguments
+    from scaletorch_amd.trainer.engine import Trainer
+
+    def run():
+        a = ScaleTorchArguments(model_name_or_path="tiny-llama", synthetic_data=True, micro_batch_size=2,
+                                sequence_length=256, total_train_steps=3, learning_rate=1e-3, dtype="bfloat16",
+                                num_hidden_layers=2, seed=11)
+        tr = Trainer(a)
+        losses = [tr.reduced_loss(tr.train_step()) for _ in range(3)]
+        tr.optimizer.sync()
+        torch.cuda.synchronize()
+        flat = torch.cat([p.detach().float().reshape(-1) for p in tr.raw_model.parameters()])
+        return losses, flat.cpu()
+
+    l1, p1 = run()
+    l2, p2 = run()
+    assert l1 == l2
+    assert torch.equal(p1, p2)
