@@ -41,9 +41,10 @@ BASELINE_TOK_S_PER_GPU = 1391.0
 # layouts).  Sizes are per GPU; the data-parallel width absorbs the rest of the job.
 LAYOUTS = {
     "dp": dict(),
-    # 3-D: TP inside an xGMI pair, 2 pipeline stages, DP over the rest; 8 micro-batches keep
-    # the 1F1B bubble at (pp-1)/(M+pp-1) = 11 %; sequence parallel shards norm/residual activations
-    "tp2pp2dp2": dict(tp=2, pp=2, sp=True, micro_batch_size=4, grad_acc=8),
+    # 3-D: TP inside an xGMI pair, 2 pipeline stages, DP over the rest; 8 micro-batches through
+    # the interleaved 1F1B schedule with 2 chunks per stage keep the bubble at
+    # (pp-1)/(V*M+pp-1) = 6 % (11 % plain 1F1B); sequence parallel shards norm/residual activations
+    "tp2pp2dp2": dict(tp=2, pp=2, sp=True, micro_batch_size=4, grad_acc=8, vpp=2),
     # long context: 32K tokens over 8 CP ranks (4K local), zig-zag chunks, GQA-sized K/V
     "cp8_32k": dict(cp=-1, seq_len=32768, micro_batch_size=1),
     # Mixtral 8x7B: one expert per GPU (EP carved out of DP), dense weights ZeRO-1 over DP x EP
@@ -66,6 +67,7 @@ def main() -> int:
     ap.add_argument("--cp", type=int, default=None)
     ap.add_argument("--ep", type=int, default=None)
     ap.add_argument("--sp", action="store_true", default=None)
+    ap.add_argument("--vpp", type=int, default=None, help="model chunks per pipeline stage (interleaved 1F1B)")
     ap.add_argument("--cp_comm", default="auto", help="auto | allgather | ring | ulysses")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) | gloo (debug rehearsals only)")
     ap.add_argument("--gc", action="store_true", help="activation checkpointing")
@@ -81,7 +83,8 @@ def main() -> int:
     ap.add_argument("--layers", type=int, default=None, help="(debug only; result marked invalid)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    preset = dict(model="llama3-8b", micro_batch_size=4, seq_len=4096, grad_acc=1, tp=1, pp=1, cp=1, ep=1, sp=False)
+    preset = dict(model="llama3-8b", micro_batch_size=4, seq_len=4096, grad_acc=1, tp=1, pp=1, cp=1, ep=1, sp=False,
+                  vpp=1)
     preset.update({k: (world if v == -1 else v) for k, v in LAYOUTS[args.layout].items()})
     for k, v in preset.items():
         if getattr(args, k) is None:
@@ -122,6 +125,7 @@ def main() -> int:
         model_name_or_path=args.model, synthetic_data=True, micro_batch_size=args.micro_batch_size,
         sequence_length=args.seq_len, gradient_accumulation_steps=ga, total_train_steps=args.warmup + args.steps,
         tensor_parallel_size=args.tp, pipeline_parallel_size=args.pp, context_parallel_size=args.cp,
+        virtual_pipeline_size=args.vpp if args.pp > 1 else 1,
         expert_parallel_size=args.ep, data_parallel_size=dp, sequence_parallel=args.sp,
         cp_comm=args.cp_comm, backend=args.backend,
         gradient_checkpointing=args.gc, recompute_granularity=args.recompute, learning_rate=3e-4, lr_scheduler_type="cosine", warmup_steps=0,
@@ -189,6 +193,7 @@ def main() -> int:
         "config": {"model": args.model, "global_batch": dp * args.ep * args.micro_batch_size * ga,
                    "micro_batch": args.micro_batch_size, "grad_accum": ga, "seq_len": args.seq_len,
                    "parallelism": par, "layout": args.layout, "sequence_parallel": args.sp, "activation_checkpointing": args.gc,
+                   "virtual_pipeline": args.vpp if args.pp > 1 else 1,
                    "lm_head": f"fused, {args.head_chunk}-token chunks" if args.fused_head else "logits + CE",
                    "grad_reduce_dtype": args.grad_reduce_dtype, "zero_stage": args.zero if dp * args.cp * args.ep > 1 else 0},
         "tokens_per_s_per_gpu": round(per_gpu, 1),

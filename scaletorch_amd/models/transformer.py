@@ -170,19 +170,32 @@ class TransformerLM(nn.Module):
     """Causal LM.  ``forward`` returns this TP rank's vocab shard of the logits
     (last PP stage) or the hidden states to send to the next stage."""
 
-    def __init__(self, cfg: ModelConfig, sequence_parallel: bool = False, layer_distribution: list[int] | None = None):
+    def __init__(self, cfg: ModelConfig, sequence_parallel: bool = False, layer_distribution: list[int] | None = None,
+                 virtual_stages: int = 1):
         super().__init__()
         self.config = self.model_config = cfg
         self.sequence_parallel = sequence_parallel and mesh.tp_size() > 1
         pp, pr = mesh.pp_size(), (mesh.pgm.pp_rank if mesh.pgm else 0)
         self.first_stage, self.last_stage = pr == 0, pr == pp - 1
-        self.layer_start, self.layer_end = stage_layer_range(cfg.num_hidden_layers, pp, pr, layer_distribution)
+        # virtual pipeline stages (interleaved 1F1B, parallel/interleaved.py): the layers are split
+        # evenly into pp*V chunks; this rank holds global chunks v*pp + pr, v = 0..V-1
+        self.virtual_stages = max(1, int(virtual_stages))
+        if self.virtual_stages > 1:
+            if layer_distribution:
+                raise ValueError("layer_distribution is not supported with virtual pipeline stages")
+            if cfg.num_hidden_layers < pp * self.virtual_stages:
+                raise ValueError(f"{cfg.num_hidden_layers} layers cannot fill {pp} x {self.virtual_stages} chunks")
+            self.chunk_ranges = [stage_layer_range(cfg.num_hidden_layers, pp * self.virtual_stages, v * pp + pr)
+                                 for v in range(self.virtual_stages)]
+        else:
+            self.chunk_ranges = [stage_layer_range(cfg.num_hidden_layers, pp, pr, layer_distribution)]
+        self.layer_start, self.layer_end = self.chunk_ranges[0][0], self.chunk_ranges[-1][1]
         sp = self.sequence_parallel
         std = cfg.initializer_range if cfg.init == "normal" else None
         if self.first_stage or (cfg.tie_word_embeddings and self.last_stage):
             self.embedding = VocabParallelEmbedding(cfg.vocab_size, cfg.hidden_size, sequence_parallel=sp, init_std=std)
         self.decoder_layers = nn.ModuleDict(
-            {str(i): DecoderLayer(cfg, i, sp) for i in range(self.layer_start, self.layer_end)})
+            {str(i): DecoderLayer(cfg, i, sp) for lo, hi in self.chunk_ranges for i in range(lo, hi)})
         if self.last_stage:
             self.final_norm = ops.RMSNorm(cfg.hidden_size, eps=cfg.rms_norm_eps)
             self.final_proj = ColumnParallelLinear(cfg.hidden_size, cfg.vocab_size, bias=False,
@@ -229,9 +242,12 @@ class TransformerLM(nn.Module):
             if not self.config.tie_word_embeddings:
                 self.final_proj.reset_parameters()
 
-    def aux_loss(self) -> torch.Tensor | None:
-        losses = [l.moe.last_aux_loss for l in self.decoder_layers.values()
-                  if l.is_moe and l.moe.last_aux_loss is not None]
+    def aux_loss(self, chunk: int | None = None) -> torch.Tensor | None:
+        """Sum of the MoE load-balancing losses of the last forward (of local chunk
+        ``chunk`` only, with virtual pipeline stages)."""
+        layers = self.decoder_layers.values() if chunk is None else \
+            [self.decoder_layers[str(i)] for i in range(*self.chunk_ranges[chunk])]
+        losses = [l.moe.last_aux_loss for l in layers if l.is_moe and l.moe.last_aux_loss is not None]
         if not losses:
             return None
         return torch.stack([x.float() for x in losses]).sum()
@@ -240,11 +256,20 @@ class TransformerLM(nn.Module):
     def forward(self, input_ids: torch.Tensor | None = None, position_ids: torch.Tensor | None = None,
                 hidden_states: torch.Tensor | None = None, gradient_checkpointing: bool = False,
                 attention_mask: torch.Tensor | None = None, labels: torch.Tensor | None = None,
-                lm_head_chunk: int | None = None) -> torch.Tensor:
+                lm_head_chunk: int | None = None, chunk: int | None = None) -> torch.Tensor:
         """Logits shard (last stage), or -- with ``labels`` (global target ids) on
         the last stage -- the mean cross-entropy from the fused chunked LM head
-        (ops/fused_head.py), which never materialises the logits."""
-        if self.first_stage:
+        (ops/fused_head.py), which never materialises the logits.  ``chunk`` (virtual
+        pipeline stages): run only local chunk v -- embedding on rank 0's chunk 0,
+        final norm + head on the last rank's last chunk, hidden states otherwise."""
+        V = self.virtual_stages
+        if chunk is None and V > 1:
+            raise ValueError("a model with virtual pipeline stages is run one chunk at a time")
+        v = 0 if chunk is None else int(chunk)
+        embeds = self.first_stage and v == 0
+        heads = self.last_stage and v == V - 1
+        lo, hi = self.chunk_ranges[v]
+        if embeds:
             x = self.embedding(input_ids)
         else:
             if hidden_states is None:
@@ -253,13 +278,14 @@ class TransformerLM(nn.Module):
         residual = None
         full = gradient_checkpointing in (True, "full") and self.training
         selective = gradient_checkpointing == "selective"
-        for layer in self.decoder_layers.values():
+        for i in range(lo, hi):
+            layer = self.decoder_layers[str(i)]
             if full:
                 x, residual = torch_checkpoint(layer, x, residual, self.cos, self.sin, position_ids,
                                                use_reentrant=False)
             else:
                 x, residual = layer(x, residual, self.cos, self.sin, position_ids, selective_recompute=selective)
-        if not self.last_stage:
+        if not heads:
             return x if residual is None else x + residual
         x = self.final_norm(x) if residual is None else self.final_norm(x, residual)[0]
         # a module call (SP: gather along seq inside the column-parallel fn), so the head's
@@ -324,5 +350,7 @@ class TransformerLM(nn.Module):
         return self.load_state_dict(sd, strict=strict)
 
 
-def build_model(cfg: ModelConfig, sequence_parallel: bool = False, layer_distribution=None) -> TransformerLM:
-    return TransformerLM(cfg, sequence_parallel=sequence_parallel, layer_distribution=layer_distribution)
+def build_model(cfg: ModelConfig, sequence_parallel: bool = False, layer_distribution=None,
+                virtual_stages: int = 1) -> TransformerLM:
+    return TransformerLM(cfg, sequence_parallel=sequence_parallel, layer_distribution=layer_distribution,
+                         virtual_stages=virtual_stages)

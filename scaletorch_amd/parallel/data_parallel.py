@@ -236,7 +236,7 @@ class GradArena:
         into ``sq_acc`` on the side stream while the rest of backward runs (the
         global-norm pass after backward then reads one scalar per arena)."""
         st = self.side_stream
-        if st is None:
+        if st is None or os.environ.get("ST_BUCKET_NORM", "1") != "1":  # 0: one pass after backward (A/B)
             return
         from ..ops import _lib
 
@@ -498,7 +498,10 @@ class DataParallel(nn.Module):
 
     def _post_backward(self) -> None:
         self._callback_queued = False
-        if self.require_backward_grad_sync:
+        # final_backward False (interleaved pipeline: a chunk's last micro-batch, other
+        # chunks still to come): buckets fire as their params become ready, but the
+        # join and the TP-partial reduction wait for the step's last backward
+        if self.require_backward_grad_sync and getattr(self, "final_backward", True):
             for a in self.arenas:
                 a.finish()
                 a.reset_counts()

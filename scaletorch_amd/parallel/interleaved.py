@@ -1,0 +1,189 @@
+"""Interleaved 1F1B pipeline schedule (virtual pipeline stages).
+
+Each of the P pipeline ranks holds V model chunks: the L layers are split evenly
+into P*V chunks and global chunk c = v*P + r lives on rank r as its local chunk v
+(the embedding on rank 0 chunk 0, the final norm + LM head on rank P-1 chunk
+V-1).  A micro-batch therefore visits the ring of ranks V times, and the
+pipeline bubble shrinks from (P-1)/(M+P-1) to (P-1)/(V*M+P-1) of the step for M
+micro-batches (Narayanan et al., "Efficient Large-Scale Language Model Training
+on GPU Clusters", 2021).  The reference has AFAB and plain 1F1B only
+(scaletorch/parallel/pipeline_parallel/pipeline_parallel.py:457-671).
+
+Step numbering (identical on every rank, M a multiple of P):
+  forward step k  -> chunk  (k mod P*V) // P,          micro-batch (k // (P*V))*P + k mod P
+  backward step k -> chunk  V-1 - (k mod P*V) // P,    same micro-batch formula
+so a forward message produced at step k is consumed by the next rank at ITS step
+k, except across the ring seam (rank P-1 -> rank 0, next chunk), where it is step
+k + P; backward messages mirror this.  ``build_schedule`` returns, per rank, the
+ordered list of compute steps and batched exchanges; ``simulate`` replays all
+ranks under RCCL semantics (one ordered p2p stream per rank: a batch starts once
+the previous one has completed; an op completes when its partner's current batch
+holds the matching op) and proves the schedule deadlock-free and order-matched.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+
+def fwd_chunk(k: int, P: int, V: int) -> int:
+    return (k % (P * V)) // P
+
+
+def bwd_chunk(k: int, P: int, V: int) -> int:
+    return V - 1 - (k % (P * V)) // P
+
+
+def micro_batch(k: int, P: int, V: int) -> int:
+    return (k // (P * V)) * P + k % P
+
+
+def num_warmup(P: int, V: int, M: int, r: int) -> int:
+    return min((P - r - 1) * 2 + (V - 1) * P, M * V)
+
+
+@dataclass
+class Exchange:
+    """One batched p2p exchange: entries are ("fwd" | "bwd", step) -- a forward
+    message carries the output of forward step `step`, a backward message the
+    input gradient of backward step `step` (the sender's numbering)."""
+    send: list = field(default_factory=list)
+    recv: list = field(default_factory=list)  # ("fwd", k): input of OUR fwd step k; ("bwd", k): grad for OUR bwd step k
+
+
+def build_schedule(P: int, V: int, M: int, r: int) -> list:
+    """Ordered actions of rank r: ("F", k), ("B", k) and Exchange objects."""
+    if M % P:
+        raise ValueError(f"interleaved 1F1B needs micro-batches ({M}) divisible by pipeline size ({P})")
+    T = M * V
+    W = num_warmup(P, V, M, r)
+    first, last = r == 0, r == P - 1
+
+    def send_fwd(k):
+        return not (last and fwd_chunk(k, P, V) == V - 1)
+
+    def recv_fwd(k):  # input of forward step k comes over the wire
+        return k < T and not (first and fwd_chunk(k, P, V) == 0)
+
+    def send_bwd(k):
+        return not (first and bwd_chunk(k, P, V) == 0)
+
+    def recv_bwd(k):
+        return k < T and not (last and bwd_chunk(k, P, V) == V - 1)
+
+    acts = []
+    if recv_fwd(0):
+        acts.append(Exchange(recv=[("fwd", 0)]))
+    for k in range(W):
+        acts.append(("F", k))
+        ex = Exchange()
+        if send_fwd(k):
+            ex.send.append(("fwd", k))
+        if recv_fwd(k + 1) and k + 1 < T:
+            ex.recv.append(("fwd", k + 1))
+        if k == W - 1 and W < T and recv_bwd(0):
+            ex.recv.append(("bwd", 0))
+        if ex.send or ex.recv:
+            acts.append(ex)
+    for j in range(T - W):
+        fk, bk = W + j, j
+        acts.append(("F", fk))
+        acts.append(("B", bk))
+        ex = Exchange()
+        if send_fwd(fk):
+            ex.send.append(("fwd", fk))
+        if send_bwd(bk):
+            ex.send.append(("bwd", bk))
+        if fk + 1 < T and recv_fwd(fk + 1):
+            ex.recv.append(("fwd", fk + 1))
+        if recv_bwd(bk + 1):
+            ex.recv.append(("bwd", bk + 1))
+        if ex.send or ex.recv:
+            acts.append(ex)
+    if W == T and recv_bwd(0):  # all-warmup rank: the first gradient arrives on its own
+        acts.append(Exchange(recv=[("bwd", 0)]))
+    for bk in range(T - W, T):
+        acts.append(("B", bk))
+        ex = Exchange()
+        if send_bwd(bk):
+            ex.send.append(("bwd", bk))
+        if recv_bwd(bk + 1):
+            ex.recv.append(("bwd", bk + 1))
+        if ex.send or ex.recv:
+            acts.append(ex)
+    return acts
+
+
+def _peer_and_key(P: int, r: int, kind: str, k: int, sending: bool):
+    """(peer rank, message key) of a message; the key names the message the same way
+    on both ends: (kind, receiver's step)."""
+    if kind == "fwd":
+        if sending:
+            dst = (r + 1) % P
+            return dst, ("fwd", k + P if r == P - 1 else k)
+        return (r - 1) % P, ("fwd", k)
+    if sending:
+        dst = (r - 1) % P
+        return dst, ("bwd", k + P if r == 0 else k)
+    return (r + 1) % P, ("bwd", k)
+
+
+def simulate(P: int, V: int, M: int) -> None:
+    """Replay every rank's schedule under ordered-stream p2p semantics; raises on a
+    deadlock, an unmatched message or a compute step whose input never arrived."""
+    scheds = [build_schedule(P, V, M, r) for r in range(P)]
+    pos = [0] * P
+    pending = [None] * P   # rank -> list of (peer, key, is_send) still open in its current batch
+    have_fwd = [set() for _ in range(P)]
+    have_bwd = [set() for _ in range(P)]
+    T = M * V
+
+    def load(r):
+        while pos[r] < len(scheds[r]) and pending[r] is None:
+            a = scheds[r][pos[r]]
+            if isinstance(a, Exchange):
+                ops = [(*_peer_and_key(P, r, kd, k, True), True) for kd, k in a.send]
+                ops += [(*_peer_and_key(P, r, kd, k, False), False) for kd, k in a.recv]
+                pending[r] = ops
+            else:
+                kind, k = a
+                if kind == "F":
+                    if not ((r == 0 and fwd_chunk(k, P, V) == 0) or k in have_fwd[r]):
+                        raise AssertionError(f"rank {r}: forward step {k} without its input")
+                else:
+                    if not ((r == P - 1 and bwd_chunk(k, P, V) == V - 1) or k in have_bwd[r]):
+                        raise AssertionError(f"rank {r}: backward step {k} without its output grad")
+                pos[r] += 1
+
+    for r in range(P):
+        load(r)
+    while True:
+        progressed = False
+        for r in range(P):
+            if not pending[r]:
+                continue
+            for op in list(pending[r]):
+                peer, key, is_send = op
+                if pending[peer] is None:
+                    continue
+                match = (r, key, not is_send)
+                if match in pending[peer]:
+                    pending[r].remove(op)
+                    pending[peer].remove(match)
+                    recv_rank = peer if is_send else r
+                    (have_fwd if key[0] == "fwd" else have_bwd)[recv_rank].add(key[1])
+                    progressed = True
+            for q in range(P):
+                if pending[q] == []:
+                    pending[q] = None
+                    pos[q] += 1
+                    load(q)
+        if all(pos[r] >= len(scheds[r]) and pending[r] is None for r in range(P)):
+            break
+        if not progressed:
+            state = {r: (pos[r], pending[r]) for r in range(P)}
+            raise AssertionError(f"p2p deadlock (P={P}, V={V}, M={M}): {state}")
+    for r in range(P):
+        nb = sum(1 for a in scheds[r] if not isinstance(a, Exchange) and a[0] == "B")
+        nf = sum(1 for a in scheds[r] if not isinstance(a, Exchange) and a[0] == "F")
+        if nf != T or nb != T:
+            raise AssertionError(f"rank {r}: {nf} forward / {nb} backward steps, expected {T}")

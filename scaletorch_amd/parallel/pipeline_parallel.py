@@ -121,7 +121,8 @@ class PipelineEngine:
     """Runs one optimizer step's worth of micro-batches through this stage."""
 
     def __init__(self, model, loss_fn, tensor_shape, dtype=torch.bfloat16, device=None,
-                 gradient_checkpointing: bool = False, aux_loss_fn=None, head_kwargs_fn=None):
+                 gradient_checkpointing: bool = False, aux_loss_fn=None, head_kwargs_fn=None,
+                 virtual_stages: int = 1):
         self.model = model  # DataParallel-wrapped stage
         self.loss_fn = loss_fn  # (logits or the fused head's loss, batch) -> scalar loss
         self.head_kwargs_fn = head_kwargs_fn  # batch -> extra model kwargs on the last stage (fused LM head)
@@ -129,6 +130,7 @@ class PipelineEngine:
         self.dtype, self.device = dtype, device
         self.gc = gradient_checkpointing
         self.aux_loss_fn = aux_loss_fn
+        self.virtual_stages = virtual_stages
 
     @property
     def _first(self):
@@ -228,6 +230,97 @@ class PipelineEngine:
             n_bwd += 1
             dx = self._backward(xo, yo, dy, last_backward=(n_bwd == num_micro))
             _p2p(send_bwd=dx)
+        wait_sends()
+        return loss_sum
+
+
+    # ------------------------------------------------------------------ interleaved 1F1B
+    def train_step_interleaved(self, data_iter, num_micro: int) -> torch.Tensor:
+        """Interleaved 1F1B over this rank's ``virtual_stages`` model chunks
+        (parallel/interleaved.py has the schedule and its deadlock-free proof by
+        simulation).  Exchanges are batched p2p on the pipeline ring; a batch with
+        a receive is joined before the data is used, send-only batches stay in
+        flight until the end of the step.  The DP gradient sync is enabled for the
+        last micro-batch of each chunk, so every bucket fires during backward."""
+        from .interleaved import Exchange, build_schedule, bwd_chunk, fwd_chunk, micro_batch
+
+        pg = mesh.pgm
+        P, r, V, M = pg.pp_world_size, pg.pp_rank, self.virtual_stages, num_micro
+        ring = pg.pp_group_ids
+        nxt, prv = ring[(r + 1) % P], ring[(r - 1) % P]
+        group = pg.pp_group
+        batches: list = []
+
+        def batch(m):
+            while len(batches) <= m:
+                batches.append(next(data_iter))
+            return batches[m]
+
+        inputs, grads = {}, {}        # fwd step -> received input; bwd step -> received output grad
+        acts = {}                     # (chunk, micro) -> (x, y)
+        outs, dxs = {}, {}            # fwd step -> output to send; bwd step -> input grad to send
+        loss_sum = torch.zeros((), dtype=torch.float32, device=self.device)
+        for a in build_schedule(P, V, M, r):
+            if isinstance(a, Exchange):
+                ops, rbufs = [], []
+                for kind, k in a.send:
+                    t = outs.pop(k) if kind == "fwd" else dxs.pop(k)
+                    peer = nxt if kind == "fwd" else prv
+                    ops.append(dist.P2POp(dist.isend, t.contiguous(), peer, group))
+                    _STATS["send_forward" if kind == "fwd" else "send_backward"] += 1
+                    trace.record("pp.send_" + ("forward" if kind == "fwd" else "backward"), t, peer=peer)
+                for kind, k in a.recv:
+                    buf = torch.empty(self.tensor_shape, dtype=self.dtype, device=self.device)
+                    peer = prv if kind == "fwd" else nxt
+                    ops.append(dist.P2POp(dist.irecv, buf, peer, group))
+                    rbufs.append((kind, k, buf))
+                    _STATS["recv_forward" if kind == "fwd" else "recv_backward"] += 1
+                    trace.record("pp.recv_" + ("forward" if kind == "fwd" else "backward"), buf, peer=peer)
+                works = dist.batch_isend_irecv(ops)
+                if rbufs:
+                    for w in works:
+                        w.wait()
+                    for kind, k, buf in rbufs:
+                        if kind == "fwd":
+                            inputs[k] = buf.requires_grad_(True)
+                        else:
+                            grads[k] = buf
+                else:
+                    _INFLIGHT.append((works, [op.tensor for op in ops]))
+                continue
+            kind, k = a
+            if kind == "F":
+                v, m = fwd_chunk(k, P, V), micro_batch(k, P, V)
+                first, last = r == 0 and v == 0, r == P - 1 and v == V - 1
+                x = None if first else inputs.pop(k)
+                b = batch(m)
+                extra = self.head_kwargs_fn(b) if (last and self.head_kwargs_fn is not None) else {}
+                y = self.model(input_ids=b["input_ids"] if first else None, position_ids=b["position_ids"],
+                               hidden_states=x, gradient_checkpointing=self.gc, chunk=v, **extra)
+                aux = self.aux_loss_fn(v) if self.aux_loss_fn is not None else None
+                if last:
+                    y = self.loss_fn(y, b) / M
+                    if aux is not None:
+                        y = y + aux / M
+                    loss_sum += y.detach().float()
+                else:
+                    if aux is not None:
+                        y = _AttachAux.apply(y, aux / M)
+                    outs[k] = y.detach()
+                acts[(v, m)] = (x, y)
+            else:
+                v, m = bwd_chunk(k, P, V), micro_batch(k, P, V)
+                x, y = acts.pop((v, m))
+                self.model.require_backward_grad_sync = m == M - 1
+                self.model.final_backward = k == M * V - 1
+                if r == P - 1 and v == V - 1:
+                    y.backward()
+                else:
+                    torch.autograd.backward(y, grads.pop(k))
+                self.model.require_backward_grad_sync = True
+                self.model.final_backward = True
+                if x is not None:
+                    dxs[k] = x.grad
         wait_sends()
         return loss_sum
 

@@ -58,6 +58,9 @@ class ParallelArguments:
     context_parallel_size: int = field(default=1)
     expert_parallel_size: int = field(default=1)
     pipeline_parallel_engine: str = field(default="1f1b", metadata={"help": "1f1b | afab"})
+    virtual_pipeline_size: int = field(default=1, metadata={"help": "model chunks per pipeline rank: > 1 runs the "
+                                                                      "interleaved 1F1B schedule (needs 1f1b and "
+                                                                      "gradient_accumulation_steps % pp == 0)"})
     backend: str = field(default="nccl", metadata={"help": "nccl (=RCCL) | gloo | hccl (maps to nccl)"})
     sequence_parallel: bool = field(default=False, metadata={"help": "Megatron-SP over the TP group"})
     cp_zigzag: bool = field(default=True, metadata={"help": "zig-zag load-balanced CP chunks"})
@@ -72,6 +75,14 @@ class ParallelArguments:
                 raise ValueError(f"{name} must be >= 1, got {getattr(self, name)}")
         if self.pipeline_parallel_engine not in {"1f1b", "afab"}:
             raise ValueError(f'pipeline_parallel_engine must be "1f1b" or "afab", got {self.pipeline_parallel_engine}')
+        if self.virtual_pipeline_size < 1:
+            raise ValueError("virtual_pipeline_size must be >= 1")
+        if self.virtual_pipeline_size > 1:
+            if self.pipeline_parallel_size < 2 or self.pipeline_parallel_engine != "1f1b":
+                raise ValueError("virtual_pipeline_size > 1 needs pipeline_parallel_size > 1 and the 1f1b engine")
+            if getattr(self, "gradient_accumulation_steps", 1) % self.pipeline_parallel_size:
+                raise ValueError("interleaved 1F1B needs gradient_accumulation_steps divisible by "
+                                 "pipeline_parallel_size")
         if self.backend not in {"nccl", "gloo", "hccl"}:
             raise ValueError(f"backend must be one of {{nccl, gloo, hccl}}, got {self.backend}")
 

@@ -89,7 +89,8 @@ class Trainer:
             prev = torch.get_default_dtype()
             torch.set_default_dtype(self.dtype if self.dtype.is_floating_point else torch.float32)
             try:
-                model = build_model(cfg, sequence_parallel=a.sequence_parallel, layer_distribution=dist_)
+                model = build_model(cfg, sequence_parallel=a.sequence_parallel, layer_distribution=dist_,
+                                    virtual_stages=a.virtual_pipeline_size)
             finally:
                 torch.set_default_dtype(prev)
         model.cos, model.sin = model.cos.float(), model.sin.float()
@@ -127,7 +128,8 @@ class Trainer:
                                            dtype=self.dtype, device=self.device,
                                            gradient_checkpointing=self.gc_mode,
                                            aux_loss_fn=model.aux_loss if cfg.is_moe else None,
-                                           head_kwargs_fn=self._head_kwargs)
+                                           head_kwargs_fn=self._head_kwargs,
+                                           virtual_stages=a.virtual_pipeline_size)
 
     # ---------------------------------------------------------------- data
     def _build_data(self, synthetic: bool):
@@ -199,7 +201,9 @@ class Trainer:
         if self.pp > 1:
             it = (self._to_device(next(self.data)) for _ in iter(int, 1))
             eng = self.pipeline
-            if a.pipeline_parallel_engine == "1f1b":
+            if a.virtual_pipeline_size > 1:
+                loss = eng.train_step_interleaved(it, ga)
+            elif a.pipeline_parallel_engine == "1f1b":
                 loss = eng.train_step_1f1b(it, ga)
             else:
                 loss = eng.train_step_afab(it, ga)

@@ -17,8 +17,9 @@ trap 'kill $hb 2>/dev/null' EXIT
 for lay in $LAYOUTS; do
   port=$((port + 1))
   echo "=== layout $lay"
+  layers=2; [ "$lay" = tp2pp2dp2 ] && layers=4  # 2 pipeline stages x 2 interleaved chunks
   timeout -k 10 ${LAYOUT_TIMEOUT:-300} python -m torch.distributed.run --nnodes 1 --nproc-per-node 8 \
-    --master-addr 127.0.0.1 --master-port $port bench.py --gpus 8 --layout "$lay" --layers 2 --steps 2 --warmup 1 \
+    --master-addr 127.0.0.1 --master-port $port bench.py --gpus 8 --layout "$lay" --layers $layers --steps 2 --warmup 1 \
     --backend gloo ${EXTRA:-} > "gpurun_out/rehearsal_$lay.log" 2>&1
   rc=$?
   echo "rc=$rc"; grep -E "HBM estimate|metric|Error|error" "gpurun_out/rehearsal_$lay.log" | head -5

@@ -34,7 +34,7 @@ import pytest  # noqa: E402
 
 @pytest.mark.slow
 @pytest.mark.parametrize("layout,model,extra,par", [
-    ("tp2pp2dp2", "tiny-llama", ["--seq_len", "64", "--micro_batch_size", "1"], "dp2tp2pp2"),
+    ("tp2pp2dp2", "tiny-llama", ["--seq_len", "64", "--micro_batch_size", "1", "--layers", "4"], "dp2tp2pp2"),
     ("cp8_32k", "tiny-llama", ["--seq_len", "256"], "dp1cp8"),
     ("mixtral_ep8", "tiny-mixtral", ["--seq_len", "64", "--micro_batch_size", "1"], "dp1ep8"),
 ])
@@ -52,4 +52,6 @@ def test_bench_layout_presets_world8_gloo(layout, model, extra, par):
     assert len(lines) == 1, out.stdout
     d = json.loads(lines[0])
     assert d["config"]["parallelism"] == par and d["config"]["layout"] == layout and d["n_gpus"] == 8
+    if layout == "tp2pp2dp2":
+        assert d["config"]["virtual_pipeline"] == 2  # interleaved 1F1B
     assert "HBM estimate" in out.stderr

@@ -145,6 +145,50 @@ def test_dense_parity_world2(kw):
     _compare(ref, res)
 
 
+@pytest.mark.parametrize("pp,v,ga,extra", [(2, 2, 2, {}), (2, 2, 4, {}), (4, 2, 4, {}),
+                                           (2, 2, 2, {"tensor_parallel_size": 2, "sequence_parallel": True})],
+                         ids=["pp2v2_ga2", "pp2v2_ga4", "pp4v2_ga4", "tp2_sp_pp2v2"])
+def test_interleaved_1f1b_parity(pp, v, ga, extra):
+    """Interleaved 1F1B (v model chunks per rank over pp x v chunks of the layers)
+    equals the single-process step on loss and every weight."""
+    layers = pp * v
+    ref = _reference("tiny-llama", ga, num_hidden_layers=layers)
+    world = pp * extra.get("tensor_parallel_size", 1)
+    res = run_workers(_worker, world, "tiny-llama", dict(pipeline_parallel_size=pp, micro_batch_size=GLOBAL_B // ga,
+                                                         gradient_accumulation_steps=ga, virtual_pipeline_size=v,
+                                                         num_hidden_layers=layers, **extra))
+    _compare(ref, res)
+
+
+def test_interleaved_schedules_are_deadlock_free():
+    """Every (P, V, M) schedule replays without deadlock under ordered-stream p2p
+    semantics, every message matched in order, every step's input present; a
+    schedule with one receive dropped is caught."""
+    from scaletorch_amd.parallel import interleaved as I
+
+    for P in (2, 3, 4, 8):
+        for V in (1, 2, 3, 4):
+            for mult in (1, 2, 3):
+                I.simulate(P, V, P * mult)
+    real = I.build_schedule
+
+    def broken(P, V, M, r):
+        acts = real(P, V, M, r)
+        if r == 1:
+            for a in acts:
+                if isinstance(a, I.Exchange) and a.recv:
+                    a.recv.pop()
+                    break
+        return acts
+
+    I.build_schedule = broken
+    try:
+        with pytest.raises(AssertionError):
+            I.simulate(4, 2, 8)
+    finally:
+        I.build_schedule = real
+
+
 @pytest.mark.parametrize("comm", ["ulysses", "allgather"])
 def test_cp4_parity_world4(comm):
     """cp=4 > Hkv=2: Ulysses replicates each kv head over 2 ranks and sums their dK/dV."""

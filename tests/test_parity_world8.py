@@ -51,6 +51,15 @@ def test_tp2_pp2_dp2_zero1_adamw():
     _compare(ref, res, atol=5e-5, rtol=5e-3)
 
 
+def test_tp2_pp2_dp2_interleaved_zero1_adamw():
+    """Interleaved 1F1B (2 chunks per pipeline rank, 4 layers) with SP and ZeRO-1 over
+    2 AdamW steps equals the single-process run."""
+    ref = _reference("tiny-llama", 4, GB, num_hidden_layers=4, **_ADAM)
+    res = run_workers(_worker, 8, "tiny-llama", dict(_TPPPDP, sequence_parallel=True, zero_stage=1,
+                                                     virtual_pipeline_size=2, num_hidden_layers=4, **_ADAM))
+    _compare(ref, res, atol=5e-5, rtol=5e-3)
+
+
 @pytest.mark.parametrize("comm", ["allgather", "ring"])
 def test_cp8(comm):
     """cp=8 (zig-zag: 16 chunks of 2 tokens) with the GQA-sized K/V transports."""
