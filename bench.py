@@ -8,10 +8,12 @@ fwd+bwd).  Weak scaling: every GPU processes
 ``--micro_batch_size x --seq_len`` tokens per micro-batch; N GPUs = DP=N
 (override the layout with --tp/--pp/--cp/--ep).
 
-Default micro-batch is 4 x 4096 tokens: the step is sized for 288 GB of HBM3E
-(226.5 GB peak at DP=1, less under ZeRO-1).  Measured on one MI355X
-(profiles/micro_batch_sweep_1gpu.log): mbs 2 -> 20.9k tok/s, mbs 4 -> 22.5k,
-mbs 6 -> 23.1k at 267 GB (too close to capacity to be the default).
+Default micro-batch is 6 x 4096 tokens with the fused chunked LM head + CE (the
+[tokens, vocab] logits never exist; the head's dW goes straight into main_grad):
+271.0 GB peak at DP=1 of 288 GB (utils/memory.py estimates 271.4; less under
+ZeRO-1 at DP > 1).  Same-box A/B on one MI355X (profiles/r02/mbs6_fused_head_ab.log):
+mbs 4 + logits/CE 700.8 ms = 23.38k tok/s, mbs 6 + fused head 1025-1033 ms =
+23.78-23.98k tok/s (+1.7-2.5 %); mbs 6 with materialised logits does not fit.
 
 Usage:
   python bench.py --gpus 1 --steps 10 --warmup 3
@@ -59,7 +61,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--layout", default="dp", choices=sorted(LAYOUTS))
     ap.add_argument("--model", default=None, help="default llama3-8b")
-    ap.add_argument("--micro_batch_size", type=int, default=None, help="default 4")
+    ap.add_argument("--micro_batch_size", type=int, default=None, help="default 6 (layout presets set their own)")
     ap.add_argument("--seq_len", type=int, default=None, help="default 4096")
     ap.add_argument("--grad_acc", type=int, default=None, help="default 1")
     ap.add_argument("--tp", type=int, default=None)
@@ -76,14 +78,14 @@ def main() -> int:
     ap.add_argument("--bucket_mb", type=float, default=256)
     ap.add_argument("--zero", type=int, default=1, help="ZeRO stage when DP > 1 (0: replicated optimizer, "
                                                          "1: sharded optimizer / reduce-scatter + all-gather)")
-    ap.add_argument("--fused_head", type=int, default=0,
-                    help="1: fused chunked LM head + CE (no logits tensor; -5.1 GB, +6 ms at mbs 4, "
-                         "profiles/r02/fused_head_ab.log)")
+    ap.add_argument("--fused_head", type=int, default=1,
+                    help="1: fused chunked LM head + CE (no logits tensor, dW straight into main_grad); "
+                         "0: logits + vocab-parallel CE")
     ap.add_argument("--head_chunk", type=int, default=4096, help="tokens per fused LM-head chunk")
     ap.add_argument("--layers", type=int, default=None, help="(debug only; result marked invalid)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    preset = dict(model="llama3-8b", micro_batch_size=4, seq_len=4096, grad_acc=1, tp=1, pp=1, cp=1, ep=1, sp=False,
+    preset = dict(model="llama3-8b", micro_batch_size=6, seq_len=4096, grad_acc=1, tp=1, pp=1, cp=1, ep=1, sp=False,
                   vpp=1)
     preset.update({k: (world if v == -1 else v) for k, v in LAYOUTS[args.layout].items()})
     for k, v in preset.items():

@@ -256,7 +256,8 @@ class TransformerLM(nn.Module):
     def forward(self, input_ids: torch.Tensor | None = None, position_ids: torch.Tensor | None = None,
                 hidden_states: torch.Tensor | None = None, gradient_checkpointing: bool = False,
                 attention_mask: torch.Tensor | None = None, labels: torch.Tensor | None = None,
-                lm_head_chunk: int | None = None, chunk: int | None = None) -> torch.Tensor:
+                lm_head_chunk: int | None = None, chunk: int | None = None,
+                lm_head_grad_scale: float | None = None) -> torch.Tensor:
         """Logits shard (last stage), or -- with ``labels`` (global target ids) on
         the last stage -- the mean cross-entropy from the fused chunked LM head
         (ops/fused_head.py), which never materialises the logits.  ``chunk`` (virtual
@@ -291,7 +292,7 @@ class TransformerLM(nn.Module):
         # a module call (SP: gather along seq inside the column-parallel fn), so the head's
         # forward pre-hook orders it after the weight's optimizer update / ZeRO-1 gather
         if labels is not None:
-            return self.final_proj(x, labels=labels, chunk=lm_head_chunk)
+            return self.final_proj(x, labels=labels, chunk=lm_head_chunk, grad_scale=lm_head_grad_scale)
         return self.final_proj(x)
 
     # ------------------------------------------------------------------ checkpoints in reference layout

@@ -80,17 +80,42 @@ def _loss_only(x, weight, tgt, valid, vocab_start, group, chunk) -> torch.Tensor
     return total / valid.sum().clamp(min=1)
 
 
+# Set on device when a direct-accumulation head (``grad_scale``) received an upstream
+# gradient other than the promised one; Trainer.health_check raises on it.
+_SCALE_MISMATCH: dict = {}
+
+
+def check_grad_scale() -> None:
+    """Raise if any direct-accumulation fused head saw an unexpected upstream gradient
+    (one host sync; call at logging steps)."""
+    for flag in _SCALE_MISMATCH.values():
+        if bool(flag.item()):
+            raise RuntimeError("fused LM head: the upstream gradient differed from its grad_scale, so the "
+                               "weight gradient written during the forward is wrong; drop grad_scale")
+
+
 class _FusedHeadCEFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, tgt, valid, vocab_start, group, chunk):
+    def forward(ctx, x, weight, tgt, valid, vocab_start, group, chunk, grad_scale):
         N = x.shape[0]
         native = _is_native(x, weight)
         n_valid = valid.sum().clamp(min=1)
         inv = 1.0 / n_valid.float()
         prepare_dgrad_weight(weight)  # W^T for the TN data-gradient GEMM (no-op off-arena)
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
-        G = (torch.empty(weight.shape, dtype=torch.float32, device=x.device)
-             if ctx.needs_input_grad[1] else None)
+        mg = getattr(weight, "main_grad", None)
+        # direct mode: the caller promises the upstream gradient (e.g. 1 / grad-accumulation
+        # steps), so dW goes straight into the fp32 main_grad arena chunk by chunk -- no
+        # [V/tp, h] fp32 buffer and no scaling pass in the backward
+        direct = grad_scale is not None and mg is not None and ctx.needs_input_grad[1] and mg.dtype == torch.float32
+        if direct:
+            inv = inv * float(grad_scale)
+            G = mg.view(weight.shape[0], -1)
+            first_beta = 0 if take_fresh(weight) else 1
+        else:
+            G = (torch.empty(weight.shape, dtype=torch.float32, device=x.device)
+                 if ctx.needs_input_grad[1] else None)
+            first_beta = 0
         total = torch.zeros((), dtype=torch.float32, device=x.device)
         for i, s in enumerate(range(0, N, chunk)):
             e = min(N, s + chunk)
@@ -104,16 +129,27 @@ class _FusedHeadCEFn(torch.autograd.Function):
             if dx is not None:
                 dx[s:e] = dgrad(dz, weight)
             if G is not None:
-                wgrad_into(G, dz, xc, 0 if i == 0 else 1)
+                wgrad_into(G, dz, xc, first_beta if i == 0 else 1)
             del z, dz
-        ctx.save_for_backward(dx, G)
-        ctx.weight = weight
+        ctx.save_for_backward(dx, None if direct else G)
+        ctx.weight, ctx.direct, ctx.grad_scale = weight, direct, grad_scale
         return total / n_valid
 
     @staticmethod
     def backward(ctx, g):
         dx, G = ctx.saved_tensors
         weight = ctx.weight
+        if ctx.direct:
+            # dX was produced pre-scaled; a different upstream gradient still rescales it
+            # exactly, but the weight gradient is already in main_grad: flag the mismatch
+            ratio = g.float() / ctx.grad_scale
+            gx = dx * ratio if ctx.needs_input_grad[0] else None
+            flag = _SCALE_MISMATCH.get(g.device)
+            if flag is None:
+                flag = _SCALE_MISMATCH[g.device] = torch.zeros((), dtype=torch.bool, device=g.device)
+            flag.logical_or_((ratio - 1.0).abs() > 1e-6)
+            _grad_ready(weight)
+            return gx, None, None, None, None, None, None, None
         gx = dx * g if ctx.needs_input_grad[0] else None  # bf16 storage, fp32 math
         gw = None
         if G is not None:
@@ -127,16 +163,20 @@ class _FusedHeadCEFn(torch.autograd.Function):
                 else:
                     m2.addcmul_(G, g)
                 _grad_ready(weight)
-        return gx, gw, None, None, None, None, None
+        return gx, gw, None, None, None, None, None, None
 
 
 def fused_linear_cross_entropy(x: torch.Tensor, weight: torch.Tensor, target: torch.Tensor, vocab_start: int = 0,
-                               group=None, ignore_index: int = -100, chunk: int | None = None) -> torch.Tensor:
+                               group=None, ignore_index: int = -100, chunk: int | None = None,
+                               grad_scale: float | None = None) -> torch.Tensor:
     """Mean CE of ``x @ weight^T`` against global token ids ``target`` (rows with
     ``ignore_index`` excluded), without materialising the logits.
 
     ``x`` [N, h] (replicated over the TP ``group``), ``weight`` [V/tp, h] this
-    rank's vocab shard starting at ``vocab_start``, ``target`` [N]."""
+    rank's vocab shard starting at ``vocab_start``, ``target`` [N].  ``grad_scale``:
+    the upstream gradient the caller will back-propagate into the returned loss
+    (the trainer's 1 / grad-accumulation steps); with a ``main_grad`` arena the weight
+    gradient is then written during the forward (``check_grad_scale`` verifies it)."""
     x = x.reshape(-1, x.shape[-1])
     t = target.reshape(-1).to(x.device)
     if t.shape[0] != x.shape[0]:
@@ -146,4 +186,4 @@ def fused_linear_cross_entropy(x: torch.Tensor, weight: torch.Tensor, target: to
     chunk = max(1, int(chunk or default_chunk()))
     if not torch.is_grad_enabled() or not (x.requires_grad or weight.requires_grad):
         return _loss_only(x, weight, tgt, valid, vocab_start, group, chunk)
-    return _FusedHeadCEFn.apply(x.contiguous(), weight, tgt, valid, vocab_start, group, chunk)
+    return _FusedHeadCEFn.apply(x.contiguous(), weight, tgt, valid, vocab_start, group, chunk, grad_scale)

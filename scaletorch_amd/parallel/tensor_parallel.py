@@ -457,7 +457,8 @@ class ColumnParallelLinear(nn.Module):
         if self.bias is not None:
             nn.init.zeros_(self.bias)
 
-    def forward(self, x: torch.Tensor, labels: torch.Tensor | None = None, chunk: int | None = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, labels: torch.Tensor | None = None, chunk: int | None = None,
+                grad_scale: float | None = None) -> torch.Tensor:
         """Logits shard ``[..., out/tp]``; with ``labels`` (LM head use) the mean
         vocab-parallel cross-entropy instead, fused and chunked so the logits are
         never materialised (ops/fused_head.py).  Both run as a module call so the
@@ -473,7 +474,8 @@ class ColumnParallelLinear(nn.Module):
                 x = CopyToTensorParallelRegion.apply(x, self.group)
             vocab_start = C.get_rank(self.group) * self.out_per_rank if self.tp > 1 else 0
             return fused_linear_cross_entropy(x, self.weight, labels, vocab_start,
-                                              group=self.group if self.tp > 1 else None, chunk=chunk)
+                                              group=self.group if self.tp > 1 else None, chunk=chunk,
+                                              grad_scale=grad_scale)
         if self.sequence_parallel and self.tp > 1:
             y = _SPColumnParallelFn.apply(x, self.weight, self.bias, self.group)
         elif self.tp > 1 or getattr(self.weight, "main_grad", None) is not None:

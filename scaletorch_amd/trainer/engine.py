@@ -163,7 +163,10 @@ class Trainer:
         a = self.args
         if not getattr(a, "fused_lm_head", False):
             return {}
-        return {"labels": batch["target_ids"], "lm_head_chunk": a.lm_head_chunk_tokens}
+        # the loss is divided by the micro-batch count before backward, so that is the
+        # head's upstream gradient: its weight gradient goes straight into main_grad
+        return {"labels": batch["target_ids"], "lm_head_chunk": a.lm_head_chunk_tokens,
+                "lm_head_grad_scale": 1.0 / a.gradient_accumulation_steps}
 
     def _loss(self, logits: torch.Tensor, batch: dict) -> torch.Tensor:
         if logits.dim() == 0:  # the fused LM head already produced the loss
@@ -308,6 +311,10 @@ class Trainer:
             from ..parallel.tensor_parallel import check_xgmi
 
             check_xgmi()
+        if getattr(self.args, "fused_lm_head", False):
+            from ..ops.fused_head import check_grad_scale
+
+            check_grad_scale()
 
     def reduced_loss(self, loss: torch.Tensor) -> float:
         """Mean loss over data-parallel replicas (last PP stage holds it); host sync."""

@@ -50,8 +50,7 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
     """Worst-rank estimate (first pipeline stage for activations, largest stage for weights).
 
     ``fused_head_chunk`` > 0: the fused chunked LM head (ops/fused_head.py) -- one
-    chunk of logits, dX and the fp32 head-gradient buffer instead of the logits
-    and their gradient."""
+    chunk of logits and dX instead of the logits and their gradient."""
     h, d = cfg.hidden_size, cfg.head_dim
     H, Hkv = cfg.num_attention_heads, cfg.num_key_value_heads
     L = cfg.num_hidden_layers
@@ -92,8 +91,8 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
         act = tokens * per_layer * layers
     head_tokens = micro_batch * seq_len / cp
     if fused_head_chunk:
-        logits = min(fused_head_chunk, head_tokens) * cfg.vocab_size / tp * 2 + head_tokens * h * 2 \
-            + cfg.vocab_size / tp * h * 4
+        # one chunk of logits + dX (the head's dW goes straight into main_grad)
+        logits = min(fused_head_chunk, head_tokens) * cfg.vocab_size / tp * 2 + head_tokens * h * 2
     else:
         logits = head_tokens * cfg.vocab_size / tp * 2 * 2  # bf16 logits + grad (last stage)
     comm = n * 2 if grad_reduce_dtype in ("bf16", "bfloat16") and dense_dp > 1 else 0.0

@@ -128,3 +128,38 @@ def test_fused_head_gpu_native(chunk):
     rel = lambda a, b: ((a.float() - b).norm() / b.norm()).item()  # noqa: E731
     assert rel(x.grad, rx.grad) < 1e-2
     assert rel(w.main_grad, rw.grad) < 1e-2
+
+
+def test_fused_head_direct_main_grad_mode():
+    """grad_scale (the trainer's 1/GA): dW is written into main_grad during the
+    forward, pre-scaled; the promised upstream gradient gives the exact result, a
+    different one still yields the exact dX and is reported by check_grad_scale."""
+    from scaletorch_amd.ops import fused_head as fh
+
+    torch.manual_seed(6)
+    N, h, V = 20, 8, 40
+    w = torch.nn.Parameter(torch.randn(V, h))
+    t = torch.randint(0, V, (N,))
+    fh._SCALE_MISMATCH.clear()
+    w.main_grad = torch.full((V, h), 9.0)
+    w._st_fresh = True
+    xs = [torch.randn(N, h, requires_grad=True) for _ in range(2)]
+    for x in xs:
+        (fused_linear_cross_entropy(x, w, t, chunk=7, grad_scale=0.5) * 0.5).backward()
+    ref_w = torch.zeros(V, h)
+    for x in xs:
+        rl, rx, rw = _ref(x, w, t)
+        (rl * 0.5).backward()
+        ref_w += rw.grad
+        assert torch.allclose(x.grad, rx.grad, rtol=1e-4, atol=1e-6)
+    assert w.grad is None
+    assert torch.allclose(w.main_grad, ref_w, rtol=1e-4, atol=1e-6)
+    fh.check_grad_scale()  # promise kept: no error
+    x = torch.randn(N, h, requires_grad=True)
+    (fused_linear_cross_entropy(x, w, t, grad_scale=0.5) * 0.25).backward()
+    rl, rx, _ = _ref(x, w, t)
+    (rl * 0.25).backward()
+    assert torch.allclose(x.grad, rx.grad, rtol=1e-4, atol=1e-6)
+    with pytest.raises(RuntimeError, match="grad_scale"):
+        fh.check_grad_scale()
+    fh._SCALE_MISMATCH.clear()
