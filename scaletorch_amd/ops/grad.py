@@ -107,7 +107,8 @@ def _wgrad_tn_ok(dy2d: torch.Tensor, x2d: torch.Tensor) -> bool:
             and dy2d.shape[0] % 64 == 0 and dy2d.shape[1] % 64 == 0 and x2d.shape[1] % 64 == 0
             and dy2d.stride(1) == 1 and x2d.stride(1) == 1 and dy2d.stride(0) % 8 == 0 and x2d.stride(0) % 8 == 0
             and dy2d.data_ptr() % 16 == 0 and x2d.data_ptr() % 16 == 0
-            and os.environ.get("ST_WGRAD_TN", "0") == "1")
+            and os.environ.get("ST_WGRAD_TN", "0") == "1"
+            and dy2d.shape[1] >= float(os.environ.get("ST_WGRAD_TN_MIN_RATIO", "0")) * x2d.shape[1])
 
 
 class WgradOperands:
@@ -133,9 +134,12 @@ def prefetch_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor):
     T = dy2d.shape[0]
     dyt = torch.empty(dy2d.shape[1], T, dtype=dy2d.dtype, device=dy2d.device)
     xt = torch.empty(x2d.shape[1], T, dtype=x2d.dtype, device=x2d.device)
-    st = _WG_STREAMS.get(dy2d.device.index)
-    if st is None:
-        st = _WG_STREAMS[dy2d.device.index] = torch.cuda.Stream(device=dy2d.device)
+    if os.environ.get("ST_WGRAD_TN_STREAM", "side") == "main":
+        st = torch.cuda.current_stream(dy2d.device)
+    else:
+        st = _WG_STREAMS.get(dy2d.device.index)
+        if st is None:
+            st = _WG_STREAMS[dy2d.device.index] = torch.cuda.Stream(device=dy2d.device)
     ready = torch.cuda.Event()
     ready.record()
     with torch.cuda.stream(st):

@@ -47,6 +47,7 @@ def main() -> int:
     ap.add_argument("--micro_batch_size", type=int, default=4)
     ap.add_argument("--seq_len", type=int, default=4096)
     ap.add_argument("--layers", type=int, default=None)
+    ap.add_argument("--fused_head", type=int, default=0, help="1: fused LM head + CE (bench.py default)")
     args = ap.parse_args()
     import torch
 
@@ -57,7 +58,7 @@ def main() -> int:
                             sequence_length=args.seq_len, total_train_steps=10_000, learning_rate=3e-4,
                             lr_scheduler_type="constant", warmup_steps=0, max_grad_norm=1.0, dtype="bfloat16",
                             num_hidden_layers=args.layers, weight_decay=0.1, betas=(0.9, 0.95),
-                            fused_lm_head=False)  # the bench.py configuration
+                            fused_lm_head=bool(args.fused_head))
     tr = Trainer(a)
     side = tr.model.side_stream
     variants = args.variants.split(",")
