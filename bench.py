@@ -203,6 +203,8 @@ def main() -> int:
         "mfu_pct_causal_flops": round(per_gpu * fpt_causal / peak * 100, 2),
         "peak_flops": peak,
         "baseline_tok_s_per_gpu": BASELINE_TOK_S_PER_GPU,
+        "vs_baseline_basis": "context only: per-GPU tok/s over the reference's Qwen3-8B TP2-DP4 S2048 row on "
+                             "8x Ascend 910B (README.md:84); BASELINE.json publishes no MI355X/Llama-3-8B number",
         "final_loss": round(final_loss, 4),
         "valid": valid,
         "max_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1) if dev.type == "cuda" else 0.0,

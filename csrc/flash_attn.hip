@@ -799,10 +799,15 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
     }
     dma_barrier();
   };
-  for (int kb = 0; kb < nkb; kb += 2) {
+  // pairs of steps with no branch between them: a conditional second step
+  // merges two copies of the AGPR accumulators, and hipcc resolved that merge by
+  // parking dQ in VGPRs (64 v_accvgpr copies a pair + spills of Q/dO fragments)
+  int kb = 0;
+  for (; kb + 1 < nkb; kb += 2) {
     step(Buf<0>(), kb);
-    if (kb + 1 < nkb) step(Buf<1>(), kb + 1);
+    step(Buf<1>(), kb + 1);
   }
+  if (kb < nkb) step(Buf<0>(), kb);
 
   agpr_fence(dqacc);
   if (my_q < p.Sq) {
@@ -990,10 +995,12 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
     g_c = g_n;
     qb_c = qb_n;
   };
-  for (int it = 0; it < total; it += 2) {
+  int it = 0;  // unconditional pairs (see the dQ kernel)
+  for (; it + 1 < total; it += 2) {
     step(Buf<0>(), it);
-    if (it + 1 < total) step(Buf<1>(), it + 1);
+    step(Buf<1>(), it + 1);
   }
+  if (it < total) step(Buf<0>(), it);
 
   agpr_fence(dkacc);
   agpr_fence(dvacc);
