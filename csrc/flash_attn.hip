@@ -831,6 +831,23 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
 // query head of the GQA group x query blocks of 64 rows staged in LDS (Q, dO,
 // lse, delta), so dK/dV of the kv head are summed in registers and written
 // once as bf16.  Rows past Sq read as zero with lse = +inf => P = dS = 0.
+// dS softmax slice of one accumulator row group (4 registers: query rows
+// rowo .. rowo+3 of the block, this lane's key): P = exp2(S c2 - lse2) (masked
+// past the causal diagonal), dS = P (dP - delta); P overwrites S in place
+ST_DEVICE void dkdv_softmax4(f32x16& s, f32x16& dp, const lds_t* st, int BQ, int rowo, int gq, float c2,
+                             bool need_mask, int thr) {
+  const f32x4 L = *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * rowo) * kLog2e;
+  const f32x4 Dl = *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * (BQ + rowo));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = 4 * gq + j;
+    float pv = fast_exp2(fmaf(s[i], c2, -L[j]));
+    if (need_mask && acc_row0(i) < thr) pv = 0.f;
+    s[i] = pv;
+    dp[i] = pv * (dp[i] - Dl[j]);
+  }
+}
+
 template <int D, int PROBE = 0>  // PROBE 1: softmax / dS VALU skipped (timing probe, wrong results)
 __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
     AttnParams p, const bf16_t* __restrict__ dout, int64_t sdb, int64_t sds, int64_t sdh,
@@ -917,63 +934,53 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
     // this wave's keys vs this query block: skip when every key is in the future
     const bool dead = p.causal && (kg - r > qstart + BQ - 1);
     if (!dead) {
+      // software-pipelined within the wave (one wave per SIMD: nothing else fills
+      // the MFMA pipe while the softmax VALU runs): half 0's softmax is issued
+      // between half 1's S/dP MFMAs, half 1's between half 0's dV/dK MFMAs
       const bool need_mask = p.causal && (kg - r + 31 > qstart);
-      bfx8 pf[2][2], gf[2][2];
+      int thr[2] = {0, 0};
+      if (need_mask) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int64_t t = kg - qstart - 32 * u - 4 * h;
+          thr[u] = t > 64 ? 64 : (int)t;
+        }
+      }
+      f32x16 s[2], dp[2];
+      s[0] = s[1] = dp[0] = dp[1] = zero16();
+      bfx8 qa[2][NKK], da[2][NKK];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        // S = Q K^T, dP = dO V^T : rows = queries (acc rows), col = key (lane).
-        // Fragments are read two k-steps ahead and a sched_barrier pins each
-        // read group above the MFMAs that precede its use: with one wave per
-        // SIMD nothing else hides the LDS latency (hipcc otherwise emits
-        // read -> wait -> MFMA for every k-step).
-        f32x16 s = zero16(), dp = zero16();
-        bfx8 qa[NKK], da[NKK];
-        qa[0] = la.rowf(qt, u, 0);
-        da[0] = la.rowf(dt_, u, 0);
-        qa[1] = la.rowf(qt, u, 1);
-        da[1] = la.rowf(dt_, u, 1);
+        qa[u][0] = la.rowf(qt, u, 0);
+        da[u][0] = la.rowf(dt_, u, 0);
+        qa[u][1] = la.rowf(qt, u, 1);
+        da[u][1] = la.rowf(dt_, u, 1);
 #pragma unroll
         for (int kk = 0; kk < NKK; ++kk) {
           if (kk + 2 < NKK) {
-            qa[kk + 2] = la.rowf(qt, u, kk + 2);
-            da[kk + 2] = la.rowf(dt_, u, kk + 2);
+            qa[u][kk + 2] = la.rowf(qt, u, kk + 2);
+            da[u][kk + 2] = la.rowf(dt_, u, kk + 2);
           }
           __builtin_amdgcn_sched_barrier(0);
-          s = mfma(qa[kk], kf[kk], s);
-          dp = mfma(da[kk], vf[kk], dp);
-        }
-        // query row of register i: 32u + acc_row0(i) + 4h
-        int thr = 0;
-        if (need_mask) {
-          const int64_t t = kg - qstart - 32 * u - 4 * h;  // row visible iff acc_row0(i) >= t
-          thr = t > 64 ? 64 : (int)t;
-        }
+          s[u] = mfma(qa[u][kk], kf[kk], s[u]);
+          dp[u] = mfma(da[u][kk], vf[kk], dp[u]);
+          if (u == 1 && !PROBE) {
 #pragma unroll
-        for (int gq = 0; gq < (PROBE ? 0 : 4); ++gq) {
-          const int rowo = 32 * u + 8 * gq + 4 * h;
-          const f32x4 L = *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * rowo) * kLog2e;
-          const f32x4 Dl =
-              *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * (BQ + rowo));
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int i = 4 * gq + j;
-            float pv = fast_exp2(fmaf(s[i], c2, -L[j]));
-            if (need_mask && acc_row0(i) < thr) pv = 0.f;
-            s[i] = pv;
-            dp[i] = pv * (dp[i] - Dl[j]);
+            for (int gq = 0; gq < 4; ++gq)  // the 4 row groups of half 0 spread over the k-steps
+              if (gq * NKK / 4 == kk) dkdv_softmax4(s[0], dp[0], st, BQ, 8 * gq + 4 * h, gq, c2, need_mask, thr[0]);
           }
         }
-        pf[u][0] = acc_frag(s, 0);
-        pf[u][1] = acc_frag(s, 1);
-        gf[u][0] = acc_frag(dp, 0);
-        gf[u][1] = acc_frag(dp, 1);
       }
-      // dV^T += dO^T P, dK^T += Q^T dS: 8 (dt, u) groups of 4 MFMAs; transposed
-      // fragments read one group ahead (same pinning as above)
+      bfx8 pf[2][2], gf[2][2];
+      pf[0][0] = acc_frag(s[0], 0);
+      pf[0][1] = acc_frag(s[0], 1);
+      gf[0][0] = acc_frag(dp[0], 0);
+      gf[0][1] = acc_frag(dp[0], 1);
+      // dV^T += dO^T P, dK^T += Q^T dS: half 0's four dt groups, then half 1's
       constexpr int NG = NDT * 2;
       bfx8 tv[NG][2], tk[NG][2];
       auto load_group = [&](int gidx) {
-        const int dt = gidx >> 1, u = gidx & 1;
+        const int dt = gidx % NDT, u = gidx / NDT;
         tv[gidx][0] = la.trf(dt_, 32 * u, 0, dt);
         tv[gidx][1] = la.trf(dt_, 32 * u, 1, dt);
         tk[gidx][0] = la.trf(qt, 32 * u, 0, dt);
@@ -984,11 +991,22 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
       for (int gi = 0; gi < NG; ++gi) {
         if (gi + 1 < NG) load_group(gi + 1);
         __builtin_amdgcn_sched_barrier(0);
-        const int dt = gi >> 1, u = gi & 1;
+        const int dt = gi % NDT, u = gi / NDT;
+        if (gi == NDT) {
+          pf[1][0] = acc_frag(s[1], 0);
+          pf[1][1] = acc_frag(s[1], 1);
+          gf[1][0] = acc_frag(dp[1], 0);
+          gf[1][1] = acc_frag(dp[1], 1);
+        }
         mfma_acc(dvacc[dt], tv[gi][0], pf[u][0]);
         mfma_acc(dvacc[dt], tv[gi][1], pf[u][1]);
         mfma_acc(dkacc[dt], tk[gi][0], gf[u][0]);
         mfma_acc(dkacc[dt], tk[gi][1], gf[u][1]);
+        if (u == 0 && !PROBE) {
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq)  // half 1's row groups spread over half 0's dt groups
+            if (gq * NDT / 4 == dt) dkdv_softmax4(s[1], dp[1], st, BQ, 32 + 8 * gq + 4 * h, gq, c2, need_mask, thr[1]);
+        }
       }
     }
     dma_barrier();
