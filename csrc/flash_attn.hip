@@ -361,10 +361,20 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(AttnParams p, bf16_t*
     const lds_t* kt = smem + BUF * TB;
     const lds_t* vt = smem + (2 + BUF) * TB;
     f32x16 s0 = zero16(), s1 = zero16();
+    // K row fragments one k-step ahead, pinned above the MFMAs that precede
+    // their use (hipcc otherwise emits read -> wait -> MFMA for every k-step)
+    bfx8 fk[NKK][2];
+    fk[0][0] = la.rowf(kt, 0, 0);
+    fk[0][1] = la.rowf(kt, 1, 0);
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) {
-      s0 = mfma(la.rowf(kt, 0, kk), qf[kk], s0);
-      s1 = mfma(la.rowf(kt, 1, kk), qf[kk], s1);
+      if (kk + 1 < NKK) {
+        fk[kk + 1][0] = la.rowf(kt, 0, kk + 1);
+        fk[kk + 1][1] = la.rowf(kt, 1, kk + 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      s0 = mfma(fk[kk][0], qf[kk], s0);
+      s1 = mfma(fk[kk][1], qf[kk], s1);
     }
     if (kb >= kb_mask) {
       const int lim = key_limit(p, kb, BN, qg, h, true);
@@ -419,10 +429,12 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(AttnParams p, bf16_t*
     }
     dma_barrier();
   };
-  for (int kb = 0; kb < nkb; kb += 2) {
+  int kb = 0;  // unconditional pairs (see the dQ kernel)
+  for (; kb + 1 < nkb; kb += 2) {
     step(Buf<0>(), kb);
-    if (kb + 1 < nkb) step(Buf<1>(), kb + 1);
+    step(Buf<1>(), kb + 1);
   }
+  if (kb < nkb) step(Buf<0>(), kb);
 
   if (my_q < p.Sq) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
