@@ -21,6 +21,7 @@ and MI355X-first changes:
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -137,6 +138,52 @@ class MoERouter(nn.Module):
         return topw, topi, aux
 
 
+class _ExpertFFNFn(torch.autograd.Function):
+    """Grouped expert SwiGLU FFN whose weight gradients are fp32 GEMMs straight into
+    ``main_grad`` (one per expert and weight, csrc/wgrad_gemm.hip or hipBLASLt with an
+    fp32 epilogue).  ``torch._grouped_mm`` only emits bf16 (its weight gradient went
+    bf16 -> fp32 copy -> add into the arena, and summed over tokens in bf16).  The
+    per-expert token counts reach the host by an async copy issued in the forward,
+    long finished by the backward: no stall."""
+
+    @staticmethod
+    def forward(ctx, x, offs, counts_host, ready, w_gu, w_dn):
+        gu = torch._grouped_mm(x, w_gu.transpose(-2, -1), offs=offs)
+        a = ops.swiglu(gu)
+        y = torch._grouped_mm(a, w_dn.transpose(-2, -1), offs=offs)
+        ctx.save_for_backward(x, gu, a, offs)
+        ctx.counts_host, ctx.ready = counts_host, ready
+        ctx.w_gu, ctx.w_dn = w_gu, w_dn
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..ops import _lib
+        from ..ops.grad import _grad_ready, take_fresh, wgrad_into
+
+        x, gu, a, offs = ctx.saved_tensors
+        w_gu, w_dn = ctx.w_gu, ctx.w_dn
+        dy = dy.contiguous()
+        da = torch._grouped_mm(dy, w_dn, offs=offs)
+        dgu = _lib.ops().swiglu_bwd(da.contiguous(), gu)
+        dx = torch._grouped_mm(dgu, w_gu, offs=offs)
+        ctx.ready.synchronize()
+        counts = ctx.counts_host.tolist()
+        for w, dout, inp in ((w_dn, dy, a), (w_gu, dgu, x)):
+            fresh = take_fresh(w)
+            off = 0
+            for e, n in enumerate(counts):
+                if n:
+                    # token counts change every step: fixed kernel choice, no per-shape timing
+                    wgrad_into(w.main_grad[e], dout[off:off + n], inp[off:off + n], 0 if fresh else 1,
+                               variant=1 if n % 64 == 0 else 0)
+                elif fresh:
+                    w.main_grad[e].zero_()
+                off += n
+            _grad_ready(w)
+        return dx, None, None, None, None, None
+
+
 class MoEExperts(nn.Module):
     """Stacked local experts: ``w_gate_up`` [E, 2I/tp, h], ``w_down`` [E, h, I/tp]."""
 
@@ -186,6 +233,15 @@ class MoEExperts(nn.Module):
             offs = torch.cumsum(counts.to(device=x.device, dtype=torch.int32), 0, dtype=torch.int32)
             if x.shape[0] == 0:
                 return self._empty(x)
+            mg_gu, mg_dn = (getattr(w, "main_grad", None) for w in (self.w_gate_up, self.w_down))
+            if (torch.is_grad_enabled() and mg_gu is not None and mg_dn is not None
+                    and mg_gu.dtype == torch.float32 and mg_dn.dtype == torch.float32 and self.inter % 8 == 0
+                    and os.environ.get("ST_MOE_FP32_WGRAD", "1") == "1"):
+                counts_host = torch.empty(counts.numel(), dtype=counts.dtype, pin_memory=True)
+                counts_host.copy_(counts, non_blocking=True)
+                ready = torch.cuda.Event()
+                ready.record()
+                return _ExpertFFNFn.apply(x.contiguous(), offs, counts_host, ready, self.w_gate_up, self.w_down)
             gu = torch._grouped_mm(x.contiguous(), self.w_gate_up.transpose(-2, -1), offs=offs)
             return torch._grouped_mm(ops.swiglu(gu), self.w_down.transpose(-2, -1), offs=offs)
         if isinstance(counts, torch.Tensor):

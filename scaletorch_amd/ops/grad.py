@@ -260,9 +260,13 @@ def accumulate_linear_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
     return None
 
 
-def wgrad_into(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, beta: int) -> None:
+def wgrad_into(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, beta: int,
+               variant: int | None = None) -> None:
     """``out = beta * out + dy2d^T x2d`` for a 2-D ``out`` (fp32 accumulator or the
-    operands' dtype), on the per-shape faster of csrc/wgrad_gemm.hip and hipBLASLt."""
+    operands' dtype), on the per-shape faster of csrc/wgrad_gemm.hip and hipBLASLt.
+    ``variant`` (0 hipBLASLt, 1 / 2 the HIP kernels) skips the per-shape pick: for
+    token counts that change every step (MoE experts) timing each new shape would
+    cost more than it saves."""
     global _ADDMM_DTYPE_OK
     if out.dtype == dy2d.dtype:
         out.addmm_(dy2d.t(), x2d, beta=beta)
@@ -273,7 +277,10 @@ def wgrad_into(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, beta: i
 
         if _lib.use_native(dy2d):
             forced = os.environ.get("ST_WGRAD_VARIANT", "")  # 0 / 1 / 2 overrides the per-shape pick (A/B)
-            variant = int(forced) if forced in ("0", "1", "2") else _wgrad_pick(dy2d, x2d)
+            if forced in ("0", "1", "2"):
+                variant = int(forced)
+            elif variant is None:
+                variant = _wgrad_pick(dy2d, x2d)
             if variant and _lib.ops().wgrad_gemm_(out, dy2d, x2d, beta, variant):
                 return
     if _ADDMM_DTYPE_OK is not False and dy2d.is_cuda and os.environ.get("ST_WGRAD_FP32_GEMM", "1") == "1":

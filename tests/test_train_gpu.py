@@ -113,6 +113,56 @@ def test_moe_grouped_gemm_matches_expert_loop():
     assert rel(gw1, ex.w_gate_up.grad) < 2e-2 and rel(gw2, ex.w_down.grad) < 2e-2
 
 
+def test_moe_expert_wgrad_into_main_grad():
+    """Experts with fp32 main_grad: weight gradients are fp32 GEMMs per expert straight
+    into main_grad (first write of a step overwrites, later micro-batches add; experts
+    without tokens are zeroed), dX via grouped GEMMs -- vs an fp64 per-expert reference."""
+    from scaletorch_amd.models import moe
+
+    if not moe._grouped_mm_available():
+        pytest.skip("torch._grouped_mm unavailable")
+    torch.manual_seed(0)
+    E, h, inter = 4, 256, 512
+    ex = moe.MoEExperts(E, h, inter).cuda().to(torch.bfloat16)
+    for w in (ex.w_gate_up, ex.w_down):
+        w.main_grad = torch.full(w.shape, 7.0, device="cuda")  # stale values: the fresh write must overwrite
+        w._st_fresh = True
+    counts = torch.tensor([64, 0, 100, 128], device="cuda")
+    xs, gs = [], []
+    for _ in range(2):  # two micro-batches: overwrite, then accumulate
+        x = torch.randn(int(counts.sum()), h, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+        y = ex(x, counts)
+        g = torch.randn_like(y)
+        y.backward(g)
+        assert ex.w_gate_up.grad is None and ex.w_down.grad is None
+        xs.append(x)
+        gs.append(g)
+    ref_gu = torch.zeros(ex.w_gate_up.shape, dtype=torch.float64, device="cuda")
+    ref_dn = torch.zeros(ex.w_down.shape, dtype=torch.float64, device="cuda")
+    w_gu, w_dn = ex.w_gate_up.detach().double(), ex.w_down.detach().double()
+    for x, g in zip(xs, gs):
+        off = 0
+        xd = x.detach().double().requires_grad_(True)
+        outs = []
+        for e, n in enumerate(counts.tolist()):
+            xe = xd[off:off + n]
+            gu = xe @ w_gu[e].t()
+            a = torch.nn.functional.silu(gu[:, :inter]) * gu[:, inter:]
+            outs.append(a @ w_dn[e].t())
+            ref_dn[e] += g[off:off + n].double().t() @ a.detach()
+            ga = (g[off:off + n].double() @ w_dn[e])
+            gg = ga * gu[:, inter:].detach() * torch.sigmoid(gu[:, :inter].detach()) * (
+                1 + gu[:, :inter].detach() * (1 - torch.sigmoid(gu[:, :inter].detach())))
+            gup = ga * torch.nn.functional.silu(gu[:, :inter].detach())
+            ref_gu[e] += torch.cat([gg, gup], 1).t() @ xe.detach()
+            off += n
+        torch.cat(outs).backward(g.double())
+        assert rel(x.grad, xd.grad) < 2e-2
+    assert torch.all(ex.w_gate_up.main_grad[1] == 0) and torch.all(ex.w_down.main_grad[1] == 0)
+    assert rel(ex.w_gate_up.main_grad, ref_gu) < 1e-2
+    assert rel(ex.w_down.main_grad, ref_dn) < 1e-2
+
+
 @pytest.mark.parametrize("ga", [1, 2])
 def test_overlapped_optimizer_matches_serial(ga):
     """Side-stream AdamW (forward-order buckets, per-module waits) + backward-time
