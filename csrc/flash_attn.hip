@@ -846,15 +846,15 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
 // dS softmax slice of one accumulator row group (4 registers: query rows
 // rowo .. rowo+3 of the block, this lane's key): P = exp2(S c2 - lse2) (masked
 // past the causal diagonal), dS = P (dP - delta); P overwrites S in place
-ST_DEVICE void dkdv_softmax4(f32x16& s, f32x16& dp, const lds_t* st, int BQ, int rowo, int gq, float c2,
-                             bool need_mask, int thr) {
+template <bool MASK>
+ST_DEVICE void dkdv_softmax4(f32x16& s, f32x16& dp, const lds_t* st, int BQ, int rowo, int gq, float c2, int thr) {
   const f32x4 L = *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * rowo) * kLog2e;
   const f32x4 Dl = *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * (BQ + rowo));
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int i = 4 * gq + j;
     float pv = fast_exp2(fmaf(s[i], c2, -L[j]));
-    if (need_mask && acc_row0(i) < thr) pv = 0.f;
+    if (MASK && acc_row0(i) < thr) pv = 0.f;
     s[i] = pv;
     dp[i] = pv * (dp[i] - Dl[j]);
   }
@@ -979,7 +979,11 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
           if (u == 1 && !PROBE) {
 #pragma unroll
             for (int gq = 0; gq < 4; ++gq)  // the 4 row groups of half 0 spread over the k-steps
-              if (gq * NKK / 4 == kk) dkdv_softmax4(s[0], dp[0], st, BQ, 8 * gq + 4 * h, gq, c2, need_mask, thr[0]);
+              if (gq * NKK / 4 == kk) {
+                // wave-uniform branch: only blocks on the causal diagonal pay for the mask
+                if (need_mask) dkdv_softmax4<true>(s[0], dp[0], st, BQ, 8 * gq + 4 * h, gq, c2, thr[0]);
+                else dkdv_softmax4<false>(s[0], dp[0], st, BQ, 8 * gq + 4 * h, gq, c2, 0);
+              }
           }
         }
       }
@@ -1017,7 +1021,10 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
         if (u == 0 && !PROBE) {
 #pragma unroll
           for (int gq = 0; gq < 4; ++gq)  // half 1's row groups spread over half 0's dt groups
-            if (gq * NDT / 4 == dt) dkdv_softmax4(s[1], dp[1], st, BQ, 32 + 8 * gq + 4 * h, gq, c2, need_mask, thr[1]);
+            if (gq * NDT / 4 == dt) {
+              if (need_mask) dkdv_softmax4<true>(s[1], dp[1], st, BQ, 32 + 8 * gq + 4 * h, gq, c2, thr[1]);
+              else dkdv_softmax4<false>(s[1], dp[1], st, BQ, 32 + 8 * gq + 4 * h, gq, c2, 0);
+            }
         }
       }
     }
