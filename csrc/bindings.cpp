@@ -53,7 +53,8 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
                  int64_t sdks, int64_t sdkh, float scale, int causal, int64_t q_offset,
                  int64_t k_offset, hipStream_t st);
 int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int M,
-                  int N, int T, int beta, int variant, hipStream_t st);
+                  int N, int T, int beta, int variant, float* ws, hipStream_t st);
+int64_t st_wgrad_ws_elems(int M, int N, int T, int variant);
 int st_xgmi_header_bytes();
 int st_xgmi_max_ranks();
 int64_t st_xgmi_create(int rank, int world, int64_t cap, int64_t epoch_base);
@@ -334,8 +335,13 @@ bool wgrad_gemm_(at::Tensor out, const at::Tensor& dy, const at::Tensor& x, int6
   const int64_t T = dy.size(0), M = dy.size(1), N = x.size(1);
   if (T > INT32_MAX || M > INT32_MAX || N > INT32_MAX) return false;
   c10::hip::HIPGuardMasqueradingAsCUDA g(out.device());
+  // tail-split partials (csrc/wgrad_gemm.hip): stream-ordered caching-allocator scratch
+  const int64_t wse = st_wgrad_ws_elems((int)M, (int)N, (int)T, (int)variant);
+  at::Tensor ws;
+  if (wse > 0) ws = at::empty({wse}, out.options());
   int rc = st_wgrad_gemm(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr<float>(),
-                         out.stride(0), (int)M, (int)N, (int)T, beta ? 1 : 0, (int)variant, cur_stream());
+                         out.stride(0), (int)M, (int)N, (int)T, beta ? 1 : 0, (int)variant,
+                         wse > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
   if (rc == -2) return false;
   ST_CHECK_RC(rc, "wgrad_gemm_");
   return true;

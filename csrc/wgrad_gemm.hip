@@ -34,6 +34,7 @@
 //     8 XCDs; the bijective remap gives each XCD a contiguous range of tiles,
 //     grouped 4 M-blocks x N so the ~32 tiles an XCD runs at once share their
 //     A and B token slices in its L2.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -91,6 +92,92 @@ ST_DEVICE void lds_dma16(const i32x4& rs, uint32_t lds_base, uint32_t voff) {
 }
 #pragma clang diagnostic pop
 
+// ---- tail split (split-K over the token range for the last, partial wave of tiles)
+// A grid of nt tiles on 256 CUs (one workgroup per CU) runs ceil(nt/256) rounds; when
+// nt % 256 != 0 the last round leaves CUs idle (down 4096x14336: 896 tiles = 3.5 rounds,
+// qkv 6144x4096: 1.5, TP-sharded projections: < 1).  The first nfull = 256 * floor(nt/256)
+// tiles run whole; each of the remaining `tail` tiles is cut into `split` token ranges,
+// so the last round is split x shorter.  Range 0 of a tail tile accumulates into C with
+// beta like a whole tile; ranges 1.. write fp32 partials to a workspace that
+// wgrad_tail_reduce adds to C in range order afterwards (same stream): deterministic,
+// no atomics, no inter-workgroup flags.
+struct SplitPlan {
+  float* ws;
+  int nfull, tail, split;
+};
+struct WItem {
+  int m0, n0;    // tile origin in the full output
+  int k0, T;     // token range [k0, k0 + T)
+  int beta;
+  float* C;      // where the tile goes: C itself, or its workspace slot
+  int64_t ldc;
+  int cm0, cn0;  // origin of the tile inside *C (m0/n0, or 0/0 in the workspace)
+};
+
+// tile index -> (bm, bn): GROUP_M M-blocks x all N-blocks per group, so the ~32 tiles one
+// XCD runs at once share their A and B token slices in its L2
+ST_DEVICE void group_tile(int idx, int nbm, int nbn, int& bm, int& bn) {
+  const int per_group = GROUP_M * nbn;
+  const int first_bm = (idx / per_group) * GROUP_M;
+  const int gsz = min(nbm - first_bm, GROUP_M);
+  const int in_group = idx % per_group;
+  bm = first_bm + in_group % gsz;
+  bn = in_group / gsz;
+}
+
+// workgroup b -> work item.  Blocks are dealt round-robin to the 8 XCDs (b % 8 shares an
+// XCD), so XCD x's j-th block takes the j-th item of a contiguous per-XCD range: first of
+// the whole tiles, then of the (range-major) tail units, keeping one XCD's concurrent
+// units on the same token range and neighbouring tiles.
+template <int TBM, int TBN>
+ST_DEVICE WItem work_item(int b, int nbm, int nbn, int T, int beta, float* C, int64_t ldc, const SplitPlan& sp) {
+  WItem w{0, 0, 0, T, beta, C, ldc, 0, 0};
+  int idx;
+  bool direct = true;
+  if (sp.split <= 1) {
+    idx = xcd_remap(b, nbm * nbn);
+  } else if (b < sp.nfull) {
+    idx = (b & 7) * (sp.nfull >> 3) + (b >> 3);
+  } else {
+    const int u = b - sp.nfull, per = (sp.tail * sp.split) >> 3;
+    const int ux = (u & 7) * per + (u >> 3);
+    const int s = ux / sp.tail, tl = ux % sp.tail;
+    idx = sp.nfull + tl;
+    w.T = T / sp.split;
+    w.k0 = s * w.T;
+    if (s > 0) {
+      direct = false;
+      w.C = sp.ws + ((int64_t)(s - 1) * sp.tail + tl) * (TBM * TBN);
+      w.ldc = TBN;
+      w.beta = 0;
+    }
+  }
+  int bm, bn;
+  group_tile(idx, nbm, nbn, bm, bn);
+  w.m0 = bm * TBM;
+  w.n0 = bn * TBN;
+  if (direct) {
+    w.cm0 = w.m0;
+    w.cn0 = w.n0;
+  }
+  return w;
+}
+
+template <int BN>
+__global__ __launch_bounds__(256) void wgrad_tail_reduce(float* __restrict__ C, int64_t ldc,
+                                                         const float* __restrict__ ws, int nbm, int nbn,
+                                                         SplitPlan sp) {
+  const int tl = blockIdx.y;
+  int bm, bn;
+  group_tile(sp.nfull + tl, nbm, nbn, bm, bn);
+  const int e = (blockIdx.x * 256 + threadIdx.x) * 4;  // element of the BM x BN tile
+  const int r = e / BN, c = e % BN;
+  f32x4* pc = (f32x4*)(C + (int64_t)(bm * BM + r) * ldc + bn * BN + c);
+  f32x4 acc = *pc;
+  for (int s = 1; s < sp.split; ++s) acc += *(const f32x4*)(ws + ((int64_t)(s - 1) * sp.tail + tl) * (BM * BN) + e);
+  *pc = acc;
+}
+
 template <int BN>
 struct Geo {
   static constexpr int WM = BN == 256 ? 2 : 4, WN = 8 / WM;  // wave grid
@@ -107,22 +194,20 @@ template <int PROBE, int BN>
 __global__ __launch_bounds__(NT, 2) void wgrad_gemm_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                            const bf16_t* __restrict__ B, int64_t ldb,
                                                            float* __restrict__ C, int64_t ldc, int M, int N,
-                                                           int T, int beta) {
+                                                           int T, int beta, SplitPlan sp) {
   using Gm = Geo<BN>;
   __shared__ __attribute__((aligned(16))) char smem_raw[NBUF * Gm::STAGE];
   lds_t* smem = (lds_t*)smem_raw;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
-  const int nbm = M / BM, nbn = N / BN, nwg = nbm * nbn;
+  const int nbm = M / BM, nbn = N / BN;
 
-  // ---- tile of this workgroup: XCD remap, then GROUP_M x nbn grouping
-  const int logical = xcd_remap((int)blockIdx.x, nwg);
-  const int per_group = GROUP_M * nbn;
-  const int first_bm = (logical / per_group) * GROUP_M;
-  const int gsz = min(nbm - first_bm, GROUP_M);
-  const int in_group = logical % per_group;
-  const int bm = first_bm + in_group % gsz, bn = in_group / gsz;
-  const int m0 = bm * BM, n0 = bn * BN;
+  // ---- work item of this workgroup: tile (XCD-aware, GROUP_M x nbn grouping), token range
+  const WItem w = work_item<BM, BN>((int)blockIdx.x, nbm, nbn, T, beta, C, ldc, sp);
+  const int m0 = w.m0, n0 = w.n0;
+  A += (int64_t)w.k0 * lda;
+  B += (int64_t)w.k0 * ldb;
+  T = w.T;
 
   // ---- DMA plan: a stage is NIMG images [32 tokens][128 features] (A images
   // first); wave w fills the 1 KiB pieces [w NDMA, (w+1) NDMA) of it.  Image
@@ -226,9 +311,9 @@ __global__ __launch_bounds__(NT, 2) void wgrad_gemm_kernel(const bf16_t* __restr
     for (int j = 0; j < Gm::FN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + am + 16 * i + 4 * G + r;
-        float* p = C + (int64_t)m * ldc + n0 + bnn + 16 * j + (lane & 15);
-        *p = beta ? *p + acc[i][j][r] : acc[i][j][r];
+        const int m = w.cm0 + am + 16 * i + 4 * G + r;
+        float* p = w.C + (int64_t)m * w.ldc + w.cn0 + bnn + 16 * j + (lane & 15);
+        *p = w.beta ? *p + acc[i][j][r] : acc[i][j][r];
       }
 }
 
@@ -275,20 +360,19 @@ template <int PROBE>  // timing probes (wrong results): 1 = no K-loop DMA, 2 = n
 __global__ __launch_bounds__(NT, 1) void wgrad8_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                        const bf16_t* __restrict__ B, int64_t ldb,
                                                        float* __restrict__ C, int64_t ldc, int M, int N, int T,
-                                                       int beta) {
+                                                       int beta, SplitPlan sp) {
   using namespace p8;
   __shared__ __attribute__((aligned(16))) char smem_raw[2 * BUFB];  // 128 KiB: two K-tiles
   lds_t* smem = (lds_t*)smem_raw;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int grp = wid >> 2, wr = grp, wc = wid & 3;
-  const int nbm = M / BM, nbn = N / 256, nwg = nbm * nbn;
-  const int logical = xcd_remap((int)blockIdx.x, nwg);
-  const int per_group = GROUP_M * nbn;
-  const int first_bm = (logical / per_group) * GROUP_M;
-  const int gsz = min(nbm - first_bm, GROUP_M);
-  const int in_group = logical % per_group;
-  const int m0 = (first_bm + in_group % gsz) * BM, n0 = (in_group / gsz) * 256;
+  const int nbm = M / BM, nbn = N / 256;
+  const WItem w = work_item<BM, 256>((int)blockIdx.x, nbm, nbn, T, beta, C, ldc, sp);
+  const int m0 = w.m0, n0 = w.n0;
+  A += (int64_t)w.k0 * lda;
+  B += (int64_t)w.k0 * ldb;
+  T = w.T;
 
   // ---- DMA plan: a half-image is 16 pieces of 1 KiB (4 token rows each); wave w
   // fills pieces 2w and 2w+1 of every half-image (source address pre-swizzled).
@@ -436,65 +520,131 @@ __global__ __launch_bounds__(NT, 1) void wgrad8_kernel(const bf16_t* __restrict_
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + (i >> 2) * 128 + wr * 64 + 16 * (i & 3) + 4 * G + r;
-        float* p = C + (int64_t)m * ldc + n0 + (j >> 1) * 128 + wc * 32 + 16 * (j & 1) + (lane & 15);
-        *p = beta ? *p + acc[i][j][r] : acc[i][j][r];
+        const int m = w.cm0 + (i >> 2) * 128 + wr * 64 + 16 * (i & 3) + 4 * G + r;
+        float* p = w.C + (int64_t)m * w.ldc + w.cn0 + (j >> 1) * 128 + wc * 32 + 16 * (j & 1) + (lane & 15);
+        *p = w.beta ? *p + acc[i][j][r] : acc[i][j][r];
       }
+}
+
+
+// ---- launch plan: kernel variant, tile width, tail split
+struct Launch {
+  int variant;  // 1 = 4-stage ring, 2 = 8-phase
+  int bn;       // tile width (256 or 128; the 8-phase kernel is 256 only)
+  int split;    // token ranges per tail tile (1 = none)
+  int nfull, tail;
+};
+
+// Rounds of whole-tile time the grid takes on `cus` CUs with the tail cut `s` ways.
+double rounds(int64_t nt, int s, int cus) {
+  const int64_t nfull = (nt / cus) * cus, tail = nt - nfull;
+  if (s <= 1 || tail == 0) return (double)((nt + cus - 1) / cus);
+  return (double)(nfull / cus) + (double)((tail * s + cus - 1) / cus) / s;
+}
+
+// Split of the last partial round (1 = leave it).  Measured on MI355X
+// (tools/bench_wgrad_split.py, T = 24576): cutting a last round that is at most half
+// full in two wins (qkv 384 tiles +18 %, down 896 +3-12 %, TP-2 out 128 tiles +54 %),
+// but a 3/4-full one cut in four loses 4-8 % (TP-2 qkv / down: the chip runs
+// power-limited, so a partly idle round is not lost time in proportion, while the
+// shorter units pay their prologue, epilogue and partial traffic four times).  Every
+// range must be a whole number of K-tiles and the units must deal evenly over the 8 XCDs.
+int pick_split(int64_t nt, int T, int bk, int cus, bool off) {
+  const char* e = std::getenv("ST_WGRAD_SPLIT");  // 0: off (A/B); N > 1: force N ways
+  const int forced = e ? std::atoi(e) : -1;
+  const int64_t tail = nt % cus;
+  if (off || forced == 0 || tail == 0) return 1;
+  auto ok = [&](int s) { return T % (s * bk) == 0 && (tail * s) % 8 == 0 && (nt / cus) * cus % 8 == 0; };
+  if (forced > 1) return ok(forced) ? forced : 1;
+  if (tail * 2 > cus) return 1;
+  for (int s = (int)std::min<int64_t>(8, cus / tail); s >= 2; --s)
+    if (ok(s)) return s;
+  return 1;
+}
+
+// -2: shape not supported (caller falls back)
+int plan(int M, int N, int T, int variant, Launch& L) {
+  if (M <= 0 || N <= 0 || T <= 0) return -2;
+  if (M % BM || N % 128 || T % BK) return -2;
+  const int cus = 256;
+  const bool nosplit = (variant & 16) != 0;  // +16: tail split off (ops/grad.py times both)
+  variant &= 15;
+  if (variant == 0) {
+    const char* ve = std::getenv("ST_WGRAD_P8");
+    variant = (ve && std::atoi(ve) == 1) ? 2 : 1;
+  }
+  L.variant = variant;
+  if (variant == 2) {
+    if (N % 256 || T % p8::BK) return -2;
+    L.bn = 256;
+  } else {
+    const char* be = std::getenv("ST_WGRAD_BN");  // force 128 / 256 (A/B)
+    int bn = be ? std::atoi(be) : 0;
+    if (bn != 128 && bn != 256) {
+      // a 256x128 tile streams ~10 % less MFMA work per LDS byte: take it only where the
+      // 256-wide grid, tail split included, would leave CUs idle for a real share of the time
+      const int64_t t128 = (int64_t)(M / BM) * (N / 128);
+      auto eff = [&](int64_t t, int bk) { return (double)t / cus / rounds(t, pick_split(t, T, bk, cus, nosplit), cus); };
+      bn = (N % 256 == 0 && eff(t128 / 2, BK) * 1.08 >= eff(t128, BK)) ? 256 : 128;
+    }
+    if (bn == 256 && N % 256) return -2;
+    L.bn = bn;
+  }
+  const int64_t nt = (int64_t)(M / BM) * (N / L.bn);
+  L.split = pick_split(nt, T, variant == 2 ? p8::BK : BK, cus, nosplit);
+  L.nfull = (int)((nt / cus) * cus);
+  L.tail = (int)(nt - L.nfull);
+  return 0;
 }
 
 }  // namespace
 
 extern "C" {
 
+// fp32 workspace elements the tail split of this launch needs (0: none).
+int64_t st_wgrad_ws_elems(int M, int N, int T, int variant) {
+  Launch L;
+  if (plan(M, N, T, variant, L) || L.split <= 1) return 0;
+  return (int64_t)(L.split - 1) * L.tail * BM * L.bn;
+}
+
 // 0 on success; -2: shape not supported by this kernel (caller falls back).
-// Tile width: 256 unless only 128 divides N or the 256-wide grid would end in a
-// partial wave of workgroups that the 128-wide one avoids (qkv 6144x4096: 384
-// vs 768 tiles; down 4096x14336: 896 vs 1792 on 256 CUs).
 // variant: 0 = default (the 4-stage kernel, or the 8-phase one when ST_WGRAD_P8=1),
-// 1 = the 4-stage kernel, 2 = the 8-phase kernel (ops/grad.py times them per shape).
+// 1 = the 4-stage kernel, 2 = the 8-phase kernel (ops/grad.py times them per shape);
+// + 16 = without the tail split.  ws: st_wgrad_ws_elems(...) fp32 elements (may be null when that is 0).
 int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int M,
-                  int N, int T, int beta, int variant, hipStream_t st) {
-  if (M <= 0 || N <= 0 || T <= 0) return -2;
-  if (M % BM || N % 128 || T % BK) return -2;
+                  int N, int T, int beta, int variant, float* ws, hipStream_t st) {
+  Launch L;
+  if (plan(M, N, T, variant, L)) return -2;
   if (lda % 8 || ldb % 8 || lda < M || ldb < N || ldc < N) return -2;
   if (((uintptr_t)A | (uintptr_t)B) % 16 || (uintptr_t)C % 4) return -2;
   // 32-bit buffer offsets: the last row of each operand must be addressable
   if (((int64_t)(T - 1) * lda + M) * 2 >= (int64_t)1 << 32) return -2;
   if (((int64_t)(T - 1) * ldb + N) * 2 >= (int64_t)1 << 32) return -2;
-  const char* pe = std::getenv("ST_WGRAD_PROBE");  // 1: no K-loop DMA (timing probe, wrong results)
+  if (L.split > 1 && (ws == nullptr || ldc % 4 || (uintptr_t)C % 16)) L.split = 1;  // the reduce reads C by 16 B
+  const SplitPlan sp{ws, L.nfull, L.tail, L.split};
+  const int nbm = M / BM, nbn = N / L.bn;
+  const int grid = L.split > 1 ? L.nfull + L.tail * L.split : nbm * nbn;
+  const char* pe = std::getenv("ST_WGRAD_PROBE");  // 1: no K-loop DMA, 2: no LDS reads (timing probes, wrong results)
   const int probe = pe ? std::atoi(pe) : 0;
-  const char* be = std::getenv("ST_WGRAD_BN");     // force 128 / 256 (A/B)
-  int bn = be ? std::atoi(be) : 0;
-  const int cus = 256;
-  if (bn != 128 && bn != 256) {
-    const int64_t t256 = (N % 256 == 0) ? (int64_t)(M / BM) * (N / 256) : -1;
-    const int64_t t128 = (int64_t)(M / BM) * (N / 128);
-    auto eff = [&](int64_t t) { return (double)t / (double)(((t + cus - 1) / cus) * cus); };
-    // a 256x128 tile streams ~10 % less MFMA work per LDS byte: switch only for a real tail win
-    bn = (t256 > 0 && eff(t256) * 1.08 >= eff(t128)) ? 256 : 128;
-  }
-  if (bn == 256 && N % 256) return -2;
   const bf16_t *a = (const bf16_t*)A, *b = (const bf16_t*)B;
   const int bt = beta ? 1 : 0;
-  if (variant == 0) {
-    const char* ve = std::getenv("ST_WGRAD_P8");
-    variant = (ve && std::atoi(ve) == 1) ? 2 : 1;
-  }
-  if (variant == 2) {
-    if (N % 256 || T % p8::BK) return -2;
-    const int g8 = (M / BM) * (N / 256);
-    if (probe == 1) wgrad8_kernel<1><<<g8, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
-    else if (probe == 2) wgrad8_kernel<2><<<g8, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
-    else wgrad8_kernel<0><<<g8, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
-    return (int)hipGetLastError();
-  }
-  const int nwg = (M / BM) * (N / bn);
-  if (bn == 256) {
-    if (probe == 1) wgrad_gemm_kernel<1, 256><<<nwg, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
-    else wgrad_gemm_kernel<0, 256><<<nwg, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
+  if (L.variant == 2) {
+    if (probe == 1) wgrad8_kernel<1><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
+    else if (probe == 2) wgrad8_kernel<2><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
+    else wgrad8_kernel<0><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
+  } else if (L.bn == 256) {
+    if (probe == 1) wgrad_gemm_kernel<1, 256><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
+    else wgrad_gemm_kernel<0, 256><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
   } else {
-    if (probe == 1) wgrad_gemm_kernel<1, 128><<<nwg, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
-    else wgrad_gemm_kernel<0, 128><<<nwg, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt);
+    if (probe == 1) wgrad_gemm_kernel<1, 128><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
+    else wgrad_gemm_kernel<0, 128><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
+  }
+  ST_HIP_CHECK(hipGetLastError());
+  if (L.split > 1) {
+    const dim3 rg(BM * L.bn / 1024, L.tail);
+    if (L.bn == 256) wgrad_tail_reduce<256><<<rg, 256, 0, st>>>(C, ldc, ws, nbm, nbn, sp);
+    else wgrad_tail_reduce<128><<<rg, 256, 0, st>>>(C, ldc, ws, nbm, nbn, sp);
   }
   return (int)hipGetLastError();
 }

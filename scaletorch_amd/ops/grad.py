@@ -186,7 +186,7 @@ def accumulate_grad(param: torch.Tensor, grad: torch.Tensor):
 
 def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> int:
     """First call per (shape, strides): time the two HIP kernels (1: 4-stage ring,
-    2: 8-phase ping-pong, csrc/wgrad_gemm.hip) against the hipBLASLt fp32-epilogue
+    2: 8-phase ping-pong, csrc/wgrad_gemm.hip; each with and without the tail split) against the hipBLASLt fp32-epilogue
     GEMM on a scratch output (5 rounds x 2 calls, same stream, interleaved) and keep
     the fastest -- 0 = hipBLASLt.  On gfx950 none wins every projection shape
     (tools/probe_wgrad.py: the 8-phase kernel +3-13 % on out/down, -1-2 % on
@@ -202,7 +202,9 @@ def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> int:
         _WGRAD_CHOICE[key] = 1
         return 1
     scratch = torch.zeros(M, N, dtype=torch.float32, device=dy2d.device)
-    arms = {v: (lambda v=v: _lib.ops().wgrad_gemm_(scratch, dy2d, x2d, 1, v)) for v in (1, 2)
+    # +16: the same kernel without the tail split (csrc/wgrad_gemm.hip), where the last
+    # partial round of tiles is left partly idle instead of being cut into token ranges
+    arms = {v: (lambda v=v: _lib.ops().wgrad_gemm_(scratch, dy2d, x2d, 1, v)) for v in (1, 2, 17, 18)
             if _lib.ops().wgrad_gemm_(scratch, dy2d, x2d, 0, v)}
     if not arms:
         _WGRAD_CHOICE[key] = 0
@@ -276,8 +278,8 @@ def wgrad_into(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, beta: i
         from . import _lib
 
         if _lib.use_native(dy2d):
-            forced = os.environ.get("ST_WGRAD_VARIANT", "")  # 0 / 1 / 2 overrides the per-shape pick (A/B)
-            if forced in ("0", "1", "2"):
+            forced = os.environ.get("ST_WGRAD_VARIANT", "")  # 0 / 1 / 2 / 17 / 18 overrides the pick (A/B)
+            if forced in ("0", "1", "2", "17", "18"):
                 variant = int(forced)
             elif variant is None:
                 variant = _wgrad_pick(dy2d, x2d)

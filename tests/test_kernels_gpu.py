@@ -342,6 +342,34 @@ def test_wgrad_gemm_8phase(T, M, N, beta, monkeypatch):
     assert rel(out, ref) < 1e-5
 
 
+@pytest.mark.parametrize("variant,bn", [(1, "256"), (1, "128"), (2, "auto")])
+@pytest.mark.parametrize("split", ["auto", "2", "4"])
+@pytest.mark.parametrize("T,M,N,beta", [(512, 6144, 4096, 1), (256, 4096, 1792 * 2, 0), (512, 512, 1024, 1)])
+def test_wgrad_gemm_tail_split(T, M, N, beta, split, variant, bn, monkeypatch):
+    """Tail split (csrc/wgrad_gemm.hip): whole tiles for the full rounds of 256 CUs, the
+    last partial round cut into token ranges whose fp32 partials are added in order --
+    qkv-like 384 tiles (256 whole + 128 split), down-like 896, and a sub-round grid;
+    vs the fp32 reference, and bitwise repeatable."""
+    if split != "auto":
+        monkeypatch.setenv("ST_WGRAD_SPLIT", split)
+    if bn != "auto":
+        monkeypatch.setenv("ST_WGRAD_BN", bn)
+    torch.manual_seed(2)
+    dy = torch.randn(T, M, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+    ramp = torch.arange(N, device="cuda", dtype=torch.float32)[None, :] * 1e-3
+    out0 = torch.randn(M, N, device="cuda") + ramp
+    ref = dy.float().t() @ x.float() + (out0 if beta else 0)
+    outs = []
+    for _ in range(2):
+        out = out0.clone()
+        assert _lib.ops().wgrad_gemm_(out, dy, x, beta, variant)
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert rel(outs[0], ref) < 1e-5
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_wgrad_gemm_unsupported_shape_declines():
     dy = torch.randn(64, 200, device="cuda", dtype=torch.bfloat16)
     x = torch.randn(64, 192, device="cuda", dtype=torch.bfloat16)

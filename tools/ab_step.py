@@ -26,6 +26,10 @@ def set_variant(tr, name: str, side) -> None:
         for kv in name.split("+"):
             k, v = kv.split("=", 1)
             os.environ[k] = v
+            if k.startswith("ST_WGRAD"):  # re-run the per-shape wgrad pick under this setting
+                from scaletorch_amd.ops import grad as G
+
+                G._WGRAD_CHOICE.clear()
         return
     for k in list(os.environ):
         if k.startswith("ST_WGRAD"):
@@ -82,7 +86,8 @@ def main() -> int:
 
     for k, v in G._WGRAD_TIMES.items():
         print("wgrad tune", k[0], k[2], {a: round(b, 3) for a, b in v.items()}, "->",
-              {0: "hipblaslt", 1: "hip 4-stage", 2: "hip 8-phase"}.get(G._WGRAD_CHOICE.get(k), "?"))
+              {0: "hipblaslt", 1: "hip 4-stage", 2: "hip 8-phase", 17: "hip 4-stage no split",
+               18: "hip 8-phase no split"}.get(G._WGRAD_CHOICE.get(k), "?"))
     print(json.dumps({v: round(statistics.median(t), 2) for v, t in times.items()}))
     return 0
 
