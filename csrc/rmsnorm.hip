@@ -204,37 +204,36 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
   }
 }
 
-// dw[col] (+)= sum_p partial[p, col].  block = 256 threads covering 256
-// columns (float4 per lane) x 4 waves splitting the partial rows; blockIdx.y
-// splits the partial rows further and combines with one fp32 atomic per
-// column per block (16 adders per address at most).
+// dw[col] (+)= sum_p partial[p, col], deterministically: a block owns 64 columns
+// (16 lanes x float4) and splits the partial rows over 16 row groups (p = g, g+16,
+// ...); the 16 group sums fold through LDS in group order and one thread per column
+// quad adds them to dw (the only writer of those columns: no atomics, so the
+// dweight -- and with it the whole step -- is bitwise repeatable).
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ partial,
-                                                     float* __restrict__ out, int P, int h,
-                                                     int splits) {
-  __shared__ float4 red[4][64];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int col = blockIdx.x * 256 + lane * 4;
-  const int per = (P + splits - 1) / splits;
-  const int p0 = blockIdx.y * per, p1 = min(P, p0 + per);
+                                                     float* __restrict__ out, int P, int h) {
+  __shared__ float4 red[16][16];
+  const int q = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int col = blockIdx.x * 64 + q * 4;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (col < h) {
-    for (int p = p0 + wid; p < p1; p += 4) {
+    for (int p = g; p < P; p += 16) {
       float4 v = ld4f(partial + (size_t)p * h + col);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
   }
-  red[wid][lane] = acc;
+  red[g][q] = acc;
   __syncthreads();
-  if (wid == 0 && col < h) {
-    float4 t = red[0][lane];
+  if (g == 0 && col < h) {
+    float4 t = red[0][q];
 #pragma unroll
-    for (int k = 1; k < 4; ++k) {
-      t.x += red[k][lane].x; t.y += red[k][lane].y; t.z += red[k][lane].z; t.w += red[k][lane].w;
+    for (int k = 1; k < 16; ++k) {
+      t.x += red[k][q].x; t.y += red[k][q].y; t.z += red[k][q].z; t.w += red[k][q].w;
     }
-    atomicAdd(out + col + 0, t.x);
-    atomicAdd(out + col + 1, t.y);
-    atomicAdd(out + col + 2, t.z);
-    atomicAdd(out + col + 3, t.w);
+    // scalar: dw may be any fp32 view into the main_grad arena (4-byte aligned)
+    out[col + 0] += t.x;
+    out[col + 1] += t.y;
+    out[col + 2] += t.z;
+    out[col + 3] += t.w;
   }
 }
 
@@ -320,12 +319,7 @@ int st_rmsnorm_bwd(const void* dy, const void* s, const void* w, const float* rs
   int rc = dres ? launch_bwd<true>(dy, s, w, rstd, dres, ds, partial, nw, rows, h, st)
                 : launch_bwd<false>(dy, s, w, rstd, nullptr, ds, partial, nw, rows, h, st);
   if (rc) return rc;
-  // enough (column-group x row-split) blocks to fill the chip: the partial
-  // rows are reduced with 4-wave strided loads, at most 16 rows per wave
-  int splits = 1;
-  while (splits < 64 && nw / splits > 64) splits *= 2;
-  dim3 grid((h + 255) / 256, splits);
-  colsum_kernel<<<grid, 256, 0, st>>>(partial, dw_out, nw, h, splits);
+  colsum_kernel<<<(h + 63) / 64, 256, 0, st>>>(partial, dw_out, nw, h);
   return (int)hipGetLastError();
 }
 

@@ -54,6 +54,27 @@ def test_rmsnorm(h, with_res):
         assert rel(r.grad, rr.grad) < 2e-2
 
 
+def test_rmsnorm_dweight_bitwise_repeatable():
+    """The dweight column sum has no atomics (csrc/rmsnorm.hip colsum_kernel): many
+    rows (256 partial blocks) give bitwise-identical weight gradients run to run."""
+    torch.manual_seed(0)
+    h = 4096
+    x = torch.randn(8192, h, device="cuda", dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(h, device="cuda")).to(torch.bfloat16)
+    gy = torch.randn(8192, h, device="cuda", dtype=torch.bfloat16)
+    grads = []
+    for _ in range(3):
+        wi = w.clone().requires_grad_(True)
+        y = ops.rms_norm(x, wi, 1e-5)
+        y.backward(gy)
+        grads.append(wi.grad.clone())
+    wr = w.float().requires_grad_(True)
+    xf = x.float()
+    (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * wr).backward(gy.float())
+    assert rel(grads[0], wr.grad) < 2e-2
+    assert torch.equal(grads[0], grads[1]) and torch.equal(grads[0], grads[2])
+
+
 @pytest.mark.parametrize("D", [64, 128])
 def test_rope_inplace(D):
     torch.manual_seed(0)

@@ -19,14 +19,14 @@ import sqlite3
 import sys
 
 CLASSES = [  # (class, regex on the kernel name), first match wins
-    ("gemm_wgrad_hip", r"wgrad8_kernel|wgrad_gemm_kernel"),
+    ("gemm_wgrad_hip", r"wgrad8_kernel|wgrad_gemm_kernel|wgrad_tail_reduce"),
     ("gemm_fp32_out(wgrad_hipblaslt)", r"Cijk_.*_BSS_|Cijk_.*BBS_BS_"),
     ("gemm_bf16(fwd+dgrad)", r"Cijk_"),
     ("flash_fwd", r"flash_fwd"),
     ("flash_bwd", r"flash_bwd"),
     ("adamw", r"adamw_kernel"),
     ("grad_norm", r"sumsq_kernel|sum_partials_kernel"),
-    ("rmsnorm", r"rmsnorm"),
+    ("rmsnorm", r"rmsnorm|colsum_kernel"),
     ("swiglu", r"swiglu"),
     ("rope", r"rope_kernel|qknorm_rope"),
     ("xent", r"xent_"),
