@@ -34,6 +34,13 @@ import os
 import sys
 import time
 
+# HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (default 4); past that,
+# streams share a queue and their kernels run in submission order.  A step drives the
+# compute stream, the optimizer side stream, the W^T stream and, at DP > 1, RCCL's
+# streams (one per communicator): give each its own queue so a collective waiting on a
+# peer never sits in front of compute.  Read when the HIP runtime starts: set before torch.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 # Qwen3-8B TP2-DP4 S2048, 8x Ascend 910B: 1,391 tok/s/GPU (README.md:84 of the
 # reference) -- the nearest published 8B row whose step does
 # real DP/TP work.  vs_baseline compares per-GPU throughput against it.

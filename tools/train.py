@@ -26,6 +26,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.realpath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# one hardware queue per stream (compute, optimizer side stream, W^T, RCCL): see bench.py
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 import torch  # noqa: E402
 
 from scaletorch_amd.dist import collectives as C  # noqa: E402
