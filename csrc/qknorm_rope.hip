@@ -193,14 +193,35 @@ __global__ __launch_bounds__(256) void qknorm_rope_bwd_kernel(
   }
 }
 
-// out[c] += sum_p partial[p][c] for c < 2D (fixed order)
+// out[c] += sum_p partial[p][c] for c < C (C % 4 == 0), in a fixed order: a block owns
+// 64 columns (16 lanes x float4) and splits the P partial rows over 16 row groups whose
+// sums fold through LDS in group order (one serial 512-row walk per column took 118 us
+// per call: 7 % of a Qwen3-0.6B step).
 __global__ __launch_bounds__(256) void partial_colsum_kernel(const float* __restrict__ partial, int P, int C,
                                                              float* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += partial[(int64_t)p * C + c];
-  out[c] += s;
+  __shared__ float4 red[16][16];
+  const int q = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 64 + q * 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < C) {
+    for (int p = g; p < P; p += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(partial + (int64_t)p * C + c);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  red[g][q] = acc;
+  __syncthreads();
+  if (g == 0 && c < C) {
+    float4 t = red[0][q];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {
+      t.x += red[k][q].x; t.y += red[k][q].y; t.z += red[k][q].z; t.w += red[k][q].w;
+    }
+    out[c + 0] += t.x;
+    out[c + 1] += t.y;
+    out[c + 2] += t.z;
+    out[c + 3] += t.w;
+  }
 }
 
 constexpr int kBwdBlocks = 512;
@@ -249,7 +270,7 @@ int st_qknorm_rope_bwd(void* dqkv, const void* xsave, const float* rstd, const v
     qknorm_rope_bwd_kernel<64><<<blocks, 256, 0, st>>>((bf16_t*)dqkv, (const bf16_t*)xsave, rstd,
                                                        (const bf16_t*)wq, (const bf16_t*)wk, cos_t, sin_t, pos, N,
                                                        S, H, NQK, NHT, max_pos, partial);
-  partial_colsum_kernel<<<(2 * D + 255) / 256, 256, 0, st>>>(partial, blocks, 2 * D, dw_out);
+  partial_colsum_kernel<<<(2 * D + 63) / 64, 256, 0, st>>>(partial, blocks, 2 * D, dw_out);
   return (int)hipGetLastError();
 }
 

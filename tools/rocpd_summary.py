@@ -48,6 +48,8 @@ def main() -> int:
     ap.add_argument("db")
     ap.add_argument("--steps", type=int, default=3, help="timed steps at the end of the run")
     ap.add_argument("--csv", default="", help="write per-kernel stats of the window here")
+    ap.add_argument("--gap_ms", type=float, default=50.0,
+                    help="AdamW launches further apart than this start a new step (below the step time)")
     args = ap.parse_args()
     c = sqlite3.connect(args.db)
     rows = c.execute("select name, start, end from kernels order by start").fetchall()
@@ -58,7 +60,7 @@ def main() -> int:
     # group AdamW launches into steps (arenas of one step launch back to back)
     groups = [[ad[0]]]
     for s, e in ad[1:]:
-        if s - groups[-1][-1][1] > 50e6:  # > 50 ms apart: a new step
+        if s - groups[-1][-1][1] > args.gap_ms * 1e6:  # far apart: a new step
             groups.append([(s, e)])
         else:
             groups[-1].append((s, e))
