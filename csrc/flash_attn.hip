@@ -864,14 +864,16 @@ template <int D, int PROBE = 0>  // PROBE 1: softmax / dS VALU skipped (timing p
 __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
     AttnParams p, const bf16_t* __restrict__ dout, int64_t sdb, int64_t sds, int64_t sdh,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dk,
-    bf16_t* __restrict__ dv) {
+    bf16_t* __restrict__ dv, int nsplit, float* __restrict__ part) {
   constexpr int BKW = 128, BQ = 64, NKK = D / 16, NDT = D / 32;
   constexpr int TB = BQ * D * 2;
   __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB + 2 * 2 * BQ * 4];
   lds_t* smem = (lds_t*)smem_raw;  // Q0 Q1 dO0 dO1 | stats[buf][lse2 | delta][BQ]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, h = lane >> 5;
   const int G = p.H / p.Hkv, BHk = p.B * p.Hkv, id = blockIdx.x;
-  const int kt_i = id / BHk;  // causal: early keys are the heaviest -> launched first
+  // causal: early keys are the heaviest -> launched first; a key tile's query work may be
+  // cut into nsplit ranges (small grids, see st_flash_bwd), each its own workgroup
+  const int kt_i = id / (BHk * nsplit), sp = (id / BHk) % nsplit;
   const int bhk = id % BHk, b = bhk / p.Hkv, hk = bhk % p.Hkv;
   const int k0 = kt_i * BKW, kw = k0 + wid * 32, my_k = kw + r;
 
@@ -901,6 +903,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
   const int nqb = (p.Sq + BQ - 1) / BQ;
   const int nq = nqb > qb0 ? nqb - qb0 : 0;
   const int total = G * nq;
+  const int it0 = (int)((int64_t)total * sp / nsplit), it1 = (int)((int64_t)total * (sp + 1) / nsplit);
 
   LdsAddr<D> la;
   la.init(lane);
@@ -926,13 +929,13 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
                (lds_t*)(stats + buf * 2 * BQ + wid * BQ), (uint32_t)((qb * BQ + lane) * 4));
     }
   };
-  if (total > 0) issue(0, qb0, 0);
+  int g_c = nq > 0 ? it0 / nq : 0, qb_c = qb0 + (nq > 0 ? it0 % nq : 0);
+  if (it0 < it1) issue(g_c, qb_c, 0);
   dma_barrier();
 
-  int g_c = 0, qb_c = qb0;
   auto step = [&](auto bufc, int it) {
     constexpr int BUF = decltype(bufc)::value;
-    const bool more = it + 1 < total;
+    const bool more = it + 1 < it1;
     int g_n = g_c, qb_n = qb_c + 1;
     if (qb_n == nqb) {
       qb_n = qb0;
@@ -1032,15 +1035,36 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
     g_c = g_n;
     qb_c = qb_n;
   };
-  int it = 0;  // unconditional pairs (see the dQ kernel)
-  for (; it + 1 < total; it += 2) {
+  int it = it0;  // unconditional pairs (see the dQ kernel)
+  for (; it + 1 < it1; it += 2) {
     step(Buf<0>(), it);
     step(Buf<1>(), it + 1);
   }
-  if (it < total) step(Buf<0>(), it);
+  if (it < it1) step(Buf<0>(), it);
 
   agpr_fence(dkacc);
   agpr_fence(dvacc);
+  if (nsplit > 1) {
+    // fp32 partials [split][B*Hkv][Sk][D] (dK block first, then dV), summed in split
+    // order by dkdv_split_reduce_kernel: deterministic
+    if (my_k < p.Sk) {
+      const int64_t blk = (int64_t)BHk * p.Sk * D;
+      float* pk = part + (int64_t)sp * 2 * blk + ((int64_t)bhk * p.Sk + my_k) * D;
+      float* pv = pk + blk;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = 32 * dt + 8 * g + 4 * h;
+          *reinterpret_cast<float4*>(pk + d) = make_float4(dkacc[dt][4 * g] * p.scale, dkacc[dt][4 * g + 1] * p.scale,
+                                                           dkacc[dt][4 * g + 2] * p.scale, dkacc[dt][4 * g + 3] * p.scale);
+          *reinterpret_cast<float4*>(pv + d) =
+              make_float4(dvacc[dt][4 * g], dvacc[dt][4 * g + 1], dvacc[dt][4 * g + 2], dvacc[dt][4 * g + 3]);
+        }
+      }
+    }
+    return;
+  }
   if (my_k < p.Sk) {
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) {
@@ -1058,6 +1082,35 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
       }
     }
   }
+}
+
+// dK / dV = sum over the query-range splits of the fp32 partials (fixed split order),
+// written as bf16 through the output strides.  One thread per 8 elements.
+__global__ __launch_bounds__(256) void dkdv_split_reduce_kernel(const float* __restrict__ part, int nsplit,
+                                                                int Hkv, int Sk, int D, int64_t total8,
+                                                                bf16_t* __restrict__ dk, bf16_t* __restrict__ dv,
+                                                                int64_t sxb, int64_t sxs, int64_t sxh) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total8) return;
+  const int D8 = D / 8;
+  const int c = (int)(t % D8);
+  const int64_t row = t / D8;  // (b * Hkv + hk) * Sk + k
+  const int k = (int)(row % Sk);
+  const int64_t bhk = row / Sk;
+  const int hk = (int)(bhk % Hkv), b = (int)(bhk / Hkv);
+  const int64_t blk = total8 * 8;
+  float ak[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, av[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < nsplit; ++s) {
+    const float* pk = part + (int64_t)s * 2 * blk + row * D + c * 8;
+    const float4 k0 = ld4f(pk), k1 = ld4f(pk + 4), v0 = ld4f(pk + blk), v1 = ld4f(pk + blk + 4);
+    ak[0] += k0.x; ak[1] += k0.y; ak[2] += k0.z; ak[3] += k0.w;
+    ak[4] += k1.x; ak[5] += k1.y; ak[6] += k1.z; ak[7] += k1.w;
+    av[0] += v0.x; av[1] += v0.y; av[2] += v0.z; av[3] += v0.w;
+    av[4] += v1.x; av[5] += v1.y; av[6] += v1.z; av[7] += v1.w;
+  }
+  const int64_t off = (int64_t)b * sxb + (int64_t)k * sxs + (int64_t)hk * sxh + c * 8;
+  st8(dk + off, pack8(ak));
+  st8(dv + off, pack8(av));
 }
 
 // ============================================================== ring-attention merge
@@ -1171,6 +1224,33 @@ int st_flash_bwd_preprocess(const void* o, const void* dout, float* delta, int B
   return (int)hipGetLastError();
 }
 
+// Query-range split of the dK/dV kernel.  It runs one workgroup (one wave per SIMD)
+// per 128-key tile of each (batch, kv head); under a causal mask tile j carries
+// (nqb - j) query blocks, so when the grid is at most one round (Qwen3-0.6B mbs 2 x
+// 2048: 256 workgroups on 256 CUs; Qwen3-1.7B 1 x 2048: 128) the kernel lasts as long
+// as its heaviest tile, ~2x the mean, or leaves CUs empty.  Cutting every tile's query
+// range into nsplit workgroups (~3 rounds) lets the heaviest-first dispatch balance
+// them; fp32 partials, reduced in split order (deterministic).
+// ST_FLASH_DKDV_SPLIT=N forces N (1 = off).
+static int dkdv_nsplit(int B, int Sk, int Hkv) {
+  const char* e = std::getenv("ST_FLASH_DKDV_SPLIT");
+  if (e) {
+    const int v = std::atoi(e);
+    if (v >= 1 && v <= 8) return v;
+  }
+  const int64_t gk = (int64_t)((Sk + 127) / 128) * B * Hkv;
+  // measured (tools/bench_flash_split.py): 128-256 workgroups -24..-41 % backward time,
+  // 512 (two rounds, already balanced by the heaviest-first order) +4 %: split <= 1 round
+  if (gk > 256) return 1;
+  const int64_t want = (768 + gk - 1) / gk;
+  return (int)(want > 8 ? 8 : want);
+}
+
+int64_t st_flash_bwd_part_elems(int B, int Sk, int Hkv, int D) {
+  const int n = dkdv_nsplit(B, Sk, Hkv);
+  return n > 1 ? (int64_t)n * 2 * B * Hkv * Sk * D : 0;
+}
+
 // dq / dk / dv: bf16 outputs with arbitrary (b, s, h) strides (D contiguous) so
 // they can be slices of one fused dQKV buffer.
 int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse,
@@ -1179,7 +1259,7 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
                  int64_t skh, int64_t svb, int64_t svs, int64_t svh, int64_t sdb, int64_t sds,
                  int64_t sdh, int64_t sdqb, int64_t sdqs, int64_t sdqh, int64_t sdkb, int64_t sdks,
                  int64_t sdkh, float scale, int causal, int64_t q_offset, int64_t k_offset,
-                 hipStream_t st) {
+                 float* part, hipStream_t st) {
   if (H % Hkv != 0) return -2;
   if (B == 0 || Sq == 0 || Sk == 0) return 0;
   if (!offsets_fit(Sq, sqs) || !offsets_fit(Sq, sds) || !offsets_fit(Sk, sks) || !offsets_fit(Sk, svs))
@@ -1190,25 +1270,32 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
   pq.sxb = sdqb; pq.sxs = sdqs; pq.sxh = sdqh;
   pk.sxb = sdkb; pk.sxs = sdks; pk.sxh = sdkh;
   const unsigned gq = (unsigned)(((Sq + 127) / 128) * B * H);
-  const unsigned gk = (unsigned)(((Sk + 127) / 128) * B * Hkv);
+  const int nsplit = part ? dkdv_nsplit(B, Sk, Hkv) : 1;
+  const unsigned gk = (unsigned)(((Sk + 127) / 128) * B * Hkv * nsplit);
   const bf16_t* dop = (const bf16_t*)dout;
   if (D == 128) {
     const char* pe = std::getenv("ST_FLASH_PROBE");  // diagnostics only (tools/probe_flash.py)
     if (pe && std::atoi(pe) == 1) {
       flash_bwd_dq_kernel<128, 1><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq);
       flash_bwd_dkdv_kernel<128, 1><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
-                                                   (bf16_t*)dv);
+                                                   (bf16_t*)dv, nsplit, part);
     } else {
       flash_bwd_dq_kernel<128><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq);
       flash_bwd_dkdv_kernel<128><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
-                                                   (bf16_t*)dv);
+                                                   (bf16_t*)dv, nsplit, part);
     }
   } else if (D == 64) {
     flash_bwd_dq_kernel<64><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq);
     flash_bwd_dkdv_kernel<64><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
-                                                  (bf16_t*)dv);
+                                                  (bf16_t*)dv, nsplit, part);
   } else {
     return -3;
+  }
+  if (nsplit > 1) {
+    ST_HIP_CHECK(hipGetLastError());
+    const int64_t total8 = (int64_t)B * Hkv * Sk * (D / 8);
+    dkdv_split_reduce_kernel<<<(unsigned)((total8 + 255) / 256), 256, 0, st>>>(
+        part, nsplit, Hkv, Sk, D, total8, (bf16_t*)dk, (bf16_t*)dv, sdkb, sdks, sdkh);
   }
   return (int)hipGetLastError();
 }

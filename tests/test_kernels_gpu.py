@@ -179,6 +179,16 @@ FLASH_CASES = [
 
 @pytest.mark.parametrize("B,Sq,Sk,H,Hkv,D,causal", FLASH_CASES)
 def test_flash_fwd_bwd(B, Sq, Sk, H, Hkv, D, causal):
+    # these short grids take the dK/dV query-range split (auto: up to 8 ranges, some
+    # of them empty for the short query ranges)
+    _flash_case(B, Sq, Sk, H, Hkv, D, causal, 1.0)
+
+
+@pytest.mark.parametrize("split", ["1", "3"])
+@pytest.mark.parametrize("B,Sq,Sk,H,Hkv,D,causal", [FLASH_CASES[1], FLASH_CASES[2], FLASH_CASES[6], FLASH_CASES[8]])
+def test_flash_dkdv_split_forced(B, Sq, Sk, H, Hkv, D, causal, split, monkeypatch):
+    """The dK/dV kernel unsplit (the long-grid path) and cut into 3 query ranges."""
+    monkeypatch.setenv("ST_FLASH_DKDV_SPLIT", split)
     _flash_case(B, Sq, Sk, H, Hkv, D, causal, 1.0)
 
 
