@@ -40,6 +40,18 @@ def _entry(rank, world, port, fn, args, q):
 
 
 def run_workers(fn, world: int, *args, timeout: float = 240.0) -> list:
+    # the free port is only reserved until _free_port returns: under pytest -n another
+    # worker's rendezvous can take it first (EADDRINUSE) -> retry on a fresh port
+    for attempt in range(3):
+        try:
+            return _run_once(fn, world, args, timeout)
+        except RuntimeError as e:
+            if "EADDRINUSE" not in str(e) or attempt == 2:
+                raise
+    raise AssertionError("unreachable")
+
+
+def _run_once(fn, world: int, args, timeout: float) -> list:
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
