@@ -23,8 +23,6 @@ res = {}
 for rnd in range(3 if len(sys.argv) <= 1 else 1):
     for arm in (sys.argv[1].split(",") if len(sys.argv) > 1 else ("full", "probe_novalu")):
         os.environ["ST_FLASH_PROBE"] = "1" if "probe" in arm else "0"
-        os.environ["ST_FLASH_DKDV_PIPE"] = "1" if "pipe" in arm else "0"
-        os.environ["ST_FLASH_DQ_PIPE"] = "1" if "dqp" in arm else "0"
         o = ops.flash_attn(q, k, v, causal=True)
         o.backward(g)
         torch.cuda.synchronize()
