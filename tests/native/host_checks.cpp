@@ -1,0 +1,67 @@
+// Host-side launch planning / validation of the HIP kernels, built with
+// -Xarch_host -fsanitize=address,undefined (tests/test_host_sanitizers.py) and run on
+// the CPU: every entry point here returns before any kernel launch, so no GPU is
+// touched.  Exercises the arithmetic that sizes grids and workspaces (wgrad tail
+// split, flash dK/dV split, RMSNorm partial rows) over a sweep of shapes, plus the
+// early-return validation of the launchers, for overflow / UB / out-of-bounds.
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#include <hip/hip_runtime.h>
+
+extern "C" {
+int64_t st_wgrad_ws_elems(int M, int N, int T, int variant);
+int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int M, int N,
+                  int T, int beta, int variant, float* ws, hipStream_t st);
+int64_t st_flash_bwd_part_elems(int B, int Sk, int Hkv, int D);
+int st_rmsnorm_bwd_nwaves(int rows);
+int st_rmsnorm_fwd(const void* x, const void* res, const void* w, void* y, void* sum_out, float* rstd, int rows,
+                   int h, float eps, hipStream_t st);
+}
+
+static int fails = 0;
+#define CHECK(c)                                                     \
+  do {                                                               \
+    if (!(c)) {                                                      \
+      std::fprintf(stderr, "FAIL %s:%d %s\n", __FILE__, __LINE__, #c); \
+      ++fails;                                                       \
+    }                                                                \
+  } while (0)
+
+int main() {
+  const int dims[] = {128, 256, 384, 1024, 2048, 3072, 4096, 6144, 7168, 14336, 28672, 128256};
+  const int toks[] = {32, 64, 96, 4096, 8192, 16384, 24576, 32768};
+  int64_t total = 0;
+  for (int M : dims)
+    for (int N : dims)
+      for (int T : toks)
+        for (int v : {0, 1, 2, 17, 18}) {
+          const int64_t e = st_wgrad_ws_elems(M, N, T, v);
+          CHECK(e >= 0);
+          // at most (split - 1) <= 7 partial copies of the last partial round (< 256 tiles)
+          CHECK(e <= (int64_t)7 * 256 * 256 * 256);
+          if (v >= 16) CHECK(e == 0);
+          total += e;
+        }
+  // shapes the kernels do not tile are declined before any launch
+  CHECK(st_wgrad_gemm(nullptr, 200, nullptr, 192, nullptr, 192, 200, 192, 64, 0, 1, nullptr, nullptr) == -2);
+  CHECK(st_wgrad_gemm(nullptr, 256, nullptr, 256, nullptr, 256, 256, 256, 0, 0, 1, nullptr, nullptr) == -2);
+  CHECK(st_wgrad_gemm(nullptr, 256, nullptr, 200, nullptr, 256, 256, 256, 64, 0, 2, nullptr, nullptr) == -2);
+  for (int B : {1, 2, 4, 6, 16})
+    for (int Sk : {1, 127, 128, 2048, 4096, 32768, 131072})
+      for (int Hkv : {1, 2, 8, 32})
+        for (int D : {64, 128}) {
+          const int64_t e = st_flash_bwd_part_elems(B, Sk, Hkv, D);
+          CHECK(e >= 0);
+          CHECK(e <= (int64_t)8 * 2 * B * Hkv * Sk * D);
+          total += e;
+        }
+  for (int rows : {0, 1, 3, 4, 5, 1000, 24576, 1 << 20}) {
+    const int nw = st_rmsnorm_bwd_nwaves(rows);
+    CHECK(nw >= 1 && nw <= 4096);
+  }
+  CHECK(st_rmsnorm_fwd(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 4, 100, 1e-5f, nullptr) == -2);
+  std::printf("host checks: %d failures (sum %lld)\n", fails, (long long)total);
+  return fails ? 1 : 0;
+}
