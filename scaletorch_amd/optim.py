@@ -30,6 +30,7 @@ import math
 import torch
 
 from .dist import collectives as C
+from .dist import trace
 from .ops import _lib
 
 
@@ -199,6 +200,7 @@ class ArenaAdamW(_ArenaOptimizer):
                                                a.exp_avg_sq[so: so + n], a.grad_flat[lo:hi],
                                                a.param_flat[lo:hi], self.clip_coef, lr, b1, b2, eps, wd, t)
                     if a.zero1:
+                        trace.record("dp.all_gather", a.param_flat[b.start: b.end], group_size=a.world, arena=a.name)
                         b.ag_handle = dist.all_gather_into_tensor(a.param_flat[b.start: b.end],
                                                                   a.param_flat[b.shard_lo: b.shard_hi],
                                                                   group=a.group, async_op=True)

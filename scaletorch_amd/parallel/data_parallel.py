@@ -38,6 +38,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..dist import collectives as C
+from ..dist import trace
 from . import mesh
 
 ALIGN = 64  # elements: keeps every param view 128-B aligned for 16-B vector loads
@@ -242,8 +243,10 @@ class GradArena:
                 if b.comm_out is None or b.comm_out.numel() != n:
                     b.comm_out = torch.empty(n, dtype=buf.dtype, device=buf.device)
                 out = b.comm_out
+            trace.record("dp.reduce_scatter", buf, group_size=self.world, arena=self.name)
             b.handle = dist.reduce_scatter_tensor(out, buf, op=op, group=self.group, async_op=True)
         else:
+            trace.record("dp.all_reduce", buf, group_size=self.world, arena=self.name)
             b.handle = dist.all_reduce(buf, op=op, group=self.group, async_op=True)
 
     def _bucket_sumsq(self, b: Bucket) -> None:
@@ -312,6 +315,7 @@ class GradArena:
         if not self.zero1:
             return
         for b in reversed(self.buckets):
+            trace.record("dp.all_gather", self.param_flat[b.start: b.end], group_size=self.world, arena=self.name)
             b.ag_handle = dist.all_gather_into_tensor(self.param_flat[b.start: b.end],
                                                       self.param_flat[b.shard_lo: b.shard_hi],
                                                       group=self.group, async_op=True)

@@ -105,6 +105,7 @@ class PerformanceMonitor:
     def __init__(self, warmup_steps: int = 2, window: int = 1000, rank: int = 0, telemetry_interval: int = 10,
                  device_index: int | None = None):
         self.warmup, self.rank = warmup_steps, rank
+        self.extra: dict = {}  # static / run-level entries merged into summary() (comm volume, PP bubble)
         self.times = deque(maxlen=window)
         self.tokens = deque(maxlen=window)
         self.telemetry = {}
@@ -195,6 +196,7 @@ class PerformanceMonitor:
         total_t = sum(self.times)
         out = {"steps_measured": len(ts), "mean_step_s": total_t / len(ts), "median_step_s": ts[len(ts) // 2],
                "tokens_per_s": sum(self.tokens) / total_t}
+        out.update(self.extra)
         for k, v in self.telemetry.items():
             if v:
                 out[f"avg_{k}"] = sum(v) / len(v)

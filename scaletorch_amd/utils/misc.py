@@ -100,3 +100,23 @@ def average_loss_across_dp_cp_ranks(loss: torch.Tensor, group) -> torch.Tensor:
     if C.get_world_size(group) > 1:
         C.all_reduce(loss, op="mean", group=group)
     return loss
+
+
+def pipeline_bubble_fraction(pp: int, micro_batches: int, virtual_stages: int = 1) -> float:
+    """Idle share of a 1F1B / AFAB pipeline step, (P-1) / (V*M + P-1) (interleaved 1F1B
+    with V model chunks per rank shrinks it V-fold); 0 without pipeline parallelism."""
+    if pp <= 1:
+        return 0.0
+    return (pp - 1) / (virtual_stages * micro_batches + pp - 1)
+
+
+def comm_per_step(before: dict, after: dict, steps: int) -> dict:
+    """Per-step calls / bytes of every communication op between two
+    ``scaletorch_amd.dist.trace.stats()`` snapshots."""
+    out = {}
+    for op, v in after.items():
+        b = before.get(op, {"calls": 0, "bytes": 0})
+        calls, nbytes = v["calls"] - b["calls"], v["bytes"] - b["bytes"]
+        if calls:
+            out[op] = {"calls": calls / max(1, steps), "bytes": nbytes / max(1, steps)}
+    return out

@@ -413,3 +413,46 @@ def test_verbose_comm_tracing_counts_pp_ops():
     s0, s1 = run_workers(_trace_worker, 2)
     assert s0["pp.send_forward"]["calls"] == 2 and s1["pp.recv_forward"]["calls"] == 2
     assert s1["pp.send_backward"]["calls"] == 2 and s0["pp.send_forward"]["bytes"] > 0
+
+
+def test_pipeline_bubble_and_comm_per_step():
+    from scaletorch_amd.utils.misc import comm_per_step, pipeline_bubble_fraction
+
+    assert pipeline_bubble_fraction(1, 8) == 0.0
+    assert abs(pipeline_bubble_fraction(2, 8) - 1 / 9) < 1e-12
+    assert abs(pipeline_bubble_fraction(2, 8, 2) - 1 / 17) < 1e-12  # interleaved: V-fold smaller
+    before = {"dp.reduce_scatter": {"calls": 4, "bytes": 400}}
+    after = {"dp.reduce_scatter": {"calls": 10, "bytes": 1000}, "dp.all_gather": {"calls": 3, "bytes": 300},
+             "idle": {"calls": 0, "bytes": 0}}
+    got = comm_per_step(before, after, 3)
+    assert got == {"dp.reduce_scatter": {"calls": 2.0, "bytes": 200.0}, "dp.all_gather": {"calls": 1.0, "bytes": 100.0}}
+
+
+def _dp_trace_worker(rank, world):
+    import torch.distributed as dist
+
+    from scaletorch_amd.dist import trace
+    from scaletorch_amd.parallel.data_parallel import GradArena
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    trace.reset()
+    ps = [torch.nn.Parameter(torch.randn(300, 7)), torch.nn.Parameter(torch.randn(50))]
+    a = GradArena(ps, dist.group.WORLD, "dense", bucket_size=1 << 20, reduce_dtype=torch.bfloat16, zero1=True)
+    for p in ps:
+        p.main_grad.fill_(rank + 1.0)
+    for b in a.buckets:
+        a.launch(b)
+    a.finish()
+    a.gather_params()
+    a.wait_params()
+    return trace.stats()
+
+
+def test_dp_collectives_are_traced():
+    """ZeRO-1 bucket reduce-scatter and parameter all-gather appear in the comm
+    counters (tools/train.py reports them per step)."""
+    from tests.dist_harness import run_workers
+
+    st = run_workers(_dp_trace_worker, 2)[0]
+    assert st["dp.reduce_scatter"]["calls"] >= 1 and st["dp.reduce_scatter"]["bytes"] > 0
+    assert st["dp.all_gather"]["calls"] >= 1

@@ -38,7 +38,9 @@ from scaletorch_amd.trainer.config import parse_args  # noqa: E402
 from scaletorch_amd.trainer.engine import Trainer  # noqa: E402
 from scaletorch_amd.utils.checkpoint import CheckpointManager, latest_checkpoint  # noqa: E402
 from scaletorch_amd.utils.device import get_theoretical_flops  # noqa: E402
+from scaletorch_amd.dist import trace as comm_trace  # noqa: E402
 from scaletorch_amd.utils.logger import PerformanceMonitor, get_logger  # noqa: E402
+from scaletorch_amd.utils.misc import comm_per_step, pipeline_bubble_fraction  # noqa: E402
 from scaletorch_amd.utils.misc import flops_per_token, rank_print, to_readable_format  # noqa: E402
 
 
@@ -83,6 +85,9 @@ def main(argv=None) -> int:
         fault_step = -1
     fault_rank = int(os.environ.get("ST_FAULT_RANK", "0"))
     monitor = PerformanceMonitor(warmup_steps=2, rank=tr.rank)
+    monitor.extra["pp_bubble_fraction"] = round(pipeline_bubble_fraction(
+        args.pipeline_parallel_size, args.gradient_accumulation_steps, args.virtual_pipeline_size), 4)
+    comm0 = None  # (step, trace.stats()) once the monitor's warm-up is over
     n_active = cfg.active_params()
     fpt = flops_per_token(n_active, cfg.num_hidden_layers, cfg.num_attention_heads, cfg.head_dim,
                           args.sequence_length)
@@ -119,6 +124,8 @@ def main(argv=None) -> int:
             loss_t = tr.train_step()
             log_now = tr.step % max(1, args.log_interval) == 0 or tr.step == total
             rec = monitor.end_iteration(tr.tokens_per_step, sync=log_now)  # events only: no device-wide sync
+            if comm0 is None and tr.step >= monitor.warmup:
+                comm0 = (tr.step, comm_trace.stats())
             if watchdog is not None:
                 watchdog.kick(tr.step)
             if prof is not None:
@@ -167,6 +174,8 @@ def main(argv=None) -> int:
         if prof is not None:
             prof.stop()
         ckpt.wait()
+        if comm0 is not None and tr.step > comm0[0]:
+            monitor.extra["comm_per_step"] = comm_per_step(comm0[1], comm_trace.stats(), tr.step - comm0[0])
         if tr.rank == 0 or _is_log_rank():
             s = monitor.summary()
             if s:
