@@ -159,11 +159,18 @@ def main() -> int:
     for _ in range(args.warmup):
         loss = tr.train_step()
     sync()
+    from scaletorch_amd.dist import trace as comm_trace
+
+    comm0 = comm_trace.stats()  # host-side counters only (a dict increment per collective)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = tr.train_step()
     sync()
     elapsed = time.perf_counter() - t0
+    from scaletorch_amd.utils.misc import comm_per_step
+
+    comm = {op: round(v["bytes"] / 1e6, 1) for op, v in
+            sorted(comm_per_step(comm0, comm_trace.stats(), args.steps).items())}
     # max over ranks
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if dist.is_initialized():
@@ -215,6 +222,7 @@ def main() -> int:
         "final_loss": round(final_loss, 4),
         "valid": valid,
         "max_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1) if dev.type == "cuda" else 0.0,
+        "comm_mb_per_step_rank0": comm,  # bytes handed to each collective per step on rank 0 (dist/trace.py)
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
