@@ -182,11 +182,18 @@ class ScatterToTensorParallelRegion(torch.autograd.Function):
         return torch.cat(C.all_gather(g.contiguous(), group=ctx.group, as_list=True), dim=-1), None
 
 
+def _trace(op: str, x: torch.Tensor, ws: int) -> None:
+    from ..dist import trace
+
+    trace.record(op, x, group_size=ws)
+
+
 def _gather_seq(x: torch.Tensor, group) -> torch.Tensor:
     """[B, S/tp, ...] -> [B, S, ...] (one all_gather_into_tensor; zero-copy when B == 1)."""
     ws = _ws(group)
     if ws == 1:
         return x
+    _trace("sp.all_gather", x, ws)
     xg = _xgmi_comm(group) if x.is_cuda else None
     gather = xg.all_gather if xg is not None else (lambda t: C.all_gather(t, group=group))
     if x.shape[0] == 1:
@@ -200,6 +207,7 @@ def _reduce_scatter_seq(x: torch.Tensor, group) -> torch.Tensor:
     ws = _ws(group)
     if ws == 1:
         return x
+    _trace("sp.reduce_scatter", x, ws)
     xg = _xgmi_comm(group) if x.is_cuda else None
     scatter = xg.reduce_scatter if xg is not None else (lambda t: C.reduce_scatter(t, group=group))
     if x.shape[0] == 1:
@@ -213,6 +221,7 @@ def _gather_seq_async(x: torch.Tensor, group):
     ws = _ws(group)
     if ws == 1:
         return lambda: x
+    _trace("sp.all_gather", x, ws)
     B = x.shape[0]
     xt = x[0].contiguous() if B == 1 else x.transpose(0, 1).contiguous()
     out, work = C.all_gather(xt, group=group, async_op=True)
@@ -228,6 +237,7 @@ def _reduce_scatter_seq_async(x: torch.Tensor, group):
     ws = _ws(group)
     if ws == 1:
         return lambda: x
+    _trace("sp.reduce_scatter", x, ws)
     B = x.shape[0]
     xt = x[0].contiguous() if B == 1 else x.transpose(0, 1).contiguous()
     out, work = C.reduce_scatter(xt, group=group, async_op=True)
