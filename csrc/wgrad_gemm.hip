@@ -269,7 +269,7 @@ __global__ __launch_bounds__(NT, 2) void wgrad_gemm_kernel(const bf16_t* __restr
   // wait (counted vmcnt) until this wave's DMA of tile kt landed, barrier (every
   // wave's DMA landed + every wave finished reading tile kt-1), refill the stage
   // tile kt-1 used with tile kt+NBUF-1, then the tile's MFMAs.
-  const int KT = T / BK;
+  const int KT = (T + BK - 1) / BK;  // a ragged last tile reads rows >= T as zeros (buffer range)
 #pragma unroll
   for (int p = 0; p < NBUF - 1; ++p)
     if (p < KT) dma(p, p);
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad8_kernel(const bf16_t* __restrict_
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  const int KT = T / p8::BK;
+  const int KT = (T + p8::BK - 1) / p8::BK;  // ragged last tile: rows >= T read as zeros
   // prologue: tile 0's four half-images; A0 + B0 retired for phase 0
 #pragma unroll
   for (int pc = 0; pc < 2; ++pc) p8_dma<0>(rsA, rsB, ldsw, vA, vB, sA, sB, 0, 0, pc);  // half-image by half-image:
@@ -565,7 +565,7 @@ int pick_split(int64_t nt, int T, int bk, int cus, bool off) {
 // -2: shape not supported (caller falls back)
 int plan(int M, int N, int T, int variant, Launch& L) {
   if (M <= 0 || N <= 0 || T <= 0) return -2;
-  if (M % BM || N % 128 || T % BK) return -2;
+  if (M % BM || N % 128) return -2;  // any T: rows past T land in LDS as zeros (MoE experts)
   const int cus = 256;
   const bool nosplit = (variant & 16) != 0;  // +16: tail split off (ops/grad.py times both)
   variant &= 15;
@@ -575,7 +575,7 @@ int plan(int M, int N, int T, int variant, Launch& L) {
   }
   L.variant = variant;
   if (variant == 2) {
-    if (N % 256 || T % p8::BK) return -2;
+    if (N % 256) return -2;
     L.bn = 256;
   } else {
     const char* be = std::getenv("ST_WGRAD_BN");  // force 128 / 256 (A/B)
@@ -618,9 +618,11 @@ int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float*
   if (plan(M, N, T, variant, L)) return -2;
   if (lda % 8 || ldb % 8 || lda < M || ldb < N || ldc < N) return -2;
   if (((uintptr_t)A | (uintptr_t)B) % 16 || (uintptr_t)C % 4) return -2;
-  // 32-bit buffer offsets: the last row of each operand must be addressable
-  if (((int64_t)(T - 1) * lda + M) * 2 >= (int64_t)1 << 32) return -2;
-  if (((int64_t)(T - 1) * ldb + N) * 2 >= (int64_t)1 << 32) return -2;
+  // 32-bit buffer offsets: every row a K-tile addresses -- up to T + 63 for a ragged last
+  // tile -- must stay below 2^32 bytes, or its offset would wrap into range instead of
+  // reading the descriptor's zero fill
+  if (((int64_t)(T + 63) * lda + M) * 2 >= (int64_t)1 << 32) return -2;
+  if (((int64_t)(T + 63) * ldb + N) * 2 >= (int64_t)1 << 32) return -2;
   if (L.split > 1 && (ws == nullptr || ldc % 4 || (uintptr_t)C % 16)) L.split = 1;  // the reduce reads C by 16 B
   const SplitPlan sp{ws, L.nfull, L.tail, L.split};
   const int nbm = M / BM, nbn = N / L.bn;

@@ -176,7 +176,7 @@ class _ExpertFFNFn(torch.autograd.Function):
                 if n:
                     # token counts change every step: fixed kernel choice, no per-shape timing
                     wgrad_into(w.main_grad[e], dout[off:off + n], inp[off:off + n], 0 if fresh else 1,
-                               variant=1 if n % 64 == 0 else 0)
+                               variant=1)  # any token count (ragged last K-tile zero-filled)
                 elif fresh:
                     w.main_grad[e].zero_()
                 off += n

@@ -401,6 +401,22 @@ def test_wgrad_gemm_tail_split(T, M, N, beta, split, variant, bn, monkeypatch):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("T", [1, 37, 100, 1000, 2047, 2100])
+def test_wgrad_gemm_ragged_tokens(T, variant):
+    """Token counts that are not a multiple of the K-tile (MoE experts): the last tile's
+    rows past T come from the buffer descriptor's zero fill; strided operands, beta = 1."""
+    torch.manual_seed(3)
+    M, N = 512, 768 if variant == 1 else 512
+    dy = torch.randn(T, M + 64, device="cuda", dtype=torch.bfloat16)[:, 32: 32 + M]
+    x = torch.randn(T, N + 128, device="cuda", dtype=torch.bfloat16)[:, 64: 64 + N]
+    out = torch.randn(M, N, device="cuda")
+    ref = dy.float().t() @ x.float() + out
+    assert _lib.ops().wgrad_gemm_(out, dy, x, 1, variant)
+    torch.cuda.synchronize()
+    assert rel(out, ref) < 1e-5
+
+
 def test_wgrad_gemm_unsupported_shape_declines():
     dy = torch.randn(64, 200, device="cuda", dtype=torch.bfloat16)
     x = torch.randn(64, 192, device="cuda", dtype=torch.bfloat16)
