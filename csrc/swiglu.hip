@@ -5,6 +5,8 @@
 // Reference: down(silu(gate(x)) * up(x)), scaletorch/models/llama.py:236-249
 // (two separate GEMMs + three elementwise kernels there; here one GEMM + one
 // bandwidth-bound kernel with 16-byte accesses).
+#include <cstdlib>
+
 #include "common.h"
 
 using namespace st;
@@ -87,9 +89,36 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restric
 
 inline dim3 grid_for(int64_t I8, int64_t N, int U) {
   const int64_t gx = (I8 + 256 * U - 1) / (256 * U);
-  const int64_t gy = N < 65535 ? N : 65535;
+  // ST_SWIGLU_ROWS caps the row dimension of the grid (blocks then walk several rows)
+  static const int64_t cap = [] {
+    const char* e = std::getenv("ST_SWIGLU_ROWS");
+    const long v = e ? std::atol(e) : 0;
+    return (int64_t)(v > 0 && v < 65535 ? v : 65535);
+  }();
+  const int64_t gy = N < cap ? N : cap;
   return dim3((unsigned)gx, (unsigned)gy);
 }
+
+// Column vectors per lane: 1 (Llama-3-8B I = 14336 -> I8 = 1792 = 7 full blocks of 256 per
+// row; 2 vectors per lane left the 4th block of a row half-empty).  Isolated at 6 x 4096 rows
+// (scripts/gpu_swiglu_ab.sh): fwd 5.19-5.32 -> 5.61 TB/s, bwd 5.20-5.25 -> 5.74 TB/s.
+// ST_SWIGLU_U = 1 / 2 / 4 / 7 for A/B.
+inline int pick_u(int64_t I8) {
+  static const int forced = [] {
+    const char* e = std::getenv("ST_SWIGLU_U");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (forced == 1 || forced == 2 || forced == 4 || forced == 7) return forced;
+  return 1;
+}
+
+#define ST_SWIGLU_DISPATCH(KERNEL, ...)                                              \
+  switch (pick_u(I8)) {                                                               \
+    case 1: KERNEL<1><<<grid_for(I8, N, 1), 256, 0, st>>>(__VA_ARGS__); break;         \
+    case 4: KERNEL<4><<<grid_for(I8, N, 4), 256, 0, st>>>(__VA_ARGS__); break;         \
+    case 7: KERNEL<7><<<grid_for(I8, N, 7), 256, 0, st>>>(__VA_ARGS__); break;         \
+    default: KERNEL<2><<<grid_for(I8, N, 2), 256, 0, st>>>(__VA_ARGS__); break;        \
+  }
 
 }  // namespace
 
@@ -97,10 +126,7 @@ extern "C" int st_swiglu_fwd(const void* gu, void* out, int64_t N, int64_t I, hi
   if (I % 8 != 0) return -2;
   const int64_t I8 = I / 8;
   if (N == 0 || I8 == 0) return 0;
-  if (I8 >= 1024)
-    swiglu_fwd_kernel<2><<<grid_for(I8, N, 2), 256, 0, st>>>((const bf16_t*)gu, (bf16_t*)out, I8, N);
-  else
-    swiglu_fwd_kernel<1><<<grid_for(I8, N, 1), 256, 0, st>>>((const bf16_t*)gu, (bf16_t*)out, I8, N);
+  ST_SWIGLU_DISPATCH(swiglu_fwd_kernel, (const bf16_t*)gu, (bf16_t*)out, I8, N)
   return (int)hipGetLastError();
 }
 
@@ -109,11 +135,6 @@ extern "C" int st_swiglu_bwd(const void* dout, const void* gu, void* dgu, int64_
   if (I % 8 != 0) return -2;
   const int64_t I8 = I / 8;
   if (N == 0 || I8 == 0) return 0;
-  if (I8 >= 1024)
-    swiglu_bwd_kernel<2><<<grid_for(I8, N, 2), 256, 0, st>>>((const bf16_t*)dout, (const bf16_t*)gu,
-                                                              (bf16_t*)dgu, I8, N);
-  else
-    swiglu_bwd_kernel<1><<<grid_for(I8, N, 1), 256, 0, st>>>((const bf16_t*)dout, (const bf16_t*)gu,
-                                                              (bf16_t*)dgu, I8, N);
+  ST_SWIGLU_DISPATCH(swiglu_bwd_kernel, (const bf16_t*)dout, (const bf16_t*)gu, (bf16_t*)dgu, I8, N)
   return (int)hipGetLastError();
 }
