@@ -71,7 +71,9 @@ def prepare_dgrad_weight(w: torch.Tensor) -> None:
         return
     st = _WT_STREAMS.get(w.device.index)
     if st is None:
-        st = _WT_STREAMS[w.device.index] = torch.cuda.Stream(device=w.device)
+        # ST_WT_STREAM_PRIORITY: HIP priority of the W^T stream (0 default, -1 high)
+        st = _WT_STREAMS[w.device.index] = torch.cuda.Stream(
+            device=w.device, priority=int(os.environ.get("ST_WT_STREAM_PRIORITY", "0")))
     ready = torch.cuda.Event()
     ready.record()
     with torch.cuda.stream(st):
