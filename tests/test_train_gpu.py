@@ -293,3 +293,37 @@ def test_training_step_bitwise_deterministic():
     l2, p2 = run()
     assert l1 == l2
     assert torch.equal(p1, p2)
+
+
+class _PrevTokenStream:
+    """Learnable synthetic task for convergence checks: random tokens, target_t =
+    input_{t-1} (needs attention to the previous position; t = 0 ignored)."""
+
+    def __init__(self, vocab, mbs, seq, device, seed=0):
+        self.vocab, self.mbs, self.seq, self.device = vocab, mbs, seq, device
+        self.gen = torch.Generator(device=device).manual_seed(seed)
+        self.pos = torch.arange(seq, device=device).unsqueeze(0).expand(mbs, seq)
+        self.epoch = 0
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        ids = torch.randint(0, self.vocab, (self.mbs, self.seq), device=self.device, generator=self.gen)
+        tgt = torch.full_like(ids, -100)
+        tgt[:, 1:] = ids[:, :-1]
+        return {"input_ids": ids, "target_ids": tgt, "position_ids": self.pos, "hidden_states": None}
+
+
+@pytest.mark.parametrize("model", ["tiny-llama", "tiny-qwen3"])
+def test_training_converges_on_a_learnable_task(model):
+    """End to end on the HIP kernels (flash fwd/bwd, fused norms / RoPE / SwiGLU, wgrad GEMMs,
+    fused AdamW on the side stream): the previous-token task is learned -- the loss falls
+    from ln(512) = 6.2 to a small fraction of it within 300 steps."""
+    tr = _tiny_trainer(model_name_or_path=model, micro_batch_size=8, sequence_length=256,
+                       total_train_steps=400, learning_rate=3e-3, max_grad_norm=1.0)
+    tr.data = _PrevTokenStream(tr.model_config.vocab_size, 8, 256, tr.device)
+    losses = [tr.reduced_loss(tr.train_step()) for _ in range(300)]
+    first, last = sum(losses[:5]) / 5, sum(losses[-10:]) / 10
+    assert first > 5.5, losses[:5]
+    assert last < 0.25 * first, (first, last, losses[::30])
