@@ -1232,7 +1232,7 @@ int st_flash_bwd_preprocess(const void* o, const void* dout, float* delta, int B
 // range into nsplit workgroups (~3 rounds) lets the heaviest-first dispatch balance
 // them; fp32 partials, reduced in split order (deterministic).
 // ST_FLASH_DKDV_SPLIT=N forces N (1 = off).
-static int dkdv_nsplit(int B, int Sk, int Hkv) {
+static int dkdv_nsplit(int B, int Sk, int Hkv, int causal) {
   const char* e = std::getenv("ST_FLASH_DKDV_SPLIT");
   if (e) {
     const int v = std::atoi(e);
@@ -1242,12 +1242,15 @@ static int dkdv_nsplit(int B, int Sk, int Hkv) {
   // measured (tools/bench_flash_split.py): 128-256 workgroups -24..-41 % backward time,
   // 512 (two rounds, already balanced by the heaviest-first order) +4 %: split <= 1 round
   if (gk > 256) return 1;
+  // without a causal mask every key tile carries the same work: a full round needs no split
+  // (off-diagonal ring-attention blocks of CP)
+  if (!causal && gk > 192) return 1;
   const int64_t want = (768 + gk - 1) / gk;
   return (int)(want > 8 ? 8 : want);
 }
 
-int64_t st_flash_bwd_part_elems(int B, int Sk, int Hkv, int D) {
-  const int n = dkdv_nsplit(B, Sk, Hkv);
+int64_t st_flash_bwd_part_elems(int B, int Sk, int Hkv, int D, int causal) {
+  const int n = dkdv_nsplit(B, Sk, Hkv, causal);
   return n > 1 ? (int64_t)n * 2 * B * Hkv * Sk * D : 0;
 }
 
@@ -1270,7 +1273,7 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
   pq.sxb = sdqb; pq.sxs = sdqs; pq.sxh = sdqh;
   pk.sxb = sdkb; pk.sxs = sdks; pk.sxh = sdkh;
   const unsigned gq = (unsigned)(((Sq + 127) / 128) * B * H);
-  const int nsplit = part ? dkdv_nsplit(B, Sk, Hkv) : 1;
+  const int nsplit = part ? dkdv_nsplit(B, Sk, Hkv, causal) : 1;
   const unsigned gk = (unsigned)(((Sk + 127) / 128) * B * Hkv * nsplit);
   const bf16_t* dop = (const bf16_t*)dout;
   if (D == 128) {
