@@ -52,7 +52,7 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
                  int64_t sds, int64_t sdh, int64_t sdqb, int64_t sdqs, int64_t sdqh, int64_t sdkb,
                  int64_t sdks, int64_t sdkh, float scale, int causal, int64_t q_offset,
                  int64_t k_offset, float* part, hipStream_t st);
-int64_t st_flash_bwd_part_elems(int B, int Sk, int Hkv, int D, int causal);
+int64_t st_flash_bwd_part_elems(int B, int Sq, int Sk, int H, int Hkv, int D, int causal);
 int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int M,
                   int N, int T, int beta, int variant, float* ws, hipStream_t st);
 int64_t st_wgrad_ws_elems(int M, int N, int T, int variant);
@@ -616,7 +616,7 @@ std::vector<at::Tensor> flash_bwd(const at::Tensor& dout, const at::Tensor& q, c
   auto dv = pick(dv_out, v.sizes(), "dv_out");
   TORCH_CHECK(dk.strides() == dv.strides(), "flash_bwd: dk_out/dv_out must share strides");
   // fp32 partials of the dK/dV query-range split (short grids only; csrc/flash_attn.hip)
-  const int64_t pe = st_flash_bwd_part_elems((int)B, (int)Sk, (int)Hkv, (int)D, causal ? 1 : 0);
+  const int64_t pe = st_flash_bwd_part_elems((int)B, (int)Sq, (int)Sk, (int)H, (int)Hkv, (int)D, causal ? 1 : 0);
   at::Tensor part;
   if (pe > 0) part = at::empty({pe}, q.options().dtype(at::kFloat));
   rc = st_flash_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),

@@ -697,14 +697,18 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
                                                               int64_t sdb, int64_t sds, int64_t sdh,
                                                               const float* __restrict__ lse,
                                                               const float* __restrict__ delta,
-                                                              bf16_t* __restrict__ dq) {
+                                                              bf16_t* __restrict__ dq, int nsplit,
+                                                              float* __restrict__ part) {
   constexpr int BM = 128, BN = 64, NKK = D / 16, NDT = D / 32;
   constexpr int TB = BN * D * 2;
   __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];  // K0 K1 V0 V1
   lds_t* smem = (lds_t*)smem_raw;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, h = lane >> 5;
   const int BH = p.B * p.H, nqt = (p.Sq + BM - 1) / BM, id = blockIdx.x;
-  const int qt = p.causal ? nqt - 1 - id / BH : id / BH;
+  // heaviest query tiles first; each tile's key range may be cut into nsplit workgroups
+  // (short causal grids, see st_flash_bwd)
+  const int rank = id / (BH * nsplit), sp = (id / BH) % nsplit;
+  const int qt = p.causal ? nqt - 1 - rank : rank;
   const int bh = id % BH, b = bh / p.H, hq = bh % p.H, hk = hq / (p.H / p.Hkv);
   const int q0 = qt * BM, my_q = q0 + wid * 32 + r;
 
@@ -731,6 +735,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
 
   int nkb, kb_mask;
   key_blocks<BM, BN>(p, q0, false, nkb, kb_mask);
+  const int kb0 = (int)((int64_t)nkb * sp / nsplit), kb1 = (int)((int64_t)nkb * (sp + 1) / nsplit);
 
   LdsAddr<D> la;
   la.init(lane);
@@ -742,15 +747,15 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) dqacc[dt] = zero16();
 
-  if (nkb > 0) {
-    sk.load(rk, smem, 0);
-    sv.load(rv, smem + 2 * TB, 0);
+  if (kb0 < kb1) {
+    sk.load(rk, smem, kb0 * BN);
+    sv.load(rv, smem + 2 * TB, kb0 * BN);
   }
   dma_barrier();
 
   auto step = [&](auto bufc, int kb) {
     constexpr int BUF = decltype(bufc)::value;
-    const bool more = kb + 1 < nkb;
+    const bool more = kb + 1 < kb1;
     if (more) {
       sk.load(rk, smem + (BUF ^ 1) * TB, (kb + 1) * BN);
       sv.load(rv, smem + (2 + (BUF ^ 1)) * TB, (kb + 1) * BN);
@@ -814,14 +819,28 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
   // pairs of steps with no branch between them: a conditional second step
   // merges two copies of the AGPR accumulators, and hipcc resolved that merge by
   // parking dQ in VGPRs (64 v_accvgpr copies a pair + spills of Q/dO fragments)
-  int kb = 0;
-  for (; kb + 1 < nkb; kb += 2) {
+  int kb = kb0;
+  for (; kb + 1 < kb1; kb += 2) {
     step(Buf<0>(), kb);
     step(Buf<1>(), kb + 1);
   }
-  if (kb < nkb) step(Buf<0>(), kb);
+  if (kb < kb1) step(Buf<0>(), kb);
 
   agpr_fence(dqacc);
+  if (nsplit > 1) {
+    // fp32 partial [split][B*H][Sq][D], summed in split order by dq_split_reduce_kernel
+    if (my_q < p.Sq) {
+      float* pq = part + ((int64_t)sp * BH + bh) * p.Sq * D + (int64_t)my_q * D;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<float4*>(pq + 32 * dt + 8 * g + 4 * h) =
+              make_float4(dqacc[dt][4 * g] * p.scale, dqacc[dt][4 * g + 1] * p.scale,
+                          dqacc[dt][4 * g + 2] * p.scale, dqacc[dt][4 * g + 3] * p.scale);
+    }
+    return;
+  }
   if (my_q < p.Sq) {
     bf16_t* row = dq +(int64_t)b * p.sxb + (int64_t)my_q * p.sxs + (int64_t)hq * p.sxh;
 #pragma unroll
@@ -1113,6 +1132,30 @@ __global__ __launch_bounds__(256) void dkdv_split_reduce_kernel(const float* __r
   st8(dv + off, pack8(av));
 }
 
+// dQ = sum over the key-range splits of the fp32 partials [split][B*H][Sq][D] (fixed split
+// order), written as bf16 through the output strides.  One thread per 8 elements.
+__global__ __launch_bounds__(256) void dq_split_reduce_kernel(const float* __restrict__ part, int nsplit, int H,
+                                                              int Sq, int D, int64_t total8, bf16_t* __restrict__ dq,
+                                                              int64_t sxb, int64_t sxs, int64_t sxh) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total8) return;
+  const int D8 = D / 8;
+  const int c = (int)(t % D8);
+  const int64_t row = t / D8;  // (b * H + hq) * Sq + q
+  const int q = (int)(row % Sq);
+  const int64_t bh = row / Sq;
+  const int hq = (int)(bh % H), b = (int)(bh / H);
+  const int64_t blk = total8 * 8;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < nsplit; ++s) {
+    const float* pq = part + (int64_t)s * blk + row * D + c * 8;
+    const float4 v0 = ld4f(pq), v1 = ld4f(pq + 4);
+    a[0] += v0.x; a[1] += v0.y; a[2] += v0.z; a[3] += v0.w;
+    a[4] += v1.x; a[5] += v1.y; a[6] += v1.z; a[7] += v1.w;
+  }
+  st8(dq + (int64_t)b * sxb + (int64_t)q * sxs + (int64_t)hq * sxh + c * 8, pack8(a));
+}
+
 // ============================================================== ring-attention merge
 __global__ __launch_bounds__(256) void lse_merge_kernel(float* __restrict__ out, float* __restrict__ lse,
                                                         const bf16_t* __restrict__ bout,
@@ -1249,9 +1292,25 @@ static int dkdv_nsplit(int B, int Sk, int Hkv, int causal) {
   return (int)(want > 8 ? 8 : want);
 }
 
-int64_t st_flash_bwd_part_elems(int B, int Sk, int Hkv, int D, int causal) {
-  const int n = dkdv_nsplit(B, Sk, Hkv, causal);
-  return n > 1 ? (int64_t)n * 2 * B * Hkv * Sk * D : 0;
+// The same key-range split exists for the dQ kernel (one workgroup per 128-query tile of
+// each (batch, head); under a causal mask tile i walks i + 1 key tiles) but stays OFF by
+// default: on the one short grid it could serve (Qwen3-1.7B 1 x 2048, 256 workgroups) it
+// measured 0.144 -> 0.155 ms slower (tools/bench_flash_split.py) -- each split re-loads the
+// tile's Q / dO fragments and writes a 128 KiB fp32 partial.  ST_FLASH_DQ_SPLIT=N forces N.
+static int dq_nsplit(int B, int Sq, int H, int causal) {
+  (void)B, (void)Sq, (void)H, (void)causal;
+  const char* e = std::getenv("ST_FLASH_DQ_SPLIT");
+  if (e) {
+    const int v = std::atoi(e);
+    if (v >= 1 && v <= 8) return v;
+  }
+  return 1;
+}
+
+// fp32 partial elements of the dK/dV and dQ splits (one buffer: dK/dV part first)
+int64_t st_flash_bwd_part_elems(int B, int Sq, int Sk, int H, int Hkv, int D, int causal) {
+  const int n = dkdv_nsplit(B, Sk, Hkv, causal), m = dq_nsplit(B, Sq, H, causal);
+  return (n > 1 ? (int64_t)n * 2 * B * Hkv * Sk * D : 0) + (m > 1 ? (int64_t)m * B * H * Sq * D : 0);
 }
 
 // dq / dk / dv: bf16 outputs with arbitrary (b, s, h) strides (D contiguous) so
@@ -1272,27 +1331,35 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
   AttnParams pq = p, pk = p;
   pq.sxb = sdqb; pq.sxs = sdqs; pq.sxh = sdqh;
   pk.sxb = sdkb; pk.sxs = sdks; pk.sxh = sdkh;
-  const unsigned gq = (unsigned)(((Sq + 127) / 128) * B * H);
   const int nsplit = part ? dkdv_nsplit(B, Sk, Hkv, causal) : 1;
+  const int qsplit = part ? dq_nsplit(B, Sq, H, causal) : 1;
+  const unsigned gq = (unsigned)(((Sq + 127) / 128) * B * H * qsplit);
+  float* qpart = part ? part + (nsplit > 1 ? (int64_t)nsplit * 2 * B * Hkv * Sk * D : 0) : nullptr;
   const unsigned gk = (unsigned)(((Sk + 127) / 128) * B * Hkv * nsplit);
   const bf16_t* dop = (const bf16_t*)dout;
   if (D == 128) {
     const char* pe = std::getenv("ST_FLASH_PROBE");  // diagnostics only (tools/probe_flash.py)
     if (pe && std::atoi(pe) == 1) {
-      flash_bwd_dq_kernel<128, 1><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq);
+      flash_bwd_dq_kernel<128, 1><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq, qsplit, qpart);
       flash_bwd_dkdv_kernel<128, 1><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
                                                    (bf16_t*)dv, nsplit, part);
     } else {
-      flash_bwd_dq_kernel<128><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq);
+      flash_bwd_dq_kernel<128><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq, qsplit, qpart);
       flash_bwd_dkdv_kernel<128><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
                                                    (bf16_t*)dv, nsplit, part);
     }
   } else if (D == 64) {
-    flash_bwd_dq_kernel<64><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq);
+    flash_bwd_dq_kernel<64><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq, qsplit, qpart);
     flash_bwd_dkdv_kernel<64><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
                                                   (bf16_t*)dv, nsplit, part);
   } else {
     return -3;
+  }
+  if (qsplit > 1) {
+    ST_HIP_CHECK(hipGetLastError());
+    const int64_t total8 = (int64_t)B * H * Sq * (D / 8);
+    dq_split_reduce_kernel<<<(unsigned)((total8 + 255) / 256), 256, 0, st>>>(qpart, qsplit, H, Sq, D, total8,
+                                                                             (bf16_t*)dq, sdqb, sdqs, sdqh);
   }
   if (nsplit > 1) {
     ST_HIP_CHECK(hipGetLastError());

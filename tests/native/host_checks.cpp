@@ -14,7 +14,7 @@ extern "C" {
 int64_t st_wgrad_ws_elems(int M, int N, int T, int variant);
 int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int M, int N,
                   int T, int beta, int variant, float* ws, hipStream_t st);
-int64_t st_flash_bwd_part_elems(int B, int Sk, int Hkv, int D, int causal);
+int64_t st_flash_bwd_part_elems(int B, int Sq, int Sk, int H, int Hkv, int D, int causal);
 int st_rmsnorm_bwd_nwaves(int rows);
 int st_rmsnorm_fwd(const void* x, const void* res, const void* w, void* y, void* sum_out, float* rstd, int rows,
                    int h, float eps, hipStream_t st);
@@ -52,9 +52,9 @@ int main() {
     for (int Sk : {1, 127, 128, 2048, 4096, 32768, 131072})
       for (int Hkv : {1, 2, 8, 32})
         for (int D : {64, 128}) {
-          const int64_t e = st_flash_bwd_part_elems(B, Sk, Hkv, D, (B + Sk) & 1);
+          const int64_t e = st_flash_bwd_part_elems(B, Sk, Sk, 4 * Hkv, Hkv, D, (B + Sk) & 1);
           CHECK(e >= 0);
-          CHECK(e <= (int64_t)8 * 2 * B * Hkv * Sk * D);
+          CHECK(e <= (int64_t)8 * 2 * B * Hkv * Sk * D + (int64_t)8 * B * 4 * Hkv * Sk * D);
           total += e;
         }
   for (int rows : {0, 1, 3, 4, 5, 1000, 24576, 1 << 20}) {

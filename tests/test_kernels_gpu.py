@@ -185,10 +185,12 @@ def test_flash_fwd_bwd(B, Sq, Sk, H, Hkv, D, causal):
 
 
 @pytest.mark.parametrize("split", ["1", "3"])
+@pytest.mark.parametrize("kernel", ["DKDV", "DQ"])
 @pytest.mark.parametrize("B,Sq,Sk,H,Hkv,D,causal", [FLASH_CASES[1], FLASH_CASES[2], FLASH_CASES[6], FLASH_CASES[8]])
-def test_flash_dkdv_split_forced(B, Sq, Sk, H, Hkv, D, causal, split, monkeypatch):
-    """The dK/dV kernel unsplit (the long-grid path) and cut into 3 query ranges."""
-    monkeypatch.setenv("ST_FLASH_DKDV_SPLIT", split)
+def test_flash_bwd_split_forced(B, Sq, Sk, H, Hkv, D, causal, kernel, split, monkeypatch):
+    """The dK/dV (query ranges) and dQ (key ranges) kernels unsplit -- the long-grid path --
+    and cut into 3 ranges whose fp32 partials are reduced in order."""
+    monkeypatch.setenv(f"ST_FLASH_{kernel}_SPLIT", split)
     _flash_case(B, Sq, Sk, H, Hkv, D, causal, 1.0)
 
 

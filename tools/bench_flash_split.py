@@ -1,9 +1,9 @@
-"""Flash-attention backward with the dK/dV query-range split off / auto on short grids
+"""Flash-attention backward with the dK/dV query-range and dQ key-range splits off / auto on short grids
 (the single-device Qwen3 rows of BASELINE.md) and on the Llama-3-8B bench shape.
 
     python tools/bench_flash_split.py
 
-One JSON line per shape: backward ms with ST_FLASH_DKDV_SPLIT=1 (off) and unset (auto).
+One JSON line per shape: backward ms with ST_FLASH_{DKDV,DQ}_SPLIT=1 (off) and unset (auto).
 """
 from __future__ import annotations
 
@@ -40,10 +40,11 @@ def main():
         grads = {}
         for _ in range(3):
             for arm in ("off", "auto"):
-                if arm == "off":
-                    os.environ["ST_FLASH_DKDV_SPLIT"] = "1"
-                else:
-                    os.environ.pop("ST_FLASH_DKDV_SPLIT", None)
+                for knob in ("ST_FLASH_DKDV_SPLIT", "ST_FLASH_DQ_SPLIT"):
+                    if arm == "off":
+                        os.environ[knob] = "1"
+                    else:
+                        os.environ.pop(knob, None)
                 grads[arm] = torch.autograd.grad(o, (q, k, v), g, retain_graph=True)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 torch.cuda.synchronize()
@@ -55,7 +56,8 @@ def main():
                 ms = s.elapsed_time(e) / 10
                 res[f"bwd_ms_{arm}"] = round(min(res.get(f"bwd_ms_{arm}", 1e9), ms), 4)
         os.environ.pop("ST_FLASH_DKDV_SPLIT", None)
-        # the split changes only the fp32 summation order of dK / dV
+        os.environ.pop("ST_FLASH_DQ_SPLIT", None)
+        # the splits change only the fp32 summation order of dQ / dK / dV
         res["max_abs_diff_dk"] = float((grads["off"][1].float() - grads["auto"][1].float()).abs().max())
         print(json.dumps(res), flush=True)
 
