@@ -21,8 +21,8 @@ design and fixes:
 * Bucket size defaults to 64 Mi elements (``--bucket_size_mb 256`` of fp32): on 8x
   MI355X (7 xGMI links/GPU, ring per-link bound) large messages amortise RCCL launch
   latency; a bucket closes at the first parameter that takes it past the size, so a
-  Llama-3-8B step issues ~66 buckets (~2 per decoder layer: gate_up alone, down + o +
-  qkv), the first right after the LM head's backward.  128 / 512 MiB measured equal on
+  Llama-3-8B step issues ~66 buckets (~2 per decoder layer of 218 M parameters),
+  the first right after the LM head's backward.  128 / 512 MiB measured equal on
   one GPU (profiles/r02/bucket_size_mbs6_ab.log).
 * Reduction dtype: fp32 (exact) or bf16 (half the xGMI bytes; the arena keeps
   accumulating in fp32 and only the cross-rank sum is bf16).
