@@ -17,6 +17,7 @@ mbs 4 + logits/CE 700.8 ms = 23.38k tok/s, mbs 6 + fused head 1025-1033 ms =
 
 Usage:
   python bench.py --gpus 1 --steps 10 --warmup 3
+  python bench.py --gpus 8 --steps 10 --warmup 3      # starts 8 ranks itself (torchrun child process)
   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8 --steps 10 --warmup 3
   torchrun --nproc-per-node 8 ... bench.py --gpus 8 --layout tp2pp2dp2   # BASELINE.json 8-GPU configs:
       dp (default) | tp2pp2dp2 | cp8_32k | mixtral_ep8  (explicit flags override a preset)
@@ -61,9 +62,45 @@ LAYOUTS = {
 }
 
 
+def _visible_gpus() -> int:
+    """Devices this process may use.  ``torch.cuda.device_count()`` counts the HIP
+    devices without creating a context on them (no GPU initialisation), so the
+    parent stays GPU-free and may start the ranks as children."""
+    import torch
+
+    return torch.cuda.device_count()
+
+
+def _self_launch(n: int, argv: list[str], backend: str) -> int:
+    """``python bench.py --gpus N`` without a launcher: start N ranks as one torchrun
+    CHILD process (never exec: the parent must not replace itself) on 127.0.0.1,
+    let rank 0's JSON line through and return the child's exit code.
+    Mirrors the reference driver building its own torchrun command per config
+    (scripts/benchmark_comprehensive.py:177-215)."""
+    import socket
+    import subprocess
+
+    if backend != "gloo":
+        have = _visible_gpus()
+        if n > have:
+            print(f"bench: --gpus {n} but only {have} GPU(s) visible; refusing to start", file=sys.stderr)
+            return 2
+    with socket.socket() as s:  # a free rendezvous port
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + argv
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", ST_BENCH_SELF_LAUNCHED="1")
+    print(f"[bench] --gpus {n} with no WORLD_SIZE: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr,
+          flush=True)
+    return subprocess.call(cmd, env=env)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU).  Without torchrun (no WORLD_SIZE) and N > 1, bench.py starts "
+                         "the N ranks itself; under torchrun it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--layout", default="dp", choices=sorted(LAYOUTS))
@@ -91,7 +128,17 @@ def main() -> int:
     ap.add_argument("--head_chunk", type=int, default=4096, help="tokens per fused LM-head chunk")
     ap.add_argument("--layers", type=int, default=None, help="(debug only; result marked invalid)")
     args = ap.parse_args()
+    launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is None:
+        args.gpus = world
+    if not launched and args.gpus > 1:
+        return _self_launch(args.gpus, sys.argv[1:], args.backend)
+    if args.gpus < 1:
+        raise SystemExit(f"--gpus must be >= 1 (got {args.gpus})")
+    if world != args.gpus:
+        # a mismatch would report a different job size than the one asked for
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     preset = dict(model="llama3-8b", micro_batch_size=6, seq_len=4096, grad_acc=1, tp=1, pp=1, cp=1, ep=1, sp=False,
                   vpp=1)
     preset.update({k: (world if v == -1 else v) for k, v in LAYOUTS[args.layout].items()})
@@ -107,13 +154,20 @@ def main() -> int:
     from scaletorch_amd.utils.device import get_theoretical_flops
     from scaletorch_amd.utils.misc import flops_per_token
 
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     mp = args.tp * args.pp * args.cp * args.ep
     if world % mp:
         raise SystemExit(f"world {world} not divisible by tp*pp*cp*ep={mp}")
     dp = world // mp
-    ga = args.grad_acc if args.pp == 1 else max(args.grad_acc, 4 * args.pp)
+    ga = args.grad_acc
+    if args.pp > 1:
+        # the (interleaved) 1F1B schedule needs >= pp micro-batches in flight -- a multiple of
+        # pp with virtual stages; fewer is an error, never silently raised
+        if ga < args.pp or (args.vpp > 1 and ga % args.pp):
+            raise SystemExit(f"--grad_acc {ga} with pp={args.pp} vpp={args.vpp}: need a multiple of pp "
+                             f"(>= {args.pp}); >= {4 * args.pp} keeps the bubble under ~20 %")
+        if ga < 4 * args.pp and int(os.environ.get("RANK", "0")) == 0:
+            print(f"[bench] note: grad_acc {ga} < 4*pp: pipeline bubble (pp-1)/(vpp*M+pp-1) = "
+                  f"{(args.pp - 1) / (args.vpp * ga + args.pp - 1):.0%}", file=sys.stderr)
     from scaletorch_amd.models import get_model_config
     from scaletorch_amd.utils.memory import estimate_rank_memory
 
@@ -149,6 +203,13 @@ def main() -> int:
     tr = Trainer(a)
     rank = tr.rank
     dev = tr.device
+    # ranks that really take part in the backend's collectives: an 8-byte all-reduce of ones
+    ranks_seen = torch.ones(1, dtype=torch.float64, device=dev)
+    if dist.is_initialized():
+        dist.all_reduce(ranks_seen)
+    ranks_seen = int(ranks_seen.item())
+    if ranks_seen != world:
+        raise SystemExit(f"all-reduce saw {ranks_seen} ranks, WORLD_SIZE={world}")
 
     def sync():
         if dist.is_initialized():
@@ -223,6 +284,11 @@ def main() -> int:
         "valid": valid,
         "max_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1) if dev.type == "cuda" else 0.0,
         "comm_mb_per_step_rank0": comm,  # bytes handed to each collective per step on rank 0 (dist/trace.py)
+        "dist_world_size": dist.get_world_size() if dist.is_initialized() else 1,
+        "backend": (("rccl" if a.backend == "nccl" else a.backend) if dist.is_initialized() else "none"),
+        "collective_ranks_seen": ranks_seen,
+        "launcher": "bench.py self-launch" if os.environ.get("ST_BENCH_SELF_LAUNCHED") else
+                    ("torchrun" if launched else "single process"),
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

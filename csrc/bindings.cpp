@@ -79,7 +79,8 @@ int st_qknorm_rope_bwd(void* dqkv, const void* xsave, const float* rstd, const v
                        int D, int64_t max_pos, float* partial, float* dw_out, hipStream_t st);
 int st_transpose_bf16(const void* src, void* dst, int R, int C, int64_t lds_src, int64_t lds_dst, hipStream_t st);
 int st_embedding_bwd(const int64_t* sorted_ids, const int64_t* order, const void* dy, int64_t ldd, float* grad,
-                     int64_t ldg, int T, int H, int64_t V, hipStream_t st);
+                     int64_t ldg, float* partial, int T, int H, int64_t V, hipStream_t st);
+int64_t st_embedding_bwd_partial_floats(int T, int H);
 int st_lse_merge(float* out, float* lse, const void* bout, const float* blse, int B, int S, int H,
                  int D, int64_t sbb, int64_t sbs, int64_t sbh, hipStream_t st);
 }
@@ -282,9 +283,12 @@ void embedding_bwd_(at::Tensor grad, const at::Tensor& dy, const at::Tensor& sor
   TORCH_CHECK(dy.size(1) % 4 == 0 && dy.stride(0) % 4 == 0 && grad.stride(0) % 4 == 0, "embedding_bwd_: H % 4");
   TORCH_CHECK(dy.size(0) < (1LL << 31) && dy.size(1) < (1LL << 31), "embedding_bwd_: dims");
   c10::hip::HIPGuardMasqueradingAsCUDA gd(dy.device());
+  // per-block partial sums of long runs (split across workgroups, reduced in block order)
+  at::Tensor partial = at::empty({st_embedding_bwd_partial_floats((int)dy.size(0), (int)dy.size(1))},
+                                 dy.options().dtype(at::kFloat));
   int rc = st_embedding_bwd(sorted_ids.data_ptr<int64_t>(), order.data_ptr<int64_t>(), dy.data_ptr(), dy.stride(0),
-                            grad.data_ptr<float>(), grad.stride(0), (int)dy.size(0), (int)dy.size(1), grad.size(0),
-                            cur_stream());
+                            grad.data_ptr<float>(), grad.stride(0), partial.data_ptr<float>(), (int)dy.size(0),
+                            (int)dy.size(1), grad.size(0), cur_stream());
   ST_CHECK_RC(rc, "embedding_bwd_");
 }
 

@@ -291,6 +291,80 @@ def collect_results(part: list, size: int, mode: str = "device", tmpdir: str | N
     return out[:size]
 
 
+def collect_results_cpu(result_part: list, size: int, tmpdir: str | None = None) -> list | None:
+    """Reference name (scaletorch/dist/gather_utils.py:74): collection through a shared directory."""
+    return collect_results(result_part, size, mode="cpu", tmpdir=tmpdir)
+
+
+def collect_results_gpu(result_part: list, size: int) -> list | None:
+    """Reference name (scaletorch/dist/gather_utils.py:181): collection over the communicator."""
+    return collect_results(result_part, size, mode="device")
+
+
+def _coalesced_buckets(tensors: list[torch.Tensor], bucket_size_mb: int) -> list[list[torch.Tensor]]:
+    """Group by (dtype, device) -- a flat buffer has one of each -- then cut each group
+    into buckets of at most ``bucket_size_mb`` (<= 0: one bucket per group).  A tensor
+    larger than the limit gets a bucket of its own."""
+    groups: dict = {}
+    for t in tensors:
+        groups.setdefault((t.dtype, t.device), []).append(t)
+    limit = bucket_size_mb * 1024 * 1024 if bucket_size_mb > 0 else None
+    out = []
+    for group in groups.values():
+        cur, cur_bytes = [], 0
+        for t in group:
+            nb = t.numel() * t.element_size()
+            if limit is not None and cur and cur_bytes + nb > limit:
+                out.append(cur)
+                cur, cur_bytes = [], 0
+            cur.append(t)
+            cur_bytes += nb
+        if cur:
+            out.append(cur)
+    return out
+
+
+def _all_reduce_coalesced(tensors: list[torch.Tensor], bucket_size_mb: int = -1, op: str = "sum",
+                          group=None) -> None:
+    """All-reduce a list of tensors in place with one collective per flat bucket
+    (reference: scaletorch/dist/collective_ops.py:868-907).  Each bucket is packed into
+    one contiguous buffer, so RCCL sees a few large messages instead of many small
+    ones -- on xGMI the per-call latency, not the bytes, dominates small tensors."""
+    if not isinstance(tensors, list):
+        raise TypeError(f"tensors must be a list, got {type(tensors)}")
+    for i, t in enumerate(tensors):
+        if not isinstance(t, torch.Tensor):
+            raise TypeError(f"item {i} is not a tensor: {type(t)}")
+    if get_world_size(group) == 1:
+        return
+    for bucket in _coalesced_buckets(tensors, bucket_size_mb):
+        flat = torch.cat([t.reshape(-1) for t in bucket])
+        all_reduce(flat, op=op, group=group)
+        off = 0
+        for t in bucket:
+            n = t.numel()
+            t.copy_(flat[off: off + n].view_as(t))
+            off += n
+
+
+def all_reduce_params(params, coalesce: bool = True, bucket_size_mb: int = -1, op: str = "sum",
+                      group=None) -> None:
+    """All-reduce parameters or buffers in place (reference: collective_ops.py:910-960),
+    coalesced into flat buckets by default."""
+    import types
+
+    if not isinstance(params, (list, types.GeneratorType)):
+        raise TypeError(f"params must be a list or generator, got {type(params)}")
+    if get_world_size(group) == 1:
+        return
+    data = [p.data if isinstance(p, torch.nn.Parameter) else p for p in params]
+    if coalesce:
+        _all_reduce_coalesced(data, bucket_size_mb, op=op, group=group)
+    else:
+        for t in data:
+            all_reduce(t, op=op, group=group)
+
+
 def all_reduce_dict(data: dict[str, torch.Tensor], op: str = "sum", group=None) -> dict[str, torch.Tensor]:
     """All-reduce a dict of tensors with ONE flat collective (reference: collective_ops.py:800-865)."""
     if get_world_size(group) == 1 or not data:

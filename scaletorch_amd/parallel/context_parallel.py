@@ -77,8 +77,12 @@ class _CPAttnFn(torch.autograd.Function):
     and the two partial results are combined by the LSE-merge kernel.  Backward:
     one flash backward per chunk over its visible prefix, writing dQ and dK/dV
     straight into their output buffers (the widest prefix first, the next one
-    added in place: the same single bf16 rounding per partial as an fp32
-    accumulator, without a full-S fp32 buffer), then ONE reduce-scatter."""
+    added in place), then ONE reduce-scatter.  Rounding: each chunk's partial is
+    rounded to bf16 once by the kernel, and the in-place bf16 add evaluates the
+    sum in fp32 and rounds once -- for the two zig-zag chunks that is bitwise the
+    result of summing the two bf16 partials in an fp32 accumulator and casting
+    once (tests/test_units.py::test_cp_dkv_inplace_add_equals_fp32_accumulation),
+    without a full-S fp32 buffer."""
 
     @staticmethod
     def forward(ctx, q, kv, H, Hkv, D, scale, zigzag):

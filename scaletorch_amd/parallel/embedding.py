@@ -5,7 +5,12 @@ tensor_parallel.py:479-507, whose backward sums with atomics).
 
 On GPU the scatter is deterministic (csrc/embedding.hip): token ids are sorted
 stably on device and one workgroup per distinct id sums its rows in token order,
-so the step is bitwise reproducible run to run.  CPU: ``index_add_`` (sequential)."""
+so the step is bitwise reproducible run to run; runs longer than 64 tokens (pad/EOS
+ids) are split over several workgroups and their pieces reduced in a fixed order.
+``grad_ids`` (optional) are the ids the backward scatters to: -1 marks a token
+whose row gets no gradient (TP: an id owned by another vocab shard), so the
+masked tokens never form one giant run of a placeholder id.
+CPU: ``index_add_`` (sequential)."""
 from __future__ import annotations
 
 import torch
@@ -16,8 +21,8 @@ from ..ops.grad import _grad_ready, take_fresh
 
 class _EmbeddingFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ids, weight):
-        ctx.save_for_backward(ids)
+    def forward(ctx, ids, weight, grad_ids):
+        ctx.save_for_backward(ids if grad_ids is None else grad_ids)
         ctx.weight = weight
         return F.embedding(ids, weight)
 
@@ -38,12 +43,13 @@ class _EmbeddingFn(torch.autograd.Function):
             _lib.ops().embedding_bwd_(mg.view(mg.shape[0], -1), rows.contiguous(), sorted_ids.contiguous(),
                                       order.contiguous())
         else:
-            mg.index_add_(0, flat, rows.to(mg.dtype))
+            keep = flat >= 0
+            mg.index_add_(0, flat[keep], rows[keep].to(mg.dtype))
         _grad_ready(w)
-        return None, None
+        return None, None, None
 
 
-def embedding(ids: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+def embedding(ids: torch.Tensor, weight: torch.Tensor, grad_ids: torch.Tensor | None = None) -> torch.Tensor:
     if getattr(weight, "main_grad", None) is not None and torch.is_grad_enabled():
-        return _EmbeddingFn.apply(ids, weight)
+        return _EmbeddingFn.apply(ids, weight, grad_ids)
     return F.embedding(ids, weight)

@@ -617,7 +617,9 @@ class VocabParallelEmbedding(nn.Module):
             return embedding(ids, self.weight)
         local = ids - self.vocab_start
         mask = (local < 0) | (local >= self.per_rank)
-        out = embedding(local.masked_fill(mask, 0), self.weight)
+        # forward reads row 0 for out-of-shard ids (zeroed below); the backward scatters
+        # only in-shard ids (-1 = skip), so 1-1/tp of the tokens do not pile onto row 0
+        out = embedding(local.masked_fill(mask, 0), self.weight, local.masked_fill(mask, -1))
         out = out.masked_fill(mask[..., None], 0.0)
         if self.sequence_parallel:
             return ReduceScatterToSequenceParallelRegion.apply(out, self.group)

@@ -292,8 +292,8 @@ class Trainer:
         try:
             self.step, self.trained_tokens = ckpt_manager.load_checkpoint(self.model, self.optimizer, path,
                                                                           self.lr_scheduler)
-        except (FileNotFoundError, KeyError, ValueError, RuntimeError) as e:
-            ok, err = 0, e
+        except Exception as e:  # noqa: BLE001 -- any local failure (corrupt/truncated file, unpickling,
+            ok, err = 0, e      # permissions) must reach the collective below, or the peers hang in it
         flag = torch.tensor([ok], dtype=torch.int32, device=self.device if C.get_world_size() > 1 else "cpu")
         if C.get_world_size() > 1:
             C.all_reduce(flag, op="min")

@@ -68,6 +68,13 @@ def is_complete(step_dir: str) -> bool:
     optimizer shards); a directory from a crash mid-save lacks some markers."""
     marks = glob.glob(os.path.join(step_dir, "complete_rank_world_size=*"))
     if not marks:
+        # written before completion markers existed: treat as complete (legacy layout),
+        # visibly, instead of silently restarting from step 0 next to it
+        if os.environ.get("ST_CKPT_ACCEPT_UNMARKED", "1") == "1":
+            logger.warning("checkpoint %s has no completion markers (legacy layout); treating it as complete "
+                           "(ST_CKPT_ACCEPT_UNMARKED=0 skips such directories)", step_dir)
+            return True
+        logger.warning("skipping checkpoint %s: no completion markers", step_dir)
         return False
     worlds = {m.rsplit("_", 1)[-1] for m in marks}
     if len(worlds) != 1:

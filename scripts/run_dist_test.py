@@ -35,7 +35,7 @@ def _dev(backend: str) -> torch.device:
     return torch.device("cpu")
 
 
-def tests(dev: torch.device):
+def collective_cases(dev: torch.device):
     r, w = D.get_rank(), D.get_world_size()
 
     def t_all_reduce_sum():
@@ -135,6 +135,31 @@ def tests(dev: torch.device):
         if r == 0:
             assert sorted(res) == sorted(j * 10 + i for j in range(w) for i in range(2)), res
 
+    def t_all_reduce_params_coalesced():
+        # mixed dtypes + a 1-MB bucket limit: several flat buckets, each one collective
+        ps = [torch.nn.Parameter(torch.full((300, 1000), float(r + 1), device=dev)),
+              torch.full((5,), r, dtype=torch.int64, device=dev),
+              torch.full((7, 3), float(2 * r), device=dev)]
+        D.all_reduce_params(ps, bucket_size_mb=1)
+        assert torch.all(ps[0].data == w * (w + 1) / 2)
+        assert torch.all(ps[1] == w * (w - 1) // 2) and torch.all(ps[2] == w * (w - 1))
+        qs = [torch.full((4,), float(r), device=dev) for _ in range(3)]
+        D.all_reduce_params((q for q in qs), coalesce=False, op="max")
+        assert all(torch.all(q == w - 1) for q in qs)
+        xs = [torch.full((3,), float(r), device=dev), torch.ones(2, 2, device=dev)]
+        D._all_reduce_coalesced(xs, op="mean")
+        assert torch.allclose(xs[0], torch.full((3,), (w - 1) / 2, device=dev)) and torch.all(xs[1] == 1)
+
+    def t_collect_results_names():
+        part = [r * 10 + i for i in range(2)]
+        res = D.collect_results_gpu(part, 2 * w)
+        if r == 0:
+            assert res == [j * 10 + i for i in range(2) for j in range(w)], res
+        tmp = D.all_gather_object(tempfile.mkdtemp() if r == 0 else None)[0]
+        res = D.collect_results_cpu(part, 2 * w - 1, tmpdir=tmp)
+        if r == 0:
+            assert res == [j * 10 + i for i in range(2) for j in range(w)][: 2 * w - 1], res
+
     def t_barrier_and_groups():
         D.barrier()
         g = D.new_group(list(range(w)))
@@ -146,7 +171,8 @@ def tests(dev: torch.device):
     return [(f.__name__[2:], f) for f in (
         t_all_reduce_sum, t_all_reduce_mean_max_min, t_all_reduce_async, t_broadcast, t_all_gather,
         t_reduce_scatter, t_reduce, t_scatter, t_gather, t_all_to_all, t_p2p_ring, t_object_collectives,
-        t_all_reduce_dict, t_sync_random_seed_and_collect, t_barrier_and_groups)]
+        t_all_reduce_dict, t_sync_random_seed_and_collect, t_all_reduce_params_coalesced, t_collect_results_names,
+        t_barrier_and_groups)]
 
 
 def main() -> int:
@@ -156,7 +182,7 @@ def main() -> int:
     rank, _, world = D.init_dist(backend=args.backend, use_cpu=args.backend == "gloo")
     dev = _dev(args.backend)
     failed = []
-    for name, fn in tests(dev):
+    for name, fn in collective_cases(dev):
         try:
             fn()
             ok = True
@@ -171,7 +197,7 @@ def main() -> int:
             for n, tb in failed:
                 print(f"--- {n}\n{tb}")
         else:
-            print(f"ALL {len(tests(dev))} PASSED")
+            print(f"ALL {len(collective_cases(dev))} PASSED")
     all_failed = D.all_gather_object(len(failed))
     D.cleanup_dist()
     return 1 if any(all_failed) else 0

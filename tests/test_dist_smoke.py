@@ -24,4 +24,4 @@ def test_run_dist_test_gloo(world):
     env = dict(os.environ, OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
-    assert "ALL 15 PASSED" in r.stdout, r.stdout[-4000:]
+    assert "ALL 17 PASSED" in r.stdout, r.stdout[-4000:]

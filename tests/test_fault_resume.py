@@ -60,3 +60,51 @@ def test_incomplete_checkpoint_is_skipped(tmp_path):
         for r in ranks:
             (d / f"complete_rank_world_size={r}_2").write_text("ok\n")
     assert latest_checkpoint(str(tmp_path)).endswith("/2")
+
+
+def test_unmarked_legacy_checkpoint_is_accepted_visibly(tmp_path, monkeypatch):
+    """A step directory written before completion markers existed is resumed from
+    (with a warning) instead of silently restarting at step 0; ST_CKPT_ACCEPT_UNMARKED=0
+    restores the strict behaviour."""
+    from scaletorch_amd.utils.checkpoint import latest_checkpoint
+
+    d = tmp_path / "3"
+    d.mkdir()
+    (d / "weights_tp_rank_world_size=0_1_pp_rank_world_size=0_1.pth").write_bytes(b"x")
+    assert latest_checkpoint(str(tmp_path)).endswith("/3")
+    monkeypatch.setenv("ST_CKPT_ACCEPT_UNMARKED", "0")
+    assert latest_checkpoint(str(tmp_path)) is None
+
+
+def _resume_corrupt_worker(rank, world, work_dir):
+    import torch
+
+    from scaletorch_amd.trainer.config import ScaleTorchArguments
+    from scaletorch_amd.trainer.engine import Trainer
+    from scaletorch_amd.utils.checkpoint import CheckpointManager
+
+    a = ScaleTorchArguments(model_name_or_path="tiny-llama", synthetic_data=True, use_cpu=True, backend="gloo",
+                            dtype="float32", data_parallel_size=2, micro_batch_size=1, sequence_length=16,
+                            total_train_steps=4, zero_stage=1, num_hidden_layers=1)
+    tr = Trainer(a)
+    tr.train_step()
+    ck = CheckpointManager(work_dir, async_save=False)
+    path = os.path.dirname(ck.save_checkpoint(tr.model, tr.optimizer, 1, 0, lr_scheduler=tr.lr_scheduler))
+    torch.distributed.barrier()
+    if rank == 1:  # truncate this rank's ZeRO-1 optimizer shard: torch.load raises a non-RuntimeError
+        shard = "optimizer_shard_rank_world_size=1_2.pth"
+        with open(os.path.join(path, shard), "r+b") as f:
+            f.truncate(37)
+    torch.distributed.barrier()
+    try:
+        tr.resume(ck, path)
+    except RuntimeError as e:
+        return f"raised: {e}"
+    return "resumed"
+
+
+def test_resume_corrupt_shard_fails_on_every_rank(tmp_path):
+    from tests.dist_harness import run_workers
+
+    out = run_workers(_resume_corrupt_worker, 2, str(tmp_path), timeout=240)
+    assert all(o.startswith("raised") for o in out), out

@@ -555,3 +555,33 @@ def test_embedding_bwd_deterministic():
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
     assert ((outs[0].double() - 0.5) - ref).abs().max().item() < 1e-3
+
+
+@pytest.mark.gpu
+def test_embedding_bwd_long_runs_and_masked_ids():
+    """Long runs split across workgroups (csrc/embedding.hip): two long runs meeting
+    inside one 64-position block, a pad-like run of 20K tokens, and -1 (TP out-of-shard)
+    ids that must be skipped -- exact vs fp64, bitwise identical run to run."""
+    from scaletorch_amd.parallel.embedding import embedding
+
+    torch.manual_seed(5)
+    V, H = 257, 512
+    parts = [torch.full((3000,), -1), torch.full((101,), 3), torch.full((130,), 4), torch.randint(0, V, (777,)),
+             torch.full((20000,), 0), torch.tensor([5]), torch.full((65,), 6)]
+    ids = torch.cat(parts)[torch.randperm(sum(p.numel() for p in parts))].cuda().reshape(1, -1)
+    T = ids.numel()
+    w = torch.nn.Parameter(torch.randn(V, H, device="cuda").bfloat16())
+    dy = torch.randn(1, T, H, device="cuda", dtype=torch.bfloat16)
+    keep = ids.reshape(-1) >= 0
+    ref = torch.zeros(V, H, dtype=torch.float64, device="cuda").index_add_(
+        0, ids.reshape(-1)[keep], dy.reshape(-1, H)[keep].double())
+    outs = []
+    for _ in range(2):
+        w.main_grad = torch.zeros(V, H, device="cuda")
+        w._st_fresh = False
+        embedding(ids.clamp(min=0), w, ids).backward(dy)
+        outs.append(w.main_grad.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    err = (outs[0].double() - ref).abs().max().item()
+    assert err < 5e-3 * max(1.0, ref.abs().max().item() / 100), err

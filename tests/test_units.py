@@ -456,3 +456,21 @@ def test_dp_collectives_are_traced():
     st = run_workers(_dp_trace_worker, 2)[0]
     assert st["dp.reduce_scatter"]["calls"] >= 1 and st["dp.reduce_scatter"]["bytes"] > 0
     assert st["dp.all_gather"]["calls"] >= 1
+
+
+def test_cp_dkv_inplace_add_equals_fp32_accumulation():
+    """The all-gather CP backward adds the second zig-zag chunk's bf16 dK/dV partial in
+    place into the first (context_parallel.py _CPAttnFn.backward).  That must equal the
+    fp32-accumulator form (sum of the two bf16 partials in fp32, one cast), bitwise."""
+    import torch
+
+    g = torch.Generator().manual_seed(0)
+    for scale in (1e-3, 1.0, 3e4):
+        a = (torch.randn(4096, 64, generator=g) * scale).bfloat16()
+        b = (torch.randn(4096, 64, generator=g) * scale * torch.rand(1, generator=g)).bfloat16()
+        acc = torch.zeros(4096, 64)
+        acc += a.float()
+        acc += b.float()
+        inplace = a.clone()
+        inplace += b
+        assert torch.equal(inplace, acc.bfloat16())

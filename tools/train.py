@@ -108,13 +108,16 @@ def main(argv=None) -> int:
         from scaletorch_amd.utils.watchdog import StepWatchdog
 
         watchdog = StepWatchdog(args.watchdog_s).start()
+    epoch_bound = not args.total_train_steps and not args.max_tokens
     stop = {"flag": False}
     signal.signal(signal.SIGTERM, lambda *_: stop.__setitem__("flag", True))
     try:
         while tr.step < total and not stop["flag"]:
             if args.max_tokens and tr.trained_tokens >= args.max_tokens:
                 break
-            if getattr(tr.data, "epoch", 0) >= args.epochs:  # --epochs: data passes
+            # --epochs bounds the run only when neither --total_train_steps nor --max_tokens is
+            # given (reference precedence: trainer/config.py:321-325)
+            if epoch_bound and getattr(tr.data, "epoch", 0) >= args.epochs:
                 log.info("completed %d epochs", args.epochs)
                 break
             if tr.step == fault_step and tr.rank == fault_rank:
