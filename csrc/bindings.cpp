@@ -56,6 +56,8 @@ int64_t st_flash_bwd_part_elems(int B, int Sq, int Sk, int H, int Hkv, int D, in
 int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int M,
                   int N, int T, int beta, int variant, float* ws, hipStream_t st);
 int64_t st_wgrad_ws_elems(int M, int N, int T, int variant);
+int st_wgrad_grouped(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int64_t strideC,
+                     int M, int N, int G, const int* offs, int T_total, int beta, hipStream_t st);
 int st_xgmi_header_bytes();
 int st_xgmi_max_ranks();
 int64_t st_xgmi_create(int rank, int world, int64_t cap, int64_t epoch_base);
@@ -349,6 +351,33 @@ bool wgrad_gemm_(at::Tensor out, const at::Tensor& dy, const at::Tensor& x, int6
                          wse > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
   if (rc == -2) return false;
   ST_CHECK_RC(rc, "wgrad_gemm_");
+  return true;
+}
+
+// out[g] fp32 [G, M, N] (+)= dy[rows of g]^T @ x[rows of g], rows of g = [offs[g-1], offs[g])
+// (int32 inclusive prefix sums on the device).  One launch for every expert; false when
+// the kernel does not tile the shape.
+bool wgrad_grouped_(at::Tensor out, const at::Tensor& dy, const at::Tensor& x, const at::Tensor& offs, int64_t beta) {
+  check_bf16_cuda(dy, "dy");
+  check_bf16_cuda(x, "x");
+  check_same_gpu(x, dy, "x");
+  check_same_gpu(out, dy, "out");
+  check_same_gpu(offs, dy, "offs");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && out.dim() == 3, "wgrad_grouped: dy [T,M], x [T,N], out [G,M,N]");
+  TORCH_CHECK(out.scalar_type() == at::kFloat, "wgrad_grouped: out must be fp32");
+  TORCH_CHECK(offs.scalar_type() == at::kInt && offs.dim() == 1 && offs.is_contiguous() && offs.size(0) == out.size(0),
+              "wgrad_grouped: offs int32 [G]");
+  TORCH_CHECK(dy.size(0) == x.size(0) && out.size(1) == dy.size(1) && out.size(2) == x.size(1),
+              "wgrad_grouped: shapes ", dy.sizes(), " x ", x.sizes(), " -> ", out.sizes());
+  if (dy.stride(1) != 1 || x.stride(1) != 1 || out.stride(2) != 1) return false;
+  const int64_t T = dy.size(0), M = dy.size(1), N = x.size(1), G = out.size(0);
+  if (T > INT32_MAX || M > INT32_MAX || N > INT32_MAX || G > INT32_MAX) return false;
+  c10::hip::HIPGuardMasqueradingAsCUDA g(out.device());
+  int rc = st_wgrad_grouped(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr<float>(),
+                            out.stride(1), out.stride(0), (int)M, (int)N, (int)G, offs.data_ptr<int>(), (int)T,
+                            beta ? 1 : 0, cur_stream());
+  if (rc == -2) return false;
+  ST_CHECK_RC(rc, "wgrad_grouped_");
   return true;
 }
 
@@ -673,6 +702,7 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("flash_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int q_offset, int k_offset) -> Tensor[]");
   m.def("flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, int q_offset, int k_offset, Tensor(a!)? dq_out=None, Tensor(b!)? dk_out=None, Tensor(c!)? dv_out=None) -> Tensor[]");
   m.def("wgrad_gemm_(Tensor(a!) out, Tensor dy, Tensor x, int beta, int variant=0) -> bool");
+  m.def("wgrad_grouped_(Tensor(a!) out, Tensor dy, Tensor x, Tensor offs, int beta) -> bool");
   m.def("xgmi_create(int rank, int world, int cap, int epoch_base) -> int", &xgmi_create);
   m.def("xgmi_handle(int id) -> Tensor", &xgmi_handle);
   m.def("xgmi_open(int id, int r, Tensor handle) -> ()", &xgmi_open);
@@ -704,6 +734,7 @@ TORCH_LIBRARY_IMPL(st_amd, CUDA, m) {
   m.impl("flash_bwd", &flash_bwd);
   m.impl("lse_merge_", &lse_merge_);
   m.impl("wgrad_gemm_", &wgrad_gemm_);
+  m.impl("wgrad_grouped_", &wgrad_grouped_);
   m.impl("qknorm_rope_fwd_", &qknorm_rope_fwd_);
   m.impl("qknorm_rope_bwd_", &qknorm_rope_bwd_);
 }

@@ -190,11 +190,36 @@ struct Geo {
   static_assert(PIECES % 8 == 0, "stage must split evenly over 8 waves");
 };
 
-template <int PROBE, int BN>
+// Grouped launch (MoE experts): G independent products C_g = beta C_g + A_g^T B_g whose
+// token ranges are [offs[g-1], offs[g]) of the same A / B (offs = inclusive prefix sum of
+// the per-expert row counts, on the device: the host never reads them).  Every group
+// has the same M x N, so the grid is G x tiles; the XCD remap runs over the whole grid,
+// so the workgroups one XCD holds at once are neighbouring tiles of the same expert.
+struct GroupPlan {
+  const int* offs;  // [G] inclusive offsets (int32), device
+  int G;
+  int64_t strideC;  // elements between consecutive C_g
+};
+
+template <int BN>
+ST_DEVICE WItem group_item(int b, int nbm, int nbn, int beta, float* C, int64_t ldc, const GroupPlan& gp) {
+  const int tiles = nbm * nbn;
+  const int idx = xcd_remap(b, gp.G * tiles);
+  const int g = idx / tiles, t = idx % tiles;
+  const int k0 = g ? gp.offs[g - 1] : 0;
+  WItem w{0, 0, k0, gp.offs[g] - k0, beta, C + (int64_t)g * gp.strideC, ldc, 0, 0};
+  int bm, bn;
+  group_tile(t, nbm, nbn, bm, bn);
+  w.m0 = w.cm0 = bm * BM;
+  w.n0 = w.cn0 = bn * BN;
+  return w;
+}
+
+template <int PROBE, int BN, bool GROUPED = false>
 __global__ __launch_bounds__(NT, 2) void wgrad_gemm_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                            const bf16_t* __restrict__ B, int64_t ldb,
                                                            float* __restrict__ C, int64_t ldc, int M, int N,
-                                                           int T, int beta, SplitPlan sp) {
+                                                           int T, int beta, SplitPlan sp, GroupPlan gp) {
   using Gm = Geo<BN>;
   __shared__ __attribute__((aligned(16))) char smem_raw[NBUF * Gm::STAGE];
   lds_t* smem = (lds_t*)smem_raw;
@@ -203,7 +228,9 @@ __global__ __launch_bounds__(NT, 2) void wgrad_gemm_kernel(const bf16_t* __restr
   const int nbm = M / BM, nbn = N / BN;
 
   // ---- work item of this workgroup: tile (XCD-aware, GROUP_M x nbn grouping), token range
-  const WItem w = work_item<BM, BN>((int)blockIdx.x, nbm, nbn, T, beta, C, ldc, sp);
+  const WItem w = GROUPED ? group_item<BN>((int)blockIdx.x, nbm, nbn, beta, C, ldc, gp)
+                          : work_item<BM, BN>((int)blockIdx.x, nbm, nbn, T, beta, C, ldc, sp);
+  if (GROUPED && w.T <= 0 && w.beta) return;  // expert received no tokens: C_g unchanged
   const int m0 = w.m0, n0 = w.n0;
   A += (int64_t)w.k0 * lda;
   B += (int64_t)w.k0 * ldb;
@@ -212,8 +239,8 @@ __global__ __launch_bounds__(NT, 2) void wgrad_gemm_kernel(const bf16_t* __restr
   // ---- DMA plan: a stage is NIMG images [32 tokens][128 features] (A images
   // first); wave w fills the 1 KiB pieces [w NDMA, (w+1) NDMA) of it.  Image
   // boundaries are 8 KiB, so a piece never straddles two images.
-  const i32x4 rsA = make_rsrc(A + m0, (uint32_t)(((int64_t)(T - 1) * lda + BM) * 2));
-  const i32x4 rsB = make_rsrc(B + n0, (uint32_t)(((int64_t)(T - 1) * ldb + BN) * 2));
+  const i32x4 rsA = make_rsrc(A + m0, (uint32_t)(T > 0 ? ((int64_t)(T - 1) * lda + BM) * 2 : 0));
+  const i32x4 rsB = make_rsrc(B + n0, (uint32_t)(T > 0 ? ((int64_t)(T - 1) * ldb + BN) * 2 : 0));
   const uint32_t sA = (uint32_t)(lda * 2), sB = (uint32_t)(ldb * 2);
   uint32_t voff[Gm::NDMA];
   bool isA[Gm::NDMA];
@@ -636,11 +663,11 @@ int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float*
     else if (probe == 2) wgrad8_kernel<2><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
     else wgrad8_kernel<0><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
   } else if (L.bn == 256) {
-    if (probe == 1) wgrad_gemm_kernel<1, 256><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
-    else wgrad_gemm_kernel<0, 256><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
+    if (probe == 1) wgrad_gemm_kernel<1, 256><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp, GroupPlan{});
+    else wgrad_gemm_kernel<0, 256><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp, GroupPlan{});
   } else {
-    if (probe == 1) wgrad_gemm_kernel<1, 128><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
-    else wgrad_gemm_kernel<0, 128><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
+    if (probe == 1) wgrad_gemm_kernel<1, 128><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp, GroupPlan{});
+    else wgrad_gemm_kernel<0, 128><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp, GroupPlan{});
   }
   ST_HIP_CHECK(hipGetLastError());
   if (L.split > 1) {
@@ -648,6 +675,32 @@ int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float*
     if (L.bn == 256) wgrad_tail_reduce<256><<<rg, 256, 0, st>>>(C, ldc, ws, nbm, nbn, sp);
     else wgrad_tail_reduce<128><<<rg, 256, 0, st>>>(C, ldc, ws, nbm, nbn, sp);
   }
+  return (int)hipGetLastError();
+}
+
+// Grouped weight gradient over G experts (MoE backward): C[g] (fp32, [G, M, N] with
+// leading stride strideC) = beta * C[g] + A[rows of g]^T B[rows of g], rows of expert g =
+// [offs[g-1], offs[g]) (int32 device prefix sums).  ONE launch for all experts, no host
+// read of the counts; the 4-stage kernel handles any row count (ragged last K-tile zero
+// filled).  T_total = rows of A / B (bounds every expert's range).  -2: unsupported shape.
+int st_wgrad_grouped(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc,
+                     int64_t strideC, int M, int N, int G, const int* offs, int T_total, int beta, hipStream_t st) {
+  if (M <= 0 || N <= 0 || G <= 0) return -2;
+  if (M % BM || N % 128 || lda % 8 || ldb % 8 || lda < M || ldb < N || ldc < N) return -2;
+  if (((uintptr_t)A | (uintptr_t)B) % 16 || (uintptr_t)C % 4) return -2;
+  if (((int64_t)(T_total + 63) * lda + M) * 2 >= (int64_t)1 << 32) return -2;
+  if (((int64_t)(T_total + 63) * ldb + N) * 2 >= (int64_t)1 << 32) return -2;
+  const int bn = (N % 256 == 0) ? 256 : 128;
+  const int64_t grid = (int64_t)G * (M / BM) * (N / bn);
+  if (grid >= (1LL << 31)) return -2;
+  const GroupPlan gp{offs, G, strideC};
+  const SplitPlan sp{nullptr, 0, 0, 1};
+  const bf16_t *a = (const bf16_t*)A, *b = (const bf16_t*)B;
+  const int bt = beta ? 1 : 0;
+  if (bn == 256)
+    wgrad_gemm_kernel<0, 256, true><<<(unsigned)grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T_total, bt, sp, gp);
+  else
+    wgrad_gemm_kernel<0, 128, true><<<(unsigned)grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T_total, bt, sp, gp);
   return (int)hipGetLastError();
 }
 

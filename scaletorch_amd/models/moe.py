@@ -140,19 +140,22 @@ class MoERouter(nn.Module):
 
 class _ExpertFFNFn(torch.autograd.Function):
     """Grouped expert SwiGLU FFN whose weight gradients are fp32 GEMMs straight into
-    ``main_grad`` (one per expert and weight, csrc/wgrad_gemm.hip or hipBLASLt with an
-    fp32 epilogue).  ``torch._grouped_mm`` only emits bf16 (its weight gradient went
-    bf16 -> fp32 copy -> add into the arena, and summed over tokens in bf16).  The
-    per-expert token counts reach the host by an async copy issued in the forward,
-    long finished by the backward: no stall."""
+    ``main_grad``.  ``torch._grouped_mm`` only emits bf16 (its weight gradient went
+    bf16 -> fp32 copy -> add into the arena, and summed over tokens in bf16).
+
+    The weight gradient of every local expert is ONE launch per weight
+    (csrc/wgrad_gemm.hip ``st_wgrad_grouped``): the expert row ranges come from the
+    device offsets, so the backward neither reads the routing counts on the host nor
+    loops over experts (the reference does the expert backward as one grouped op too,
+    scaletorch/models/npu_patch.py:94-127).  Shapes the kernel does not tile fall back
+    to per-expert GEMMs after one host read of the counts."""
 
     @staticmethod
-    def forward(ctx, x, offs, counts_host, ready, w_gu, w_dn):
+    def forward(ctx, x, offs, w_gu, w_dn):
         gu = torch._grouped_mm(x, w_gu.transpose(-2, -1), offs=offs)
         a = ops.swiglu(gu)
         y = torch._grouped_mm(a, w_dn.transpose(-2, -1), offs=offs)
         ctx.save_for_backward(x, gu, a, offs)
-        ctx.counts_host, ctx.ready = counts_host, ready
         ctx.w_gu, ctx.w_dn = w_gu, w_dn
         return y
 
@@ -167,21 +170,22 @@ class _ExpertFFNFn(torch.autograd.Function):
         da = torch._grouped_mm(dy, w_dn, offs=offs)
         dgu = _lib.ops().swiglu_bwd(da.contiguous(), gu)
         dx = torch._grouped_mm(dgu, w_gu, offs=offs)
-        ctx.ready.synchronize()
-        counts = ctx.counts_host.tolist()
+        counts = None
         for w, dout, inp in ((w_dn, dy, a), (w_gu, dgu, x)):
             fresh = take_fresh(w)
-            off = 0
-            for e, n in enumerate(counts):
-                if n:
-                    # token counts change every step: fixed kernel choice, no per-shape timing
-                    wgrad_into(w.main_grad[e], dout[off:off + n], inp[off:off + n], 0 if fresh else 1,
-                               variant=1)  # any token count (ragged last K-tile zero-filled)
-                elif fresh:
-                    w.main_grad[e].zero_()
-                off += n
+            if not _lib.ops().wgrad_grouped_(w.main_grad, dout, inp, offs, 0 if fresh else 1):
+                if counts is None:  # fallback: per-expert GEMMs (one host read of the counts)
+                    counts = torch.diff(offs, prepend=offs.new_zeros(1)).tolist()
+                off = 0
+                for e, n in enumerate(counts):
+                    if n:
+                        wgrad_into(w.main_grad[e], dout[off:off + n], inp[off:off + n], 0 if fresh else 1,
+                                   variant=1)
+                    elif fresh:
+                        w.main_grad[e].zero_()
+                    off += n
             _grad_ready(w)
-        return dx, None, None, None, None, None
+        return dx, None, None, None
 
 
 class MoEExperts(nn.Module):
@@ -237,11 +241,7 @@ class MoEExperts(nn.Module):
             if (torch.is_grad_enabled() and mg_gu is not None and mg_dn is not None
                     and mg_gu.dtype == torch.float32 and mg_dn.dtype == torch.float32 and self.inter % 8 == 0
                     and os.environ.get("ST_MOE_FP32_WGRAD", "1") == "1"):
-                counts_host = torch.empty(counts.numel(), dtype=counts.dtype, pin_memory=True)
-                counts_host.copy_(counts, non_blocking=True)
-                ready = torch.cuda.Event()
-                ready.record()
-                return _ExpertFFNFn.apply(x.contiguous(), offs, counts_host, ready, self.w_gate_up, self.w_down)
+                return _ExpertFFNFn.apply(x.contiguous(), offs, self.w_gate_up, self.w_down)
             gu = torch._grouped_mm(x.contiguous(), self.w_gate_up.transpose(-2, -1), offs=offs)
             return torch._grouped_mm(ops.swiglu(gu), self.w_down.transpose(-2, -1), offs=offs)
         if isinstance(counts, torch.Tensor):

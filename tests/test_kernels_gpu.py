@@ -585,3 +585,27 @@ def test_embedding_bwd_long_runs_and_masked_ids():
     assert torch.equal(outs[0], outs[1])
     err = (outs[0].double() - ref).abs().max().item()
     assert err < 5e-3 * max(1.0, ref.abs().max().item() / 100), err
+
+
+@pytest.mark.parametrize("N", [256, 384])
+@pytest.mark.parametrize("beta", [0, 1])
+def test_wgrad_grouped_matches_per_expert(N, beta):
+    """One-launch grouped weight gradient (csrc/wgrad_gemm.hip st_wgrad_grouped): expert
+    row ranges from device offsets (empty experts, ragged counts, one > 1 K-tile),
+    beta 0 overwrites / 1 accumulates (an empty expert with beta 0 is zeroed)."""
+    torch.manual_seed(4)
+    M = 512
+    counts = torch.tensor([37, 0, 300, 1, 64, 0, 1000], device="cuda", dtype=torch.int32)
+    T = int(counts.sum())
+    offs = torch.cumsum(counts, 0, dtype=torch.int32)
+    dy = torch.randn(T, M, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+    out = torch.randn(counts.numel(), M, N, device="cuda")
+    ref = out.clone() if beta else torch.zeros_like(out)
+    off = 0
+    for e, n in enumerate(counts.tolist()):
+        ref[e] += dy[off:off + n].float().t() @ x[off:off + n].float()
+        off += n
+    assert _lib.ops().wgrad_grouped_(out, dy, x, offs, beta)
+    torch.cuda.synchronize()
+    assert rel(out, ref) < 1e-5
