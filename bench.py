@@ -57,8 +57,11 @@ LAYOUTS = {
     "tp2pp2dp2": dict(tp=2, pp=2, sp=True, micro_batch_size=4, grad_acc=8, vpp=2),
     # long context: 32K tokens over 8 CP ranks (4K local), zig-zag chunks, GQA-sized K/V
     "cp8_32k": dict(cp=-1, seq_len=32768, micro_batch_size=1),
-    # Mixtral 8x7B: one expert per GPU (EP carved out of DP), dense weights ZeRO-1 over DP x EP
-    "mixtral_ep8": dict(model="mixtral-8x7b", ep=-1, micro_batch_size=2),
+    # Mixtral 8x7B: one expert per GPU (EP carved out of DP), dense weights ZeRO-1 over DP x EP;
+    # static-capacity dispatch (1.25x the mean rows per rank pair: no host sync per layer) in 2
+    # chunks, each chunk's all-to-all overlapping the other's expert GEMMs; dropped rows reported
+    "mixtral_ep8": dict(model="mixtral-8x7b", ep=-1, micro_batch_size=2, moe_capacity_factor=1.25,
+                        moe_ep_chunks=2),
 }
 
 
@@ -127,6 +130,9 @@ def main() -> int:
                          "0: logits + vocab-parallel CE")
     ap.add_argument("--head_chunk", type=int, default=4096, help="tokens per fused LM-head chunk")
     ap.add_argument("--layers", type=int, default=None, help="(debug only; result marked invalid)")
+    ap.add_argument("--moe_capacity_factor", type=float, default=None,
+                    help="EP dispatch: 0 dropless (one host read of the counts per layer), > 0 static capacity")
+    ap.add_argument("--moe_ep_chunks", type=int, default=None, help="EP dispatch chunks (capacity mode)")
     args = ap.parse_args()
     launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -140,7 +146,7 @@ def main() -> int:
         # a mismatch would report a different job size than the one asked for
         raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     preset = dict(model="llama3-8b", micro_batch_size=6, seq_len=4096, grad_acc=1, tp=1, pp=1, cp=1, ep=1, sp=False,
-                  vpp=1)
+                  vpp=1, moe_capacity_factor=0.0, moe_ep_chunks=1)
     preset.update({k: (world if v == -1 else v) for k, v in LAYOUTS[args.layout].items()})
     for k, v in preset.items():
         if getattr(args, k) is None:
@@ -195,6 +201,7 @@ def main() -> int:
         max_grad_norm=1.0, grad_reduce_dtype=args.grad_reduce_dtype, bucket_size_mb=args.bucket_mb,
         num_hidden_layers=args.layers, dtype="bfloat16", weight_decay=0.1, betas=(0.9, 0.95),
         zero_stage=args.zero, fused_lm_head=bool(args.fused_head), lm_head_chunk_tokens=args.head_chunk,
+        moe_capacity_factor=args.moe_capacity_factor, moe_ep_chunks=args.moe_ep_chunks,
     )
     if args.backend == "gloo" and torch.cuda.is_available():  # 1-GPU multi-rank rehearsal
         from scaletorch_amd.dist.gloo_staging import stage_gloo_cuda_p2p
@@ -239,6 +246,11 @@ def main() -> int:
     elapsed = float(t.item())
     final_loss = tr.reduced_loss(loss)
     tr.health_check()
+    moe_info = None
+    if tr.model_config.is_moe:  # capacity dispatch: rows dropped in the last step (read after the timing)
+        drops = [m.dropped_rows for m in tr.raw_model.modules() if getattr(m, "dropped_rows", None) is not None]
+        moe_info = {"capacity_factor": args.moe_capacity_factor, "ep_chunks": args.moe_ep_chunks,
+                    "dropped_rows_last_step": int(sum(int(d) for d in drops)) if drops else 0}
 
     tokens_per_step = tr.tokens_per_step  # global: dp*ep*mbs*ga*seq
     tok_s = tokens_per_step * args.steps / elapsed
@@ -284,6 +296,7 @@ def main() -> int:
         "valid": valid,
         "max_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1) if dev.type == "cuda" else 0.0,
         "comm_mb_per_step_rank0": comm,  # bytes handed to each collective per step on rank 0 (dist/trace.py)
+        "moe_dispatch": moe_info,
         "dist_world_size": dist.get_world_size() if dist.is_initialized() else 1,
         "backend": (("rccl" if a.backend == "nccl" else a.backend) if dist.is_initialized() else "none"),
         "collective_ranks_seen": ranks_seen,

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import math
 import os
+from typing import NamedTuple
 
 import torch
 import torch.nn as nn
@@ -58,6 +59,114 @@ def all_to_all_rows(x, out_splits, in_splits, group):
     if C.get_world_size(group) == 1:
         return x
     return _AllToAll.apply(x, out_splits, in_splits, group)
+
+
+# ---------------------------------------------------------------- capacity-bounded dispatch
+# EP dispatch options (trainer: --moe_capacity_factor / --moe_ep_chunks)
+_DISPATCH = {"capacity_factor": 0.0, "chunks": 1}
+
+
+def set_moe_dispatch(capacity_factor: float = 0.0, chunks: int = 1) -> None:
+    _DISPATCH.update(capacity_factor=float(capacity_factor), chunks=max(1, int(chunks)))
+
+
+class _A2AStart(torch.autograd.Function):
+    """Equal-split all-to-all of rows issued asynchronously: RCCL runs it on its own
+    stream and the host continues; ``_A2AWait`` makes the consumer's stream wait for it
+    (no host block on RCCL).  Backward: the reverse equal-split exchange."""
+
+    @staticmethod
+    def forward(ctx, x, holder, group):
+        trace.record("ep.all_to_all", x, group_size=C.get_world_size(group))
+        ctx.group = group
+        out, work = C.all_to_all(x.contiguous(), group=group, async_op=True)
+        holder.append(work)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        trace.record("ep.all_to_all_bwd", g, group_size=C.get_world_size(ctx.group))
+        return C.all_to_all(g.contiguous(), group=ctx.group), None, None
+
+
+class _A2AWait(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, holder):
+        for w in holder:
+            if w is not None:
+                w.wait()
+        holder.clear()
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+class CapacityPlan(NamedTuple):
+    send_idx: torch.Tensor    # [ep*cap] expert-sorted row feeding each send slot
+    send_valid: torch.Tensor  # [ep*cap] slot holds a row (else zero padding)
+    kept: torch.Tensor        # [ep, El] rows per (destination, local expert) after truncation
+    back_idx: torch.Tensor    # [rows] slot each expert-sorted row returns from
+    keep_row: torch.Tensor    # [rows] row was sent (not dropped)
+    cap: int
+
+
+def capacity_plan(counts: torch.Tensor, ep: int, cap: int, rows: int) -> CapacityPlan:
+    """Sender side of the static-capacity dispatch, all on the device.  ``counts`` [E]:
+    rows per global expert of the expert-sorted buffer (``rows`` = T*k, host-known).
+    Destination d (experts [d*El, (d+1)*El)) gets its first ``cap`` rows in expert
+    order; the rest are dropped (the truncation takes the last local experts' rows)."""
+    dev = counts.device
+    El = counts.numel() // ep
+    mat = counts.view(ep, El).long()
+    cum = torch.cumsum(mat, 1) - mat
+    kept = torch.clamp(torch.minimum(mat, cap - cum), min=0)
+    dcount = mat.sum(1)
+    dend = torch.cumsum(dcount, 0)
+    dstart = dend - dcount
+    dkept = kept.sum(1)
+    j = torch.arange(cap, device=dev)
+    send_valid = (j[None, :] < dkept[:, None]).reshape(-1)
+    send_idx = torch.where(send_valid, (dstart[:, None] + j[None, :]).reshape(-1), 0)
+    p = torch.arange(rows, device=dev)
+    d = torch.searchsorted(dend, p, right=True).clamp(max=ep - 1)
+    jp = p - dstart[d]
+    keep_row = jp < dkept[d]
+    back_idx = torch.where(keep_row, d * cap + jp, 0)
+    return CapacityPlan(send_idx, send_valid, kept, back_idx, keep_row, cap)
+
+
+def capacity_receive_order(recv_kept: torch.Tensor, cap: int):
+    """Receiver side: the static [ep*cap] received rows (block s = source s: its rows for
+    local expert 0, 1, ..., then padding) -> expert-major order.  Returns ``order`` (a
+    permutation: row i of the expert input = received row order[i]; the valid rows of
+    every expert first, then every padding row) and the per-expert inclusive ``offs``
+    (int32) of the grouped GEMMs.  Device only: no host read of the counts."""
+    ep, El = recv_kept.shape
+    dev = recv_kept.device
+    total = ep * cap
+    rk = recv_kept.long()
+    within = torch.cumsum(rk, 1) - rk
+    src_start = torch.arange(ep, device=dev)[:, None] * cap + within
+    counts_es = rk.t().reshape(-1)
+    src_start_es = src_start.t().reshape(-1)
+    ends = torch.cumsum(counts_es, 0)
+    starts = ends - counts_es
+    V = ends[-1]
+    i = torch.arange(total, device=dev)
+    blk = torch.searchsorted(ends, i, right=True).clamp(max=ep * El - 1)
+    order_valid = src_start_es[blk] + (i - starts[blk])
+    ktot = rk.sum(1)
+    padc = cap - ktot
+    pend = torch.cumsum(padc, 0)
+    pstart = pend - padc
+    ip = (i - V).clamp(min=0)
+    ps = torch.searchsorted(pend, ip, right=True).clamp(max=ep - 1)
+    order_pad = ps * cap + ktot[ps] + (ip - pstart[ps])
+    order = torch.where(i < V, order_valid, order_pad)
+    offs = torch.cumsum(rk.sum(0), 0).to(torch.int32)
+    return order, offs
 
 
 _GMM_OK: bool | None = None
@@ -255,6 +364,8 @@ class MoEExperts(nn.Module):
             gu = torch.matmul(xe, self.w_gate_up[e].t())
             outs.append(torch.matmul(ops.swiglu(gu), self.w_down[e].t()))
             off += n
+        if off < x.shape[0]:  # capacity padding rows past the last expert: zero output, connected
+            outs.append(x[off:] * 0)
         if not outs:
             return self._empty(x)
         return torch.cat(outs, 0)
@@ -285,6 +396,7 @@ class MoELayer(nn.Module):
         for p in self.experts.parameters():
             p._st_expert = True  # reduced over the expert-DP group, not dense-DP
         self.last_aux_loss: torch.Tensor | None = None
+        self.dropped_rows: torch.Tensor | None = None  # capacity dispatch: rows dropped in the last forward
 
     def reset_parameters(self) -> None:
         self.router.reset_parameters()
@@ -317,6 +429,9 @@ class MoELayer(nn.Module):
                 topw = CopyToTensorParallelRegion.apply(topw, tp_group)
         shape = x.shape
         self.last_aux_loss = aux if self.training else None
+        if self.ep > 1 and _DISPATCH["capacity_factor"] > 0:
+            out = self._forward_ep_capacity(x2, topw, topi).view(shape)
+            return self._tp_reduce(out, tp_group)
         # stable sort of the T*k (token, slot) entries by global expert + row gather
         perm = ops.moe.permutation(topi, self.num_experts)
         counts = perm.counts
@@ -337,12 +452,64 @@ class MoELayer(nn.Module):
             yr = ye.index_select(0, torch.argsort(order))  # back to [src][expert] for the return trip
             y = all_to_all_rows(yr, send_splits, recv_splits, group)
         out = ops.moe.combine(y, topw, perm).view(shape)
+        return self._tp_reduce(out, tp_group)
+
+    def _tp_reduce(self, out: torch.Tensor, tp_group) -> torch.Tensor:
         # expert down-projections are TP partial sums: reduce once, after the combine
         if self.sequence_parallel:
-            out = ReduceScatterToSequenceParallelRegion.apply(out, tp_group)
-        elif mesh.tp_size() > 1:
-            out = ReduceFromTensorParallelRegion.apply(out, tp_group)
+            return ReduceScatterToSequenceParallelRegion.apply(out, tp_group)
+        if mesh.tp_size() > 1:
+            return ReduceFromTensorParallelRegion.apply(out, tp_group)
         return out
+
+    def _forward_ep_capacity(self, x2: torch.Tensor, topw: torch.Tensor, topi: torch.Tensor) -> torch.Tensor:
+        """Expert-parallel MoE with static per-(source, destination) capacity: every
+        buffer size is known on the host, so no routing count is ever read back (the
+        dropless path reads one [2, ep] count matrix per layer).  The tokens go in
+        ``moe_ep_chunks`` chunks: all dispatch all-to-alls are issued first (async,
+        RCCL's stream), then chunk c's expert GEMMs run while chunk c+1's rows are in
+        flight, and each chunk's combine all-to-all overlaps the next chunk's experts.
+        Rows past a destination's capacity are dropped (their combine weight has
+        nothing to add: the token keeps its residual), counted in ``dropped_rows``
+        (a device scalar).  Reference: dispatch_tokens / gather_tokens,
+        scaletorch/parallel/expert_parallel/ep_comms.py:41-171 (host-synced splits)."""
+        group = mesh.pgm.ep_group
+        ep, k = self.ep, self.top_k
+        T = x2.shape[0]
+        nch = max(1, min(_DISPATCH["chunks"], T))
+        cf = _DISPATCH["capacity_factor"]
+        bounds = [T * c // nch for c in range(nch + 1)]
+        dropped = torch.zeros((), dtype=torch.int64, device=x2.device)
+        stage = []
+        for c in range(nch):
+            a, b = bounds[c], bounds[c + 1]
+            perm = ops.moe.permutation(topi[a:b], self.num_experts)
+            xs = ops.moe.gather_rows(x2[a:b], perm)
+            rows = (b - a) * k
+            cap = max(1, math.ceil(cf * rows / ep))
+            plan = capacity_plan(perm.counts, ep, cap, rows)
+            send = torch.where(plan.send_valid[:, None], xs.index_select(0, plan.send_idx), xs.new_zeros(()))
+            recv_kept = C.all_to_all(plan.kept.to(torch.int32).contiguous(), group=group)  # [src, local expert]
+            holder: list = []
+            r = _A2AStart.apply(send, holder, group)
+            stage.append((perm, topw[a:b], plan, recv_kept, r, holder))
+            dropped = dropped + (rows - plan.keep_row.sum())
+        back = []
+        for perm, tw, plan, recv_kept, r, holder in stage:
+            r = _A2AWait.apply(r, holder)
+            order, _ = capacity_receive_order(recv_kept, plan.cap)
+            ye = self.experts(r.index_select(0, order), recv_kept.sum(0))
+            inv = torch.empty_like(order).scatter_(0, order, torch.arange(order.numel(), device=order.device))
+            h2: list = []
+            yb = _A2AStart.apply(ye.index_select(0, inv), h2, group)
+            back.append((perm, tw, plan, yb, h2))
+        outs = []
+        for perm, tw, plan, yb, h2 in back:
+            yb = _A2AWait.apply(yb, h2)
+            ys = torch.where(plan.keep_row[:, None], yb.index_select(0, plan.back_idx), yb.new_zeros(()))
+            outs.append(ops.moe.combine(ys, tw, perm))
+        self.dropped_rows = dropped
+        return torch.cat(outs, 0) if len(outs) > 1 else outs[0]
 
     # reference checkpoint names: experts.experts.{e}.{gate,up,down}_proj.weight
     def reference_items(self) -> dict[str, torch.Tensor]:

@@ -67,6 +67,13 @@ class ParallelArguments:
     tp_comm: str = field(default="rccl", metadata={"help": "TP all-reduce transport: rccl | xgmi (custom one-/two-shot over IPC peer memory, dist/xgmi.py)"})
     cp_comm: str = field(default="auto", metadata={"help": "CP transport: auto (allgather for cp <= 2, ring above) | allgather (overlapped K/V all-gather) | ring (p2p rotation overlapped with block compute) | ulysses (head all-to-all)"})
     layer_distribution: str | None = field(default=None, metadata={"help": "comma list of layers per PP stage"})
+    moe_capacity_factor: float = field(default=0.0, metadata={
+        "help": "EP dispatch: 0 = dropless (exact splits: one host read of the routing counts per MoE layer); "
+                "> 0 = static per-(source, destination) capacity ceil(f * T * k / ep) rows: no host sync, rows "
+                "past the capacity are dropped (counted in the layer's dropped_rows)"})
+    moe_ep_chunks: int = field(default=1, metadata={
+        "help": "EP dispatch pipelining (capacity mode): the tokens are dispatched in this many chunks, each "
+                "chunk's all-to-all overlapping the previous chunk's expert GEMMs"})
 
     def __post_init__(self) -> None:
         for name in ("data_parallel_size", "tensor_parallel_size", "pipeline_parallel_size",
@@ -83,6 +90,8 @@ class ParallelArguments:
             if getattr(self, "gradient_accumulation_steps", 1) % self.pipeline_parallel_size:
                 raise ValueError("interleaved 1F1B needs gradient_accumulation_steps divisible by "
                                  "pipeline_parallel_size")
+        if self.moe_capacity_factor < 0 or self.moe_ep_chunks < 1:
+            raise ValueError("moe_capacity_factor must be >= 0 and moe_ep_chunks >= 1")
         if self.backend not in {"nccl", "gloo", "hccl"}:
             raise ValueError(f"backend must be one of {{nccl, gloo, hccl}}, got {self.backend}")
 

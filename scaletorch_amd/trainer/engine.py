@@ -61,6 +61,9 @@ class Trainer:
 
             set_tp_comm(a.tp_comm)
         from ..models.attention_backends import set_use_flash_attention
+        from ..models.moe import set_moe_dispatch
+
+        set_moe_dispatch(a.moe_capacity_factor, a.moe_ep_chunks)
 
         set_use_flash_attention(a.use_flash_attention)
         if a.context_parallel_size > 1:

@@ -287,6 +287,16 @@ def test_moe_ep2_parity():
     _compare_moe(ref, res)
 
 
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_moe_ep2_capacity_dispatch_parity(chunks):
+    """Sync-free static-capacity dispatch (capacity = every row: nothing dropped), with the
+    tokens pipelined in chunks through async all-to-alls: same step as one process."""
+    ref = _reference("tiny-moe")
+    res = run_workers(_worker, 2, "tiny-moe", dict(expert_parallel_size=2, micro_batch_size=2,
+                                                   moe_capacity_factor=2.0, moe_ep_chunks=chunks))
+    _compare_moe(ref, res)
+
+
 class _RcclSemantics:
     """Stands in for torch.distributed inside data_parallel.py: forwards everything,
     but executes all_reduce / reduce_scatter_tensor with RCCL's contract (ReduceOp.AVG,

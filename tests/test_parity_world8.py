@@ -89,7 +89,9 @@ def test_tp2_cp2_dp2():
     dict(expert_parallel_size=8, micro_batch_size=1),
     dict(expert_parallel_size=4, data_parallel_size=2, micro_batch_size=1),
     dict(expert_parallel_size=4, tensor_parallel_size=2, micro_batch_size=2),
-], ids=["ep8", "ep4_dp2", "ep4_tp2"])
+    dict(expert_parallel_size=8, micro_batch_size=1, moe_capacity_factor=8.0, moe_ep_chunks=2),
+    dict(expert_parallel_size=4, tensor_parallel_size=2, micro_batch_size=2, moe_capacity_factor=4.0),
+], ids=["ep8", "ep4_dp2", "ep4_tp2", "ep8_capacity_chunked", "ep4_tp2_capacity"])
 def test_mixtral_ep(kw):
     """Mixtral-style MoE (8 experts, top-2): EP carved out of data parallelism, dense
     grads reduced over DP x EP, expert grads over expert-DP."""

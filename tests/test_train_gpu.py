@@ -327,3 +327,32 @@ def test_training_converges_on_a_learnable_task(model):
     first, last = sum(losses[:5]) / 5, sum(losses[-10:]) / 10
     assert first > 5.5, losses[:5]
     assert last < 0.25 * first, (first, last, losses[::30])
+
+
+def test_moe_experts_ignore_capacity_padding_rows():
+    """Capacity dispatch hands the experts a static [ep*cap, h] buffer whose rows past the
+    last expert's offset are padding: the valid rows' outputs and every gradient must
+    equal the unpadded run (grouped GEMMs + grouped fp32 wgrad read only offs ranges)."""
+    from scaletorch_amd.models import moe
+
+    if not moe._grouped_mm_available():
+        pytest.skip("torch._grouped_mm unavailable")
+    torch.manual_seed(2)
+    E, h, inter = 4, 256, 512
+    ex = moe.MoEExperts(E, h, inter).cuda().to(torch.bfloat16)
+    counts = torch.tensor([40, 0, 100, 9], device="cuda")
+    V = int(counts.sum())
+    x = torch.randn(V, h, device="cuda", dtype=torch.bfloat16)
+    g = torch.randn(V, h, device="cuda", dtype=torch.bfloat16)
+    res = []
+    for pad in (0, 77):
+        for w in (ex.w_gate_up, ex.w_down):
+            w.main_grad = torch.zeros(w.shape, device="cuda")
+            w._st_fresh = True
+        xp = torch.cat([x, torch.zeros(pad, h, device="cuda", dtype=torch.bfloat16)]).requires_grad_(True)
+        y = ex(xp, counts)
+        y.backward(torch.cat([g, torch.zeros(pad, h, device="cuda", dtype=torch.bfloat16)]))
+        res.append((y[:V].float(), xp.grad[:V].float(), ex.w_gate_up.main_grad.clone(), ex.w_down.main_grad.clone()))
+    torch.cuda.synchronize()
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)

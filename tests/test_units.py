@@ -474,3 +474,56 @@ def test_cp_dkv_inplace_add_equals_fp32_accumulation():
         inplace = a.clone()
         inplace += b
         assert torch.equal(inplace, acc.bfloat16())
+
+
+def test_moe_capacity_plan_simulated_exchange():
+    """Static-capacity EP dispatch (models/moe.py capacity_plan / capacity_receive_order),
+    simulated for 4 ranks in one process: every kept row lands on its expert's rank, in
+    expert-major order with the right per-expert offsets, padding rows last; dropped
+    rows are exactly the overflow past each destination's capacity (last experts first)."""
+    import torch
+
+    from scaletorch_amd.models.moe import capacity_plan, capacity_receive_order
+
+    g = torch.Generator().manual_seed(1)
+    ep, El, rows, cap = 4, 3, 40, 9
+    E = ep * El
+    sends, plans = [], []
+    for r in range(ep):
+        ids = torch.randint(0, E, (rows,), generator=g)
+        ids[:12] = 5  # overflow destination 1 on every rank
+        srt, _ = torch.sort(ids, stable=True)
+        counts = torch.bincount(srt, minlength=E)
+        plan = capacity_plan(counts, ep, cap, rows)
+        # a sorted row is identified by (rank, global expert, position within the expert)
+        pos = torch.arange(rows) - (torch.cumsum(counts, 0) - counts)[srt]
+        tag = torch.stack([torch.full((rows,), r), srt, pos], 1)
+        send = torch.where(plan.send_valid[:, None], tag[plan.send_idx], torch.full((1, 3), -1))
+        sends.append(send.view(ep, cap, 3))
+        plans.append((plan, counts, srt))
+        # drops: per destination the overflow past cap, taken from its last experts
+        mat = counts.view(ep, El)
+        assert int((~plan.keep_row).sum()) == int((mat.sum(1) - cap).clamp(min=0).sum())
+        assert torch.equal(plan.kept.sum(1), mat.sum(1).clamp(max=cap))
+    for d in range(ep):
+        recv = torch.cat([sends[s][d] for s in range(ep)])  # the all-to-all
+        recv_kept = torch.stack([plans[s][0].kept[d] for s in range(ep)])
+        order, offs = capacity_receive_order(recv_kept, cap)
+        assert torch.equal(torch.sort(order).values, torch.arange(ep * cap))  # a permutation
+        xe = recv[order]
+        V = int(recv_kept.sum())
+        assert (xe[V:] == -1).all() and (xe[:V] >= 0).all()
+        start = 0
+        for e in range(El):
+            block = xe[start:int(offs[e])]
+            assert (block[:, 1] == d * El + e).all()
+            assert block.shape[0] == int(recv_kept[:, e].sum())
+            start = int(offs[e])
+    # the return trip: each kept sorted row comes back from the slot it was sent from
+    for r in range(ep):
+        plan = plans[r][0]
+        flat = torch.arange(ep * cap)
+        got = torch.where(plan.keep_row, flat[plan.back_idx], -1)
+        sent_from = torch.full((rows,), -1)
+        sent_from[plan.send_idx[plan.send_valid]] = flat[plan.send_valid]
+        assert torch.equal(got, sent_from)
