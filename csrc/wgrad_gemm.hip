@@ -193,8 +193,11 @@ struct Geo {
 // Grouped launch (MoE experts): G independent products C_g = beta C_g + A_g^T B_g whose
 // token ranges are [offs[g-1], offs[g]) of the same A / B (offs = inclusive prefix sum of
 // the per-expert row counts, on the device: the host never reads them).  Every group
-// has the same M x N, so the grid is G x tiles; the XCD remap runs over the whole grid,
-// so the workgroups one XCD holds at once are neighbouring tiles of the same expert.
+// has the same M x N, so the grid is G x tiles, expert-major: the ~256 workgroups in
+// flight at any time belong to ONE expert (as in a per-expert launch), and the XCD remap
+// runs inside each expert's tiles.  (Remapping over the whole grid put a different
+// expert on every XCD: 8 experts' operands competing for the Infinity Cache, 26 % slower
+// on the Mixtral proxy, profiles/r03/moe_grouped_wgrad.md.)
 struct GroupPlan {
   const int* offs;  // [G] inclusive offsets (int32), device
   int G;
@@ -204,8 +207,7 @@ struct GroupPlan {
 template <int BN>
 ST_DEVICE WItem group_item(int b, int nbm, int nbn, int beta, float* C, int64_t ldc, const GroupPlan& gp) {
   const int tiles = nbm * nbn;
-  const int idx = xcd_remap(b, gp.G * tiles);
-  const int g = idx / tiles, t = idx % tiles;
+  const int g = b / tiles, t = xcd_remap(b % tiles, tiles);
   const int k0 = g ? gp.offs[g - 1] : 0;
   WItem w{0, 0, k0, gp.offs[g] - k0, beta, C + (int64_t)g * gp.strideC, ldc, 0, 0};
   int bm, bn;

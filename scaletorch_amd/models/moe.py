@@ -282,7 +282,8 @@ class _ExpertFFNFn(torch.autograd.Function):
         counts = None
         for w, dout, inp in ((w_dn, dy, a), (w_gu, dgu, x)):
             fresh = take_fresh(w)
-            if not _lib.ops().wgrad_grouped_(w.main_grad, dout, inp, offs, 0 if fresh else 1):
+            grouped = os.environ.get("ST_MOE_GROUPED_WGRAD", "1") == "1"  # 0: per-expert launches (A/B)
+            if not (grouped and _lib.ops().wgrad_grouped_(w.main_grad, dout, inp, offs, 0 if fresh else 1)):
                 if counts is None:  # fallback: per-expert GEMMs (one host read of the counts)
                     counts = torch.diff(offs, prepend=offs.new_zeros(1)).tolist()
                 off = 0

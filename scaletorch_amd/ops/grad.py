@@ -93,6 +93,16 @@ def dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return dy.matmul(w)
 
 
+def dgrad_into(dy2: torch.Tensor, w: torch.Tensor, out: torch.Tensor) -> None:
+    """``out = dY W`` for 2-D ``dy2`` / ``out`` (a row block of a larger dX), TN layout
+    when a current W^T copy exists."""
+    if getattr(w, "_st_wt_epoch", -1) == _WT_EPOCH[0] and dy2.is_cuda:
+        torch.cuda.current_stream().wait_event(w._st_wt_done)
+        torch.matmul(dy2, w._st_wt.t(), out=out)
+        return
+    torch.matmul(dy2, w, out=out)
+
+
 # ---------------------------------------------------------------- weight-gradient GEMM layout
 # dW = dY^T X with both operands token-major is an "NT" GEMM (neither operand
 # K-contiguous); hipBLASLt's TN kernels on token-contiguous copies dY^T [out, T]

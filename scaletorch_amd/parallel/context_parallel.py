@@ -159,18 +159,25 @@ def _chunks_of(rank: int, S: int, cp: int, s: int, zigzag: bool):
 
 def _ring_exchange(tensors: list[torch.Tensor], group, cp: int, rank: int):
     """Async send of ``tensors`` to the next CP rank / receive from the previous one."""
+    recv = [torch.empty_like(t) for t in tensors]
+    return recv, _ring_p2p(tensors, recv, group, cp, rank)
+
+
+def _ring_p2p(sends: list[torch.Tensor], recvs: list[torch.Tensor], group, cp: int, rank: int):
+    """Post ``sends`` to the next CP rank and ``recvs`` from the previous one (async, one
+    batch).  Messages between a pair of ranks match in issue order, so every rank must
+    post its receives in the order its predecessor sends."""
     import torch.distributed as dist
 
     nxt = C.global_rank_of(group, (rank + 1) % cp)
     prv = C.global_rank_of(group, (rank - 1) % cp)
-    recv = [torch.empty_like(t) for t in tensors]
     ops = []
-    for t in tensors:
+    for t in sends:
         trace.record("cp.ring_send_recv", t, peer=f"{nxt}<-{prv}", group_size=cp)
-    for t, r in zip(tensors, recv):
         ops.append(dist.P2POp(dist.isend, t, nxt, group))
+    for r in recvs:
         ops.append(dist.P2POp(dist.irecv, r, prv, group))
-    return recv, dist.batch_isend_irecv(ops)
+    return dist.batch_isend_irecv(ops) if ops else []
 
 
 class _RingAttnFn(torch.autograd.Function):
@@ -212,6 +219,14 @@ class _RingAttnFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        """K/V rotate as in the forward.  The fp32 dK/dV accumulator of a block follows
+        it one step BEHIND: at step j a rank computes its partial for the block in hand
+        into a fresh buffer, and only then adds the accumulator that the previous rank
+        sent at the end of ITS step j-1 -- received during this step's flash backward --
+        and forwards the sum (async) without waiting for that send.  After cp steps
+        every accumulator is home; only the last hop is exposed.  Per-pair message order
+        (K/V_0, A_0, K/V_1, A_1, ...) is matched by posting each step's accumulator
+        receive before its K/V receive."""
         q, kv, out = ctx.saved_tensors[:3]
         lses = ctx.saved_tensors[3:]
         H, Hkv, D, scale, zigzag = ctx.meta
@@ -222,12 +237,19 @@ class _RingAttnFn(torch.autograd.Function):
         dout = dout.contiguous()
         dq = torch.zeros(q.shape, dtype=torch.float32, device=q.device)
         cur = kv.contiguous()
-        dkv = torch.zeros(kv.shape, dtype=torch.float32, device=q.device)
+        in_flight = []  # (tensor, works) of accumulator sends: kept alive until they complete
         for j in range(cp):
             src = (rank - j) % cp
-            pending = None
+            recvs = []
+            a_in = kv_next = None
+            if j >= 1:  # accumulator of this block from the previous rank (its step j-1)
+                a_in = torch.empty(kv.shape, dtype=torch.float32, device=q.device)
+                recvs.append(a_in)
             if j < cp - 1:
-                nxt_kv, pending = _ring_exchange([cur], group, cp, rank)
+                kv_next = torch.empty_like(cur)
+                recvs.append(kv_next)
+            works = _ring_p2p([cur] if j < cp - 1 else [], recvs, group, cp, rank)
+            part = torch.zeros(kv.shape, dtype=torch.float32, device=q.device)
             for (ko, kn, kg) in _chunks_of(src, S, cp, s, zigzag):
                 kc, vc = cur[:, ko: ko + kn, :Hkv], cur[:, ko: ko + kn, Hkv:]
                 for i, (qo, qn, qg) in enumerate(qch):
@@ -236,19 +258,23 @@ class _RingAttnFn(torch.autograd.Function):
                     g_q, g_k, g_v = ops.flash_attn_bwd(dout[:, qo: qo + qn], q[:, qo: qo + qn], kc, vc,
                                                        out[:, qo: qo + qn].contiguous(), lses[i], scale, True,
                                                        qg, kg)
-                    dq[:, qo: qo + qn] += g_q.float()
-                    dkv[:, ko: ko + kn, :Hkv] += g_k.float()
-                    dkv[:, ko: ko + kn, Hkv:] += g_v.float()
-            # the dK/dV accumulator travels with its K/V block (cp hops in total -> back home)
-            moved, pend2 = _ring_exchange([dkv], group, cp, rank)
-            if pending is not None:
-                for w in pending:
-                    w.wait()
-                cur = nxt_kv[0]
-            for w in pend2:
+                    dq[:, qo: qo + qn].add_(g_q)  # fp32 += bf16: one pass, no upcast copy
+                    part[:, ko: ko + kn, :Hkv].add_(g_k)
+                    part[:, ko: ko + kn, Hkv:].add_(g_v)
+            for w in works:
                 w.wait()
-            dkv = moved[0]
-        return dq.to(q.dtype), dkv.to(kv.dtype), None, None, None, None, None
+            if a_in is not None:
+                part.add_(a_in)
+            in_flight.append((part, _ring_p2p([part], [], group, cp, rank)))
+            if kv_next is not None:
+                cur = kv_next
+        home = torch.empty(kv.shape, dtype=torch.float32, device=q.device)
+        for w in _ring_p2p([], [home], group, cp, rank):  # own block's accumulator, last hop
+            w.wait()
+        for _, works in in_flight:
+            for w in works:
+                w.wait()
+        return dq.to(q.dtype), home.to(kv.dtype), None, None, None, None, None
 
 
 def _merge(acc: torch.Tensor, lse: torch.Tensor, bo: torch.Tensor, bl: torch.Tensor) -> None:
@@ -376,12 +402,17 @@ def set_cp_comm(mode: str) -> None:
 
 
 def resolve_cp_comm(cp: int) -> str:
-    """``auto``: the overlapped K/V all-gather at cp <= 2 (one exchange, the local
-    diagonal hides it), the ring above (per-step p2p hidden behind each block's
-    flash compute; the gathered K/V and its exposed tail grow with cp)."""
+    """``auto`` = the overlapped K/V all-gather at every cp.  On a fully connected
+    xGMI node RCCL's all-gather / reduce-scatter drive all 7 links of a GPU at once,
+    while the ring's point-to-point hops each use the ONE link to the next rank: at
+    cp = 8 and 32K tokens a layer's K/V all-gather is 7 x 16 MiB over 7 links versus 7
+    sequential 16 MiB hops (plus 7 fp32 dK/dV hops of 32 MiB) over one.  The gathered
+    K/V costs 128 MiB per layer of HBM (4 GiB over 32 layers), nothing at 288 GB.
+    ``ring`` stays selectable (--cp_comm ring) for multi-node CP where the ring's
+    neighbour traffic is what the network favours."""
     if _CP_COMM != "auto":
         return _CP_COMM
-    return "allgather" if cp <= 2 else "ring"
+    return "allgather"
 
 
 def context_parallel_attention(qkv: torch.Tensor, cos, sin, position_ids, H: int, Hkv: int, D: int,

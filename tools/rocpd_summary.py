@@ -9,6 +9,7 @@ prints per-step milliseconds, the device-busy union (time with >= 1 kernel
 running) and the idle remainder of the wall window.
 
   python tools/rocpd_summary.py gpurun_out/prof/run_results.db --steps 3 --csv profiles/x.csv
+  python tools/rocpd_summary.py gpurun_out/prof/run_kernel_trace.csv --steps 3   # csv output format
 """
 from __future__ import annotations
 
@@ -22,6 +23,8 @@ CLASSES = [  # (class, regex on the kernel name), first match wins
     ("gemm_wgrad_hip", r"wgrad8_kernel|wgrad_gemm_kernel|wgrad_tail_reduce"),
     ("gemm_fp32_out(wgrad_hipblaslt)", r"Cijk_.*_BSS_|Cijk_.*BBS_BS_"),
     ("gemm_bf16(fwd+dgrad)", r"Cijk_"),
+    ("grouped_gemm(experts)", r"grouped|Grouped"),
+    ("moe_route/permute/combine", r"moe_|topk|permute|combine|gather_rows"),
     ("flash_fwd", r"flash_fwd"),
     ("flash_bwd", r"flash_bwd"),
     ("adamw", r"adamw_kernel"),
@@ -51,8 +54,13 @@ def main() -> int:
     ap.add_argument("--gap_ms", type=float, default=50.0,
                     help="AdamW launches further apart than this start a new step (below the step time)")
     args = ap.parse_args()
-    c = sqlite3.connect(args.db)
-    rows = c.execute("select name, start, end from kernels order by start").fetchall()
+    if args.db.endswith(".csv"):  # rocprofv3 --output-format csv: *_kernel_trace.csv
+        with open(args.db, newline="") as f:
+            rows = sorted(((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                           for r in csv.DictReader(f)), key=lambda r: r[1])
+    else:
+        c = sqlite3.connect(args.db)
+        rows = c.execute("select name, start, end from kernels order by start").fetchall()
     ad = [(s, e) for n, s, e in rows if "adamw_kernel" in n]
     if len(ad) < args.steps + 1:
         print("not enough AdamW launches to find step boundaries", file=sys.stderr)
