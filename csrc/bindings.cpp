@@ -58,6 +58,10 @@ int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float*
 int64_t st_wgrad_ws_elems(int M, int N, int T, int variant);
 int st_wgrad_grouped(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int64_t strideC,
                      int M, int N, int G, const int* offs, int T_total, int beta, hipStream_t st);
+int64_t st_grouped_gemm_slots(int T, int G);
+int st_grouped_gemm_bm();
+int st_grouped_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t strideW, void* Y, int64_t ldy,
+                    const int* offs, const int* tile_end, int T, int G, int N, int K, int wn, hipStream_t st);
 int st_xgmi_header_bytes();
 int st_xgmi_max_ranks();
 int64_t st_xgmi_create(int rank, int world, int64_t cap, int64_t epoch_base);
@@ -379,6 +383,37 @@ bool wgrad_grouped_(at::Tensor out, const at::Tensor& dy, const at::Tensor& x, c
   if (rc == -2) return false;
   ST_CHECK_RC(rc, "wgrad_grouped_");
   return true;
+}
+
+// Grouped expert GEMM (csrc/grouped_gemm.hip): y[T, N] = x[T, K] @ (wn ? w[g] : w[g]^T) over the
+// row ranges [offs[g-1], offs[g]); w is [G, N, K] (wn = false) or [G, K, N] (wn = true).  Rows
+// of y past offs[G-1] are left unwritten.  Returns an undefined tensor when the kernel does
+// not tile the shape (caller falls back).
+at::Tensor grouped_gemm(const at::Tensor& x, const at::Tensor& w, const at::Tensor& offs, bool wn) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "w");
+  check_same_gpu(w, x, "w");
+  check_same_gpu(offs, x, "offs");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 3, "grouped_gemm: x [T, K], w [G, ., .]");
+  TORCH_CHECK(offs.scalar_type() == at::kInt && offs.dim() == 1 && offs.is_contiguous() && offs.size(0) == w.size(0),
+              "grouped_gemm: offs int32 [G]");
+  const int64_t T = x.size(0), K = x.size(1), G = w.size(0);
+  const int64_t N = wn ? w.size(2) : w.size(1);
+  TORCH_CHECK((wn ? w.size(1) : w.size(2)) == K, "grouped_gemm: inner dims ", x.sizes(), " x ", w.sizes());
+  if (x.stride(1) != 1 || w.stride(2) != 1 || T == 0 || T > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
+    return at::Tensor();
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  const int bm = st_grouped_gemm_bm();
+  // per-group M-tile counts -> inclusive prefix (device; the host never reads the offsets)
+  at::Tensor counts = at::diff(offs, 1, 0, at::zeros({1}, offs.options()));
+  at::Tensor tile_end = at::cumsum(at::floor_divide(counts + (bm - 1), bm), 0, at::kInt);
+  at::Tensor y = at::empty({T, N}, x.options());
+  int rc = st_grouped_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(1), w.stride(0), y.data_ptr(),
+                           y.stride(0), offs.data_ptr<int>(), tile_end.data_ptr<int>(), (int)T, (int)G, (int)N,
+                           (int)K, wn ? 1 : 0, cur_stream());
+  if (rc == -2) return at::Tensor();
+  ST_CHECK_RC(rc, "grouped_gemm");
+  return y;
 }
 
 // ---------------------------------------------------------------- xGMI all-reduce
@@ -703,6 +738,7 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, int q_offset, int k_offset, Tensor(a!)? dq_out=None, Tensor(b!)? dk_out=None, Tensor(c!)? dv_out=None) -> Tensor[]");
   m.def("wgrad_gemm_(Tensor(a!) out, Tensor dy, Tensor x, int beta, int variant=0) -> bool");
   m.def("wgrad_grouped_(Tensor(a!) out, Tensor dy, Tensor x, Tensor offs, int beta) -> bool");
+  m.def("grouped_gemm(Tensor x, Tensor w, Tensor offs, bool wn) -> Tensor");
   m.def("xgmi_create(int rank, int world, int cap, int epoch_base) -> int", &xgmi_create);
   m.def("xgmi_handle(int id) -> Tensor", &xgmi_handle);
   m.def("xgmi_open(int id, int r, Tensor handle) -> ()", &xgmi_open);
@@ -735,6 +771,7 @@ TORCH_LIBRARY_IMPL(st_amd, CUDA, m) {
   m.impl("lse_merge_", &lse_merge_);
   m.impl("wgrad_gemm_", &wgrad_gemm_);
   m.impl("wgrad_grouped_", &wgrad_grouped_);
+  m.impl("grouped_gemm", &grouped_gemm);
   m.impl("qknorm_rope_fwd_", &qknorm_rope_fwd_);
   m.impl("qknorm_rope_bwd_", &qknorm_rope_bwd_);
 }

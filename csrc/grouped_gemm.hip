@@ -1,0 +1,276 @@
+// Grouped (MoE expert) GEMM for gfx950 with a DEVICE offset table:
+//   for every group g:  Y[rows of g] = X[rows of g] @ op(W[g])
+//   rows of g = [offs[g-1], offs[g])  (int32 inclusive prefix sums, never read by the host)
+//
+// Two weight layouts, one kernel template:
+//   * WT (forward):      W[g] is [N][K] (K contiguous)  -> Y = X W^T   (x @ w.t() per expert)
+//   * WN (data grad):    W[g] is [K][N] (N contiguous)  -> Y = X W     (dy @ w per expert)
+// X / Y are token-major [T][K] / [T][N] with row strides.  Reference: the grouped-matmul
+// autograd of scaletorch/models/npu_patch.py:94-127 (npu_grouped_matmul); on ROCm,
+// torch._grouped_mm runs one small hipBLASLt GEMM per group after reading the offsets on
+// the host (profiles/r03/moe_qwen3_30b_a3b_proxy_breakdown.txt: ~1,500 launches and 56 ms
+// of idle per step at 128 experts) -- this is ONE launch per product.
+//
+// Design (CDNA4-first; the synchronisation skeleton is the 4-stage ring of
+// csrc/wgrad_gemm.hip):
+//   * 256 x BN output tile (BN = 256 or 128), 8 waves, 16x16x32 bf16 MFMA, K in 32-wide
+//     tiles through a ring of 4 LDS stages (3 in flight), LDS-DMA from inline asm with
+//     counted vmcnt + raw barriers.
+//   * grid = (ceil(T/256) + G) M-tile slots x N-tiles (an upper bound of sum_g ceil(n_g/256));
+//     a workgroup maps its slot to (group, M-tile) by a binary search of the per-group
+//     tile-count prefix (device, computed by the caller); surplus slots exit at once.
+//   * rows past a group's end: the buffer descriptor's range ends at the group's last
+//     row, so they load as zeros and are not stored.
+//   * LDS images, both conflict-free by construction:
+//       row image (X, and W in WT layout): [16-row block][8-k chunk (4)][row (16)][16 B] --
+//         a fragment read (two ds_read_b64 per lane) covers one 256-B bank row per
+//         32-lane half;
+//       column image (W in WN layout): [64-col block][k (32)][128 B] with the 32-B column
+//         slot XOR-swizzled by (k >> 1) & 3, read by ds_read_b64_tr_b16 (k down the
+//         lane's fragment); the 8 k-rows a 32-lane half reads land in 8 distinct 32-B slots.
+//     The MFMA's 32 k-slots hold k = {4g..4g+3} U {16+4g..16+4g+3} for lane group g
+//     (the same permutation for both operands, so the products pair correctly).
+#include <type_traits>
+
+#include "common.h"
+
+using namespace st;
+
+namespace {
+
+typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bfx4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) char lds_t;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 256, BK = 32, NT = 512, NBUF = 4;
+
+ST_DEVICE i32x4 make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  i32x4 r;
+  r[0] = (int)__builtin_amdgcn_readfirstlane((uint32_t)a);
+  r[1] = (int)(__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) & 0xffffu);
+  r[2] = (int)__builtin_amdgcn_readfirstlane(bytes);
+  r[3] = 0x00020000;
+  return r;
+}
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved: nothing else in this kernel uses it
+ST_DEVICE void lds_dma16(const i32x4& rs, uint32_t lds_base, uint32_t voff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(lds_base), "v"(voff), "s"(rs)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+ST_DEVICE bfx4 lds_b64(const lds_t* p) { return *(const bfx4 __attribute__((address_space(3)))*)p; }
+ST_DEVICE bfx4 lds_tr(const lds_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((bfx4 __attribute__((address_space(3)))*)p);
+}
+ST_DEVICE bfx8 cat8(bfx4 a, bfx4 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7); }
+
+template <int BN, bool WN>
+struct Geo {
+  static constexpr int WM = BN == 256 ? 2 : 4, WNV = 8 / WM;  // wave grid
+  static constexpr int TM = BM / WM, TN = BN / WNV;           // per-wave tile
+  static constexpr int FM = TM / 16, FN = TN / 16;
+  static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int A_PIECES = A_BYTES / 1024, PIECES = STAGE / 1024;
+  static constexpr int NDMA = PIECES / 8;
+  static_assert(PIECES % 8 == 0, "stage must split evenly over 8 waves");
+};
+
+// first g with tile_end[g] > s (tile_end = inclusive prefix of per-group M-tile counts)
+ST_DEVICE int find_group(const int* __restrict__ tile_end, int G, int s) {
+  int lo = 0, hi = G;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (tile_end[mid] <= s) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+template <int BN, bool WN>
+__global__ __launch_bounds__(NT, 1) void grouped_gemm_kernel(const bf16_t* __restrict__ X, int64_t ldx,
+                                                             const bf16_t* __restrict__ W, int64_t ldw,
+                                                             int64_t strideW, bf16_t* __restrict__ Y, int64_t ldy,
+                                                             const int* __restrict__ offs,
+                                                             const int* __restrict__ tile_end, int G, int N,
+                                                             int K) {
+  using Gm = Geo<BN, WN>;
+  __shared__ __attribute__((aligned(16))) char smem_raw[NBUF * Gm::STAGE];
+  lds_t* smem = (lds_t*)smem_raw;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nbn = N / BN;
+
+  // ---- work item: (M-tile slot, N-tile); slot -> (group, M-tile of the group)
+  const int b = (int)blockIdx.x;
+  const int slot = b / nbn, nt = b % nbn;
+  const int total_slots = tile_end[G - 1];
+  if (slot >= total_slots) return;  // uniform over the workgroup: no barrier reached yet
+  const int g = find_group(tile_end, G, slot);
+  const int first_slot = g ? tile_end[g - 1] : 0;
+  const int row0 = (g ? offs[g - 1] : 0) + (slot - first_slot) * BM;
+  const int rows = min(BM, offs[g] - row0);  // >= 1 by construction
+  const int n0 = nt * BN;
+
+  // ---- operands: X rows [row0, row0 + rows) -- the descriptor ends at the last valid
+  // row, so DMA of rows past it (next group / past T) reads zeros
+  const bf16_t* xb = X + (int64_t)row0 * ldx;
+  const i32x4 rsX = make_rsrc(xb, (uint32_t)(((int64_t)(rows - 1) * ldx + K) * 2));
+  const bf16_t* wb = W + (int64_t)g * strideW + (WN ? (int64_t)n0 : (int64_t)n0 * ldw);
+  const i32x4 rsW = make_rsrc(wb, (uint32_t)(WN ? ((int64_t)(K - 1) * ldw + BN) * 2
+                                               : ((int64_t)(BN - 1) * ldw + K) * 2));
+  const uint32_t sX = (uint32_t)(ldx * 2), sW = (uint32_t)(ldw * 2);
+
+  // ---- DMA plan: wave w fills the 1-KiB pieces [w NDMA, (w+1) NDMA) of a stage
+  uint32_t voff[Gm::NDMA];
+  bool isA[Gm::NDMA];
+#pragma unroll
+  for (int i = 0; i < Gm::NDMA; ++i) {
+    const int p = wid * Gm::NDMA + i;  // wave-uniform
+    isA[i] = p < Gm::A_PIECES;
+    if (isA[i] || !WN) {  // row image piece: 16 rows x 4 chunks of 8 k
+      const int q = isA[i] ? p : p - Gm::A_PIECES;
+      const int r = q * 16 + (lane & 15), kc = lane >> 4;
+      voff[i] = (uint32_t)r * (isA[i] ? sX : sW) + (uint32_t)(kc * 16);
+    } else {  // column image piece: 8 k-rows x 128 B of one 64-column block
+      const int q = p - Gm::A_PIECES;
+      const int cb = q >> 2, kr = (q & 3) * 8 + (lane >> 3);
+      const int phys = (lane & 7) >> 1;
+      const int logical = ((phys ^ ((kr >> 1) & 3)) << 1) | (lane & 1);  // 16-B chunk in the 128-B row
+      voff[i] = (uint32_t)kr * sW + (uint32_t)((cb * 64 + logical * 8) * 2);
+    }
+  }
+  const uint32_t dma_base =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem + (uint32_t)(wid * Gm::NDMA * 1024));
+  auto dma = [&](int buf, int kt) {
+    const uint32_t kx = (uint32_t)(kt * BK * 2);                  // row images: k along the row
+    const uint32_t kw = WN ? (uint32_t)(kt * BK) * sW : kx;       // column image: k = row
+#pragma unroll
+    for (int i = 0; i < Gm::NDMA; ++i)
+      lds_dma16(isA[i] ? rsX : rsW, dma_base + buf * Gm::STAGE + i * 1024, voff[i] + (isA[i] ? kx : kw));
+  };
+
+  // ---- fragment read plan
+  const int gq = lane >> 4, rr = lane & 15;
+  const int wm = wid / Gm::WNV, wn = wid % Gm::WNV;
+  const int am = wm * Gm::TM, bnn = wn * Gm::TN;
+  int aoff[Gm::FM], boff[Gm::FN];
+#pragma unroll
+  for (int f = 0; f < Gm::FM; ++f)  // row image: block (am/16 + f), chunk gq>>1, row rr, half gq&1
+    aoff[f] = ((am >> 4) + f) * 1024 + (gq >> 1) * 256 + rr * 16 + 8 * (gq & 1);
+#pragma unroll
+  for (int f = 0; f < Gm::FN; ++f) {
+    const int nn = bnn + 16 * f;
+    if (WN) {  // lane 4q+p of group gq: k-row 4gq+q, columns 4p..4p+3 of the 16-col slot
+      const int q = (lane >> 2) & 3, p = lane & 3;
+      const int kr = 4 * gq + q, slot = (nn & 63) >> 4;
+      boff[f] = Gm::A_BYTES + (nn >> 6) * 4096 + kr * 128 + 32 * (slot ^ ((kr >> 1) & 3)) + 8 * p;
+    } else {
+      boff[f] = Gm::A_BYTES + (nn >> 4) * 1024 + (gq >> 1) * 256 + rr * 16 + 8 * (gq & 1);
+    }
+  }
+
+  f32x4 acc[Gm::FM][Gm::FN];
+#pragma unroll
+  for (int i = 0; i < Gm::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < Gm::FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
+
+  const int KT = K / BK;
+#pragma unroll
+  for (int p = 0; p < NBUF - 1; ++p)
+    if (p < KT) dma(p, p);
+
+  auto step = [&](auto bufc, int kt) {
+    constexpr int BUF = decltype(bufc)::value;
+    if (kt + 2 < KT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * Gm::NDMA) : "memory");
+    else if (kt + 1 < KT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Gm::NDMA) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + NBUF - 1 < KT) dma((BUF + NBUF - 1) % NBUF, kt + NBUF - 1);
+    const lds_t* st = smem + BUF * Gm::STAGE;
+    bfx8 af[Gm::FM], bf[Gm::FN];
+#pragma unroll
+    for (int j = 0; j < Gm::FN; ++j) {
+      if (WN) bf[j] = cat8(lds_tr(st + boff[j]), lds_tr(st + boff[j] + 16 * 128));
+      else bf[j] = cat8(lds_b64(st + boff[j]), lds_b64(st + boff[j] + 512));
+    }
+#pragma unroll
+    for (int i = 0; i < Gm::FM; ++i) af[i] = cat8(lds_b64(st + aoff[i]), lds_b64(st + aoff[i] + 512));
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < Gm::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < Gm::FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("" ::: "memory");
+  };
+  for (int kt = 0; kt < KT; kt += NBUF) {
+    step(std::integral_constant<int, 0>(), kt);
+    if (kt + 1 < KT) step(std::integral_constant<int, 1>(), kt + 1);
+    if (kt + 2 < KT) step(std::integral_constant<int, 2>(), kt + 2);
+    if (kt + 3 < KT) step(std::integral_constant<int, 3>(), kt + 3);
+  }
+
+  // ---- epilogue: 16x16 C/D row = 4 (lane>>4) + reg (M), column = lane & 15 (N); rows past
+  // the group's end are not stored
+  bf16_t* yb = Y + (int64_t)row0 * ldy + n0 + bnn + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < Gm::FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = am + 16 * i + 4 * gq + r;
+      if (m < rows) {
+#pragma unroll
+        for (int j = 0; j < Gm::FN; ++j) yb[(int64_t)m * ldy + 16 * j] = f2bf(acc[i][j][r]);
+      }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+// M-tile slots to launch for T rows in G groups (upper bound of sum_g ceil(n_g / 256)).
+int64_t st_grouped_gemm_slots(int T, int G) { return (int64_t)(T + BM - 1) / BM + G; }
+int st_grouped_gemm_bm() { return BM; }
+
+// Y[T, N] (bf16, rows of each group) = X[T, K] @ (wn ? W[g] : W[g]^T); W[g] is [K][N] when
+// wn, else [N][K].  offs / tile_end: int32 [G] device (tile_end = inclusive prefix of
+// ceil(n_g / 256)).  0 on success, -2 unsupported shape.
+int st_grouped_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t strideW, void* Y, int64_t ldy,
+                    const int* offs, const int* tile_end, int T, int G, int N, int K, int wn, hipStream_t st) {
+  if (T <= 0 || G <= 0 || N <= 0 || K <= 0) return -2;
+  if (K % BK || N % 128) return -2;
+  if (ldx % 8 || ldw % 8 || ldy % 8 || ldx < K || ldy < N || (wn ? ldw < N : ldw < K)) return -2;
+  if (((uintptr_t)X | (uintptr_t)W | (uintptr_t)Y) % 16) return -2;
+  if (((int64_t)(T + BM) * ldx) * 2 >= (int64_t)1 << 32) return -2;  // 32-bit buffer offsets
+  if ((wn ? (int64_t)K * ldw : (int64_t)N * ldw) * 2 >= (int64_t)1 << 32) return -2;
+  const int bn = (N % 256 == 0) ? 256 : 128;
+  const int64_t grid = st_grouped_gemm_slots(T, G) * (N / bn);
+  if (grid >= (1LL << 31)) return -2;
+  const bf16_t *x = (const bf16_t*)X, *w = (const bf16_t*)W;
+  bf16_t* y = (bf16_t*)Y;
+#define LAUNCH(BNV, WNV)                                                                                   \
+  grouped_gemm_kernel<BNV, WNV><<<(unsigned)grid, NT, 0, st>>>(x, ldx, w, ldw, strideW, y, ldy, offs, tile_end, \
+                                                               G, N, K)
+  if (bn == 256) {
+    if (wn) LAUNCH(256, true); else LAUNCH(256, false);
+  } else {
+    if (wn) LAUNCH(128, true); else LAUNCH(128, false);
+  }
+#undef LAUNCH
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

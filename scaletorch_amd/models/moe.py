@@ -247,10 +247,26 @@ class MoERouter(nn.Module):
         return topw, topi, aux
 
 
+def _gmm(x: torch.Tensor, w: torch.Tensor, offs: torch.Tensor, wn: bool) -> torch.Tensor:
+    """Per-expert ``x[rows of g] @ (w[g] if wn else w[g]^T)`` with device offsets: ONE launch
+    of csrc/grouped_gemm.hip (``ST_MOE_HIP_GMM=0``, or a shape it does not tile, falls back
+    to ``torch._grouped_mm``, which on ROCm runs a GEMM per expert)."""
+    from ..ops import _lib
+
+    K = x.shape[1]
+    N = w.shape[2] if wn else w.shape[1]
+    if (os.environ.get("ST_MOE_HIP_GMM", "1") == "1" and _lib.use_native(x) and x.dtype == torch.bfloat16
+            and x.stride(1) == 1 and x.stride(0) % 8 == 0 and w.is_contiguous() and K % 32 == 0 and N % 128 == 0
+            and x.shape[0] > 0):
+        return _lib.ops().grouped_gemm(x, w, offs, wn)
+    return torch._grouped_mm(x, w if wn else w.transpose(-2, -1), offs=offs)
+
+
 class _ExpertFFNFn(torch.autograd.Function):
-    """Grouped expert SwiGLU FFN whose weight gradients are fp32 GEMMs straight into
-    ``main_grad``.  ``torch._grouped_mm`` only emits bf16 (its weight gradient went
-    bf16 -> fp32 copy -> add into the arena, and summed over tokens in bf16).
+    """Grouped expert SwiGLU FFN: forward and data-gradient GEMMs are one launch each over
+    all local experts (``_gmm``, csrc/grouped_gemm.hip), and the weight gradients are
+    fp32 GEMMs straight into ``main_grad``.  (``torch._grouped_mm``'s own backward only
+    emits bf16: its weight gradient went bf16 -> fp32 copy -> add into the arena.)
 
     The weight gradient of every local expert is ONE launch per weight
     (csrc/wgrad_gemm.hip ``st_wgrad_grouped``): the expert row ranges come from the
@@ -261,9 +277,9 @@ class _ExpertFFNFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, offs, w_gu, w_dn):
-        gu = torch._grouped_mm(x, w_gu.transpose(-2, -1), offs=offs)
+        gu = _gmm(x, w_gu, offs, wn=False)
         a = ops.swiglu(gu)
-        y = torch._grouped_mm(a, w_dn.transpose(-2, -1), offs=offs)
+        y = _gmm(a, w_dn, offs, wn=False)
         ctx.save_for_backward(x, gu, a, offs)
         ctx.w_gu, ctx.w_dn = w_gu, w_dn
         return y
@@ -276,9 +292,9 @@ class _ExpertFFNFn(torch.autograd.Function):
         x, gu, a, offs = ctx.saved_tensors
         w_gu, w_dn = ctx.w_gu, ctx.w_dn
         dy = dy.contiguous()
-        da = torch._grouped_mm(dy, w_dn, offs=offs)
+        da = _gmm(dy, w_dn, offs, wn=True)
         dgu = _lib.ops().swiglu_bwd(da.contiguous(), gu)
-        dx = torch._grouped_mm(dgu, w_gu, offs=offs)
+        dx = _gmm(dgu, w_gu, offs, wn=True)
         counts = None
         for w, dout, inp in ((w_dn, dy, a), (w_gu, dgu, x)):
             fresh = take_fresh(w)

@@ -115,6 +115,10 @@ class ProcessGroupManager:
         self.tp_group, self.tp_group_ids = self._family(("tp",))
         self.cp_group, self.cp_group_ids = self._family(("cp",))
         self.pp_group, self.pp_group_ids = self._family(("pp",))
+        # pipeline gradients travel on their own communicator: each direction is then a
+        # FIFO of its own, so a receive posted ahead (activations) can never sit in front
+        # of a send the peer is waiting for (gradients) -- parallel/pipeline_parallel.py
+        self.pp_bwd_group, _ = self._family(("pp",), channel="pp_bwd")
         self.ep_group, self.ep_group_ids = self._family(("ep",))
         self.dp_group, self.dp_group_ids = self._family(("dp",))
         self.cp_dp_group, self.cp_dp_group_ids = self._family(("dp", "cp"))

@@ -6,14 +6,16 @@ Differences:
   same even split with the remainder on the first stages, or an explicit
   ``layer_distribution``); embedding lives on the first stage, final
   norm + LM head on the last;
-* every exchange is non-blocking (``batch_isend_irecv``); the paired
-  send-forward/recv-backward of the 1F1B steady state is ONE grouped RCCL call;
-  a received tensor is waited for right before its first use, and a pure send
-  is never waited on the compute path: its work handle (and the tensor) is kept
-  until the end of the step, so the next micro-batch's compute does not stall
-  until the peer has posted its receive (the reference blocked on every
-  send/recv, pp_comms.py:181-186).  The RCCL issue order is unchanged, so this
-  cannot introduce a p2p deadlock;
+* every exchange is non-blocking, and receives are POSTED AHEAD: activations
+  travel on the pipeline communicator and gradients on a second one
+  (``mesh.pp_bwd_group``), so each direction between two stages is its own FIFO
+  and a receive posted early can never block a send the peer is waiting for.
+  The engine keeps the next micro-batch's receive in flight in each direction
+  (``_Mailbox``, depth 2) and waits (a stream wait on RCCL) right before the
+  data is used, so the transfer runs under the current micro-batch's forward /
+  backward; a send is never waited on the compute path (its handle and tensor
+  are kept until the end of the step).  The reference blocked on every
+  send/recv (pp_comms.py:181-186);
 * the schedule owns the loss (the reference stored it on the DP wrapper and
   crashed with PP+DP), losses stay on device (one host sync
   per step, at logging), and the DP gradient sync is enabled only for the last
@@ -117,6 +119,56 @@ def bidirectional_pipeline_communicate(operation: str, send_tensor, recv_shapes,
     raise ValueError(operation)
 
 
+class _Recv:
+    """One posted receive; ``get()`` waits for it (stream-ordered on RCCL)."""
+
+    __slots__ = ("buf", "works")
+
+    def __init__(self, shape, dtype, device, peer, group, kind):
+        self.buf = torch.empty(shape, dtype=dtype, device=device)
+        _STATS["recv_" + kind] += 1
+        trace.record("pp.recv_" + kind, self.buf, peer=peer)
+        self.works = dist.batch_isend_irecv([dist.P2POp(dist.irecv, self.buf, peer, group)])
+
+    def get(self) -> torch.Tensor:
+        for w in self.works:
+            w.wait()
+        self.works = ()
+        return self.buf
+
+
+class _Mailbox:
+    """Receives of ONE direction from one peer, posted ``depth`` ahead in the order the
+    peer sends them (a FIFO on that direction's own communicator), at most ``total``."""
+
+    def __init__(self, total: int, shape, dtype, device, peer, group, kind: str, depth: int = 2):
+        self.total, self.posted = total, 0
+        self.args = (shape, dtype, device, peer, group, kind)
+        self.q: deque = deque()
+        self.depth = depth
+        self.fill()
+
+    def fill(self) -> None:
+        while len(self.q) < self.depth and self.posted < self.total:
+            self.q.append(_Recv(*self.args))
+            self.posted += 1
+
+    def take(self) -> _Recv:
+        """Next receive (still in flight); the one after it is posted right away."""
+        r = self.q.popleft()
+        self.fill()
+        return r
+
+
+def _send(t: torch.Tensor, peer: int, group, kind: str) -> None:
+    """Async send kept in flight until ``wait_sends`` (end of step)."""
+    t = t.contiguous()
+    _STATS["send_" + kind] += 1
+    trace.record("pp.send_" + kind, t, peer=peer)
+    works = dist.batch_isend_irecv([dist.P2POp(dist.isend, t, peer, group)])
+    _INFLIGHT.append((works, [t]))
+
+
 class PipelineEngine:
     """Runs one optimizer step's worth of micro-batches through this stage."""
 
@@ -167,72 +219,80 @@ class PipelineEngine:
         self.model.require_backward_grad_sync = True
         return x.grad if x is not None else None
 
+    def _mailboxes(self, num_micro: int):
+        """(activation mailbox or None, gradient mailbox or None) of this stage."""
+        pg = mesh.pgm
+        bwd_group = getattr(pg, "pp_bwd_group", None) or pg.pp_group
+        rf = None if self._first else _Mailbox(num_micro, self.tensor_shape, self.dtype, self.device,
+                                               pg.pp_prev_rank, pg.pp_group, "forward")
+        rb = None if self._last else _Mailbox(num_micro, self.tensor_shape, self.dtype, self.device,
+                                              pg.pp_next_rank, bwd_group, "backward")
+        return rf, rb, bwd_group
+
     def train_step_afab(self, data_iter, num_micro: int) -> torch.Tensor:
+        pg = mesh.pgm
+        rf, rb, bwd_group = self._mailboxes(num_micro)
         ins, outs = deque(), deque()
         loss_sum = torch.zeros((), dtype=torch.float32, device=self.device)
         for _ in range(num_micro):
-            x = _p2p(recv_fwd_shape=self.tensor_shape, dtype=self.dtype, device=self.device)[0]
+            x = rf.take().get().requires_grad_(True) if rf is not None else None
             batch = next(data_iter)
             y = self._forward(batch, x, num_micro)
             if not self._last:
-                _p2p(send_fwd=y.detach())
+                _send(y.detach(), pg.pp_next_rank, pg.pp_group, "forward")
             else:
                 loss_sum += y.detach().float()
             ins.append(x)
             outs.append(y)
         for i in range(num_micro):
-            dy = _p2p(recv_bwd_shape=self.tensor_shape, dtype=self.dtype, device=self.device)[1]
+            dy = rb.take().get() if rb is not None else None
             x, y = ins.popleft(), outs.popleft()
             dx = self._backward(x, y, dy, last_backward=(i == num_micro - 1))
-            _p2p(send_bwd=dx)
+            if not self._first:
+                _send(dx, pg.pp_prev_rank, bwd_group, "backward")
         wait_sends()
         return loss_sum
 
     def train_step_1f1b(self, data_iter, num_micro: int) -> torch.Tensor:
+        """1F1B: warm-up forwards, steady one-forward-one-backward, cool-down backwards.
+        The next micro-batch's activation and gradient receives are always in flight
+        (``_Mailbox``), so each transfer overlaps the compute before its use."""
         pg = mesh.pgm
         warmup = min(pg.pp_world_size - pg.pp_rank - 1, num_micro)
         steady = num_micro - warmup
+        rf, rb, bwd_group = self._mailboxes(num_micro)
         ins, outs = deque(), deque()
         loss_sum = torch.zeros((), dtype=torch.float32, device=self.device)
         n_bwd = 0
 
-        def fwd(x):
-            batch = next(data_iter)
-            y = self._forward(batch, x, num_micro)
+        def fwd():
+            x = rf.take().get().requires_grad_(True) if rf is not None else None
+            y = self._forward(next(data_iter), x, num_micro)
             if self._last:
                 loss_sum.add_(y.detach().float())
-            return y
+            else:
+                _send(y.detach(), pg.pp_next_rank, pg.pp_group, "forward")
+            ins.append(x)
+            outs.append(y)
+
+        def bwd():
+            nonlocal n_bwd
+            dy = rb.take().get() if rb is not None else None
+            xo, yo = ins.popleft(), outs.popleft()
+            n_bwd += 1
+            dx = self._backward(xo, yo, dy, last_backward=(n_bwd == num_micro))
+            if not self._first:
+                _send(dx, pg.pp_prev_rank, bwd_group, "backward")
 
         for _ in range(warmup):
-            x = _p2p(recv_fwd_shape=self.tensor_shape, dtype=self.dtype, device=self.device)[0]
-            y = fwd(x)
-            _p2p(send_fwd=None if self._last else y.detach())
-            ins.append(x)
-            outs.append(y)
-        x = _p2p(recv_fwd_shape=self.tensor_shape, dtype=self.dtype, device=self.device)[0] if steady > 0 else None
-        for i in range(steady):
-            y = fwd(x)
-            dy = _p2p(send_fwd=None if self._last else y.detach(), recv_bwd_shape=self.tensor_shape,
-                      dtype=self.dtype, device=self.device)[1]
-            ins.append(x)
-            outs.append(y)
-            xo, yo = ins.popleft(), outs.popleft()
-            n_bwd += 1
-            dx = self._backward(xo, yo, dy, last_backward=(n_bwd == num_micro))
-            if i == steady - 1:
-                x = None
-                _p2p(send_bwd=dx)
-            else:
-                x = _p2p(send_bwd=dx, recv_fwd_shape=self.tensor_shape, dtype=self.dtype, device=self.device)[0]
+            fwd()
+        for _ in range(steady):
+            fwd()
+            bwd()
         for _ in range(warmup):
-            xo, yo = ins.popleft(), outs.popleft()
-            dy = _p2p(recv_bwd_shape=self.tensor_shape, dtype=self.dtype, device=self.device)[1]
-            n_bwd += 1
-            dx = self._backward(xo, yo, dy, last_backward=(n_bwd == num_micro))
-            _p2p(send_bwd=dx)
+            bwd()
         wait_sends()
         return loss_sum
-
 
     # ------------------------------------------------------------------ interleaved 1F1B
     def train_step_interleaved(self, data_iter, num_micro: int) -> torch.Tensor:

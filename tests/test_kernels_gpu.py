@@ -609,3 +609,27 @@ def test_wgrad_grouped_matches_per_expert(N, beta):
     assert _lib.ops().wgrad_grouped_(out, dy, x, offs, beta)
     torch.cuda.synchronize()
     assert rel(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("N,K", [(256, 512), (384, 256), (1536, 2048)])
+@pytest.mark.parametrize("wn", [False, True])
+def test_grouped_gemm_matches_per_expert(N, K, wn):
+    """One-launch grouped expert GEMM (csrc/grouped_gemm.hip) vs an fp32 per-expert reference:
+    empty experts, 1-row, ragged and > 256-row groups, both weight layouts ([G,N,K]: x w^T;
+    [G,K,N]: x w), a strided x, BN 256 and 128.  Rows past the last offset stay untouched."""
+    torch.manual_seed(6)
+    counts = torch.tensor([37, 0, 300, 1, 256, 0, 513], device="cuda", dtype=torch.int32)
+    G, T = counts.numel(), int(counts.sum())
+    offs = torch.cumsum(counts, 0, dtype=torch.int32)
+    xb = torch.randn(T + 5, K + 64, device="cuda", dtype=torch.bfloat16)
+    x = xb[:, 32: 32 + K]
+    w = torch.randn(G, K, N, device="cuda", dtype=torch.bfloat16) if wn else \
+        torch.randn(G, N, K, device="cuda", dtype=torch.bfloat16)
+    y = _lib.ops().grouped_gemm(x, w, offs, wn)
+    torch.cuda.synchronize()
+    off = 0
+    for e, n in enumerate(counts.tolist()):
+        ref = x[off:off + n].float() @ (w[e].float() if wn else w[e].float().t())
+        if n:
+            assert rel(y[off:off + n].float(), ref) < 1e-2, (e, n)
+        off += n
