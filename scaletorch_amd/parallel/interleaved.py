@@ -187,3 +187,90 @@ def simulate(P: int, V: int, M: int) -> None:
         nf = sum(1 for a in scheds[r] if not isinstance(a, Exchange) and a[0] == "F")
         if nf != T or nb != T:
             raise AssertionError(f"rank {r}: {nf} forward / {nb} backward steps, expected {T}")
+
+
+def simulate_channels(P: int, V: int, M: int, depth: int = 2) -> None:
+    """Replay every rank's schedule as the engine runs it (pipeline_parallel.py): each
+    message travels on a CHANNEL = (direction, ring seam or not), i.e. one direction
+    between one pair of ranks on its own communicator, whose stream runs that rank's ops
+    on the channel in issue order; receives are posted ``depth`` ahead of their use in
+    schedule order; a send is issued after the compute step that produced its tensor;
+    each rank's compute steps run in schedule order, a step waiting for its input.
+    Raises on a deadlock.  (``simulate`` proves the stricter one-ordered-stream model.)"""
+    scheds = [build_schedule(P, V, M, r) for r in range(P)]
+    T = M * V
+
+    def chan(kind, sender):
+        seam = (kind == "fwd" and sender == P - 1) or (kind == "bwd" and sender == 0)
+        return (kind, seam, sender)
+
+    # per rank: the compute steps in order, and the sends each step releases
+    steps, sends_after, recv_order = [], [], []
+    for r in range(P):
+        st, rel, ro = [], {}, {"fwd": [], "bwd": []}
+        last_step = None
+        for a in scheds[r]:
+            if isinstance(a, Exchange):
+                for kd, k in a.send:
+                    rel.setdefault(last_step, []).append((kd, k))
+                for kd, k in a.recv:
+                    ro[kd].append(k)
+            else:
+                st.append(a)
+                last_step = a
+        steps.append(st)
+        sends_after.append(rel)
+        recv_order.append(ro)
+    # channel queues: sender side (issued sends), receiver side (posted receives)
+    sq: dict = {}
+    rq: dict = {}
+    posted = [{"fwd": 0, "bwd": 0} for _ in range(P)]
+    delivered = [set() for _ in range(P)]  # (kind, receiver step) that arrived
+
+    def post(r):
+        for kd in ("fwd", "bwd"):
+            sender = (r - 1) % P if kd == "fwd" else (r + 1) % P
+            c = chan(kd, sender)
+            used = sum(1 for key in delivered[r] if key[0] == kd)
+            while posted[r][kd] < len(recv_order[r][kd]) and posted[r][kd] < used + depth:
+                rq.setdefault(c, []).append(recv_order[r][kd][posted[r][kd]])
+                posted[r][kd] += 1
+
+    pos = [0] * P
+    for r in range(P):
+        post(r)
+    while True:
+        progressed = False
+        for r in range(P):  # compute steps whose input has arrived
+            while pos[r] < len(steps[r]):
+                kind, k = steps[r][pos[r]]
+                need = None
+                if kind == "F" and not (r == 0 and fwd_chunk(k, P, V) == 0):
+                    need = ("fwd", k)
+                if kind == "B" and not (r == P - 1 and bwd_chunk(k, P, V) == V - 1):
+                    need = ("bwd", k)
+                if need is not None and need not in delivered[r]:
+                    break
+                for kd, kk in sends_after[r].get((kind, k), []):
+                    _, key = _peer_and_key(P, r, kd, kk, True)
+                    sq.setdefault(chan(kd, r), []).append(key[1])
+                pos[r] += 1
+                progressed = True
+        for c in list(sq):  # deliver matched channel heads
+            kd, _, sender = c
+            recv_rank = (sender + 1) % P if kd == "fwd" else (sender - 1) % P
+            while sq.get(c) and rq.get(c) and sq[c][0] == rq[c][0]:
+                delivered[recv_rank].add((kd, sq[c].pop(0)))
+                rq[c].pop(0)
+                progressed = True
+            if sq.get(c) and rq.get(c) and sq[c][0] != rq[c][0]:
+                raise AssertionError(f"channel {c}: send {sq[c][0]} meets receive {rq[c][0]} (order mismatch)")
+        for r in range(P):
+            post(r)
+        if all(pos[r] == len(steps[r]) for r in range(P)):
+            break
+        if not progressed:
+            raise AssertionError(f"channel deadlock (P={P}, V={V}, M={M}): steps at {pos}")
+    for r in range(P):
+        if len(steps[r]) != 2 * T:
+            raise AssertionError(f"rank {r}: {len(steps[r])} compute steps, expected {2 * T}")

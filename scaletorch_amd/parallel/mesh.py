@@ -119,6 +119,11 @@ class ProcessGroupManager:
         # FIFO of its own, so a receive posted ahead (activations) can never sit in front
         # of a send the peer is waiting for (gradients) -- parallel/pipeline_parallel.py
         self.pp_bwd_group, _ = self._family(("pp",), channel="pp_bwd")
+        # the interleaved schedule's ring seam (last stage -> first stage activations, first
+        # -> last gradients) on two more: at pp = 2 the seam pair is the SAME pair as the
+        # forward one, and sharing its communicator would put both directions in one queue
+        self.pp_seam_group, _ = self._family(("pp",), channel="pp_seam")
+        self.pp_seam_bwd_group, _ = self._family(("pp",), channel="pp_seam_bwd")
         self.ep_group, self.ep_group_ids = self._family(("ep",))
         self.dp_group, self.dp_group_ids = self._family(("dp",))
         self.cp_dp_group, self.cp_dp_group_ids = self._family(("dp", "cp"))

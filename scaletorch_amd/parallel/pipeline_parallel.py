@@ -298,9 +298,9 @@ class PipelineEngine:
     def train_step_interleaved(self, data_iter, num_micro: int) -> torch.Tensor:
         """Interleaved 1F1B over this rank's ``virtual_stages`` model chunks
         (parallel/interleaved.py has the schedule and its deadlock-free proof by
-        simulation).  Exchanges are batched p2p on the pipeline ring; a batch with
-        a receive is joined before the data is used, send-only batches stay in
-        flight until the end of the step.  The DP gradient sync is enabled for the
+        simulation).  Activations and gradients travel on their own communicators
+        (one FIFO per direction), receives are posted two ahead and waited right
+        before use, sends stay in flight until the end of the step.  The DP gradient sync is enabled for the
         last micro-batch of each chunk, so every bucket fires during backward."""
         from .interleaved import Exchange, build_schedule, bwd_chunk, fwd_chunk, micro_batch
 
@@ -308,7 +308,17 @@ class PipelineEngine:
         P, r, V, M = pg.pp_world_size, pg.pp_rank, self.virtual_stages, num_micro
         ring = pg.pp_group_ids
         nxt, prv = ring[(r + 1) % P], ring[(r - 1) % P]
+        # one communicator per (direction, seam): every channel carries ONE direction
+        # between ONE pair of ranks, so a receive posted ahead only ever waits for its
+        # own sender (interleaved.simulate_channels replays this model)
         group = pg.pp_group
+        bwd_group = getattr(pg, "pp_bwd_group", None) or group
+        seam_group = getattr(pg, "pp_seam_group", None) or group
+        seam_bwd_group = getattr(pg, "pp_seam_bwd_group", None) or bwd_group
+        fwd_out = seam_group if r == P - 1 else group        # our forward sends
+        fwd_in = seam_group if r == 0 else group             # our forward receives
+        bwd_out = seam_bwd_group if r == 0 else bwd_group    # our gradient sends
+        bwd_in = seam_bwd_group if r == P - 1 else bwd_group  # our gradient receives
         batches: list = []
 
         def batch(m):
@@ -316,43 +326,36 @@ class PipelineEngine:
                 batches.append(next(data_iter))
             return batches[m]
 
-        inputs, grads = {}, {}        # fwd step -> received input; bwd step -> received output grad
+        sched = build_schedule(P, V, M, r)
+        # receives per direction, in schedule order (= the sender's order on that
+        # direction's communicator): posted 2 ahead by the mailboxes, waited at use
+        n_recv = {"fwd": 0, "bwd": 0}
+        for a in sched:
+            if isinstance(a, Exchange):
+                for kind, _ in a.recv:
+                    n_recv[kind] += 1
+        box = {"fwd": _Mailbox(n_recv["fwd"], self.tensor_shape, self.dtype, self.device, prv, fwd_in, "forward"),
+               "bwd": _Mailbox(n_recv["bwd"], self.tensor_shape, self.dtype, self.device, nxt, bwd_in,
+                               "backward")}
+        inputs, grads = {}, {}        # fwd step -> posted receive of its input; bwd step -> of its output grad
         acts = {}                     # (chunk, micro) -> (x, y)
         outs, dxs = {}, {}            # fwd step -> output to send; bwd step -> input grad to send
         loss_sum = torch.zeros((), dtype=torch.float32, device=self.device)
-        for a in build_schedule(P, V, M, r):
+        for a in sched:
             if isinstance(a, Exchange):
-                ops, rbufs = [], []
                 for kind, k in a.send:
-                    t = outs.pop(k) if kind == "fwd" else dxs.pop(k)
-                    peer = nxt if kind == "fwd" else prv
-                    ops.append(dist.P2POp(dist.isend, t.contiguous(), peer, group))
-                    _STATS["send_forward" if kind == "fwd" else "send_backward"] += 1
-                    trace.record("pp.send_" + ("forward" if kind == "fwd" else "backward"), t, peer=peer)
+                    if kind == "fwd":
+                        _send(outs.pop(k), nxt, fwd_out, "forward")
+                    else:
+                        _send(dxs.pop(k), prv, bwd_out, "backward")
                 for kind, k in a.recv:
-                    buf = torch.empty(self.tensor_shape, dtype=self.dtype, device=self.device)
-                    peer = prv if kind == "fwd" else nxt
-                    ops.append(dist.P2POp(dist.irecv, buf, peer, group))
-                    rbufs.append((kind, k, buf))
-                    _STATS["recv_forward" if kind == "fwd" else "recv_backward"] += 1
-                    trace.record("pp.recv_" + ("forward" if kind == "fwd" else "backward"), buf, peer=peer)
-                works = dist.batch_isend_irecv(ops)
-                if rbufs:
-                    for w in works:
-                        w.wait()
-                    for kind, k, buf in rbufs:
-                        if kind == "fwd":
-                            inputs[k] = buf.requires_grad_(True)
-                        else:
-                            grads[k] = buf
-                else:
-                    _INFLIGHT.append((works, [op.tensor for op in ops]))
+                    (inputs if kind == "fwd" else grads)[k] = box[kind].take()
                 continue
             kind, k = a
             if kind == "F":
                 v, m = fwd_chunk(k, P, V), micro_batch(k, P, V)
                 first, last = r == 0 and v == 0, r == P - 1 and v == V - 1
-                x = None if first else inputs.pop(k)
+                x = None if first else inputs.pop(k).get().requires_grad_(True)
                 b = batch(m)
                 extra = self.head_kwargs_fn(b) if (last and self.head_kwargs_fn is not None) else {}
                 y = self.model(input_ids=b["input_ids"] if first else None, position_ids=b["position_ids"],
@@ -376,7 +379,7 @@ class PipelineEngine:
                 if r == P - 1 and v == V - 1:
                     y.backward()
                 else:
-                    torch.autograd.backward(y, grads.pop(k))
+                    torch.autograd.backward(y, grads.pop(k).get())
                 self.model.require_backward_grad_sync = True
                 self.model.final_backward = True
                 if x is not None:

@@ -162,6 +162,19 @@ def test_interleaved_1f1b_parity(pp, v, ga, extra):
     _compare(ref, res)
 
 
+def test_interleaved_schedules_deadlock_free_with_posted_receives():
+    """The engine's model (pipeline_parallel.py): one communicator per direction and ring
+    seam, receives posted 1-3 ahead, sends issued after their compute step -- every
+    (P, V, M) completes with every channel matched in order."""
+    from scaletorch_amd.parallel import interleaved as I
+
+    for P in (2, 3, 4, 8):
+        for V in (1, 2, 3, 4):
+            for M in (P, 2 * P, 4 * P):
+                for depth in (1, 2, 3):
+                    I.simulate_channels(P, V, M, depth)
+
+
 def test_interleaved_schedules_are_deadlock_free():
     """Every (P, V, M) schedule replays without deadlock under ordered-stream p2p
     semantics, every message matched in order, every step's input present; a
