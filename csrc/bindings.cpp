@@ -70,6 +70,10 @@ int st_xgmi_open(int64_t id, int r, const void* handle64);
 int st_xgmi_set_peer(int64_t id, int r, int64_t peer_id);
 int st_xgmi_all_reduce(int64_t id, const void* in, void* out, int64_t n, int dtype, int mode, int blocks,
                        hipStream_t st);
+int st_xgmi_pair(int64_t id, const void* in, void* out, int64_t n, int dtype, int mode, int partner, int blocks,
+                 hipStream_t st);
+int st_xgmi_collective_sim(const int64_t* ids, const void* const* ins, void* const* outs, const int* partners,
+                           int world, int64_t n, int dtype, int mode, int blocks, hipStream_t st);
 int st_xgmi_all_reduce_sim(const int64_t* ids, const void* const* ins, void* const* outs, int world, int64_t n,
                            int dtype, int mode, int blocks, hipStream_t st);
 int st_xgmi_error(int64_t id);
@@ -449,7 +453,19 @@ static int64_t xgmi_count(int64_t mode, int64_t world, const at::Tensor& inp, co
     TORCH_CHECK(inp.numel() == world * out.numel(), "xgmi reduce_scatter: input must hold world x out elements");
     return out.numel();
   }
-  TORCH_CHECK(mode == 0 || mode == 1, "xgmi: mode 0..3");
+  if (mode == 4) {
+    TORCH_CHECK(inp.numel() == out.numel() && inp.numel() % world == 0, "xgmi all_to_all: world equal chunks");
+    return inp.numel() / world;
+  }
+  if (mode == 5) {
+    TORCH_CHECK(out.numel() == 2 * inp.numel(), "xgmi pair all_gather: out must hold 2 x input elements");
+    return inp.numel();
+  }
+  if (mode == 6) {
+    TORCH_CHECK(inp.numel() == 2 * out.numel(), "xgmi pair reduce_scatter: input must hold 2 x out elements");
+    return out.numel();
+  }
+  TORCH_CHECK(mode == 0 || mode == 1, "xgmi: mode 0..6");
   TORCH_CHECK(inp.numel() == out.numel(), "xgmi all_reduce: same size");
   return inp.numel();
 }
@@ -468,11 +484,27 @@ void xgmi_all_reduce(int64_t id, const at::Tensor& inp, at::Tensor out, int64_t 
                               (int)mode, (int)blocks, cur_stream());
   TORCH_CHECK(rc == 0, "xgmi collective failed (", rc, "): size must be a multiple of 8 and fit the buffer");
 }
+// pair collective (mode 5 all-gather / 6 reduce-scatter) with `partner` over multiple paths
+void xgmi_pair(int64_t id, const at::Tensor& inp, at::Tensor out, int64_t mode, int64_t partner, int64_t blocks) {
+  TORCH_CHECK(mode == 5 || mode == 6, "xgmi_pair: mode 5 or 6");
+  TORCH_CHECK(inp.is_cuda() && out.is_cuda() && inp.device() == out.device(), "xgmi: GPU tensors");
+  TORCH_CHECK(inp.is_contiguous() && out.is_contiguous() && inp.scalar_type() == out.scalar_type(),
+              "xgmi: contiguous, same dtype");
+  TORCH_CHECK(inp.scalar_type() == at::kBFloat16 || inp.scalar_type() == at::kFloat, "xgmi: bf16 or fp32");
+  TORCH_CHECK(inp.data_ptr() != out.data_ptr(), "xgmi pair: out-of-place only");
+  const int world = st_xgmi_world(id);
+  TORCH_CHECK(world > 0, "xgmi: unknown communicator");
+  const int64_t n = xgmi_count(mode, world, inp, out);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(inp.device());
+  int rc = st_xgmi_pair(id, inp.data_ptr(), out.data_ptr(), n, inp.scalar_type() == at::kBFloat16 ? 0 : 1, (int)mode,
+                        (int)partner, (int)blocks, cur_stream());
+  TORCH_CHECK(rc == 0, "xgmi pair collective failed (", rc, ")");
+}
 void xgmi_set_timeout(int64_t id, double seconds) {
   TORCH_CHECK(st_xgmi_set_timeout(id, seconds) == 0, "xgmi_set_timeout: bad id or value");
 }
 void xgmi_all_reduce_sim(std::vector<int64_t> ids, std::vector<at::Tensor> ins, std::vector<at::Tensor> outs,
-                         int64_t mode, int64_t blocks) {
+                         int64_t mode, int64_t blocks, c10::OptionalArrayRef<int64_t> partners) {
   const size_t w = ids.size();
   TORCH_CHECK(w >= 1 && ins.size() == w && outs.size() == w, "xgmi_all_reduce_sim: one in/out per rank");
   std::vector<const void*> ip(w);
@@ -489,7 +521,12 @@ void xgmi_all_reduce_sim(std::vector<int64_t> ids, std::vector<at::Tensor> ins, 
   }
   TORCH_CHECK(ins[0].scalar_type() == at::kBFloat16 || ins[0].scalar_type() == at::kFloat, "xgmi: bf16 or fp32");
   c10::hip::HIPGuardMasqueradingAsCUDA g(ins[0].device());
-  int rc = st_xgmi_all_reduce_sim(ids.data(), ip.data(), op.data(), (int)w, n,
+  std::vector<int> pr;
+  if (partners.has_value()) {
+    TORCH_CHECK(partners->size() == w, "xgmi_all_reduce_sim: one partner per rank");
+    for (int64_t x : *partners) pr.push_back((int)x);
+  }
+  int rc = st_xgmi_collective_sim(ids.data(), ip.data(), op.data(), pr.empty() ? nullptr : pr.data(), (int)w, n,
                                   ins[0].scalar_type() == at::kBFloat16 ? 0 : 1, (int)mode, (int)blocks,
                                   cur_stream());
   TORCH_CHECK(rc == 0, "xgmi_all_reduce_sim failed (", rc, ")");
@@ -744,8 +781,9 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("xgmi_open(int id, int r, Tensor handle) -> ()", &xgmi_open);
   m.def("xgmi_set_peer(int id, int r, int peer) -> ()", &xgmi_set_peer);
   m.def("xgmi_all_reduce(int id, Tensor inp, Tensor(a!) out, int mode, int blocks) -> ()", &xgmi_all_reduce);
-  m.def("xgmi_all_reduce_sim(int[] ids, Tensor[] ins, Tensor(a!)[] outs, int mode, int blocks) -> ()",
+  m.def("xgmi_all_reduce_sim(int[] ids, Tensor[] ins, Tensor(a!)[] outs, int mode, int blocks, int[]? partners=None) -> ()",
         &xgmi_all_reduce_sim);
+  m.def("xgmi_pair(int id, Tensor inp, Tensor(a!) out, int mode, int partner, int blocks) -> ()", &xgmi_pair);
   m.def("xgmi_error(int id) -> int", &xgmi_error);
   m.def("xgmi_set_timeout(int id, float seconds) -> ()", &xgmi_set_timeout);
   m.def("xgmi_destroy(int id) -> ()", &xgmi_destroy);

@@ -64,6 +64,7 @@ struct Job {
   int rank;
   int* err;
   uint64_t timeout;  // spin bound in s_memrealtime ticks (100 MHz)
+  int partner;       // pair collectives (modes 5, 6): the other rank of the pair
 };
 struct Jobs {
   Job j[kMaxRanks];
@@ -101,6 +102,32 @@ ST_DEVICE bool block_barrier(const Peers& P, int rank, int world, int phase, uin
   __syncthreads();
   // every wave acquires (invalidates its CU's vector L1 / non-coherent L2 lines)
   // before reading what the peers published
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  return ok;
+}
+
+// The same handshake between the two ranks of a pair only (flags in each other's header).
+ST_DEVICE bool pair_barrier(const Peers& P, int rank, int partner, int phase, uint32_t epoch, int* err,
+                            uint64_t timeout) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  bool ok = true;
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(flag_ptr(P.buf[partner], phase, blockIdx.x, rank), epoch, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* mine = flag_ptr(P.buf[rank], phase, blockIdx.x, partner);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+        atomicExch(err, 1);
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   return ok;
 }
@@ -313,6 +340,139 @@ __global__ __launch_bounds__(kThreads) void reducescatter_kernel(Peers P, Jobs J
   }
 }
 
+// All-to-all (equal splits): every rank contributes W chunks of n8 vectors (chunk d for
+// rank d); out = [from rank 0 | from rank 1 | ...].  PUSH: block b writes slice b of
+// chunk d straight into rank d's area at slot [my rank] over the d-link (all W-1 links
+// busy at once, posted writes), then the per-block handshake, then every rank copies
+// its own area out.  The EP token dispatch / combine and the Ulysses head exchange.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void alltoall_kernel(Peers P, Jobs J, int world, int64_t n8, int64_t cap,
+                                                            uint32_t epoch) {
+  const Job& jb = J.j[blockIdx.y];
+  const int rank = jb.rank;
+  const T* __restrict__ in = (const T*)jb.in;
+  T* __restrict__ out = (T*)jb.out;
+  const int parity = epoch & 1;
+  const int64_t per = (n8 + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = blockIdx.x * per, hi = min(n8, lo + per);
+  for (int i = 0; i < world; ++i) {
+    const int d = (rank + i) % world;  // start with a different peer on every rank: spread the links
+    const rsrc_t dst = buf_rsrc(P.buf[d], cap);
+    for (int64_t v = lo + threadIdx.x; v < hi; v += blockDim.x)
+      put8<T>(dst, area_off<T>(0, parity, cap, (int64_t)rank * n8 + v), in + ((int64_t)d * n8 + v) * 8);
+  }
+  if (!block_barrier(P, rank, world, 0, epoch, jb.err, jb.timeout)) return;
+  const rsrc_t mine = buf_rsrc(P.buf[rank], cap);
+  for (int r = 0; r < world; ++r)
+    for (int64_t v = lo + threadIdx.x; v < hi; v += blockDim.x)
+      get8<T>(mine, area_off<T>(0, parity, cap, (int64_t)r * n8 + v), out + ((int64_t)r * n8 + v) * 8);
+}
+
+// ---- pair collectives over MULTIPLE paths (a 2-rank TP group on one node has ONE direct
+// xGMI link; the other W-2 GPUs' links are idle for it).  Block b's slice takes path
+// b % (1 + nrelay): path 0 = written straight into the partner's area over the direct
+// link, path i = written into relay R[i-1]'s memory (slot [my rank]) and read from there
+// by the partner -- two hops, through links the direct path does not use.  The relay GPU
+// runs nothing: its memory is only a staging area.  Relays = every other rank, in rank
+// order (both partners agree).  Only the pair synchronises (flags in each other's
+// header); relay slots are disjoint per source rank.
+ST_DEVICE int relay_of(int i, int rank, int partner) {  // i-th rank that is neither
+  const int lo = min(rank, partner), hi = max(rank, partner);
+  int r = i;
+  if (r >= lo) ++r;
+  if (r >= hi) ++r;
+  return r;
+}
+
+// where block b's slice of `src`'s message lives after the write: (buffer rank, byte offset)
+template <typename T>
+ST_DEVICE void pair_loc(int world, int src, int dst, int64_t per, int64_t cap, int parity, int& owner,
+                        uint32_t& base) {
+  const int npath = world - 1;  // direct + (world - 2) relays
+  const int path = blockIdx.x % npath;
+  if (path == 0) {
+    owner = dst;
+    base = area_off<T>(0, parity, cap, (int64_t)blockIdx.x * per);
+  } else {
+    owner = relay_of(path - 1, src, dst);
+    const int64_t slot = cap / kMaxRanks;  // bytes per source rank in a relay's area 1
+    const int64_t lb = blockIdx.x / npath;  // compacted block index on this path
+    base = (uint32_t)(kHeader + (int64_t)(2 + parity) * cap + (int64_t)src * slot +
+                      lb * per * 8 * (int64_t)sizeof(T));
+  }
+}
+
+// Pair all-gather: each of the two ranks contributes n8 vectors; out = [lower rank's |
+// higher rank's].
+template <typename T>
+__global__ __launch_bounds__(kThreads) void pair_allgather_kernel(Peers P, Jobs J, int world, int64_t n8,
+                                                                  int64_t cap, uint32_t epoch) {
+  const Job& jb = J.j[blockIdx.y];
+  const int rank = jb.rank, partner = jb.partner;
+  const T* __restrict__ in = (const T*)jb.in;
+  T* __restrict__ out = (T*)jb.out;
+  const int parity = epoch & 1;
+  const int64_t per = (n8 + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = blockIdx.x * per, hi = min(n8, lo + per);
+  const int me = rank < partner ? 0 : 1;
+  int owner;
+  uint32_t base;
+  pair_loc<T>(world, rank, partner, per, cap, parity, owner, base);  // where my slice goes
+  const rsrc_t dst = buf_rsrc(P.buf[owner], cap);
+  for (int64_t v = lo + threadIdx.x; v < hi; v += blockDim.x) {
+    put8<T>(dst, base + (uint32_t)((v - lo) * 8 * sizeof(T)), in + v * 8);
+    *reinterpret_cast<u32x4*>(out + ((int64_t)me * n8 + v) * 8) = *reinterpret_cast<const u32x4*>(in + v * 8);
+    if constexpr (sizeof(T) == 4)
+      *reinterpret_cast<u32x4*>(out + ((int64_t)me * n8 + v) * 8 + 4) = *reinterpret_cast<const u32x4*>(in + v * 8 + 4);
+  }
+  if (!pair_barrier(P, rank, partner, 0, epoch, jb.err, jb.timeout)) return;
+  pair_loc<T>(world, partner, rank, per, cap, parity, owner, base);  // where the partner's slice is
+  const rsrc_t src = buf_rsrc(P.buf[owner], cap);
+  for (int64_t v = lo + threadIdx.x; v < hi; v += blockDim.x)
+    get8<T>(src, base + (uint32_t)((v - lo) * 8 * sizeof(T)), out + ((int64_t)(1 - me) * n8 + v) * 8);
+}
+
+// Pair reduce-scatter: each rank contributes 2 x n8 vectors ([chunk of the lower rank |
+// chunk of the higher rank]); out = the sum of both ranks' chunk for me (fp32, lower
+// rank's term first: bitwise the same on both).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void pair_reducescatter_kernel(Peers P, Jobs J, int world, int64_t n8,
+                                                                      int64_t cap, uint32_t epoch) {
+  const Job& jb = J.j[blockIdx.y];
+  const int rank = jb.rank, partner = jb.partner;
+  const T* __restrict__ in = (const T*)jb.in;
+  T* __restrict__ out = (T*)jb.out;
+  const int parity = epoch & 1;
+  const int64_t per = (n8 + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = blockIdx.x * per, hi = min(n8, lo + per);
+  const int me = rank < partner ? 0 : 1;
+  int owner;
+  uint32_t base;
+  pair_loc<T>(world, rank, partner, per, cap, parity, owner, base);  // the partner's chunk goes out
+  const rsrc_t dst = buf_rsrc(P.buf[owner], cap);
+  for (int64_t v = lo + threadIdx.x; v < hi; v += blockDim.x)
+    put8<T>(dst, base + (uint32_t)((v - lo) * 8 * sizeof(T)), in + ((int64_t)(1 - me) * n8 + v) * 8);
+  if (!pair_barrier(P, rank, partner, 0, epoch, jb.err, jb.timeout)) return;
+  pair_loc<T>(world, partner, rank, per, cap, parity, owner, base);
+  const rsrc_t src = buf_rsrc(P.buf[owner], cap);
+  for (int64_t v = lo + threadIdx.x; v < hi; v += blockDim.x) {
+    float a[8], b[8];
+    sh_load8<T>(src, base + (uint32_t)((v - lo) * 8 * sizeof(T)), b);  // partner's term
+    const T* mine = in + ((int64_t)me * n8 + v) * 8;
+    if constexpr (sizeof(T) == 2) {
+      BF8 x = *reinterpret_cast<const BF8*>(mine);
+      unpack8(x, a);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = mine[i];
+    }
+    float s[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = me == 0 ? a[i] + b[i] : b[i] + a[i];
+    store_local8<T>(out + v * 8, s);
+  }
+}
+
 struct Comm {
   int rank = 0, world = 1;
   int64_t cap = 0;  // bytes per data area
@@ -325,9 +485,10 @@ struct Comm {
   uint64_t timeout = 200000000ull;  // 2 s of s_memrealtime ticks
 };
 
-// mode: 0 one-shot all-reduce, 1 two-shot all-reduce, 2 all-gather, 3 reduce-scatter.
-// n = elements of the per-rank CONTRIBUTION (all-gather) / of the OUTPUT (reduce-scatter) /
-// of the tensor (all-reduce).
+// mode: 0 one-shot all-reduce, 1 two-shot all-reduce, 2 all-gather, 3 reduce-scatter,
+// 4 all-to-all, 5 pair all-gather, 6 pair reduce-scatter.
+// n = elements of the per-rank CONTRIBUTION (all-gather, pair all-gather) / of the OUTPUT
+// (reduce-scatter, pair reduce-scatter) / of one chunk (all-to-all) / of the tensor (all-reduce).
 template <typename T>
 static void launch_t(const Peers& P, const Jobs& J, dim3 grid, int world, int64_t n8, int64_t cap, int mode,
                      uint32_t epoch, hipStream_t st) {
@@ -335,7 +496,10 @@ static void launch_t(const Peers& P, const Jobs& J, dim3 grid, int world, int64_
     case 0: oneshot_kernel<T><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch); break;
     case 1: twoshot_kernel<T><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch); break;
     case 2: allgather_kernel<T><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch); break;
-    default: reducescatter_kernel<T><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch); break;
+    case 3: reducescatter_kernel<T><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch); break;
+    case 4: alltoall_kernel<T><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch); break;
+    case 5: pair_allgather_kernel<T><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch); break;
+    default: pair_reducescatter_kernel<T><<<grid, kThreads, 0, st>>>(P, J, world, n8, cap, epoch); break;
   }
 }
 
@@ -437,7 +601,9 @@ static int launch(const Peers& P, const Jobs& J, int njobs, int world, int64_t n
 
 // bytes of one data area a collective of n elements needs on each rank
 static int64_t area_bytes(int mode, int world, int64_t n, int64_t elt) {
-  return mode == 3 ? (int64_t)world * n * elt : n * elt;
+  if (mode == 3 || mode == 4) return (int64_t)world * n * elt;
+  if (mode == 5 || mode == 6) return n * elt * kMaxRanks;  // a relay slot (cap / 8) must hold a path's share
+  return n * elt;
 }
 
 // Collective of n elements (dtype 0 = bf16, 1 = fp32); mode 0 = one-shot all-reduce,
@@ -447,7 +613,7 @@ static int64_t area_bytes(int mode, int world, int64_t n, int64_t elt) {
 int st_xgmi_all_reduce(int64_t id, const void* in, void* out, int64_t n, int dtype, int mode, int blocks,
                        hipStream_t st) {
   Comm* c = get(id);
-  if (!c || mode < 0 || mode > 3) return -2;
+  if (!c || mode < 0 || mode > 4) return -2;
   const int64_t elt = dtype == 0 ? 2 : 4;
   if (n % 8 || area_bytes(mode, c->world, n, elt) > c->cap || ((uintptr_t)in | (uintptr_t)out) % 16) return -2;
   for (int r = 0; r < c->world; ++r)
@@ -456,6 +622,24 @@ int st_xgmi_all_reduce(int64_t id, const void* in, void* out, int64_t n, int dty
   if (blocks <= 0 || blocks > kMaxBlocks) blocks = kMaxBlocks;
   Jobs J{};
   J.j[0] = Job{in, out, c->rank, c->err, c->timeout};
+  return launch(c->peers, J, 1, c->world, n, c->cap, dtype, mode, blocks, ++c->epoch, st);
+}
+
+// Pair collective (mode 5 all-gather / 6 reduce-scatter) between this rank and `partner`
+// over the direct link plus 2-hop paths through every other rank's memory.  Both
+// partners must call it in the same order; the other ranks need not call anything.
+int st_xgmi_pair(int64_t id, const void* in, void* out, int64_t n, int dtype, int mode, int partner, int blocks,
+                 hipStream_t st) {
+  Comm* c = get(id);
+  if (!c || (mode != 5 && mode != 6) || partner < 0 || partner >= c->world || partner == c->rank) return -2;
+  const int64_t elt = dtype == 0 ? 2 : 4;
+  if (n % 8 || area_bytes(mode, c->world, n, elt) > c->cap || ((uintptr_t)in | (uintptr_t)out) % 16) return -2;
+  for (int r = 0; r < c->world; ++r)
+    if (!c->peers.buf[r]) return -3;
+  if (n == 0) return 0;
+  if (blocks <= 0 || blocks > kMaxBlocks) blocks = kMaxBlocks;
+  Jobs J{};
+  J.j[0] = Job{in, out, c->rank, c->err, c->timeout, partner};
   return launch(c->peers, J, 1, c->world, n, c->cap, dtype, mode, blocks, ++c->epoch, st);
 }
 
@@ -474,21 +658,35 @@ int st_xgmi_set_timeout(int64_t id, double seconds) {
 
 // Simulation: comms ids[0..world) (wired with st_xgmi_set_peer, one process)
 // all-reduce ins[r] -> outs[r] in ONE launch (rank r = blockIdx.y).
+int st_xgmi_collective_sim(const int64_t* ids, const void* const* ins, void* const* outs, const int* partners,
+                           int world, int64_t n, int dtype, int mode, int blocks, hipStream_t st);
+
 int st_xgmi_all_reduce_sim(const int64_t* ids, const void* const* ins, void* const* outs, int world, int64_t n,
                            int dtype, int mode, int blocks, hipStream_t st) {
+  return st_xgmi_collective_sim(ids, ins, outs, nullptr, world, n, dtype, mode, blocks, st);
+}
+
+// Simulation of any mode; partners[r] = rank r's pair partner (modes 5 / 6; every rank in a
+// pair), may be null otherwise.
+int st_xgmi_collective_sim(const int64_t* ids, const void* const* ins, void* const* outs, const int* partners,
+                           int world, int64_t n, int dtype, int mode, int blocks, hipStream_t st) {
   if (world < 1 || world > kMaxRanks) return -2;
   Jobs J{};
   Comm* c0 = get(ids[0]);
   if (!c0 || c0->world != world) return -2;
   const int64_t elt = dtype == 0 ? 2 : 4;
-  if (mode < 0 || mode > 3 || n % 8 || area_bytes(mode, world, n, elt) > c0->cap) return -2;
+  if (mode < 0 || mode > 6 || n % 8 || area_bytes(mode, world, n, elt) > c0->cap) return -2;
+  if ((mode == 5 || mode == 6) && partners == nullptr) return -2;
   if (blocks <= 0 || blocks > kMaxBlocks) blocks = kMaxBlocks;
   uint32_t epoch = 0;
   for (int r = 0; r < world; ++r) {
     Comm* c = get(ids[r]);
     if (!c || c->rank != r || c->world != world || c->cap != c0->cap) return -2;
     if (((uintptr_t)ins[r] | (uintptr_t)outs[r]) % 16) return -2;
-    J.j[r] = Job{ins[r], outs[r], r, c->err, c->timeout};
+    const int partner = partners ? partners[r] : -1;
+    if ((mode == 5 || mode == 6) && (partner < 0 || partner >= world || partner == r || partners[partner] != r))
+      return -2;
+    J.j[r] = Job{ins[r], outs[r], r, c->err, c->timeout, partner};
     epoch = ++c->epoch;  // every comm advances together
   }
   if (n == 0) return 0;

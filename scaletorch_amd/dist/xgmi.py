@@ -19,6 +19,15 @@ each of the others, so a TP group can all-reduce by READING its peers' buffers:
   then block b of every rank pulls slice b of ALL peers' data at once (all 7
   links busy) -- the sequence-parallel activation gather / gradient scatter;
 * up to 256 workgroups (one per CU) pull at once, sized by message;
+* ``all_to_all(t)``: equal-split exchange by PUSH -- every rank writes chunk d
+  straight into rank d's buffer (all 7 links, posted writes), one handshake, a local
+  copy out: the EP token dispatch/combine (reference ep_comms.py:14-38, RCCL
+  all_to_all_single there);
+* ``pair_all_gather`` / ``pair_reduce_scatter``: a 2-rank group (TP = 2) has ONE
+  direct link; these split the message over the direct link AND 2-hop paths through
+  the memory of every other GPU of the node (the relay GPU runs nothing), so all 7
+  links of each partner carry a share.  The communicator spans the node; only the
+  pair calls it (``XgmiComm(node_group)``, any disjoint pairs at once);
 * every wait is bounded (``ST_XGMI_TIMEOUT_S``, default 2 s): a peer that never
   arrives sets an error word instead of hanging the GPU; ``check()`` (polled by the
   trainer at every logging step, tensor_parallel.check_xgmi) turns it into an
@@ -50,7 +59,8 @@ def _blocks_for(nbytes: int) -> int:
     return int(min(256, max(8, nbytes // (64 << 10))))
 
 
-_MODES = {"oneshot": 0, "twoshot": 1, "all_gather": 2, "reduce_scatter": 3}
+_MODES = {"oneshot": 0, "twoshot": 1, "all_gather": 2, "reduce_scatter": 3, "all_to_all": 4,
+          "pair_all_gather": 5, "pair_reduce_scatter": 6}
 
 
 class XgmiAllReduce:
@@ -142,10 +152,55 @@ class XgmiAllReduce:
         return out
 
     @staticmethod
-    def collective_sim(comms, ins, outs, op: str) -> None:
-        """Simulation of ``op`` (all_gather | reduce_scatter) across ``comms`` in ONE launch."""
-        nbytes = (ins[0] if op == "all_gather" else outs[0]).numel() * ins[0].element_size()
-        _ops().xgmi_all_reduce_sim([c.id for c in comms], ins, outs, _MODES[op], _blocks_for(nbytes))
+    def collective_sim(comms, ins, outs, op: str, partners: list[int] | None = None) -> None:
+        """Simulation of ``op`` (all_gather | reduce_scatter | all_to_all | pair_all_gather |
+        pair_reduce_scatter; pairs: ``partners[r]``) across ``comms`` in ONE launch."""
+        world = len(comms)
+        if op in ("all_gather", "pair_all_gather"):
+            nbytes = ins[0].numel() * ins[0].element_size()
+        elif op == "all_to_all":
+            nbytes = ins[0].numel() * ins[0].element_size() // world
+        else:
+            nbytes = outs[0].numel() * outs[0].element_size()
+        _ops().xgmi_all_reduce_sim([c.id for c in comms], ins, outs, _MODES[op], _blocks_for(nbytes), partners)
+
+    def all_to_all(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Equal-split all-to-all of dim 0 ([world * n] per rank: chunk d goes to rank d;
+        out[r-th chunk] came from rank r) -- RCCL when the kernels do not apply."""
+        if out is None:
+            out = torch.empty_like(t)
+        if not self.supports(t) or out.data_ptr() % 16 or t.shape[0] % self.world:
+            dist.all_to_all_single(out, t.contiguous(), group=self.group)
+            return out
+        _ops().xgmi_all_reduce(self.id, t, out, _MODES["all_to_all"],
+                               _blocks_for(t.numel() * t.element_size() // self.world))
+        return out
+
+    def _pair_ok(self, n_elems: int, t: torch.Tensor) -> bool:
+        # a relay holds a path's share of the message in a slot of cap / 8 bytes
+        return (t.is_cuda and t.dtype in (torch.bfloat16, torch.float32) and t.is_contiguous()
+                and n_elems % 8 == 0 and n_elems * t.element_size() * 8 <= self.cap and t.data_ptr() % 16 == 0)
+
+    def pair_all_gather(self, t: torch.Tensor, partner: int, out: torch.Tensor | None = None) -> torch.Tensor:
+        """2-rank all-gather with ``partner`` (a rank of this communicator's group) over
+        the direct link + 2-hop relays: out = [lower rank's t | higher rank's t]."""
+        if out is None:
+            out = torch.empty((2 * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        if not self._pair_ok(t.numel(), t) or out.data_ptr() % 16:
+            raise ValueError("pair_all_gather: message does not fit the kernels (use the pair's RCCL group)")
+        _ops().xgmi_pair(self.id, t, out, _MODES["pair_all_gather"], partner, _blocks_for(t.numel() * t.element_size()))
+        return out
+
+    def pair_reduce_scatter(self, t: torch.Tensor, partner: int, out: torch.Tensor | None = None) -> torch.Tensor:
+        """2-rank reduce-scatter with ``partner``: t = [chunk of the lower rank | chunk of the
+        higher rank]; out = this rank's chunk summed over the pair (fp32, fixed order)."""
+        if out is None:
+            out = torch.empty((t.shape[0] // 2,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        if not self._pair_ok(out.numel(), t) or out.data_ptr() % 16:
+            raise ValueError("pair_reduce_scatter: message does not fit the kernels (use the pair's RCCL group)")
+        _ops().xgmi_pair(self.id, t, out, _MODES["pair_reduce_scatter"], partner,
+                         _blocks_for(out.numel() * out.element_size()))
+        return out
 
     def all_reduce(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         """Sum of ``t`` over the group into ``out`` (default: in place)."""

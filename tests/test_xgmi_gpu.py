@@ -163,3 +163,61 @@ def test_xgmi_absent_peer_times_out_and_check_raises():
     finally:
         for c in comms:
             c.close()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("n", [8, 4096 + 8, 200_000])
+def test_xgmi_all_to_all_simulated(world, dtype, n):
+    """Push all-to-all (mode 4): rank r's chunk s of the output is rank s's chunk r, bitwise,
+    over several epochs (both buffer parities)."""
+    assert _lib.load(), _lib.load_error()
+    comms = XgmiAllReduce.simulate(world, max_bytes=8 << 20)
+    try:
+        torch.manual_seed(2)
+        for _ in range(3):
+            xs = [torch.randn(world * n, device="cuda", dtype=dtype) for _ in range(world)]
+            outs = [torch.empty_like(x) for x in xs]
+            XgmiAllReduce.collective_sim(comms, xs, outs, "all_to_all")
+            torch.cuda.synchronize()
+            for c in comms:
+                c.check()
+            for r in range(world):
+                ref = torch.cat([xs[s][r * n:(r + 1) * n] for s in range(world)])
+                assert torch.equal(outs[r], ref)
+    finally:
+        for c in comms:
+            c.close()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("n", [8, 4096 + 8, 200_000])
+def test_xgmi_pair_multipath_simulated(world, dtype, n):
+    """Pair all-gather / reduce-scatter over the direct path + 2-hop relays through the
+    other ranks' memory (modes 5 / 6), all world/2 pairs at once: AG bitwise the
+    concatenation in rank order; RS the pair sum rounded once, identical on both partners."""
+    assert _lib.load(), _lib.load_error()
+    comms = XgmiAllReduce.simulate(world, max_bytes=8 << 20)
+    partners = [r ^ 1 for r in range(world)]
+    try:
+        torch.manual_seed(3)
+        for _ in range(3):
+            xs = [torch.randn(n, device="cuda", dtype=dtype) for _ in range(world)]
+            outs = [torch.empty(2 * n, device="cuda", dtype=dtype) for _ in range(world)]
+            XgmiAllReduce.collective_sim(comms, xs, outs, "pair_all_gather", partners)
+            big = [torch.randn(2 * n, device="cuda", dtype=dtype) for _ in range(world)]
+            rs = [torch.empty(n, device="cuda", dtype=dtype) for _ in range(world)]
+            XgmiAllReduce.collective_sim(comms, big, rs, "pair_reduce_scatter", partners)
+            torch.cuda.synchronize()
+            for c in comms:
+                c.check()
+            for r in range(world):
+                lo, hi = min(r, partners[r]), max(r, partners[r])
+                assert torch.equal(outs[r], torch.cat([xs[lo], xs[hi]]))
+                me = 0 if r == lo else 1
+                ref = (big[lo][me * n:(me + 1) * n].float() + big[hi][me * n:(me + 1) * n].float()).to(dtype)
+                assert torch.equal(rs[r], ref)
+    finally:
+        for c in comms:
+            c.close()
