@@ -234,3 +234,60 @@ class XgmiAllReduce:
 
 
 XgmiComm = XgmiAllReduce  # the communicator carries all three collectives
+
+
+def _max_bytes_default() -> int:
+    import os
+
+    return int(float(os.environ.get("ST_XGMI_MAX_MB", "512")) * (1 << 20))
+
+
+def node_group():
+    """The process group of the ranks on this node (collective over the WORLD: every rank
+    creates every node's group, in the same order)."""
+    world = dist.get_world_size()
+    hosts = [None] * world
+    dist.all_gather_object(hosts, socket.gethostname())
+    mine = None
+    for h in sorted(set(hosts)):
+        ranks = [r for r in range(world) if hosts[r] == h]
+        g = dist.new_group(ranks=ranks)
+        if h == socket.gethostname():
+            mine = (g, ranks)
+    return mine
+
+
+class PairPath:
+    """A 2-rank group's multipath transport: the node-wide communicator plus this rank's
+    partner (its node-group rank) -- ``all_gather`` / ``reduce_scatter`` in the 2-rank
+    group's rank order over the direct link and 2-hop relays."""
+
+    def __init__(self, comm: XgmiAllReduce, partner: int, lower: bool):
+        self.comm, self.partner, self.lower = comm, partner, lower
+
+    def fits(self, n_elems: int, t: torch.Tensor) -> bool:
+        return self.comm._pair_ok(n_elems, t)
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        return self.comm.pair_all_gather(t, self.partner)
+
+    def reduce_scatter(self, t: torch.Tensor) -> torch.Tensor:
+        return self.comm.pair_reduce_scatter(t, self.partner)
+
+
+def setup_pair_path(pair_group) -> PairPath | None:
+    """Collective over the WORLD (call on every rank, at start-up): the node communicator
+    and, for ranks whose ``pair_group`` has 2 ranks on this node with group rank order =
+    node rank order, their PairPath (else None)."""
+    ng, ranks = node_group()
+    comm = XgmiAllReduce(ng, max_bytes=_max_bytes_default())
+    if pair_group is None or dist.get_world_size(pair_group) != 2:
+        return None
+    me = dist.get_rank()
+    other = dist.get_global_rank(pair_group, 1 - dist.get_rank(pair_group))
+    if other not in ranks:
+        return None
+    lower = me < other
+    if lower != (dist.get_rank(pair_group) == 0):  # the pair ops order by node rank
+        return None
+    return PairPath(comm, ranks.index(other), lower)

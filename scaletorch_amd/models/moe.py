@@ -63,11 +63,46 @@ def all_to_all_rows(x, out_splits, in_splits, group):
 
 # ---------------------------------------------------------------- capacity-bounded dispatch
 # EP dispatch options (trainer: --moe_capacity_factor / --moe_ep_chunks)
-_DISPATCH = {"capacity_factor": 0.0, "chunks": 1}
+_DISPATCH = {"capacity_factor": 0.0, "chunks": 1, "comm": "rccl"}
+_EP_XGMI: dict = {}      # id(ep group) -> dist/xgmi.XgmiAllReduce
+_EP_STREAMS: dict = {}   # device -> side stream of the xGMI all-to-alls
 
 
-def set_moe_dispatch(capacity_factor: float = 0.0, chunks: int = 1) -> None:
-    _DISPATCH.update(capacity_factor=float(capacity_factor), chunks=max(1, int(chunks)))
+def set_moe_dispatch(capacity_factor: float = 0.0, chunks: int = 1, comm: str = "rccl") -> None:
+    if comm not in ("rccl", "xgmi"):
+        raise ValueError(f"ep_comm must be rccl or xgmi, got {comm!r}")
+    _DISPATCH.update(capacity_factor=float(capacity_factor), chunks=max(1, int(chunks)), comm=comm)
+
+
+def setup_ep_xgmi(group) -> None:
+    """Create the EP group's xGMI communicator (collective over the group, at start-up):
+    the capacity dispatch's equal-split all-to-alls then PUSH rows straight into the
+    peers' buffers over all 7 links (csrc/xgmi_allreduce.hip mode 4)."""
+    from ..dist.xgmi import XgmiAllReduce, _max_bytes_default
+
+    if group is not None and C.get_world_size(group) > 1:
+        _EP_XGMI[id(group)] = XgmiAllReduce(group, max_bytes=_max_bytes_default())
+
+
+def _ep_a2a(x: torch.Tensor, group, async_op: bool):
+    """Equal-split all-to-all: the xGMI push kernel when set up and the message fits
+    (on a side stream when ``async_op``), else RCCL.  Returns out or (out, work)."""
+    comm = _EP_XGMI.get(id(group)) if (_DISPATCH["comm"] == "xgmi" and x.is_cuda) else None
+    if comm is None or not comm.supports(x) or x.shape[0] % comm.world:
+        return C.all_to_all(x, group=group, async_op=async_op)
+    if not async_op:
+        return comm.all_to_all(x)
+    from ..parallel.tensor_parallel import _StreamWork
+
+    st = _EP_STREAMS.get(x.device.index)
+    if st is None:
+        st = _EP_STREAMS[x.device.index] = torch.cuda.Stream(device=x.device)
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        out = comm.all_to_all(x)
+    x.record_stream(st)
+    out.record_stream(torch.cuda.current_stream())
+    return out, _StreamWork(st)
 
 
 class _A2AStart(torch.autograd.Function):
@@ -79,14 +114,14 @@ class _A2AStart(torch.autograd.Function):
     def forward(ctx, x, holder, group):
         trace.record("ep.all_to_all", x, group_size=C.get_world_size(group))
         ctx.group = group
-        out, work = C.all_to_all(x.contiguous(), group=group, async_op=True)
+        out, work = _ep_a2a(x.contiguous(), group, async_op=True)
         holder.append(work)
         return out
 
     @staticmethod
     def backward(ctx, g):
         trace.record("ep.all_to_all_bwd", g, group_size=C.get_world_size(ctx.group))
-        return C.all_to_all(g.contiguous(), group=ctx.group), None, None
+        return _ep_a2a(g.contiguous(), ctx.group, async_op=False), None, None
 
 
 class _A2AWait(torch.autograd.Function):

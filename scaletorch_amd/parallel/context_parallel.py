@@ -222,11 +222,11 @@ class _RingAttnFn(torch.autograd.Function):
         """K/V rotate as in the forward.  The fp32 dK/dV accumulator of a block follows
         it one step BEHIND: at step j a rank computes its partial for the block in hand
         into a fresh buffer, and only then adds the accumulator that the previous rank
-        sent at the end of ITS step j-1 -- received during this step's flash backward --
-        and forwards the sum (async) without waiting for that send.  After cp steps
-        every accumulator is home; only the last hop is exposed.  Per-pair message order
-        (K/V_0, A_0, K/V_1, A_1, ...) is matched by posting each step's accumulator
-        receive before its K/V receive."""
+        finished at the end of ITS step j-1 -- exchanged in the same async batch as this
+        step's K/V, so it travels during this step's flash backward -- and forwards the
+        sum with the next step's batch.  After cp steps every accumulator is home; only
+        the last hop is exposed.  Within each batch the accumulator precedes the K/V
+        block on both ends (messages between a pair match in issue order)."""
         q, kv, out = ctx.saved_tensors[:3]
         lses = ctx.saved_tensors[3:]
         H, Hkv, D, scale, zigzag = ctx.meta
@@ -237,18 +237,24 @@ class _RingAttnFn(torch.autograd.Function):
         dout = dout.contiguous()
         dq = torch.zeros(q.shape, dtype=torch.float32, device=q.device)
         cur = kv.contiguous()
-        in_flight = []  # (tensor, works) of accumulator sends: kept alive until they complete
+        a_out = None  # accumulator finished last step, forwarded in this step's exchange
         for j in range(cp):
             src = (rank - j) % cp
-            recvs = []
+            sends, recvs = [], []
             a_in = kv_next = None
+            if a_out is not None:
+                sends.append(a_out)
+            if j < cp - 1:
+                sends.append(cur)
             if j >= 1:  # accumulator of this block from the previous rank (its step j-1)
                 a_in = torch.empty(kv.shape, dtype=torch.float32, device=q.device)
                 recvs.append(a_in)
             if j < cp - 1:
                 kv_next = torch.empty_like(cur)
                 recvs.append(kv_next)
-            works = _ring_p2p([cur] if j < cp - 1 else [], recvs, group, cp, rank)
+            # one batch: the accumulator and K/V travel in the same group in both directions
+            # (at cp = 2 next == prev: separate send-only groups would meet head-on)
+            works = _ring_p2p(sends, recvs, group, cp, rank)  # joined below, after this step's compute
             part = torch.zeros(kv.shape, dtype=torch.float32, device=q.device)
             for (ko, kn, kg) in _chunks_of(src, S, cp, s, zigzag):
                 kc, vc = cur[:, ko: ko + kn, :Hkv], cur[:, ko: ko + kn, Hkv:]
@@ -265,15 +271,13 @@ class _RingAttnFn(torch.autograd.Function):
                 w.wait()
             if a_in is not None:
                 part.add_(a_in)
-            in_flight.append((part, _ring_p2p([part], [], group, cp, rank)))
+            a_out = part
             if kv_next is not None:
                 cur = kv_next
         home = torch.empty(kv.shape, dtype=torch.float32, device=q.device)
-        for w in _ring_p2p([], [home], group, cp, rank):  # own block's accumulator, last hop
+        works = _ring_p2p([a_out], [home], group, cp, rank)  # own block's accumulator: the last hop
+        for w in works:
             w.wait()
-        for _, works in in_flight:
-            for w in works:
-                w.wait()
         return dq.to(q.dtype), home.to(kv.dtype), None, None, None, None, None
 
 

@@ -55,6 +55,18 @@ def set_tp_comm(kind: str) -> None:
     _TP_COMM = kind
 
 
+_PAIR: list = [None]  # dist/xgmi.PairPath of a 2-rank TP group (multipath SP collectives)
+
+
+def setup_tp_pair_path(group) -> None:
+    """Collective over the WORLD at start-up (--tp_comm xgmi, tp = 2 on one node): the SP
+    all-gather / reduce-scatter of the 2-rank TP group then runs over the direct link
+    plus 2-hop relays through the other GPUs (dist/xgmi.py pair collectives)."""
+    from ..dist.xgmi import setup_pair_path
+
+    _PAIR[0] = setup_pair_path(group)
+
+
 class _StreamWork:
     """Async handle for an all-reduce issued on a side stream."""
 
@@ -196,6 +208,9 @@ def _gather_seq(x: torch.Tensor, group) -> torch.Tensor:
         return x
     _trace("sp.all_gather", x, ws)
     xg = _xgmi_comm(group) if x.is_cuda else None
+    pair = _PAIR[0] if (xg is not None and ws == 2) else None
+    if pair is not None and pair.fits(x.numel(), x):
+        xg = pair  # multipath: direct link + 2-hop relays
     gather = xg.all_gather if xg is not None else (lambda t: C.all_gather(t, group=group))
     if x.shape[0] == 1:
         return gather(x[0].contiguous()).unsqueeze(0)
@@ -210,6 +225,9 @@ def _reduce_scatter_seq(x: torch.Tensor, group) -> torch.Tensor:
         return x
     _trace("sp.reduce_scatter", x, ws)
     xg = _xgmi_comm(group) if x.is_cuda else None
+    pair = _PAIR[0] if (xg is not None and ws == 2) else None
+    if pair is not None and pair.fits(x.numel() // 2, x):
+        xg = pair  # multipath: direct link + 2-hop relays
     scatter = xg.reduce_scatter if xg is not None else (lambda t: C.reduce_scatter(t, group=group))
     if x.shape[0] == 1:
         return scatter(x[0].contiguous()).unsqueeze(0)

@@ -71,6 +71,9 @@ class ParallelArguments:
         "help": "EP dispatch: 0 = dropless (exact splits: one host read of the routing counts per MoE layer); "
                 "> 0 = static per-(source, destination) capacity ceil(f * T * k / ep) rows: no host sync, rows "
                 "past the capacity are dropped (counted in the layer's dropped_rows)"})
+    ep_comm: str = field(default="rccl", metadata={
+        "help": "EP all-to-all transport of the capacity dispatch: rccl | xgmi (push all-to-all over IPC peer "
+                "memory, dist/xgmi.py; falls back to RCCL for messages it does not take)"})
     moe_ep_chunks: int = field(default=1, metadata={
         "help": "EP dispatch pipelining (capacity mode): the tokens are dispatched in this many chunks, each "
                 "chunk's all-to-all overlapping the previous chunk's expert GEMMs"})
@@ -90,6 +93,8 @@ class ParallelArguments:
             if getattr(self, "gradient_accumulation_steps", 1) % self.pipeline_parallel_size:
                 raise ValueError("interleaved 1F1B needs gradient_accumulation_steps divisible by "
                                  "pipeline_parallel_size")
+        if self.ep_comm not in {"rccl", "xgmi"}:
+            raise ValueError(f"ep_comm must be rccl or xgmi, got {self.ep_comm}")
         if self.moe_capacity_factor < 0 or self.moe_ep_chunks < 1:
             raise ValueError("moe_capacity_factor must be >= 0 and moe_ep_chunks >= 1")
         if self.backend not in {"nccl", "gloo", "hccl"}:

@@ -57,13 +57,21 @@ class Trainer:
 
                 debug.enable(timeout_s=a.timeout_s)
         if a.tensor_parallel_size > 1:
-            from ..parallel.tensor_parallel import set_tp_comm
+            from ..parallel.tensor_parallel import set_tp_comm, setup_tp_pair_path
 
             set_tp_comm(a.tp_comm)
+            if (a.tp_comm == "xgmi" and a.tensor_parallel_size == 2 and a.backend == "nccl"
+                    and torch.cuda.is_available() and not a.use_cpu):
+                setup_tp_pair_path(mesh.tp_group())  # collective over the world, before any model code
         from ..models.attention_backends import set_use_flash_attention
         from ..models.moe import set_moe_dispatch
 
-        set_moe_dispatch(a.moe_capacity_factor, a.moe_ep_chunks)
+        set_moe_dispatch(a.moe_capacity_factor, a.moe_ep_chunks, a.ep_comm)
+        if (a.ep_comm == "xgmi" and a.expert_parallel_size > 1 and a.backend == "nccl" and torch.cuda.is_available()
+                and not a.use_cpu):
+            from ..models.moe import setup_ep_xgmi
+
+            setup_ep_xgmi(mesh.pgm.ep_group)  # collective over each EP group, at start-up
 
         set_use_flash_attention(a.use_flash_attention)
         if a.context_parallel_size > 1:

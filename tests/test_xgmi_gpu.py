@@ -72,7 +72,7 @@ def _ipc_worker(rank, world, port, q):
 
         xgmi.dist.all_gather_object = fake_gather
         try:
-            comm = xgmi.XgmiAllReduce(max_bytes=1 << 20, oneshot_max=64 << 10)
+            comm = xgmi.XgmiAllReduce(max_bytes=1 << 20, oneshot_max=64 << 10)  # noqa: F841
         except RuntimeError as e:
             q.put((rank, "skip", str(e)))
             return
@@ -84,6 +84,24 @@ def _ipc_worker(rank, world, port, q):
             torch.cuda.synchronize()
             comm.check()
             res.append(x.float().sum().item())
+        # push all-to-all over real IPC mappings: chunk s of the output = rank s's chunk for me
+        n = 4096
+        x = torch.arange(world * n, device="cuda", dtype=torch.float32) + 1e5 * rank
+        y = comm.all_to_all(x)
+        torch.cuda.synchronize()
+        comm.check()
+        ok_a2a = all(torch.equal(y[s * n:(s + 1) * n], torch.arange(rank * n, (rank + 1) * n, device="cuda",
+                                                                     dtype=torch.float32) + 1e5 * s)
+                     for s in range(world))
+        res.append(bool(ok_a2a))
+        if world % 2 == 0:  # multipath pair all-gather (relays = the other processes' buffers)
+            partner = rank ^ 1
+            x = torch.full((2048,), float(rank), device="cuda", dtype=torch.bfloat16)
+            y = comm.pair_all_gather(x, partner)
+            torch.cuda.synchronize()
+            comm.check()
+            lo, hi = min(rank, partner), max(rank, partner)
+            res.append(bool((y[:2048] == lo).all() and (y[2048:] == hi).all()))
         q.put((rank, "ok", res))
         comm.close()
     except Exception as e:  # noqa: BLE001
@@ -109,8 +127,9 @@ def test_xgmi_ipc_processes_same_gpu(world):
     if "skip" in kinds:
         pytest.skip(f"IPC open on a shared GPU unsupported here: {got}")
     assert kinds == {"ok"}, got
-    sums = [v for _, _, v in sorted(got)]
-    assert all(s == sums[0] for s in sums)  # identical reduced tensors on every rank
+    res = [v for _, _, v in sorted(got)]
+    assert all(r[:2] == res[0][:2] for r in res)  # identical reduced tensors on every rank
+    assert all(all(r[2:]) for r in res), res  # all-to-all / pair all-gather correct on every rank
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
