@@ -13,23 +13,21 @@
 //
 // Design (CDNA4-first; the synchronisation skeleton is the 4-stage ring of
 // csrc/wgrad_gemm.hip):
-//   * 256 x BN output tile (BN = 256 or 128), 8 waves, 16x16x32 bf16 MFMA, K in 32-wide
-//     tiles through a ring of 4 LDS stages (3 in flight), LDS-DMA from inline asm with
-//     counted vmcnt + raw barriers.
+//   * 256 x BN output tile (BN = 256 or 128), 8 waves, 16x16x32 bf16 MFMA, K in 64-wide
+//     tiles, double-buffered (128 KiB of LDS at BN = 256): tile kt+1's LDS-DMA (inline asm,
+//     so hipcc does not drain it) is issued right after the barrier that retires tile kt
+//     and runs under tile kt's MFMAs.
 //   * grid = (ceil(T/256) + G) M-tile slots x N-tiles (an upper bound of sum_g ceil(n_g/256));
 //     a workgroup maps its slot to (group, M-tile) by a binary search of the per-group
 //     tile-count prefix (device, computed by the caller); surplus slots exit at once.
 //   * rows past a group's end: the buffer descriptor's range ends at the group's last
 //     row, so they load as zeros and are not stored.
-//   * LDS images, both conflict-free by construction:
-//       row image (X, and W in WT layout): [16-row block][8-k chunk (4)][row (16)][16 B] --
-//         a fragment read (two ds_read_b64 per lane) covers one 256-B bank row per
-//         32-lane half;
-//       column image (W in WN layout): [64-col block][k (32)][128 B] with the 32-B column
-//         slot XOR-swizzled by (k >> 1) & 3, read by ds_read_b64_tr_b16 (k down the
-//         lane's fragment); the 8 k-rows a 32-lane half reads land in 8 distinct 32-B slots.
-//     The MFMA's 32 k-slots hold k = {4g..4g+3} U {16+4g..16+4g+3} for lane group g
-//     (the same permutation for both operands, so the products pair correctly).
+//   * LDS images, both filled by DMA pieces of 8 rows x 128 B (full lines from HBM) and
+//     conflict-free for their reads by construction:
+//       row image (X, and W in WT layout): [row][8 chunks of 8 k], chunk c of row r at
+//         c ^ ((r >> 1) & 7) -- the A/B fragment of a 32-k sub-step is ONE ds_read_b128;
+//       column image (W in WN layout): [64-col block][k][4 x 32-B column slots], slot at
+//         slot ^ csw(k), read by ds_read_b64_tr_b16 (k down the lane's fragment).
 #include <type_traits>
 
 #include "common.h"
@@ -43,7 +41,7 @@ typedef __bf16 bfx4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) char lds_t;
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 256, BK = 32, NT = 512, NBUF = 4;
+constexpr int BM = 256, BK = 64, NT = 512;
 
 ST_DEVICE i32x4 make_rsrc(const void* base, uint32_t bytes) {
   const uint64_t a = (uint64_t)base;
@@ -65,11 +63,18 @@ ST_DEVICE void lds_dma16(const i32x4& rs, uint32_t lds_base, uint32_t voff) {
 }
 #pragma clang diagnostic pop
 
-ST_DEVICE bfx4 lds_b64(const lds_t* p) { return *(const bfx4 __attribute__((address_space(3)))*)p; }
+ST_DEVICE bfx8 lds_b128(const lds_t* p) { return *(const bfx8 __attribute__((address_space(3)))*)p; }
 ST_DEVICE bfx4 lds_tr(const lds_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((bfx4 __attribute__((address_space(3)))*)p);
 }
 ST_DEVICE bfx8 cat8(bfx4 a, bfx4 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7); }
+
+// row image: [row][8 x 16-B chunks of k], chunk c of row r stored at c ^ rsw(r): the 16
+// rows x 2 chunks a ds_read_b128 lane group touches land in 16 distinct 16-B slots
+ST_DEVICE int rsw(int r) { return (r >> 1) & 7; }
+// column image: [64-col block][k][4 x 32-B column slots], slot stored at slot ^ csw(k): the
+// 8 k-rows of a transposed-read half land in 8 distinct 32-B slots
+ST_DEVICE int csw(int k) { return ((k >> 1) & 1) | (((k >> 3) & 1) << 1); }
 
 template <int BN, bool WN>
 struct Geo {
@@ -101,7 +106,7 @@ __global__ __launch_bounds__(NT, 1) void grouped_gemm_kernel(const bf16_t* __res
                                                              const int* __restrict__ tile_end, int G, int N,
                                                              int K) {
   using Gm = Geo<BN, WN>;
-  __shared__ __attribute__((aligned(16))) char smem_raw[NBUF * Gm::STAGE];
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * Gm::STAGE];
   lds_t* smem = (lds_t*)smem_raw;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -127,52 +132,58 @@ __global__ __launch_bounds__(NT, 1) void grouped_gemm_kernel(const bf16_t* __res
                                                : ((int64_t)(BN - 1) * ldw + K) * 2));
   const uint32_t sX = (uint32_t)(ldx * 2), sW = (uint32_t)(ldw * 2);
 
-  // ---- DMA plan: wave w fills the 1-KiB pieces [w NDMA, (w+1) NDMA) of a stage
+  // ---- DMA plan: every 1-KiB piece is 8 rows x 128 B (8 rows of 64 k, or 8 k-rows of 64
+  // columns); wave w fills pieces [w NDMA, (w+1) NDMA) of a stage, lane L the 16 B at L*16
   uint32_t voff[Gm::NDMA];
   bool isA[Gm::NDMA];
 #pragma unroll
   for (int i = 0; i < Gm::NDMA; ++i) {
     const int p = wid * Gm::NDMA + i;  // wave-uniform
     isA[i] = p < Gm::A_PIECES;
-    if (isA[i] || !WN) {  // row image piece: 16 rows x 4 chunks of 8 k
-      const int q = isA[i] ? p : p - Gm::A_PIECES;
-      const int r = q * 16 + (lane & 15), kc = lane >> 4;
-      voff[i] = (uint32_t)r * (isA[i] ? sX : sW) + (uint32_t)(kc * 16);
-    } else {  // column image piece: 8 k-rows x 128 B of one 64-column block
-      const int q = p - Gm::A_PIECES;
-      const int cb = q >> 2, kr = (q & 3) * 8 + (lane >> 3);
-      const int phys = (lane & 7) >> 1;
-      const int logical = ((phys ^ ((kr >> 1) & 3)) << 1) | (lane & 1);  // 16-B chunk in the 128-B row
+    const int q = isA[i] ? p : p - Gm::A_PIECES;
+    const int pr = q * 8 + (lane >> 3), pc = lane & 7;  // row of the image, physical 16-B chunk
+    if (isA[i] || !WN) {
+      voff[i] = (uint32_t)pr * (isA[i] ? sX : sW) + (uint32_t)((pc ^ rsw(pr)) * 16);
+    } else {  // column image: block cb = q / 8, k-row kr, logical 32-B slot
+      const int cb = q >> 3, kr = (q & 7) * 8 + (lane >> 3);
+      const int logical = (((pc >> 1) ^ csw(kr)) << 1) | (pc & 1);
       voff[i] = (uint32_t)kr * sW + (uint32_t)((cb * 64 + logical * 8) * 2);
     }
   }
   const uint32_t dma_base =
       __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem + (uint32_t)(wid * Gm::NDMA * 1024));
   auto dma = [&](int buf, int kt) {
-    const uint32_t kx = (uint32_t)(kt * BK * 2);                  // row images: k along the row
-    const uint32_t kw = WN ? (uint32_t)(kt * BK) * sW : kx;       // column image: k = row
+    const uint32_t kx = (uint32_t)(kt * BK * 2);             // row images: k along the row
+    const uint32_t kw = WN ? (uint32_t)(kt * BK) * sW : kx;  // column image: k = row
 #pragma unroll
     for (int i = 0; i < Gm::NDMA; ++i)
       lds_dma16(isA[i] ? rsX : rsW, dma_base + buf * Gm::STAGE + i * 1024, voff[i] + (isA[i] ? kx : kw));
   };
 
-  // ---- fragment read plan
+  // ---- fragment read plan (16x16x32, natural k order: lane group gq holds k 8gq..8gq+7
+  // of a 32-k sub-step = 16-B chunk 4s + gq)
   const int gq = lane >> 4, rr = lane & 15;
   const int wm = wid / Gm::WNV, wn = wid % Gm::WNV;
   const int am = wm * Gm::TM, bnn = wn * Gm::TN;
-  int aoff[Gm::FM], boff[Gm::FN];
+  int aoff[Gm::FM][2], boff[Gm::FN][2];
 #pragma unroll
-  for (int f = 0; f < Gm::FM; ++f)  // row image: block (am/16 + f), chunk gq>>1, row rr, half gq&1
-    aoff[f] = ((am >> 4) + f) * 1024 + (gq >> 1) * 256 + rr * 16 + 8 * (gq & 1);
+  for (int f = 0; f < Gm::FM; ++f) {
+    const int r = am + 16 * f + rr;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) aoff[f][st] = r * 128 + 16 * ((4 * st + gq) ^ rsw(r));
+  }
 #pragma unroll
   for (int f = 0; f < Gm::FN; ++f) {
     const int nn = bnn + 16 * f;
-    if (WN) {  // lane 4q+p of group gq: k-row 4gq+q, columns 4p..4p+3 of the 16-col slot
+    if (WN) {  // lane 4q+p of group gq: k-row 8gq+q (+4 for the 2nd read, +32 per sub-step)
       const int q = (lane >> 2) & 3, p = lane & 3;
-      const int kr = 4 * gq + q, slot = (nn & 63) >> 4;
-      boff[f] = Gm::A_BYTES + (nn >> 6) * 4096 + kr * 128 + 32 * (slot ^ ((kr >> 1) & 3)) + 8 * p;
+      const int kr = 8 * gq + q, sl = (nn & 63) >> 4;
+      boff[f][0] = Gm::A_BYTES + (nn >> 6) * 8192 + kr * 128 + 32 * (sl ^ csw(kr)) + 8 * p;
+      boff[f][1] = boff[f][0] + 4 * 128;  // k-rows 8gq+4..8gq+7: same swizzle (csw ignores k bit 2)
     } else {
-      boff[f] = Gm::A_BYTES + (nn >> 4) * 1024 + (gq >> 1) * 256 + rr * 16 + 8 * (gq & 1);
+      const int r = nn + rr;
+#pragma unroll
+      for (int st = 0; st < 2; ++st) boff[f][st] = Gm::A_BYTES + r * 128 + 16 * ((4 * st + gq) ^ rsw(r));
     }
   }
 
@@ -184,42 +195,40 @@ __global__ __launch_bounds__(NT, 1) void grouped_gemm_kernel(const bf16_t* __res
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
 
+  // ---- K loop: double-buffered 64-k tiles; tile kt+1's DMA is issued right after the
+  // barrier that retires tile kt, and runs under tile kt's MFMAs
   const int KT = K / BK;
-#pragma unroll
-  for (int p = 0; p < NBUF - 1; ++p)
-    if (p < KT) dma(p, p);
-
-  auto step = [&](auto bufc, int kt) {
+  dma(0, 0);
+  auto tile = [&](auto bufc, int kt) {
     constexpr int BUF = decltype(bufc)::value;
-    if (kt + 2 < KT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * Gm::NDMA) : "memory");
-    else if (kt + 1 < KT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Gm::NDMA) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + NBUF - 1 < KT) dma((BUF + NBUF - 1) % NBUF, kt + NBUF - 1);
-    const lds_t* st = smem + BUF * Gm::STAGE;
-    bfx8 af[Gm::FM], bf[Gm::FN];
+    if (kt + 1 < KT) dma(BUF ^ 1, kt + 1);
+    const lds_t* stg = smem + BUF * Gm::STAGE;
 #pragma unroll
-    for (int j = 0; j < Gm::FN; ++j) {
-      if (WN) bf[j] = cat8(lds_tr(st + boff[j]), lds_tr(st + boff[j] + 16 * 128));
-      else bf[j] = cat8(lds_b64(st + boff[j]), lds_b64(st + boff[j] + 512));
+    for (int st = 0; st < 2; ++st) {
+      bfx8 af[Gm::FM], bf[Gm::FN];
+#pragma unroll
+      for (int j = 0; j < Gm::FN; ++j) {
+        if (WN) bf[j] = cat8(lds_tr(stg + boff[j][0] + st * 32 * 128), lds_tr(stg + boff[j][1] + st * 32 * 128));
+        else bf[j] = lds_b128(stg + boff[j][st]);
+      }
+#pragma unroll
+      for (int i = 0; i < Gm::FM; ++i) af[i] = lds_b128(stg + aoff[i][st]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < Gm::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < Gm::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
-#pragma unroll
-    for (int i = 0; i < Gm::FM; ++i) af[i] = cat8(lds_b64(st + aoff[i]), lds_b64(st + aoff[i] + 512));
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < Gm::FM; ++i)
-#pragma unroll
-      for (int j = 0; j < Gm::FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
     asm volatile("" ::: "memory");
   };
-  for (int kt = 0; kt < KT; kt += NBUF) {
-    step(std::integral_constant<int, 0>(), kt);
-    if (kt + 1 < KT) step(std::integral_constant<int, 1>(), kt + 1);
-    if (kt + 2 < KT) step(std::integral_constant<int, 2>(), kt + 2);
-    if (kt + 3 < KT) step(std::integral_constant<int, 3>(), kt + 3);
+  for (int kt = 0; kt < KT; kt += 2) {
+    tile(std::integral_constant<int, 0>(), kt);
+    if (kt + 1 < KT) tile(std::integral_constant<int, 1>(), kt + 1);
   }
 
   // ---- epilogue: 16x16 C/D row = 4 (lane>>4) + reg (M), column = lane & 15 (N); rows past
@@ -251,7 +260,7 @@ int st_grouped_gemm_bm() { return BM; }
 int st_grouped_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t strideW, void* Y, int64_t ldy,
                     const int* offs, const int* tile_end, int T, int G, int N, int K, int wn, hipStream_t st) {
   if (T <= 0 || G <= 0 || N <= 0 || K <= 0) return -2;
-  if (K % BK || N % 128) return -2;
+  if (K % BK || N % 128) return -2;  // K: whole 64-k tiles
   if (ldx % 8 || ldw % 8 || ldy % 8 || ldx < K || ldy < N || (wn ? ldw < N : ldw < K)) return -2;
   if (((uintptr_t)X | (uintptr_t)W | (uintptr_t)Y) % 16) return -2;
   if (((int64_t)(T + BM) * ldx) * 2 >= (int64_t)1 << 32) return -2;  // 32-bit buffer offsets
