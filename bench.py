@@ -58,9 +58,10 @@ LAYOUTS = {
     # long context: 32K tokens over 8 CP ranks (4K local), zig-zag chunks, GQA-sized K/V
     "cp8_32k": dict(cp=-1, seq_len=32768, micro_batch_size=1),
     # Mixtral 8x7B: one expert per GPU (EP carved out of DP), dense weights ZeRO-1 over DP x EP;
-    # static-capacity dispatch (1.25x the mean rows per rank pair: no host sync per layer) in 2
-    # chunks, each chunk's all-to-all overlapping the other's expert GEMMs; dropped rows reported
-    "mixtral_ep8": dict(model="mixtral-8x7b", ep=-1, micro_batch_size=2, moe_capacity_factor=1.25,
+    # static-capacity dispatch (2x the mean rows per rank pair: no host sync per layer; at 1.25x
+    # the random-init router overflowed 5 % of the rows, profiles/r03/rehearsal) in 2 chunks, each
+    # chunk's all-to-all overlapping the other's expert GEMMs; dropped rows are reported
+    "mixtral_ep8": dict(model="mixtral-8x7b", ep=-1, micro_batch_size=2, moe_capacity_factor=2.0,
                         moe_ep_chunks=2),
 }
 
