@@ -102,7 +102,7 @@ class MLP(nn.Module):
         self.down_proj.reset_parameters()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return self.down_proj(ops.swiglu(self.gate_up_proj(x)))
+        return self.down_proj(self.gate_up_proj(x), act="swiglu")
 
 
 class DecoderLayer(nn.Module):

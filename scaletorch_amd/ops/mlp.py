@@ -71,3 +71,44 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
     if getattr(weight, "main_grad", None) is not None and torch.is_grad_enabled():
         return _LinearFn.apply(x, weight, bias)
     return F.linear(x, weight, bias)
+
+
+class _SwiGLULinearFn(torch.autograd.Function):
+    """y = swiglu(gu) W^T without keeping swiglu(gu): the activation is recomputed in
+    backward (one elementwise pass over gu) for the weight gradient, so a layer keeps
+    gu [T, 2I] but not a [T, I] -- 1/3 of the MLP's saved activations (112 MiB per
+    Llama-3-8B layer and 4096-token sample), which is what lets the 1-GPU step hold a
+    larger micro-batch in 288 GB.  Reference: down(silu(gate(x)) * up(x)),
+    scaletorch/models/llama.py:236-249 (autograd keeps every intermediate)."""
+
+    @staticmethod
+    def forward(ctx, gu, weight):
+        gu = gu.contiguous()
+        ctx.save_for_backward(gu, weight)
+        if gu.requires_grad:
+            prepare_dgrad_weight(weight)
+        return F.linear(_lib.ops().swiglu_fwd(gu), weight)
+
+    @staticmethod
+    def backward(ctx, dy):
+        gu, weight = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        da = dgrad(dy, weight)
+        if ctx.needs_input_grad[1]:
+            a = _lib.ops().swiglu_fwd(gu)  # recomputed
+            accumulate_linear_wgrad(weight, dy2, a.reshape(-1, a.shape[-1]))
+            del a
+        return _lib.ops().swiglu_bwd(da.contiguous(), gu), None
+
+
+def swiglu_linear(gu: torch.Tensor, weight: torch.Tensor) -> torch.Tensor | None:
+    """Fused SwiGLU + down projection that recomputes the activation in backward, or
+    None when it does not apply (CPU, no main_grad, shapes the kernels skip, or
+    ST_MLP_RECOMPUTE_ACT=0)."""
+    import os
+
+    if (os.environ.get("ST_MLP_RECOMPUTE_ACT", "1") == "1" and torch.is_grad_enabled()
+            and getattr(weight, "main_grad", None) is not None and _lib.use_native(gu)
+            and gu.dtype == torch.bfloat16 and gu.shape[-1] % 16 == 0):
+        return _SwiGLULinearFn.apply(gu, weight)
+    return None

@@ -680,9 +680,18 @@ class RowParallelLinear(nn.Module):
         if self.bias is not None:
             nn.init.zeros_(self.bias)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        from ..ops.mlp import linear
+    def forward(self, x: torch.Tensor, act: str | None = None) -> torch.Tensor:
+        """``act="swiglu"``: x is a fused gate|up output and the SwiGLU is applied here,
+        on one rank with the activation recomputed in backward (ops.mlp.swiglu_linear)."""
+        from .. import ops
+        from ..ops.mlp import linear, swiglu_linear
 
+        if act == "swiglu":
+            if self.tp == 1 and self.bias is None:
+                y = swiglu_linear(x, self.weight)
+                if y is not None:
+                    return y
+            x = ops.swiglu(x)
         if not self.input_is_parallel and self.tp > 1:
             x = ScatterToTensorParallelRegion.apply(x, self.group)
         if self.tp > 1 and not self.sequence_parallel:

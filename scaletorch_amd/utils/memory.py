@@ -17,6 +17,8 @@ from dataclasses import dataclass
 HBM_GB = 288.0
 _ACT_ATTN = 14  # bytes per (token, layer, hidden element): norms, QKV, attention out, residual
 _ACT_MLP = 20   # gate|up output, SwiGLU output, down input (dense MLP with I = 3.5 h)
+_ACT_SWIGLU = 7  # the SwiGLU output alone (I = 3.5 h bf16): not kept when it is recomputed
+                 # in backward (ops/mlp.swiglu_linear: one rank, ST_MLP_RECOMPUTE_ACT=1)
 
 
 @dataclass
@@ -33,7 +35,11 @@ class MemoryEstimate:
         return (self.params_gb + self.grads_gb + self.optimizer_gb + self.activations_gb + self.logits_gb
                 + self.comm_gb)
 
-    def fits(self, capacity_gb: float = HBM_GB, headroom_gb: float = 16.0) -> bool:
+    def fits(self, capacity_gb: float = HBM_GB, headroom_gb: float | None = None) -> bool:
+        import os
+
+        if headroom_gb is None:  # allocator fragmentation + workspaces; ST_HBM_HEADROOM_GB overrides
+            headroom_gb = float(os.environ.get("ST_HBM_HEADROOM_GB", "16"))
         return self.total_gb + headroom_gb <= capacity_gb
 
     def summary(self) -> str:
@@ -46,7 +52,7 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
                          micro_batch: int = 1, seq_len: int = 4096, grad_acc: int = 1, zero1: bool = False,
                          sequence_parallel: bool = False, gradient_checkpointing: bool = False,
                          pp_engine: str = "1f1b", grad_reduce_dtype: str = "bf16",
-                         fused_head_chunk: int = 0) -> MemoryEstimate:
+                         fused_head_chunk: int = 0, recompute_swiglu: bool | None = None) -> MemoryEstimate:
     """Worst-rank estimate (first pipeline stage for activations, largest stage for weights).
 
     ``fused_head_chunk`` > 0: the fused chunked LM head (ops/fused_head.py) -- one
@@ -78,7 +84,12 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
         k_eff = cfg.num_experts_per_tok * cfg.moe_intermediate_size / max(1, cfg.intermediate_size)
     else:
         k_eff = 1.0
-    per_layer = _ACT_ATTN * h + _ACT_MLP * h * k_eff * cfg.intermediate_size / (3.5 * h)
+    if recompute_swiglu is None:
+        import os
+
+        recompute_swiglu = os.environ.get("ST_MLP_RECOMPUTE_ACT", "1") == "1"
+    mlp_b = _ACT_MLP - (_ACT_SWIGLU if (recompute_swiglu and tp == 1 and not cfg.is_moe) else 0)
+    per_layer = _ACT_ATTN * h + mlp_b * h * k_eff * cfg.intermediate_size / (3.5 * h)
     if tp > 1:
         per_layer = per_layer / tp if sequence_parallel else 8 * h + (per_layer - 8 * h) / tp
     if gradient_checkpointing == "selective":  # attention activations kept, norm + MLP recomputed
