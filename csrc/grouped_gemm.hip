@@ -28,6 +28,7 @@
 //         c ^ ((r >> 1) & 7) -- the A/B fragment of a 32-k sub-step is ONE ds_read_b128;
 //       column image (W in WN layout): [64-col block][k][4 x 32-B column slots], slot at
 //         slot ^ csw(k), read by ds_read_b64_tr_b16 (k down the lane's fragment).
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(NT, 1) void grouped_gemm_kernel(const bf16_t* __res
                                                              int64_t strideW, bf16_t* __restrict__ Y, int64_t ldy,
                                                              const int* __restrict__ offs,
                                                              const int* __restrict__ tile_end, int G, int N,
-                                                             int K) {
+                                                             int K, int order) {
   using Gm = Geo<BN, WN>;
   __shared__ __attribute__((aligned(16))) char smem_raw[2 * Gm::STAGE];
   lds_t* smem = (lds_t*)smem_raw;
@@ -112,9 +113,22 @@ __global__ __launch_bounds__(NT, 1) void grouped_gemm_kernel(const bf16_t* __res
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nbn = N / BN;
 
-  // ---- work item: (M-tile slot, N-tile); slot -> (group, M-tile of the group)
-  const int b = (int)blockIdx.x;
-  const int slot = b / nbn, nt = b % nbn;
+  // ---- work item: (M-tile slot, N-tile); slot -> (group, M-tile of the group).
+  // order 1: XCD-aware remap, then super-rows of 8 slots walked N-tile-major, so the ~32
+  // workgroups an XCD holds at once share 8 X tiles and 4 weight tiles in its L2;
+  // order 0: slot-major (each X tile swept across all N-tiles before the next)
+  int slot, nt;
+  if (order == 1) {
+    const int nslots = (int)gridDim.x / nbn;
+    const int idx = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    const int per = 8 * nbn, grp = idx / per, in = idx % per;
+    const int gsz = min(8, nslots - grp * 8);
+    slot = grp * 8 + in % gsz;
+    nt = in / gsz;
+  } else {
+    slot = (int)blockIdx.x / nbn;
+    nt = (int)blockIdx.x % nbn;
+  }
   const int total_slots = tile_end[G - 1];
   if (slot >= total_slots) return;  // uniform over the workgroup: no barrier reached yet
   const int g = find_group(tile_end, G, slot);
@@ -270,9 +284,11 @@ int st_grouped_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, int6
   if (grid >= (1LL << 31)) return -2;
   const bf16_t *x = (const bf16_t*)X, *w = (const bf16_t*)W;
   bf16_t* y = (bf16_t*)Y;
+  const char* oe = std::getenv("ST_GMM_ORDER");  // 0: slot-major tile order (A/B)
+  const int order = oe ? std::atoi(oe) : 1;
 #define LAUNCH(BNV, WNV)                                                                                   \
   grouped_gemm_kernel<BNV, WNV><<<(unsigned)grid, NT, 0, st>>>(x, ldx, w, ldw, strideW, y, ldy, offs, tile_end, \
-                                                               G, N, K)
+                                                               G, N, K, order)
   if (bn == 256) {
     if (wn) LAUNCH(256, true); else LAUNCH(256, false);
   } else {

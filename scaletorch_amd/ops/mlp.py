@@ -102,12 +102,15 @@ class _SwiGLULinearFn(torch.autograd.Function):
 
 
 def swiglu_linear(gu: torch.Tensor, weight: torch.Tensor) -> torch.Tensor | None:
-    """Fused SwiGLU + down projection that recomputes the activation in backward, or
-    None when it does not apply (CPU, no main_grad, shapes the kernels skip, or
-    ST_MLP_RECOMPUTE_ACT=0)."""
+    """Fused SwiGLU + down projection that recomputes the activation in backward
+    (``ST_MLP_RECOMPUTE_ACT=1``), or None (the default, and on CPU / without main_grad /
+    shapes the kernels skip).  Off by default: on one MI355X at Llama-3-8B micro-batch 6
+    it saves 22 GB but costs 14.5 ms/step (1026.8 vs 1012.3 ms), and the micro-batch 7 / 8
+    it makes room for run at the same tokens/s (23.86k / 24.23k vs 24.28k,
+    profiles/r03/swiglu_recompute_mbs.log) -- a memory lever for longer sequences."""
     import os
 
-    if (os.environ.get("ST_MLP_RECOMPUTE_ACT", "1") == "1" and torch.is_grad_enabled()
+    if (os.environ.get("ST_MLP_RECOMPUTE_ACT", "0") == "1" and torch.is_grad_enabled()
             and getattr(weight, "main_grad", None) is not None and _lib.use_native(gu)
             and gu.dtype == torch.bfloat16 and gu.shape[-1] % 16 == 0):
         return _SwiGLULinearFn.apply(gu, weight)

@@ -18,7 +18,7 @@ HBM_GB = 288.0
 _ACT_ATTN = 14  # bytes per (token, layer, hidden element): norms, QKV, attention out, residual
 _ACT_MLP = 20   # gate|up output, SwiGLU output, down input (dense MLP with I = 3.5 h)
 _ACT_SWIGLU = 7  # the SwiGLU output alone (I = 3.5 h bf16): not kept when it is recomputed
-                 # in backward (ops/mlp.swiglu_linear: one rank, ST_MLP_RECOMPUTE_ACT=1)
+                 # in backward (ops/mlp.swiglu_linear: one rank, opt-in ST_MLP_RECOMPUTE_ACT=1)
 
 
 @dataclass
@@ -87,7 +87,7 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
     if recompute_swiglu is None:
         import os
 
-        recompute_swiglu = os.environ.get("ST_MLP_RECOMPUTE_ACT", "1") == "1"
+        recompute_swiglu = os.environ.get("ST_MLP_RECOMPUTE_ACT", "0") == "1"
     mlp_b = _ACT_MLP - (_ACT_SWIGLU if (recompute_swiglu and tp == 1 and not cfg.is_moe) else 0)
     per_layer = _ACT_ATTN * h + mlp_b * h * k_eff * cfg.intermediate_size / (3.5 * h)
     if tp > 1:
