@@ -358,12 +358,13 @@ def test_moe_experts_ignore_capacity_padding_rows():
         assert rel(a, b) < 1e-3
 
 
-def test_swiglu_linear_recompute_matches_reference():
+def test_swiglu_linear_recompute_matches_reference(monkeypatch):
     """SwiGLU + down projection with the activation recomputed in backward
     (ops/mlp.swiglu_linear): output, d(gate|up) and the fp32 main_grad weight gradient
     vs an fp32 autograd reference; nothing but gu is saved."""
     from scaletorch_amd.ops.mlp import swiglu_linear
 
+    monkeypatch.setenv("ST_MLP_RECOMPUTE_ACT", "1")
     torch.manual_seed(9)
     T, I, h = 512, 1024, 256
     gu = (torch.randn(T, 2 * I, device="cuda") * 2).bfloat16().requires_grad_(True)
