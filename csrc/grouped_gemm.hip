@@ -284,8 +284,10 @@ int st_grouped_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, int6
   if (grid >= (1LL << 31)) return -2;
   const bf16_t *x = (const bf16_t*)X, *w = (const bf16_t*)W;
   bf16_t* y = (bf16_t*)Y;
-  const char* oe = std::getenv("ST_GMM_ORDER");  // 0: slot-major tile order (A/B)
-  const int order = oe ? std::atoi(oe) : 1;
+  // 1: XCD-grouped tile order -- measured 2-19 % SLOWER than slot-major on every MoE and
+  // dense shape (profiles/r03/grouped_gemm_order_ab.log): slot-major stays the default
+  const char* oe = std::getenv("ST_GMM_ORDER");
+  const int order = oe ? std::atoi(oe) : 0;
 #define LAUNCH(BNV, WNV)                                                                                   \
   grouped_gemm_kernel<BNV, WNV><<<(unsigned)grid, NT, 0, st>>>(x, ldx, w, ldw, strideW, y, ldy, offs, tile_end, \
                                                                G, N, K, order)
