@@ -1337,6 +1337,30 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
   float* qpart = part ? part + (nsplit > 1 ? (int64_t)nsplit * 2 * B * Hkv * Sk * D : 0) : nullptr;
   const unsigned gk = (unsigned)(((Sk + 127) / 128) * B * Hkv * nsplit);
   const bf16_t* dop = (const bf16_t*)dout;
+  // ST_FLASH_BWD_CONCURRENT=1: the dQ kernel (and its split reduce) runs on a second stream
+  // beside dK/dV, so the dispatcher fills each kernel's causal tail with the other's
+  // workgroups; joined with an event before returning (same stream order for callers)
+  const char* ce = std::getenv("ST_FLASH_BWD_CONCURRENT");  // read per call: same-process A/B
+  const bool concurrent = ce && std::atoi(ce) == 1;
+  hipStream_t sq = st;
+  hipEvent_t ev_join = nullptr;
+  if (concurrent && D == 128) {
+    static hipStream_t side[16] = {};
+    static hipEvent_t fork_ev[16] = {}, join_ev[16] = {};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 16) {
+      if (!side[dev]) {
+        ST_HIP_CHECK(hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking));
+        ST_HIP_CHECK(hipEventCreateWithFlags(&fork_ev[dev], hipEventDisableTiming));
+        ST_HIP_CHECK(hipEventCreateWithFlags(&join_ev[dev], hipEventDisableTiming));
+      }
+      ST_HIP_CHECK(hipEventRecord(fork_ev[dev], st));
+      ST_HIP_CHECK(hipStreamWaitEvent(side[dev], fork_ev[dev], 0));
+      sq = side[dev];
+      ev_join = join_ev[dev];
+    }
+  }
   if (D == 128) {
     const char* pe = std::getenv("ST_FLASH_PROBE");  // diagnostics only (tools/probe_flash.py)
     if (pe && std::atoi(pe) == 1) {
@@ -1344,7 +1368,7 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
       flash_bwd_dkdv_kernel<128, 1><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
                                                    (bf16_t*)dv, nsplit, part);
     } else {
-      flash_bwd_dq_kernel<128><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq, qsplit, qpart);
+      flash_bwd_dq_kernel<128><<<gq, 256, 0, sq>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq, qsplit, qpart);
       flash_bwd_dkdv_kernel<128><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
                                                    (bf16_t*)dv, nsplit, part);
     }
@@ -1358,8 +1382,13 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
   if (qsplit > 1) {
     ST_HIP_CHECK(hipGetLastError());
     const int64_t total8 = (int64_t)B * H * Sq * (D / 8);
-    dq_split_reduce_kernel<<<(unsigned)((total8 + 255) / 256), 256, 0, st>>>(qpart, qsplit, H, Sq, D, total8,
+    dq_split_reduce_kernel<<<(unsigned)((total8 + 255) / 256), 256, 0, sq>>>(qpart, qsplit, H, Sq, D, total8,
                                                                              (bf16_t*)dq, sdqb, sdqs, sdqh);
+  }
+  if (ev_join) {  // rejoin: everything after this call on `st` sees dQ
+    ST_HIP_CHECK(hipGetLastError());
+    ST_HIP_CHECK(hipEventRecord(ev_join, sq));
+    ST_HIP_CHECK(hipStreamWaitEvent(st, ev_join, 0));
   }
   if (nsplit > 1) {
     ST_HIP_CHECK(hipGetLastError());
