@@ -1337,11 +1337,13 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
   float* qpart = part ? part + (nsplit > 1 ? (int64_t)nsplit * 2 * B * Hkv * Sk * D : 0) : nullptr;
   const unsigned gk = (unsigned)(((Sk + 127) / 128) * B * Hkv * nsplit);
   const bf16_t* dop = (const bf16_t*)dout;
-  // ST_FLASH_BWD_CONCURRENT=1: the dQ kernel (and its split reduce) runs on a second stream
-  // beside dK/dV, so the dispatcher fills each kernel's causal tail with the other's
-  // workgroups; joined with an event before returning (same stream order for callers)
+  // the dQ kernel (and its split reduce) runs on a second stream beside dK/dV, so the
+  // dispatcher fills each kernel's causal tail with the other's workgroups; joined with an
+  // event before returning (same stream order for callers).  Same-process A/B at Llama-3-8B
+  // mbs 6: 993.2 vs 996.2 ms/step median, lower in all 4 rounds
+  // (profiles/r03/flash_bwd_concurrent_ab.log); ST_FLASH_BWD_CONCURRENT=0 serialises them.
   const char* ce = std::getenv("ST_FLASH_BWD_CONCURRENT");  // read per call: same-process A/B
-  const bool concurrent = ce && std::atoi(ce) == 1;
+  const bool concurrent = !ce || std::atoi(ce) != 0;
   hipStream_t sq = st;
   hipEvent_t ev_join = nullptr;
   if (concurrent && D == 128) {

@@ -247,6 +247,24 @@ def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> int:
     return choice
 
 
+_WGRAD_SIDE: dict = {}
+
+
+def wgrad_side_stream(device: torch.device):
+    """The stream linear weight gradients run on when ``ST_WGRAD_STREAM=side`` (else None):
+    the dW GEMM then overlaps the backward's next data-gradient GEMM and its memory-bound
+    elementwise kernels instead of following them on one stream.  Readers of main_grad
+    (DP bucket launches, the post-backward join) wait for this stream."""
+    import os
+
+    if device.type != "cuda" or os.environ.get("ST_WGRAD_STREAM", "main") != "side":
+        return None
+    st = _WGRAD_SIDE.get(device.index)
+    if st is None:
+        st = _WGRAD_SIDE[device.index] = torch.cuda.Stream(device=device)
+    return st
+
+
 def accumulate_linear_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, pre=None):
     """dW = dy^T x, accumulated into ``param.main_grad`` in fp32 when present.
 
@@ -269,7 +287,17 @@ def accumulate_linear_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
         torch.ops.aten.addmm.dtype_out(m2, pre.dyt, pre.xt.t(), torch.float32, beta=beta, alpha=1, out=m2)
         _grad_ready(param)
         return None
-    wgrad_into(mg.view(mg.shape[0], -1), dy2d, x2d, beta)
+    ws = wgrad_side_stream(dy2d.device) if mg.dtype == torch.float32 else None
+    if ws is not None:
+        ready = torch.cuda.Event()
+        ready.record()
+        ws.wait_event(ready)
+        with torch.cuda.stream(ws):
+            wgrad_into(mg.view(mg.shape[0], -1), dy2d, x2d, beta)
+        dy2d.record_stream(ws)  # autograd frees them when this node returns
+        x2d.record_stream(ws)
+    else:
+        wgrad_into(mg.view(mg.shape[0], -1), dy2d, x2d, beta)
     _grad_ready(param)
     return None
 

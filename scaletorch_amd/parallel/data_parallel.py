@@ -81,6 +81,16 @@ def _aligned(n: int) -> int:
     return math.ceil(n / ALIGN) * ALIGN
 
 
+def _wait_wgrad_stream(stream, device) -> None:
+    """Order ``stream`` after every weight gradient issued so far on the side wgrad
+    stream (ops/grad.py ``ST_WGRAD_STREAM=side``); no-op otherwise."""
+    from ..ops.grad import wgrad_side_stream
+
+    ws = wgrad_side_stream(device)
+    if ws is not None:
+        stream.wait_stream(ws)
+
+
 class GradArena:
     """Flat parameter + fp32 gradient storage for one reduction group.
 
@@ -222,8 +232,11 @@ class GradArena:
             ev.record()
             with torch.cuda.stream(st):
                 st.wait_event(ev)
+                _wait_wgrad_stream(st, g.device)
                 self._launch_comm(b, g)
             return
+        if g.is_cuda:
+            _wait_wgrad_stream(torch.cuda.current_stream(), g.device)
         self._launch_comm(b, g)
 
     def _launch_comm(self, b: Bucket, g: torch.Tensor) -> None:
@@ -268,6 +281,7 @@ class GradArena:
         ev.record()
         with torch.cuda.stream(st):
             st.wait_event(ev)
+            _wait_wgrad_stream(st, g.device)
             if self.sq_count == 0:
                 if self.sq_acc is None:
                     self.sq_acc = torch.zeros(1, dtype=torch.float32, device=g.device)
@@ -520,6 +534,8 @@ class DataParallel(nn.Module):
 
     def _post_backward(self) -> None:
         self._callback_queued = False
+        if torch.cuda.is_available():  # side-stream weight gradients land before anyone reads them
+            _wait_wgrad_stream(torch.cuda.current_stream(), torch.device("cuda", torch.cuda.current_device()))
         # final_backward False (interleaved pipeline: a chunk's last micro-batch, other
         # chunks still to come): buckets fire as their params become ready, but the
         # join and the TP-partial reduction wait for the step's last backward
