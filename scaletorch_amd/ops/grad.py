@@ -254,7 +254,11 @@ def wgrad_side_stream(device: torch.device):
     """The stream linear weight gradients run on when ``ST_WGRAD_STREAM=side`` (else None):
     the dW GEMM then overlaps the backward's next data-gradient GEMM and its memory-bound
     elementwise kernels instead of following them on one stream.  Readers of main_grad
-    (DP bucket launches, the post-backward join) wait for this stream."""
+    (DP bucket launches, the post-backward join) wait for this stream.  Measured at
+    Llama-3-8B mbs 6 it is 3x SLOWER (2981 vs 1002 ms/step, profiles/r03/wgrad_side_stream_ab.log):
+    dY / X stay allocated until the side stream catches up (record_stream), and at 271 GB
+    of 288 the caching allocator then frees and re-allocates synchronously.  Kept opt-in for
+    configurations with memory to spare."""
     import os
 
     if device.type != "cuda" or os.environ.get("ST_WGRAD_STREAM", "main") != "side":
