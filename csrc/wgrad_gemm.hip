@@ -368,30 +368,41 @@ __global__ __launch_bounds__(NT, 2) void wgrad_gemm_kernel(const bf16_t* __restr
 namespace p8 {
 constexpr int BK = 64;
 constexpr int IMGB = BK * RB;    // [64 tokens][128 features]: 16 KiB
-constexpr int BUFB = 4 * IMGB;   // A0 A1 B0 B1: 64 KiB per K-tile
 
-// half-image X of K-tile kt -> buffer buf.  X: 0 = A0, 1 = B0, 2 = B1, 3 = A1.  A plain
-// function, not a lambda: a closure captured by the phase lambda would pin the
-// operand arrays in scratch.
-template <int X>
-ST_DEVICE void p8_dma(const i32x4& rsA, const i32x4& rsB, uint32_t ldsw, const uint32_t (&vA)[2],
-                      const uint32_t (&vB)[2], uint32_t sA, uint32_t sB, int buf, int kt, int piece) {
-  constexpr bool isA = (X == 0 || X == 3);
-  constexpr int img = X == 0 ? 0 : X == 3 ? 1 : X == 1 ? 2 : 3;
-  constexpr uint32_t col = (X == 2 || X == 3) ? 256u : 0u;  // byte offset of feature 128
-  const uint32_t koff = (uint32_t)(kt * BK) * (isA ? sA : sB) + col;
-  const uint32_t v = piece ? (isA ? vA[1] : vB[1]) : (isA ? vA[0] : vB[0]);
-  lds_dma16(isA ? rsA : rsB, ldsw + (uint32_t)(buf * BUFB + img * IMGB + piece * 1024), v + koff);
-}
 }  // namespace p8
 
-template <int PROBE>  // timing probes (wrong results): 1 = no K-loop DMA, 2 = no K-loop LDS reads
+// Half-images live in a ring of SLOTS 16-KiB slots: half-image n = 4 kt + X (X in issue
+// order: 0 = A0, 1 = B0, 2 = B1, 3 = A1) in slot n % SLOTS; phase P of tile kt issues
+// half-image 4 kt + P + LEAD, LEAD = SLOTS - 4, into the slot last read at phase <= P of
+// tile kt - 1.  SLOTS = 8 (LEAD 4) is the two-K-tile double buffer; written as a ring it
+// runs 1-2 % faster than the buffer-indexed form it replaced (profiles/r03/wgrad_ring.md).
+// Deeper leads (9 / 10 slots, the whole 160 KiB) measured 13-15 % SLOWER: the slot index
+// is no longer a power of two, and its per-read address adds cost 19 % with the DMA off.
+// Probes on the same box (gate_up / down at T = 24,576): no K-loop DMA 1.60 PF/s; DMA from
+// an L2-hot source 1.33; DMA never waited for 1.23; as shipped 1.24 -- the DMA's cost is
+// its traffic through the CU and the L2 misses, not its latency, so a deeper ring cannot
+// buy it back.
+template <int X>
+ST_DEVICE void ring_dma(const i32x4& rsA, const i32x4& rsB, uint32_t ldsw, const uint32_t (&vA)[2],
+                        const uint32_t (&vB)[2], uint32_t sA, uint32_t sB, int slot, int kt, int piece) {
+  constexpr bool isA = (X == 0 || X == 3);
+  constexpr uint32_t col = (X == 2 || X == 3) ? 256u : 0u;  // byte offset of feature 128
+  const uint32_t koff = (uint32_t)(kt * p8::BK) * (isA ? sA : sB) + col;
+  const uint32_t v = piece ? (isA ? vA[1] : vB[1]) : (isA ? vA[0] : vB[0]);
+  lds_dma16(isA ? rsA : rsB, ldsw + (uint32_t)(slot * p8::IMGB + piece * 1024), v + koff);
+}
+
+// PROBE (timing probes, wrong results): 1 = no K-loop DMA, 2 = no K-loop LDS reads,
+// 3 = DMA never waited for in the loop, 4 = every DMA from K-tile 0 (L2-hot)
+template <int PROBE, int SLOTS = 8>
 __global__ __launch_bounds__(NT, 1) void wgrad8_kernel(const bf16_t* __restrict__ A, int64_t lda,
-                                                       const bf16_t* __restrict__ B, int64_t ldb,
-                                                       float* __restrict__ C, int64_t ldc, int M, int N, int T,
-                                                       int beta, SplitPlan sp) {
+                                                           const bf16_t* __restrict__ B, int64_t ldb,
+                                                           float* __restrict__ C, int64_t ldc, int M, int N,
+                                                           int T, int beta, SplitPlan sp) {
   using namespace p8;
-  __shared__ __attribute__((aligned(16))) char smem_raw[2 * BUFB];  // 128 KiB: two K-tiles
+  constexpr int LEAD = SLOTS - 4;
+  static_assert(LEAD >= 4 && LEAD <= 6, "lead of 4..6 half-images");
+  __shared__ __attribute__((aligned(16))) char smem_raw[SLOTS * IMGB];
   lds_t* smem = (lds_t*)smem_raw;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -403,8 +414,6 @@ __global__ __launch_bounds__(NT, 1) void wgrad8_kernel(const bf16_t* __restrict_
   B += (int64_t)w.k0 * ldb;
   T = w.T;
 
-  // ---- DMA plan: a half-image is 16 pieces of 1 KiB (4 token rows each); wave w
-  // fills pieces 2w and 2w+1 of every half-image (source address pre-swizzled).
   const i32x4 rsA = make_rsrc(A + m0, (uint32_t)(((int64_t)(T - 1) * lda + BM) * 2));
   const i32x4 rsB = make_rsrc(B + n0, (uint32_t)(((int64_t)(T - 1) * ldb + 256) * 2));
   const uint32_t sA = (uint32_t)(lda * 2), sB = (uint32_t)(ldb * 2);
@@ -417,9 +426,6 @@ __global__ __launch_bounds__(NT, 1) void wgrad8_kernel(const bf16_t* __restrict_
     vB[i] = (uint32_t)row * sB + c;
   }
   const uint32_t ldsw = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem + (uint32_t)(wid * 2048));
-  // half-image X of K-tile kt into buffer buf (p8_dma); X: 0 = A0, 1 = B0, 2 = B1, 3 = A1 (the issue order)
-  // ---- fragment read plan (T10 image (b), as the 4-stage kernel): lane group G
-  // reads token rows 8G..8G+7 (+32 for the second 32-token half of the tile)
   const int G = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
   int aoff[4][2], boff[2][2];
 #pragma unroll
@@ -450,27 +456,35 @@ __global__ __launch_bounds__(NT, 1) void wgrad8_kernel(const bf16_t* __restrict_
   };
 
   const int KT = (T + p8::BK - 1) / p8::BK;  // ragged last tile: rows >= T read as zeros
-  // prologue: tile 0's four half-images; A0 + B0 retired for phase 0
+  const int NH = 4 * KT;             // half-images of the whole K loop
+  // prologue: half-images 0 .. LEAD-1; 0 (A0) and 1 (B0) retired for phase 0
 #pragma unroll
-  for (int pc = 0; pc < 2; ++pc) p8_dma<0>(rsA, rsB, ldsw, vA, vB, sA, sB, 0, 0, pc);  // half-image by half-image:
+  for (int pc = 0; pc < 2; ++pc) ring_dma<0>(rsA, rsB, ldsw, vA, vB, sA, sB, 0, 0, pc);
 #pragma unroll
-  for (int pc = 0; pc < 2; ++pc) p8_dma<1>(rsA, rsB, ldsw, vA, vB, sA, sB, 0, 0, pc);  // the counted waits retire
+  for (int pc = 0; pc < 2; ++pc) ring_dma<1>(rsA, rsB, ldsw, vA, vB, sA, sB, 1, 0, pc);
 #pragma unroll
-  for (int pc = 0; pc < 2; ++pc) p8_dma<2>(rsA, rsB, ldsw, vA, vB, sA, sB, 0, 0, pc);  // whole half-images in
+  for (int pc = 0; pc < 2; ++pc) ring_dma<2>(rsA, rsB, ldsw, vA, vB, sA, sB, 2, 0, pc);
 #pragma unroll
-  for (int pc = 0; pc < 2; ++pc) p8_dma<3>(rsA, rsB, ldsw, vA, vB, sA, sB, 0, 0, pc);  // issue order
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  for (int pc = 0; pc < 2; ++pc) ring_dma<3>(rsA, rsB, ldsw, vA, vB, sA, sB, 3, 0, pc);
+  if (LEAD > 4 && NH > 4) {
+#pragma unroll
+    for (int pc = 0; pc < 2; ++pc) ring_dma<0>(rsA, rsB, ldsw, vA, vB, sA, sB, 4, 1, pc);
+  }
+  if (LEAD > 5 && NH > 5) {
+#pragma unroll
+    for (int pc = 0; pc < 2; ++pc) ring_dma<1>(rsA, rsB, ldsw, vA, vB, sA, sB, 5, 1, pc);
+  }
+  if (NH >= LEAD) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (LEAD - 2)) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   bar();
   if (grp == 1) bar();  // the stagger: waves 4-7 run one barrier behind
 
-  auto phase = [&](auto bufc, auto pc, int kt) {
-    constexpr int BUF = decltype(bufc)::value, P = decltype(pc)::value;
+  auto phase = [&](auto pc, int kt) {
+    constexpr int P = decltype(pc)::value;
     constexpr int MQ = (P == 0 || P == 1) ? 0 : 1, NQ = (P == 0 || P == 3) ? 0 : 1;
-    const bool more = kt + 1 < KT;
-    const lds_t* st = smem + BUF * BUFB;
-    const lds_t* ai = st + (MQ ? IMGB : 0);
-    // A fragments 0-1 before the barrier, 2-3 after it under the first MFMAs (balances
-    // the read sections: p0 would otherwise carry 24 of a tile's 48 reads)
+    const int n0h = 4 * kt;
+    // half-image slots read this phase: A0 = n0h, B0 = n0h + 1, B1 = n0h + 2, A1 = n0h + 3
+    const lds_t* ai = smem + ((n0h + (MQ ? 3 : 0)) % SLOTS) * IMGB;
     if constexpr (PROBE != 2 && (P == 0 || P == 2)) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -478,7 +492,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad8_kernel(const bf16_t* __restrict_
         for (int ks = 0; ks < 2; ++ks) af[i][ks] = lds_tr(ai + aoff[i][0] + ks * 32 * RB, ai + aoff[i][1] + ks * 32 * RB);
     }
     if constexpr (PROBE != 2 && (P == 0 || P == 1)) {
-      const lds_t* bi = st + (2 + NQ) * IMGB;
+      const lds_t* bi = smem + ((n0h + 1 + NQ) % SLOTS) * IMGB;
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -488,11 +502,15 @@ __global__ __launch_bounds__(NT, 1) void wgrad8_kernel(const bf16_t* __restrict_
           else b1[j][ks] = v;
         }
     }
-    // retire what the NEXT phase reads: this phase's DMA is issued after the wait
-    // (under the MFMAs), so only the previous phase's half-image may stay in flight
-    if (more) {
-      if constexpr (P == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    // retire what the NEXT phase reads (p3 -> A0/B0 of kt+1, p0 -> B1, p1 -> A1, p2 -> none):
+    // the last LEAD-3 (LEAD-2 at p2) half-images issued may stay in flight, unless the
+    // issue stream was cut short at the end of the loop
+    const int issue = n0h + P + LEAD;  // this phase's DMA (issued under its MFMAs)
+    if (PROBE == 3) {
+      // probe: DMA issued, never waited for inside the loop (wrong results)
+    } else if (issue <= NH) {
+      if constexpr (P == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (LEAD - 2)) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (LEAD - 3)) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -503,6 +521,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad8_kernel(const bf16_t* __restrict_
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) af[i][ks] = lds_tr(ai + aoff[i][0] + ks * 32 * RB, ai + aoff[i][1] + ks * 32 * RB);
     }
+    const int islot = issue % SLOTS, ikt = PROBE == 4 ? 0 : kt + (P + LEAD) / 4;  // probe 4: L2-hot source
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -514,10 +533,11 @@ __global__ __launch_bounds__(NT, 1) void wgrad8_kernel(const bf16_t* __restrict_
           acc[MQ * 4 + i][NQ * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bv,
                                                                                  acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
         }
-      // the next tile's half-image, one 1-KiB piece after the 4th and the 8th MFMA
-      if ((i == 0 || i == 1) && more && PROBE != 1) {
+      // the next half-image, one 1-KiB piece after the 4th and the 8th MFMA (spread over
+      // the section instead, after the 8th and 16th: same time)
+      if ((i == 0 || i == 1) && issue < NH && PROBE != 1) {
         __builtin_amdgcn_sched_barrier(0);
-        p8_dma<P>(rsA, rsB, ldsw, vA, vB, sA, sB, BUF ^ 1, kt + 1, i);
+        ring_dma<(P + LEAD) % 4>(rsA, rsB, ldsw, vA, vB, sA, sB, islot, ikt, i);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -528,21 +548,15 @@ __global__ __launch_bounds__(NT, 1) void wgrad8_kernel(const bf16_t* __restrict_
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
-  for (int kt = 0; kt < KT; kt += 2) {
-    phase(I0(), I0(), kt);
-    phase(I0(), I1(), kt);
-    phase(I0(), I2(), kt);
-    phase(I0(), I3(), kt);
-    if (kt + 1 < KT) {
-      phase(I1(), I0(), kt + 1);
-      phase(I1(), I1(), kt + 1);
-      phase(I1(), I2(), kt + 1);
-      phase(I1(), I3(), kt + 1);
-    }
+  for (int kt = 0; kt < KT; ++kt) {
+    phase(I0(), kt);
+    phase(I1(), kt);
+    phase(I2(), kt);
+    phase(I3(), kt);
   }
   if (grp == 0) bar();  // same barrier count in both groups
+  if (PROBE == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  // ---- epilogue: 16x16 C/D row = 4 (lane>>4) + reg, column = lane & 15
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -663,6 +677,8 @@ int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float*
   if (L.variant == 2) {
     if (probe == 1) wgrad8_kernel<1><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
     else if (probe == 2) wgrad8_kernel<2><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
+    else if (probe == 3) wgrad8_kernel<3><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
+    else if (probe == 4) wgrad8_kernel<4><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
     else wgrad8_kernel<0><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
   } else if (L.bn == 256) {
     if (probe == 1) wgrad_gemm_kernel<1, 256><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp, GroupPlan{});
