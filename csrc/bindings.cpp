@@ -51,8 +51,10 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
                  int64_t sks, int64_t skh, int64_t svb, int64_t svs, int64_t svh, int64_t sdb,
                  int64_t sds, int64_t sdh, int64_t sdqb, int64_t sdqs, int64_t sdqh, int64_t sdkb,
                  int64_t sdks, int64_t sdkh, float scale, int causal, int64_t q_offset,
-                 int64_t k_offset, float* part, hipStream_t st);
+                 int64_t k_offset, float* part, void* dsw, hipStream_t st);
 int64_t st_flash_bwd_part_elems(int B, int Sq, int Sk, int H, int Hkv, int D, int causal);
+int64_t st_flash_bwd_ds_elems(int B, int Sq, int Sk, int H, int D, int causal, int64_t q_offset,
+                              int64_t k_offset);
 int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int M,
                   int N, int T, int beta, int variant, float* ws, hipStream_t st);
 int64_t st_wgrad_ws_elems(int M, int N, int T, int variant);
@@ -724,13 +726,19 @@ std::vector<at::Tensor> flash_bwd(const at::Tensor& dout, const at::Tensor& q, c
   const int64_t pe = st_flash_bwd_part_elems((int)B, (int)Sq, (int)Sk, (int)H, (int)Hkv, (int)D, causal ? 1 : 0);
   at::Tensor part;
   if (pe > 0) part = at::empty({pe}, q.options().dtype(at::kFloat));
+  // dS workspace of the dS-materialising backward (transient: freed on return)
+  const int64_t dse = st_flash_bwd_ds_elems((int)B, (int)Sq, (int)Sk, (int)H, (int)D, causal ? 1 : 0, q_offset,
+                                            k_offset);
+  at::Tensor dsw;
+  if (dse > 0) dsw = at::empty({dse}, q.options());
   rc = st_flash_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
                     delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), (int)B, (int)Sq, (int)Sk, (int)H, (int)Hkv, (int)D, q.stride(0), q.stride(1),
                     q.stride(2), k.stride(0), k.stride(1), k.stride(2), v.stride(0), v.stride(1),
                     v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2), dq.stride(0),
                     dq.stride(1), dq.stride(2), dk.stride(0), dk.stride(1), dk.stride(2),
                     (float)scale, causal ? 1 : 0, q_offset, k_offset,
-                    pe > 0 ? part.data_ptr<float>() : nullptr, cur_stream());
+                    pe > 0 ? part.data_ptr<float>() : nullptr, dse > 0 ? dsw.data_ptr() : nullptr,
+                    cur_stream());
   ST_CHECK_RC(rc, "flash_bwd");
   return {dq, dk, dv};
 }

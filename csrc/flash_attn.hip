@@ -300,6 +300,46 @@ ST_DEVICE int key_limit(const AttnParams& p, int kb, int BN, int64_t qg, int h, 
   return (int)lim - 4 * h;
 }
 
+// ---- dS workspace of the dS-materialising backward (ST_FLASH_BWD_DS) ----
+// The dK/dV kernel already holds dS = P (dP - delta) for every (query, key) it
+// visits; instead of the dQ kernel recomputing S, dP and the softmax for the
+// same pairs (3 of its MFMA products and all of its exp work), dK/dV stores dS
+// once (bf16) and dQ becomes one product per tile, dQ^T += K^T dS^T.  With 288 GB
+// of HBM the transient causal workspace (B*H*Sq*Sk bytes: 3.2 GB for Llama-3-8B
+// at 6 x 4096) is affordable.
+//
+// Layout: per (b, q-head), the 64-key x 128-query tiles (kb, qt) that the dQ
+// kernel visits, query tile major, key block minor, compact under the causal mask:
+// tile (qt, kb) sits at prefix(qt) + kb, prefix(n) = sum_{t<n} nkb(t).  A tile is
+// a dS^T image [64 keys][128 queries] stored as plain 256-byte rows, so each dK/dV
+// step completes whole 128-byte lines; the dQ kernel applies the LDS XOR swizzle
+// (lds_off<128>) on the DMA source side, like DmaStager, and reads the tile with the
+// same transposed-read addressing as its K tile.
+//
+// nkb(t) of query tile t (128 rows) is key_blocks<128, 64>'s nkb:
+//   causal: clamp(2t + e, 0, NKB), e = floor((q_offset + 127 - k_offset) / 64) + 1
+//   full:   NKB = ceil(Sk / 64)
+__host__ __device__ inline int64_t ds_floordiv64(int64_t x) { return x >= 0 ? x / 64 : -((-x + 63) / 64); }
+__host__ __device__ inline int ds_nkb(int causal, int Sk, int64_t q_offset, int64_t k_offset, int t) {
+  const int NKB = (Sk + 63) / 64;
+  if (!causal) return NKB;
+  const int64_t v = 2 * (int64_t)t + ds_floordiv64(q_offset + 127 - k_offset) + 1;
+  return v < 0 ? 0 : (v > NKB ? NKB : (int)v);
+}
+__host__ __device__ inline int64_t ds_prefix(int causal, int Sk, int64_t q_offset, int64_t k_offset, int n) {
+  const int64_t NKB = (Sk + 63) / 64;
+  if (n <= 0) return 0;
+  if (!causal) return (int64_t)n * NKB;
+  const int64_t e = ds_floordiv64(q_offset + 127 - k_offset) + 1;
+  // first t with 2t + e >= 1 (t0) and with 2t + e >= NKB (t1); t1 >= t0 since NKB >= 1
+  auto ceil_half = [](int64_t x) { return x >= 0 ? (x + 1) / 2 : -((-x) / 2); };
+  int64_t t0 = ceil_half(1 - e), t1 = ceil_half(NKB - e);
+  t0 = t0 < 0 ? 0 : (t0 > n ? n : t0);
+  t1 = t1 < t0 ? t0 : (t1 > n ? n : t1);
+  return (t1 - t0) * (t0 + t1 - 1) + e * (t1 - t0) + (n - t1) * NKB;
+}
+constexpr int kDsTile = 64 * 128;  // bf16 elements of one dS^T tile (16 KiB)
+
 // ============================================================== forward
 template <int D>
 __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(AttnParams p, bf16_t* __restrict__ o,
@@ -857,6 +897,159 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
   }
 }
 
+// ============================================================== backward: dQ from stored dS
+// dS-materialising backward (ST_FLASH_BWD_DS): dQ^T += K^T dS^T over the visible
+// key blocks, both operands by transposed LDS reads of LDS-DMA'd tiles (K as in
+// the dQ kernel above; dS^T tiles written pre-swizzled by the dK/dV kernel, copied
+// linearly).  One MFMA product per tile instead of three and no softmax, so the
+// kernel is bound by the bytes it streams into LDS (measured ~14 B/clk/CU with one
+// head per workgroup, where every dS tile brought its own copy of the K tile): one
+// workgroup now serves GH query heads of one kv head -- each K tile is staged once
+// for GH dS tiles and its fragments are read once per wave for GH heads' MFMAs.
+// 4 waves x 32 queries; dQ of the GH heads stays in AGPRs (GH x D/32 tiles).
+template <int D, int GH>
+__global__ __launch_bounds__(256, 1) void flash_bwd_dq_ds_kernel(AttnParams p, const bf16_t* __restrict__ dsw,
+                                                                 bf16_t* __restrict__ dq, int nsplit,
+                                                                 float* __restrict__ part) {
+  constexpr int BM = 128, BN = 64, NDT = D / 32;
+  constexpr int TK = BN * D * 2, TS = kDsTile * 2;
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * TK + 2 * GH * TS];  // K0 K1 | dS[buf][head]
+  lds_t* smem = (lds_t*)smem_raw;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int G = p.H / p.Hkv, NG = G / GH;  // head groups per kv head
+  const int BHG = p.B * p.Hkv * NG, nqt = (p.Sq + BM - 1) / BM, id = blockIdx.x;
+  const int rank = id / (BHG * nsplit), sp = (id / BHG) % nsplit;
+  const int qt = p.causal ? nqt - 1 - rank : rank;
+  const int bhg = id % BHG, b = bhg / (p.Hkv * NG), hk = (bhg / NG) % p.Hkv;
+  const int hq0 = hk * G + (bhg % NG) * GH;  // first query head of this workgroup
+  const int q0 = qt * BM, my_q = q0 + wid * 32 + r;
+
+  const rsrc_t rk = make_rsrc(p.k + (int64_t)b * p.skb + (int64_t)hk * p.skh, p.Sk, p.sks, D);
+  const int64_t per_bh = ds_prefix(p.causal, p.Sk, p.q_offset, p.k_offset, nqt);
+  // the GH heads' tile regions as rows of 128 bf16 (64 rows a tile); offsets fit 32 bits (host check)
+  const rsrc_t rs = make_rsrc(dsw + ((int64_t)b * p.H + hq0) * per_bh * kDsTile, (int)(GH * per_bh * 64), 128, 128);
+  const uint32_t t0 = (uint32_t)ds_prefix(p.causal, p.Sk, p.q_offset, p.k_offset, qt);
+
+  int nkb, kb_mask;
+  key_blocks<BM, BN>(p, q0, false, nkb, kb_mask);
+  const int kb0 = (int)((int64_t)nkb * sp / nsplit), kb1 = (int)((int64_t)nkb * (sp + 1) / nsplit);
+
+  LdsAddr<D> la;
+  la.init(lane);
+  // transposed-read addresses of a dS^T image for this wave's 32 query columns
+  // (LdsAddr::trf with dt = wid, which is not a compile-time index here)
+  int sa[2];
+  {
+    const int g = (lane >> 4) & 1, q = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) sa[hf] = lds_off<128>(4 * h + q + 8 * hf, 4 * wid + 2 * g + (pp >> 1)) + 8 * (pp & 1);
+  }
+  DmaStager<D, BN> sk;
+  sk.init(wid, lane, p.sks);
+  // the GH 16 KiB dS^T tiles of key block kb, 4 KiB of each per wave; lane l of a
+  // wave-instruction fetches the plain-layout chunk that belongs at LDS byte 16 l of
+  // the XOR-swizzled image (swizzle on the source side, as DmaStager)
+  uint32_t sv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int a = wid * (TS / 4) + i * 1024 + lane * 16, row = a >> 8, pos = (a >> 4) & 15;
+    sv[i] = (uint32_t)(row * 256 + 16 * (pos ^ swz<128>(row)));
+  }
+  const uint32_t head_stride = (uint32_t)(per_bh * TS);
+  auto load_ds = [&](lds_t* dst, int kb) {
+    const uint32_t o = (t0 + (uint32_t)kb) * (uint32_t)TS;
+#pragma unroll
+    for (int j = 0; j < GH; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        lds_dma16(rs, dst + j * TS + wid * (TS / 4) + i * 1024, o + (uint32_t)j * head_stride + sv[i]);
+  };
+
+  f32x16 dqacc[GH][NDT];
+#pragma unroll
+  for (int j = 0; j < GH; ++j)
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) dqacc[j][dt] = zero16();
+
+  if (kb0 < kb1) {
+    sk.load(rk, smem, kb0 * BN);
+    load_ds(smem + 2 * TK, kb0);
+  }
+  dma_barrier();
+
+  auto step = [&](auto bufc, int kb) {
+    constexpr int BUF = decltype(bufc)::value;
+    if (kb + 1 < kb1) {
+      sk.load(rk, smem + (BUF ^ 1) * TK, (kb + 1) * BN);
+      load_ds(smem + 2 * TK + (BUF ^ 1) * GH * TS, kb + 1);
+    }
+    const lds_t* kt = smem + BUF * TK;
+    const lds_t* st = smem + 2 * TK + BUF * GH * TS;
+    // B operands: dS^T columns of this wave's 32 queries per head, k-steps (key half u, s)
+    bfx8 g[GH][4];
+#pragma unroll
+    for (int j = 0; j < GH; ++j)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const lds_t* bp = st + j * TS + (32 * (u >> 1) + 16 * (u & 1)) * 256;
+        g[j][u] = lds_tr(bp + sa[0], bp + sa[1]);
+      }
+    bfx8 tk[NDT][4];
+    auto load_t = [&](int dt) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) tk[dt][u] = la.trf(kt, 32 * (u >> 1), u & 1, dt);
+    };
+    load_t(0);
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      if (dt + 1 < NDT) load_t(dt + 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < GH; ++j)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) mfma_acc(dqacc[j][dt], tk[dt][u], g[j][u]);
+    }
+    dma_barrier();
+  };
+  int kb = kb0;
+  for (; kb + 1 < kb1; kb += 2) {
+    step(Buf<0>(), kb);
+    step(Buf<1>(), kb + 1);
+  }
+  if (kb < kb1) step(Buf<0>(), kb);
+
+#pragma unroll
+  for (int j = 0; j < GH; ++j) agpr_fence(dqacc[j]);
+  if (my_q >= p.Sq) return;
+#pragma unroll
+  for (int j = 0; j < GH; ++j) {
+    const int hq = hq0 + j;
+    if (nsplit > 1) {
+      float* pq = part + ((int64_t)sp * p.B * p.H + (int64_t)b * p.H + hq) * p.Sq * D + (int64_t)my_q * D;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg)
+          *reinterpret_cast<float4*>(pq + 32 * dt + 8 * gg + 4 * h) =
+              make_float4(dqacc[j][dt][4 * gg] * p.scale, dqacc[j][dt][4 * gg + 1] * p.scale,
+                          dqacc[j][dt][4 * gg + 2] * p.scale, dqacc[j][dt][4 * gg + 3] * p.scale);
+    } else {
+      bf16_t* row = dq + (int64_t)b * p.sxb + (int64_t)my_q * p.sxs + (int64_t)hq * p.sxh;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          const int d = 32 * dt + 8 * gg + 4 * h;
+          uint2 w;
+          w.x = pack_bf16x2(dqacc[j][dt][4 * gg + 0] * p.scale, dqacc[j][dt][4 * gg + 1] * p.scale);
+          w.y = pack_bf16x2(dqacc[j][dt][4 * gg + 2] * p.scale, dqacc[j][dt][4 * gg + 3] * p.scale);
+          *reinterpret_cast<uint2*>(row + d) = w;
+        }
+      }
+    }
+  }
+}
+
 // ============================================================== backward: dK, dV
 // One workgroup = 128 keys (4 waves x 32) of one (b, kv-head); iterates every
 // query head of the GQA group x query blocks of 64 rows staged in LDS (Q, dO,
@@ -879,11 +1072,14 @@ ST_DEVICE void dkdv_softmax4(f32x16& s, f32x16& dp, const lds_t* st, int BQ, int
   }
 }
 
-template <int D, int PROBE = 0>  // PROBE 1: softmax / dS VALU skipped (timing probe, wrong results)
+// PROBE 1: softmax / dS VALU skipped (timing probe, wrong results).
+// WDS: also store dS^T tiles into the dS workspace `dsw` (see ds_prefix) for
+// flash_bwd_dq_ds_kernel.
+template <int D, int PROBE = 0, bool WDS = false>
 __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
     AttnParams p, const bf16_t* __restrict__ dout, int64_t sdb, int64_t sds, int64_t sdh,
     const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dk,
-    bf16_t* __restrict__ dv, int nsplit, float* __restrict__ part) {
+    bf16_t* __restrict__ dv, int nsplit, float* __restrict__ part, bf16_t* __restrict__ dsw) {
   constexpr int BKW = 128, BQ = 64, NKK = D / 16, NDT = D / 32;
   constexpr int TB = BQ * D * 2;
   __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB + 2 * 2 * BQ * 4];
@@ -919,7 +1115,17 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
     const int64_t first_q = p.k_offset + k0 - p.q_offset;
     qb0 = first_q <= 0 ? 0 : (int)((first_q) / BQ);
   }
+  // dS workspace: every 128-query tile the dQ kernel reads from this key tile must be
+  // written whole, so start at an even 64-query block (a dead block stores zeros)
+  if constexpr (WDS) qb0 &= ~1;
   const int nqb = (p.Sq + BQ - 1) / BQ;
+  const int nqt128 = (p.Sq + 127) / 128;
+  const int64_t ds_per_bh = WDS ? ds_prefix(p.causal, p.Sk, p.q_offset, p.k_offset, nqt128) : 0;
+  const int ds_kb = (k0 >> 6) + (wid >> 1), ds_row = (wid & 1) * 32 + r;
+  // 16-byte chunk c (8 queries) of this lane's key row of a dS^T tile
+  auto ds_store = [&](bf16_t* tile, int c, uint4 w) {
+    *reinterpret_cast<uint4*>(tile + ds_row * 128 + 8 * c) = w;
+  };
   const int nq = nqb > qb0 ? nqb - qb0 : 0;
   const int total = G * nq;
   const int it0 = (int)((int64_t)total * sp / nsplit), it1 = (int)((int64_t)total * (sp + 1) / nsplit);
@@ -967,6 +1173,19 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
     const int64_t qstart = p.q_offset + (int64_t)qb_c * BQ;  // global index of the block's row 0
     // this wave's keys vs this query block: skip when every key is in the future
     const bool dead = p.causal && (kg - r > qstart + BQ - 1);
+    bf16_t* ds_tile = nullptr;  // this wave's dS^T tile when the dQ kernel reads it
+    const int ds_ch0 = (qb_c & 1) * 8;
+    if constexpr (WDS) {
+      const int qt = qb_c >> 1;
+      if (ds_kb < ds_nkb(p.causal, p.Sk, p.q_offset, p.k_offset, qt))
+        ds_tile = dsw + (((int64_t)b * p.H + hk * G + g_c) * ds_per_bh +
+                         ds_prefix(p.causal, p.Sk, p.q_offset, p.k_offset, qt) + ds_kb) *
+                            kDsTile;
+      if (dead && ds_tile) {  // 4 stores, as a live step issues (the barrier's vmcnt counts them)
+#pragma unroll
+        for (int c = 0; c < 8; c += 2) ds_store(ds_tile, ds_ch0 + c + h, make_uint4(0u, 0u, 0u, 0u));
+      }
+    }
     if (!dead) {
       // software-pipelined within the wave (one wave per SIMD: nothing else fills
       // the MFMA pipe while the softmax VALU runs): half 0's softmax is issued
@@ -1014,6 +1233,24 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
       pf[0][1] = acc_frag(s[0], 1);
       gf[0][0] = acc_frag(dp[0], 0);
       gf[0][1] = acc_frag(dp[0], 1);
+      // fragment k-step s of a 32-query half u holds query groups 2s (low 8 bytes) and
+      // 2s + 1 (high), 4 queries of each per lane half: one v_permlane32_swap per dword
+      // gives lanes 0-31 all of group 2s and lanes 32-63 all of group 2s + 1 -> one
+      // 16-byte store per lane for chunks 4u + 2s (+1) of the 64-query block (T21)
+      auto ds_half = [&](int u) {
+        if constexpr (WDS) {
+          if (ds_tile) {
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+              const u32x4 w = __builtin_bit_cast(u32x4, gf[u][s2]);
+              const auto x = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+              const auto y = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+              ds_store(ds_tile, ds_ch0 + 4 * u + 2 * s2 + h, make_uint4(x[0], y[0], x[1], y[1]));
+            }
+          }
+        }
+      };
+      ds_half(0);
       // dV^T += dO^T P, dK^T += Q^T dS: half 0's four dt groups, then half 1's
       constexpr int NG = NDT * 2;
       bfx8 tv[NG][2], tk[NG][2];
@@ -1035,6 +1272,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
           pf[1][1] = acc_frag(s[1], 1);
           gf[1][0] = acc_frag(dp[1], 0);
           gf[1][1] = acc_frag(dp[1], 1);
+          ds_half(1);
         }
         mfma_acc(dvacc[dt], tv[gi][0], pf[u][0]);
         mfma_acc(dvacc[dt], tv[gi][1], pf[u][1]);
@@ -1050,7 +1288,16 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
         }
       }
     }
-    dma_barrier();
+    if constexpr (WDS) {
+      // the step's 4 dS^T stores were issued after its DMA: retire the (older) DMA and
+      // leave the stores in flight across the barrier -- vmcnt counts in issue order
+      if (ds_tile) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      dma_barrier();
+    }
     g_c = g_n;
     qb_c = qb_n;
   };
@@ -1313,15 +1560,30 @@ int64_t st_flash_bwd_part_elems(int B, int Sq, int Sk, int H, int Hkv, int D, in
   return (n > 1 ? (int64_t)n * 2 * B * Hkv * Sk * D : 0) + (m > 1 ? (int64_t)m * B * H * Sq * D : 0);
 }
 
+// bf16 elements of the dS workspace of the dS-materialising backward, 0 when that
+// path is off (ST_FLASH_BWD_DS=0) or its per-(b, head) region would not fit the
+// 32-bit buffer offsets of flash_bwd_dq_ds_kernel.
+int64_t st_flash_bwd_ds_elems(int B, int Sq, int Sk, int H, int D, int causal, int64_t q_offset,
+                              int64_t k_offset) {
+  const char* e = std::getenv("ST_FLASH_BWD_DS");  // read per call: same-process A/B
+  if (e && std::atoi(e) == 0) return 0;
+  if (D != 128 && D != 64) return 0;
+  const int64_t per_bh = ds_prefix(causal, Sk, q_offset, k_offset, (Sq + 127) / 128);
+  // one dQ workgroup addresses up to 4 heads' regions through one buffer descriptor
+  if (4 * per_bh * (int64_t)kDsTile * 2 >= (int64_t(1) << 31) - (1 << 20)) return 0;
+  return (int64_t)B * H * per_bh * kDsTile;
+}
+
 // dq / dk / dv: bf16 outputs with arbitrary (b, s, h) strides (D contiguous) so
-// they can be slices of one fused dQKV buffer.
+// they can be slices of one fused dQKV buffer.  `dsw` (st_flash_bwd_ds_elems bf16
+// elements, or null) selects the dS-materialising backward.
 int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse,
                  const float* delta, void* dq, void* dk, void* dv, int B, int Sq, int Sk, int H,
                  int Hkv, int D, int64_t sqb, int64_t sqs, int64_t sqh, int64_t skb, int64_t sks,
                  int64_t skh, int64_t svb, int64_t svs, int64_t svh, int64_t sdb, int64_t sds,
                  int64_t sdh, int64_t sdqb, int64_t sdqs, int64_t sdqh, int64_t sdkb, int64_t sdks,
                  int64_t sdkh, float scale, int causal, int64_t q_offset, int64_t k_offset,
-                 float* part, hipStream_t st) {
+                 float* part, void* dsw, hipStream_t st) {
   if (H % Hkv != 0) return -2;
   if (B == 0 || Sq == 0 || Sk == 0) return 0;
   if (!offsets_fit(Sq, sqs) || !offsets_fit(Sq, sds) || !offsets_fit(Sk, sks) || !offsets_fit(Sk, svs))
@@ -1337,6 +1599,38 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
   float* qpart = part ? part + (nsplit > 1 ? (int64_t)nsplit * 2 * B * Hkv * Sk * D : 0) : nullptr;
   const unsigned gk = (unsigned)(((Sk + 127) / 128) * B * Hkv * nsplit);
   const bf16_t* dop = (const bf16_t*)dout;
+  if (dsw && (D == 128 || D == 64)) {
+    // dK/dV (storing dS^T tiles), then dQ = dS K from the workspace, in stream order
+    bf16_t* ds = (bf16_t*)dsw;
+    // query heads per dQ workgroup (sharing each staged K tile): 4, 2 or 1
+    const int G = H / Hkv, GH = G % 4 == 0 ? 4 : (G % 2 == 0 ? 2 : 1);
+    const unsigned gds = (unsigned)(((Sq + 127) / 128) * B * Hkv * (G / GH) * qsplit);
+    if (D == 128) {
+      flash_bwd_dkdv_kernel<128, 0, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
+                                                             (bf16_t*)dv, nsplit, part, ds);
+      if (GH == 4) flash_bwd_dq_ds_kernel<128, 4><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
+      else if (GH == 2) flash_bwd_dq_ds_kernel<128, 2><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
+      else flash_bwd_dq_ds_kernel<128, 1><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
+    } else {
+      flash_bwd_dkdv_kernel<64, 0, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
+                                                            (bf16_t*)dv, nsplit, part, ds);
+      if (GH == 4) flash_bwd_dq_ds_kernel<64, 4><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
+      else if (GH == 2) flash_bwd_dq_ds_kernel<64, 2><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
+      else flash_bwd_dq_ds_kernel<64, 1><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
+    }
+    ST_HIP_CHECK(hipGetLastError());
+    if (qsplit > 1) {
+      const int64_t total8 = (int64_t)B * H * Sq * (D / 8);
+      dq_split_reduce_kernel<<<(unsigned)((total8 + 255) / 256), 256, 0, st>>>(qpart, qsplit, H, Sq, D, total8,
+                                                                               (bf16_t*)dq, sdqb, sdqs, sdqh);
+    }
+    if (nsplit > 1) {
+      const int64_t total8 = (int64_t)B * Hkv * Sk * (D / 8);
+      dkdv_split_reduce_kernel<<<(unsigned)((total8 + 255) / 256), 256, 0, st>>>(
+          part, nsplit, Hkv, Sk, D, total8, (bf16_t*)dk, (bf16_t*)dv, sdkb, sdks, sdkh);
+    }
+    return (int)hipGetLastError();
+  }
   // the dQ kernel (and its split reduce) runs on a second stream beside dK/dV, so the
   // dispatcher fills each kernel's causal tail with the other's workgroups; joined with an
   // event before returning (same stream order for callers).  Same-process A/B at Llama-3-8B
@@ -1368,16 +1662,16 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
     if (pe && std::atoi(pe) == 1) {
       flash_bwd_dq_kernel<128, 1><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq, qsplit, qpart);
       flash_bwd_dkdv_kernel<128, 1><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
-                                                   (bf16_t*)dv, nsplit, part);
+                                                   (bf16_t*)dv, nsplit, part, nullptr);
     } else {
       flash_bwd_dq_kernel<128><<<gq, 256, 0, sq>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq, qsplit, qpart);
       flash_bwd_dkdv_kernel<128><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
-                                                   (bf16_t*)dv, nsplit, part);
+                                                   (bf16_t*)dv, nsplit, part, nullptr);
     }
   } else if (D == 64) {
     flash_bwd_dq_kernel<64><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq, qsplit, qpart);
     flash_bwd_dkdv_kernel<64><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
-                                                  (bf16_t*)dv, nsplit, part);
+                                                  (bf16_t*)dv, nsplit, part, nullptr);
   } else {
     return -3;
   }

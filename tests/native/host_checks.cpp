@@ -15,6 +15,7 @@ int64_t st_wgrad_ws_elems(int M, int N, int T, int variant);
 int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int M, int N,
                   int T, int beta, int variant, float* ws, hipStream_t st);
 int64_t st_flash_bwd_part_elems(int B, int Sq, int Sk, int H, int Hkv, int D, int causal);
+int64_t st_flash_bwd_ds_elems(int B, int Sq, int Sk, int H, int D, int causal, int64_t q_offset, int64_t k_offset);
 int st_rmsnorm_bwd_nwaves(int rows);
 int st_rmsnorm_fwd(const void* x, const void* res, const void* w, void* y, void* sum_out, float* rstd, int rows,
                    int h, float eps, hipStream_t st);
@@ -57,6 +58,28 @@ int main() {
           CHECK(e <= (int64_t)8 * 2 * B * Hkv * Sk * D + (int64_t)8 * B * 4 * Hkv * Sk * D);
           total += e;
         }
+  // dS workspace of the dS-materialising flash backward: the closed-form tile count equals
+  // the sum over 128-query tiles of the visible 64-key blocks (key_blocks' causal limit)
+  for (int Sq : {1, 64, 127, 128, 320, 4096})
+    for (int Sk : {1, 64, 200, 384, 4096})
+      for (int64_t qo : {0, 32, 96, 300, 1000})
+        for (int64_t ko : {0, 32, 160, 5000})
+          for (int causal : {0, 1}) {
+            const int NKB = (Sk + 63) / 64;
+            int64_t want = 0;
+            for (int t = 0; t < (Sq + 127) / 128; ++t) {
+              int64_t n = NKB;
+              if (causal) {
+                const int64_t last = qo + 128 * t + 127 - ko;
+                const int64_t lim = last < 0 ? 0 : last / 64 + 1;
+                n = lim < n ? lim : n;
+              }
+              want += n;
+            }
+            const int64_t e = st_flash_bwd_ds_elems(2, Sq, Sk, 8, 128, causal, qo, ko);
+            CHECK(e == 2 * 8 * want * 64 * 128);
+            total += e;
+          }
   for (int rows : {0, 1, 3, 4, 5, 1000, 24576, 1 << 20}) {
     const int nw = st_rmsnorm_bwd_nwaves(rows);
     CHECK(nw >= 1 && nw <= 4096);

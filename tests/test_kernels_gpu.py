@@ -195,6 +195,50 @@ def test_flash_bwd_split_forced(B, Sq, Sk, H, Hkv, D, causal, kernel, split, mon
 
 
 
+@pytest.mark.parametrize("B,Sq,Sk,H,Hkv,D,causal", FLASH_CASES)
+def test_flash_bwd_recompute_path(B, Sq, Sk, H, Hkv, D, causal, monkeypatch):
+    """The dQ kernel that recomputes S / dP itself (ST_FLASH_BWD_DS=0) -- the default
+    path above stores dS from the dK/dV kernel and derives dQ from it."""
+    monkeypatch.setenv("ST_FLASH_BWD_DS", "0")
+    _flash_case(B, Sq, Sk, H, Hkv, D, causal, 1.0)
+
+
+@pytest.mark.parametrize("ds", ["0", "1"])
+@pytest.mark.parametrize("q_off,k_off", [(32, 0), (0, 32), (96, 160), (300, 0), (0, 0), (1000, 0)])
+def test_flash_bwd_unaligned_offsets(q_off, k_off, ds, monkeypatch):
+    """Causal blocks at global offsets that are not multiples of the 64-row tiles (ring /
+    zig-zag CP blocks): the dS workspace must cover every (query tile, key block) pair the
+    dQ kernel reads, including query blocks the dK/dV kernel would otherwise skip."""
+    monkeypatch.setenv("ST_FLASH_BWD_DS", ds)
+    torch.manual_seed(0)
+    B, Sq, Sk, H, Hkv, D = 1, 320, 384, 4, 2, 128
+    q = torch.randn(B, Sq, H, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, Sk, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, Sk, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    out, lse = ops.flash_attn_fwd(q, k, v, scale, True, q_off, k_off)
+    dout = torch.randn_like(out)
+    dq, dk, dv = ops.flash_attn_bwd(dout, q, k, v, out, lse, scale, True, q_off, k_off)
+    rq, rk, rv = ops.attention.flash_bwd_ref(dout, q, k, v, out, lse, scale, True, q_off, k_off)
+    assert torch.isfinite(dq.float()).all() and torch.isfinite(dk.float()).all()
+    assert rel(dq, rq) < 2e-2 and rel(dk, rk) < 2e-2 and rel(dv, rv) < 2e-2
+
+
+def test_flash_bwd_ds_bitwise_repeatable():
+    """The dS-materialising backward has no atomics: two runs agree bitwise."""
+    torch.manual_seed(0)
+    B, S, H, Hkv, D = 2, 1024, 8, 2, 128
+    q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    out, lse = ops.flash_attn_fwd(q, k, v, 1 / math.sqrt(D), True)
+    dout = torch.randn_like(out)
+    a = ops.flash_attn_bwd(dout, q, k, v, out, lse, 1 / math.sqrt(D), True)
+    b = ops.flash_attn_bwd(dout, q, k, v, out, lse, 1 / math.sqrt(D), True)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("qscale", [6.0, 30.0])
 def test_flash_large_logits(qscale):
     """Peaked softmax: exercises the deferred (thresholded) O rescale."""
