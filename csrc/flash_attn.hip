@@ -311,10 +311,13 @@ ST_DEVICE int key_limit(const AttnParams& p, int kb, int BN, int64_t qg, int h, 
 // Layout: per (b, q-head), the 64-key x 128-query tiles (kb, qt) that the dQ
 // kernel visits, query tile major, key block minor, compact under the causal mask:
 // tile (qt, kb) sits at prefix(qt) + kb, prefix(n) = sum_{t<n} nkb(t).  A tile is
-// a dS^T image [64 keys][128 queries] stored as plain 256-byte rows, so each dK/dV
-// step completes whole 128-byte lines; the dQ kernel applies the LDS XOR swizzle
-// (lds_off<128>) on the DMA source side, like DmaStager, and reads the tile with the
-// same transposed-read addressing as its K tile.
+// a dS^T tile [64 keys][128 queries] (16 KiB) in the dK/dV kernel's STORE order:
+// [key half (32 keys)][query chunk c (8 queries)][key k (32)][8 queries], key rows
+// XOR-permuted by the chunk (k ^ 4 (c & 3)).  Each store instruction of the dK/dV
+// kernel then writes 1 KiB contiguous (two chunks of its 32 keys, after a
+// v_permlane32_swap), and the dQ kernel DMAs the tile linearly into LDS, where the
+// XOR makes its transposed reads (4 keys x 16 queries per 16-lane group, 4 chunks per
+// 32-lane half) bank-conflict free.  See ds_off().
 //
 // nkb(t) of query tile t (128 rows) is key_blocks<128, 64>'s nkb:
 //   causal: clamp(2t + e, 0, NKB), e = floor((q_offset + 127 - k_offset) / 64) + 1
@@ -339,6 +342,8 @@ __host__ __device__ inline int64_t ds_prefix(int causal, int Sk, int64_t q_offse
   return (t1 - t0) * (t0 + t1 - 1) + e * (t1 - t0) + (n - t1) * NKB;
 }
 constexpr int kDsTile = 64 * 128;  // bf16 elements of one dS^T tile (16 KiB)
+// byte offset of (key k, 16-byte query chunk c) inside a dS^T tile
+ST_DEVICE int ds_off(int k, int c) { return 8192 * (k >> 5) + 512 * c + 16 * ((k & 31) ^ (4 * (c & 3))); }
 
 // ============================================================== forward
 template <int D>
@@ -936,25 +941,21 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_ds_kernel(AttnParams p, c
 
   LdsAddr<D> la;
   la.init(lane);
-  // transposed-read addresses of a dS^T image for this wave's 32 query columns
-  // (LdsAddr::trf with dt = wid, which is not a compile-time index here)
+  // transposed-read addresses into a dS^T tile (ds_off layout) for this wave's 32 query
+  // columns: read hf of k-step (half u, s) takes keys 32u + 16s + 8hf + 4h + q, chunk
+  // 4 wid + 2g + (pp >> 1), bytes 8 (pp & 1) -- the k order of LdsAddr::trf
   int sa[2];
   {
     const int g = (lane >> 4) & 1, q = (lane >> 2) & 3, pp = lane & 3;
 #pragma unroll
-    for (int hf = 0; hf < 2; ++hf) sa[hf] = lds_off<128>(4 * h + q + 8 * hf, 4 * wid + 2 * g + (pp >> 1)) + 8 * (pp & 1);
+    for (int hf = 0; hf < 2; ++hf) sa[hf] = ds_off(8 * hf + 4 * h + q, 4 * wid + 2 * g + (pp >> 1)) + 8 * (pp & 1);
   }
   DmaStager<D, BN> sk;
   sk.init(wid, lane, p.sks);
-  // the GH 16 KiB dS^T tiles of key block kb, 4 KiB of each per wave; lane l of a
-  // wave-instruction fetches the plain-layout chunk that belongs at LDS byte 16 l of
-  // the XOR-swizzled image (swizzle on the source side, as DmaStager)
+  // the GH 16 KiB dS^T tiles of key block kb, 4 KiB of each per wave, copied linearly
   uint32_t sv[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int a = wid * (TS / 4) + i * 1024 + lane * 16, row = a >> 8, pos = (a >> 4) & 15;
-    sv[i] = (uint32_t)(row * 256 + 16 * (pos ^ swz<128>(row)));
-  }
+  for (int i = 0; i < 4; ++i) sv[i] = (uint32_t)(wid * (TS / 4) + i * 1024 + lane * 16);
   const uint32_t head_stride = (uint32_t)(per_bh * TS);
   auto load_ds = [&](lds_t* dst, int kb) {
     const uint32_t o = (t0 + (uint32_t)kb) * (uint32_t)TS;
@@ -991,7 +992,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_ds_kernel(AttnParams p, c
     for (int j = 0; j < GH; ++j)
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const lds_t* bp = st + j * TS + (32 * (u >> 1) + 16 * (u & 1)) * 256;
+        const lds_t* bp = st + j * TS + 8192 * (u >> 1) + 256 * (u & 1);  // keys 32(u>>1) + 16(u&1)
         g[j][u] = lds_tr(bp + sa[0], bp + sa[1]);
       }
     bfx8 tk[NDT][4];
@@ -1072,7 +1073,8 @@ ST_DEVICE void dkdv_softmax4(f32x16& s, f32x16& dp, const lds_t* st, int BQ, int
   }
 }
 
-// PROBE 1: softmax / dS VALU skipped (timing probe, wrong results).
+// PROBE 1: softmax / dS VALU skipped; PROBE 2 (with WDS): dS stores skipped (timing
+// probes, wrong results).
 // WDS: also store dS^T tiles into the dS workspace `dsw` (see ds_prefix) for
 // flash_bwd_dq_ds_kernel.
 template <int D, int PROBE = 0, bool WDS = false>
@@ -1122,9 +1124,10 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
   const int nqt128 = (p.Sq + 127) / 128;
   const int64_t ds_per_bh = WDS ? ds_prefix(p.causal, p.Sk, p.q_offset, p.k_offset, nqt128) : 0;
   const int ds_kb = (k0 >> 6) + (wid >> 1), ds_row = (wid & 1) * 32 + r;
-  // 16-byte chunk c (8 queries) of this lane's key row of a dS^T tile
+  // 16-byte chunk c (8 queries) of this lane's key of a dS^T tile (ds_off)
   auto ds_store = [&](bf16_t* tile, int c, uint4 w) {
-    *reinterpret_cast<uint4*>(tile + ds_row * 128 + 8 * c) = w;
+    if constexpr (PROBE != 2)
+      *reinterpret_cast<uint4*>(reinterpret_cast<char*>(tile) + ds_off(ds_row, c)) = w;
   };
   const int nq = nqb > qb0 ? nqb - qb0 : 0;
   const int total = G * nq;
@@ -1217,7 +1220,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
           __builtin_amdgcn_sched_barrier(0);
           s[u] = mfma(qa[u][kk], kf[kk], s[u]);
           dp[u] = mfma(da[u][kk], vf[kk], dp[u]);
-          if (u == 1 && !PROBE) {
+          if (u == 1 && PROBE != 1) {
 #pragma unroll
             for (int gq = 0; gq < 4; ++gq)  // the 4 row groups of half 0 spread over the k-steps
               if (gq * NKK / 4 == kk) {
@@ -1278,7 +1281,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
         mfma_acc(dvacc[dt], tv[gi][1], pf[u][1]);
         mfma_acc(dkacc[dt], tk[gi][0], gf[u][0]);
         mfma_acc(dkacc[dt], tk[gi][1], gf[u][1]);
-        if (u == 0 && !PROBE) {
+        if (u == 0 && PROBE != 1) {
 #pragma unroll
           for (int gq = 0; gq < 4; ++gq)  // half 1's row groups spread over half 0's dt groups
             if (gq * NDT / 4 == dt) {
@@ -1605,7 +1608,12 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
     // query heads per dQ workgroup (sharing each staged K tile): 4, 2 or 1
     const int G = H / Hkv, GH = G % 4 == 0 ? 4 : (G % 2 == 0 ? 2 : 1);
     const unsigned gds = (unsigned)(((Sq + 127) / 128) * B * Hkv * (G / GH) * qsplit);
-    if (D == 128) {
+    const char* pe = std::getenv("ST_FLASH_PROBE");  // diagnostics only (tools/bench_flash_bwd_ds.py)
+    if (D == 128 && pe && std::atoi(pe) == 2) {
+      flash_bwd_dkdv_kernel<128, 2, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
+                                                             (bf16_t*)dv, nsplit, part, ds);
+      flash_bwd_dq_ds_kernel<128, 4><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
+    } else if (D == 128) {
       flash_bwd_dkdv_kernel<128, 0, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
                                                              (bf16_t*)dv, nsplit, part, ds);
       if (GH == 4) flash_bwd_dq_ds_kernel<128, 4><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);

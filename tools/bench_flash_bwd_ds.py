@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Flash-attention backward A/B at the bench layer shape (Llama-3-8B, micro-batch 6:
 B6 S4096 H32/8 D128, causal): the recompute dQ kernel beside dK/dV (ST_FLASH_BWD_DS=0,
-concurrent streams; "recompute_serial": the same on one stream) vs the dS-materialising backward (ST_FLASH_BWD_DS=1: dK/dV stores
-dS^T tiles, dQ = dS K from them).  Interleaved rounds in one process; prints one JSON
+concurrent streams; "recompute_serial": the same on one stream) vs the dS-materialising
+backward (ST_FLASH_BWD_DS=1: dK/dV stores dS^T tiles, dQ = dS K from them).
+PROBE_STORES=1 adds a timing arm with the dS stores skipped (wrong dQ).  Interleaved rounds in one process; prints one JSON
 line with the best time per arm and the rel. difference of the two arms' gradients.
 
   python tools/bench_flash_bwd_ds.py [B] [S]
@@ -30,11 +31,14 @@ scale = 1 / math.sqrt(D)
 out, lse = ops.flash_attn_fwd(q, k, v, scale, True)
 dout = torch.randn_like(out)
 fl_fwd = 4 * B * H * S * S * D / 2
-arms = {"recompute": ("0", "1"), "recompute_serial": ("0", "0"), "ds": ("1", "1")}
+arms = {"recompute": ("0", "1", "0"), "recompute_serial": ("0", "0", "0"), "ds": ("1", "1", "0")}
+if os.environ.get("PROBE_STORES") == "1":  # dS path with the dK/dV kernel's dS stores skipped (wrong dQ)
+    arms["ds_nostore_probe"] = ("1", "1", "2")
 best, grads = {}, {}
 for rnd in range(5):
-    for name, (ds, conc) in arms.items():
+    for name, (ds, conc, probe) in arms.items():
         os.environ["ST_FLASH_BWD_DS"], os.environ["ST_FLASH_BWD_CONCURRENT"] = ds, conc
+        os.environ["ST_FLASH_PROBE"] = probe
         grads[name] = ops.flash_attn_bwd(dout, q, k, v, out, lse, scale, True)
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
