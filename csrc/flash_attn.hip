@@ -346,7 +346,7 @@ constexpr int kDsTile = 64 * 128;  // bf16 elements of one dS^T tile (16 KiB)
 ST_DEVICE int ds_off(int k, int c) { return 8192 * (k >> 5) + 512 * c + 16 * ((k & 31) ^ (4 * (c & 3))); }
 
 // ============================================================== forward
-template <int D>
+template <int D, bool XCD = true>  // XCD: XCD-aware workgroup order (ST_FLASH_XCD=0 -> off, A/B)
 __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(AttnParams p, bf16_t* __restrict__ o,
                                                            int64_t sob, int64_t sos, int64_t soh,
                                                            float* __restrict__ lse) {
@@ -356,8 +356,25 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(AttnParams p, bf16_t*
   lds_t* smem = (lds_t*)smem_raw;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, h = lane >> 5;
   const int BH = p.B * p.H, nqt = (p.Sq + BM - 1) / BM, id = blockIdx.x;
-  const int qt = p.causal ? nqt - 1 - id / BH : id / BH;
-  const int bh = id % BH, b = bh / p.H, hq = bh % p.H, hk = hq / (p.H / p.Hkv);
+  int rank, b, hq;
+  const int G = p.H / p.Hkv, BHk = p.B * p.Hkv;
+  if (XCD && BHk % 8 == 0) {
+    // XCD-aware order (T1): the dispatcher deals workgroups round-robin to the 8 XCDs, so
+    // XCD x = id % 8 takes every (batch, kv head) pair with index = x mod 8, all G query
+    // heads of each: the K / V tiles its workgroups stream are shared by G concurrent
+    // workgroups in that XCD's L2 instead of one per XCD.  Heaviest query tiles first.
+    const int j = id >> 3, per_rank = (BHk >> 3) * G, rem = j % per_rank;
+    rank = j / per_rank;
+    const int bhk = (id & 7) + 8 * (rem / G);
+    b = bhk / p.Hkv;
+    hq = (bhk % p.Hkv) * G + rem % G;
+  } else {
+    rank = id / BH;
+    b = (id % BH) / p.H;
+    hq = id % p.H;
+  }
+  const int qt = p.causal ? nqt - 1 - rank : rank;
+  const int hk = hq / G;
   const int q0 = qt * BM, my_q = q0 + wid * 32 + r;
 
   const rsrc_t rq = make_rsrc(p.q + (int64_t)b * p.sqb + (int64_t)hq * p.sqh, p.Sq, p.sqs, D);
@@ -1084,8 +1101,12 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
     bf16_t* __restrict__ dv, int nsplit, float* __restrict__ part, bf16_t* __restrict__ dsw) {
   constexpr int BKW = 128, BQ = 64, NKK = D / 16, NDT = D / 32;
   constexpr int TB = BQ * D * 2;
-  __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB + 2 * 2 * BQ * 4];
-  lds_t* smem = (lds_t*)smem_raw;  // Q0 Q1 dO0 dO1 | stats[buf][lse2 | delta][BQ]
+  // Q / dO / stats ring: 2 slots, or 3 when storing dS (tiles issued two steps ahead, so
+  // the dS stores of a step get a step and a half to retire before a barrier waits on
+  // the DMA issued after them -- vmcnt counts stores too, in issue order)
+  constexpr int NB = WDS ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * NB * TB + NB * 2 * BQ * 4];
+  lds_t* smem = (lds_t*)smem_raw;  // Q[NB] dO[NB] | stats[slot][lse2 | delta][BQ]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, h = lane >> 5;
   const int G = p.H / p.Hkv, BHk = p.B * p.Hkv, id = blockIdx.x;
   // causal: early keys are the heaviest -> launched first; a key tile's query work may be
@@ -1124,10 +1145,20 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
   const int nqt128 = (p.Sq + 127) / 128;
   const int64_t ds_per_bh = WDS ? ds_prefix(p.causal, p.Sk, p.q_offset, p.k_offset, nqt128) : 0;
   const int ds_kb = (k0 >> 6) + (wid >> 1), ds_row = (wid & 1) * 32 + r;
-  // 16-byte chunk c (8 queries) of this lane's key of a dS^T tile (ds_off)
-  auto ds_store = [&](bf16_t* tile, int c, uint4 w) {
+  // dS stores are buffer stores into one (batch, q-head)'s workspace region: scalar
+  // base + soffset per step, lane-constant VGPR offset, the (u, s2) part an immediate --
+  // no per-store address arithmetic.  Chunk c = ch0 + 4u + 2 s2 + h of this lane's key:
+  // ds_off = 8192 (k >> 5) + 512 c + 16 ((k & 31) ^ 4 (c & 3)), c & 3 = 2 s2 + h.
+  // A step whose tile the dQ kernel never reads stores past the region's end, where
+  // buffer stores are dropped -- every step still issues exactly 4 (ring_wait counts).
+  const uint32_t ds_region = (uint32_t)(ds_per_bh * kDsTile * 2);
+  uint32_t ds_voff[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+    ds_voff[s2] = (uint32_t)(8192 * (ds_row >> 5) + 512 * h + 16 * ((ds_row & 31) ^ (8 * s2 + 4 * h)));
+  auto ds_store = [&](rsrc_t rs, uint32_t soff, int u, int s2, u32x4 w) {
     if constexpr (PROBE != 2)
-      *reinterpret_cast<uint4*>(reinterpret_cast<char*>(tile) + ds_off(ds_row, c)) = w;
+      __builtin_amdgcn_raw_buffer_store_b128(w, rs, (int)(ds_voff[s2] + 2048 * u + 1024 * s2), (int)soff, 0);
   };
   const int nq = nqb > qb0 ? nqb - qb0 : 0;
   const int total = G * nq;
@@ -1138,7 +1169,11 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
   DmaStager<D, BQ> sq, sd;
   sq.init(wid, lane, p.sqs);
   sd.init(wid, lane, sds);
-  float* stats = (float*)(smem_raw + 4 * TB);
+  float* stats = (float*)(smem_raw + 2 * NB * TB);
+  // WDS: every step issues exactly 4 dS stores per wave (a step whose tile the dQ kernel
+  // never reads stores into a dummy tile past the workspace), so the ring's waits are
+  // fixed counts: DMA instructions per issue(), and stores per step
+  constexpr int kDmaPerIssue = 2 * DmaStager<D, BQ>::NI;  // + 1 (stats) on waves 0, 1
 
   f32x16 dkacc[NDT], dvacc[NDT];
 #pragma unroll
@@ -1150,43 +1185,91 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
   auto issue = [&](int g, int qb, int buf) {
     const int hq = hk * G + g;
     sq.load(make_rsrc(p.q + (int64_t)b * p.sqb + (int64_t)hq * p.sqh, p.Sq, p.sqs, D), smem + buf * TB, qb * BQ);
-    sd.load(make_rsrc(dout + (int64_t)b * sdb + (int64_t)hq * sdh, p.Sq, sds, D), smem + (2 + buf) * TB, qb * BQ);
+    sd.load(make_rsrc(dout + (int64_t)b * sdb + (int64_t)hq * sdh, p.Sq, sds, D), smem + (NB + buf) * TB, qb * BQ);
     if (wid < 2) {
       const int64_t row = ((int64_t)b * p.H + hq) * p.Sq;
       lds_dma4(make_rsrc_f32((wid == 0 ? lse : delta) + row, p.Sq),
                (lds_t*)(stats + buf * 2 * BQ + wid * BQ), (uint32_t)((qb * BQ + lane) * 4));
     }
   };
+  // iteration order: heads outer, query blocks inner (a reversed, heads-inner sweep that
+  // lets concurrent key tiles of one kv head share Q / dO tiles in L2 measured neutral)
+  auto advance = [&](int& g, int& qb) {  // next (head, query block) of the iteration
+    if (++qb == nqb) {
+      qb = qb0;
+      ++g;
+    }
+  };
+  // WDS wait at the end of a step: everything but the youngest `N` vector-memory ops
+  // (the previous and this step's dS stores, plus the DMA issued two steps ahead when
+  // there was one) has landed; then the barrier publishes the tiles and retires reads
+  auto ring_wait = [&](bool ahead) {
+    if (!ahead) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    else if (wid < 2) {
+      if constexpr (kDmaPerIssue == 8) asm volatile("s_waitcnt vmcnt(17) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(13) lgkmcnt(0)" ::: "memory");
+    } else {
+      if constexpr (kDmaPerIssue == 8) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  static_assert(kDmaPerIssue == 8 || kDmaPerIssue == 4, "ring_wait counts");
   int g_c = nq > 0 ? it0 / nq : 0, qb_c = qb0 + (nq > 0 ? it0 % nq : 0);
   if (it0 < it1) issue(g_c, qb_c, 0);
-  dma_barrier();
+  if constexpr (WDS) {
+    int g1 = g_c, qb1 = qb_c;
+    advance(g1, qb1);
+    if (it0 + 1 < it1) issue(g1, qb1, 1);
+    // 8 (dropped, out-of-range) stores standing in for the dS stores that follow a DMA in
+    // the steady state (the previous and the current step's), so ring_wait's counts hold
+    // from the start
+    const rsrc_t rs0 = make_rsrc(dsw, (int)(ds_per_bh * 64), 128, 128);
+    const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) ds_store(rs0, ds_region, c >> 2, (c >> 1) & 1, z);
+    ring_wait(it0 + 1 < it1);  // slot 0 landed; slot 1 may still be in flight
+  } else {
+    dma_barrier();
+  }
 
   auto step = [&](auto bufc, int it) {
-    constexpr int BUF = decltype(bufc)::value;
-    const bool more = it + 1 < it1;
-    int g_n = g_c, qb_n = qb_c + 1;
-    if (qb_n == nqb) {
-      qb_n = qb0;
-      ++g_n;
+    constexpr int BUF = decltype(bufc)::value;  // ring slot of this step
+    int g_n = g_c, qb_n = qb_c;
+    advance(g_n, qb_n);
+    bool ahead = false;
+    if constexpr (WDS) {
+      int g2 = g_n, qb2 = qb_n;
+      advance(g2, qb2);
+      ahead = it + 2 < it1;
+      if (ahead) issue(g2, qb2, (BUF + 2) % 3);
+    } else {
+      if (it + 1 < it1) issue(g_n, qb_n, BUF ^ 1);
     }
-    if (more) issue(g_n, qb_n, BUF ^ 1);
     const lds_t* qt = smem + BUF * TB;
-    const lds_t* dt_ = smem + (2 + BUF) * TB;
+    const lds_t* dt_ = smem + (NB + BUF) * TB;
     const lds_t* st = (const lds_t*)(stats + BUF * 2 * BQ);
     const int64_t qstart = p.q_offset + (int64_t)qb_c * BQ;  // global index of the block's row 0
     // this wave's keys vs this query block: skip when every key is in the future
     const bool dead = p.causal && (kg - r > qstart + BQ - 1);
-    bf16_t* ds_tile = nullptr;  // this wave's dS^T tile when the dQ kernel reads it
-    const int ds_ch0 = (qb_c & 1) * 8;
+    // this wave's dS^T tile: region of (b, q-head), byte offset of the tile's 64-query half
+    const rsrc_t ds_rs = make_rsrc(dsw + ((int64_t)b * p.H + hk * G + g_c) * ds_per_bh * kDsTile,
+                                   (int)(ds_per_bh * 64), 128, 128);
+    uint32_t ds_soff = 0;
     if constexpr (WDS) {
       const int qt = qb_c >> 1;
-      if (ds_kb < ds_nkb(p.causal, p.Sk, p.q_offset, p.k_offset, qt))
-        ds_tile = dsw + (((int64_t)b * p.H + hk * G + g_c) * ds_per_bh +
-                         ds_prefix(p.causal, p.Sk, p.q_offset, p.k_offset, qt) + ds_kb) *
-                            kDsTile;
-      if (dead && ds_tile) {  // 4 stores, as a live step issues (the barrier's vmcnt counts them)
+      ds_soff = ds_kb < ds_nkb(p.causal, p.Sk, p.q_offset, p.k_offset, qt)
+                    ? (uint32_t)((ds_prefix(p.causal, p.Sk, p.q_offset, p.k_offset, qt) + ds_kb) * kDsTile * 2 +
+                                 512 * 8 * (qb_c & 1))
+                    : ds_region;  // never read by the dQ kernel: dropped
+      // wave-uniform (ds_kb comes from the wave index): keep it scalar, or hipcc wraps
+      // every store in a readfirstlane waterfall loop (T20)
+      ds_soff = __builtin_amdgcn_readfirstlane(ds_soff);
+      if (dead) {  // 4 stores, as a live step issues (ring_wait counts them)
+        const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int c = 0; c < 8; c += 2) ds_store(ds_tile, ds_ch0 + c + h, make_uint4(0u, 0u, 0u, 0u));
+        for (int c = 0; c < 4; ++c) ds_store(ds_rs, ds_soff, c >> 1, c & 1, z);
       }
     }
     if (!dead) {
@@ -1242,14 +1325,13 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
       // 16-byte store per lane for chunks 4u + 2s (+1) of the 64-query block (T21)
       auto ds_half = [&](int u) {
         if constexpr (WDS) {
-          if (ds_tile) {
 #pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-              const u32x4 w = __builtin_bit_cast(u32x4, gf[u][s2]);
-              const auto x = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
-              const auto y = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
-              ds_store(ds_tile, ds_ch0 + 4 * u + 2 * s2 + h, make_uint4(x[0], y[0], x[1], y[1]));
-            }
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const u32x4 w = __builtin_bit_cast(u32x4, gf[u][s2]);
+            const auto x = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+            const auto y = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+            const u32x4 v4 = {x[0], y[0], x[1], y[1]};
+            ds_store(ds_rs, ds_soff, u, s2, v4);
           }
         }
       };
@@ -1291,25 +1373,27 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
         }
       }
     }
-    if constexpr (WDS) {
-      // the step's 4 dS^T stores were issued after its DMA: retire the (older) DMA and
-      // leave the stores in flight across the barrier -- vmcnt counts in issue order
-      if (ds_tile) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    } else {
-      dma_barrier();
-    }
+    if constexpr (WDS) ring_wait(ahead);
+    else dma_barrier();
     g_c = g_n;
     qb_c = qb_n;
   };
-  int it = it0;  // unconditional pairs (see the dQ kernel)
-  for (; it + 1 < it1; it += 2) {
-    step(Buf<0>(), it);
-    step(Buf<1>(), it + 1);
+  int it = it0;  // unconditional groups of steps (see the dQ kernel); the slot is a constant
+  if constexpr (WDS) {
+    for (; it + 2 < it1; it += 3) {
+      step(Buf<0>(), it);
+      step(Buf<1>(), it + 1);
+      step(Buf<2>(), it + 2);
+    }
+    if (it < it1) step(Buf<0>(), it);
+    if (it + 1 < it1) step(Buf<1>(), it + 1);
+  } else {
+    for (; it + 1 < it1; it += 2) {
+      step(Buf<0>(), it);
+      step(Buf<1>(), it + 1);
+    }
+    if (it < it1) step(Buf<0>(), it);
   }
-  if (it < it1) step(Buf<0>(), it);
 
   agpr_fence(dkacc);
   agpr_fence(dvacc);
@@ -1488,13 +1572,19 @@ int st_flash_fwd(const void* q, const void* k, const void* v, void* o, float* ls
   // (read per call so tests can switch it; one getenv per launch)
   const char* ppe = std::getenv("ST_FLASH_PP");
   const int pp = ppe ? std::atoi(ppe) : 0;
+  const char* xe = std::getenv("ST_FLASH_XCD");  // XCD-aware workgroup order (default on)
+  const bool xcd = !xe || std::atoi(xe) != 0;
   if (D == 128 && pp) {
     const unsigned grid2 = (unsigned)(((Sq + 255) / 256) * B * H);
     flash_fwd_pp_kernel<128><<<grid2, 512, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
-  } else if (D == 128)
-    flash_fwd_kernel<128><<<grid, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
+  } else if (D == 128 && xcd)
+    flash_fwd_kernel<128, true><<<grid, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
+  else if (D == 128)
+    flash_fwd_kernel<128, false><<<grid, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
+  else if (D == 64 && xcd)
+    flash_fwd_kernel<64, true><<<grid, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
   else if (D == 64)
-    flash_fwd_kernel<64><<<grid, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
+    flash_fwd_kernel<64, false><<<grid, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
   else
     return -3;
   return (int)hipGetLastError();

@@ -50,11 +50,31 @@ for rnd in range(5):
         best[name] = min(best.get(name, 1e9), s.elapsed_time(e) / 5)
 
 
+# forward at the same shape: XCD-aware workgroup order on / off (ST_FLASH_XCD), interleaved
+fwd = {}
+for rnd in range(5):
+    for xcd in ("1", "0"):
+        os.environ["ST_FLASH_XCD"] = xcd
+        ops.flash_attn_fwd(q, k, v, scale, True)
+        torch.cuda.synchronize()
+        fs, fe = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        fs.record()
+        for _ in range(5):
+            ops.flash_attn_fwd(q, k, v, scale, True)
+        fe.record()
+        fe.synchronize()
+        fwd[xcd] = min(fwd.get(xcd, 1e9), fs.elapsed_time(fe) / 5)
+os.environ["ST_FLASH_XCD"] = "1"
+fwd_ms = fwd["1"]
+
+
 def rel(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm()).item()
 
 
-res = {"shape": [B, S, H, Hkv, D], "bwd_ms": {k2: round(v2, 4) for k2, v2 in best.items()},
+res = {"shape": [B, S, H, Hkv, D], "fwd_ms": round(fwd_ms, 4), "fwd_tflops": round(fl_fwd / fwd_ms / 1e9, 1),
+       "fwd_ms_xcd_off": round(fwd["0"], 4),
+       "bwd_ms": {k2: round(v2, 4) for k2, v2 in best.items()},
        "tflops_5matmul": {k2: round(2.5 * fl_fwd / v2 / 1e9, 1) for k2, v2 in best.items()},
        "rel_diff": {n: rel(a, b) for n, a, b in zip(("dq", "dk", "dv"), grads["ds"], grads["recompute"])}}
 print(json.dumps(res), flush=True)
