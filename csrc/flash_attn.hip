@@ -311,13 +311,14 @@ ST_DEVICE int key_limit(const AttnParams& p, int kb, int BN, int64_t qg, int h, 
 // Layout: per (b, q-head), the 64-key x 128-query tiles (kb, qt) that the dQ
 // kernel visits, query tile major, key block minor, compact under the causal mask:
 // tile (qt, kb) sits at prefix(qt) + kb, prefix(n) = sum_{t<n} nkb(t).  A tile is
-// a dS^T tile [64 keys][128 queries] (16 KiB) in the dK/dV kernel's STORE order:
-// [key half (32 keys)][query chunk c (8 queries)][key k (32)][8 queries], key rows
-// XOR-permuted by the chunk (k ^ 4 (c & 3)).  Each store instruction of the dK/dV
-// kernel then writes 1 KiB contiguous (two chunks of its 32 keys, after a
-// v_permlane32_swap), and the dQ kernel DMAs the tile linearly into LDS, where the
-// XOR makes its transposed reads (4 keys x 16 queries per 16-lane group, 4 chunks per
-// 32-lane half) bank-conflict free.  See ds_off().
+// a dS^T tile [64 keys][128 queries] (16 KiB) in the dK/dV kernel's STORE order: one
+// 1 KiB block per (key half wp, 64-query half qh, 32-query half u, 16-query group s),
+// holding each lane's raw bf16 MFMA fragment -- lane (key r, half h) has the queries
+// 16s + 4h + 0..3 (bytes 0-7) and 16s + 8 + 4h + 0..3 (bytes 8-15) -- at
+// 16 (32 h + (r ^ (8 s + 4 h))).  So every dK/dV store instruction writes 1 KiB
+// contiguous with no lane shuffles, and the dQ kernel DMAs the tile linearly into LDS
+// where the XOR keeps its transposed reads (4 keys x 16 queries per 16-lane group)
+// bank-conflict free.
 //
 // nkb(t) of query tile t (128 rows) is key_blocks<128, 64>'s nkb:
 //   causal: clamp(2t + e, 0, NKB), e = floor((q_offset + 127 - k_offset) / 64) + 1
@@ -342,8 +343,10 @@ __host__ __device__ inline int64_t ds_prefix(int causal, int Sk, int64_t q_offse
   return (t1 - t0) * (t0 + t1 - 1) + e * (t1 - t0) + (n - t1) * NKB;
 }
 constexpr int kDsTile = 64 * 128;  // bf16 elements of one dS^T tile (16 KiB)
-// byte offset of (key k, 16-byte query chunk c) inside a dS^T tile
-ST_DEVICE int ds_off(int k, int c) { return 8192 * (k >> 5) + 512 * c + 16 * ((k & 31) ^ (4 * (c & 3))); }
+// byte offset of lane (key k in 0..63, half h)'s 16-byte fragment of block (qh, u, s)
+ST_DEVICE int ds_off(int k, int qh, int u, int s, int h) {
+  return 8192 * (k >> 5) + 4096 * qh + 2048 * u + 1024 * s + 512 * h + 16 * ((k & 31) ^ (8 * s + 4 * h));
+}
 
 // ============================================================== forward
 template <int D, bool XCD = true>  // XCD: XCD-aware workgroup order (ST_FLASH_XCD=0 -> off, A/B)
@@ -959,13 +962,15 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_ds_kernel(AttnParams p, c
   LdsAddr<D> la;
   la.init(lane);
   // transposed-read addresses into a dS^T tile (ds_off layout) for this wave's 32 query
-  // columns: read hf of k-step (half u, s) takes keys 32u + 16s + 8hf + 4h + q, chunk
-  // 4 wid + 2g + (pp >> 1), bytes 8 (pp & 1) -- the k order of LdsAddr::trf
+  // columns 32 wid + 16 g + 4 pp + 0..3: read hf of k-step (key half u, s) takes keys
+  // 32u + 16s + 8hf + 4h + q (the k order of LdsAddr::trf); queries 16g + 4pp of the 32-query
+  // half wid & 1 are fragment piece pp >> 1 of the writer's lane half pp & 1, block s = g
   int sa[2];
   {
     const int g = (lane >> 4) & 1, q = (lane >> 2) & 3, pp = lane & 3;
 #pragma unroll
-    for (int hf = 0; hf < 2; ++hf) sa[hf] = ds_off(8 * hf + 4 * h + q, 4 * wid + 2 * g + (pp >> 1)) + 8 * (pp & 1);
+    for (int hf = 0; hf < 2; ++hf)
+      sa[hf] = ds_off(8 * hf + 4 * h + q, wid >> 1, wid & 1, g, pp & 1) + 8 * (pp >> 1);
   }
   DmaStager<D, BN> sk;
   sk.init(wid, lane, p.sks);
@@ -1148,14 +1153,14 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
   // dS stores are buffer stores into one (batch, q-head)'s workspace region: scalar
   // base + soffset per step, lane-constant VGPR offset, the (u, s2) part an immediate --
   // no per-store address arithmetic.  Chunk c = ch0 + 4u + 2 s2 + h of this lane's key:
-  // ds_off = 8192 (k >> 5) + 512 c + 16 ((k & 31) ^ 4 (c & 3)), c & 3 = 2 s2 + h.
+  // ds_off = 8192 (k >> 5) + 4096 qh + 2048 u + 1024 s2 + 512 h + 16 ((k & 31) ^ (8 s2 + 4 h)).
   // A step whose tile the dQ kernel never reads stores past the region's end, where
   // buffer stores are dropped -- every step still issues exactly 4 (ring_wait counts).
   const uint32_t ds_region = (uint32_t)(ds_per_bh * kDsTile * 2);
   uint32_t ds_voff[2];
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
-    ds_voff[s2] = (uint32_t)(8192 * (ds_row >> 5) + 512 * h + 16 * ((ds_row & 31) ^ (8 * s2 + 4 * h)));
+    ds_voff[s2] = (uint32_t)ds_off(ds_row, 0, 0, s2, h) - 1024 * s2;  // + 2048 u + 1024 s2 as immediates
   auto ds_store = [&](rsrc_t rs, uint32_t soff, int u, int s2, u32x4 w) {
     if constexpr (PROBE != 2)
       __builtin_amdgcn_raw_buffer_store_b128(w, rs, (int)(ds_voff[s2] + 2048 * u + 1024 * s2), (int)soff, 0);
@@ -1261,7 +1266,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
       const int qt = qb_c >> 1;
       ds_soff = ds_kb < ds_nkb(p.causal, p.Sk, p.q_offset, p.k_offset, qt)
                     ? (uint32_t)((ds_prefix(p.causal, p.Sk, p.q_offset, p.k_offset, qt) + ds_kb) * kDsTile * 2 +
-                                 512 * 8 * (qb_c & 1))
+                                 4096 * (qb_c & 1))
                     : ds_region;  // never read by the dQ kernel: dropped
       // wave-uniform (ds_kb comes from the wave index): keep it scalar, or hipcc wraps
       // every store in a readfirstlane waterfall loop (T20)
@@ -1319,20 +1324,12 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
       pf[0][1] = acc_frag(s[0], 1);
       gf[0][0] = acc_frag(dp[0], 0);
       gf[0][1] = acc_frag(dp[0], 1);
-      // fragment k-step s of a 32-query half u holds query groups 2s (low 8 bytes) and
-      // 2s + 1 (high), 4 queries of each per lane half: one v_permlane32_swap per dword
-      // gives lanes 0-31 all of group 2s and lanes 32-63 all of group 2s + 1 -> one
-      // 16-byte store per lane for chunks 4u + 2s (+1) of the 64-query block (T21)
+      // the dK MFMA's B fragments (k-step s2 of 32-query half u) are stored as they are:
+      // one 16-byte store per lane, 1 KiB contiguous per instruction (ds_off)
       auto ds_half = [&](int u) {
         if constexpr (WDS) {
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const u32x4 w = __builtin_bit_cast(u32x4, gf[u][s2]);
-            const auto x = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
-            const auto y = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
-            const u32x4 v4 = {x[0], y[0], x[1], y[1]};
-            ds_store(ds_rs, ds_soff, u, s2, v4);
-          }
+          for (int s2 = 0; s2 < 2; ++s2) ds_store(ds_rs, ds_soff, u, s2, __builtin_bit_cast(u32x4, gf[u][s2]));
         }
       };
       ds_half(0);

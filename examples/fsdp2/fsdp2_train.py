@@ -146,4 +146,7 @@ def load(model, opt, path: str, use_dcp: bool) -> int:
 if __name__ == "__main__":
     main()
     if dist.is_initialized():
+        # every rank past its checkpoint I/O before the gloo pairs are torn down (an
+        # occasional rank-0 abort at teardown was seen under a loaded test runner)
+        dist.barrier()
         dist.destroy_process_group()
