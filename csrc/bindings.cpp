@@ -51,7 +51,7 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
                  int64_t sks, int64_t skh, int64_t svb, int64_t svs, int64_t svh, int64_t sdb,
                  int64_t sds, int64_t sdh, int64_t sdqb, int64_t sdqs, int64_t sdqh, int64_t sdkb,
                  int64_t sdks, int64_t sdkh, float scale, int causal, int64_t q_offset,
-                 int64_t k_offset, float* part, void* dsw, hipStream_t st);
+                 int64_t k_offset, float* part, void* dsw, int phases, hipStream_t st);
 int64_t st_flash_bwd_part_elems(int B, int Sq, int Sk, int H, int Hkv, int D, int causal);
 int64_t st_flash_bwd_ds_elems(int B, int Sq, int Sk, int H, int D, int causal, int64_t q_offset,
                               int64_t k_offset);
@@ -737,10 +737,95 @@ std::vector<at::Tensor> flash_bwd(const at::Tensor& dout, const at::Tensor& q, c
                     v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2), dq.stride(0),
                     dq.stride(1), dq.stride(2), dk.stride(0), dk.stride(1), dk.stride(2),
                     (float)scale, causal ? 1 : 0, q_offset, k_offset,
-                    pe > 0 ? part.data_ptr<float>() : nullptr, dse > 0 ? dsw.data_ptr() : nullptr,
+                    pe > 0 ? part.data_ptr<float>() : nullptr, dse > 0 ? dsw.data_ptr() : nullptr, 3,
                     cur_stream());
   ST_CHECK_RC(rc, "flash_bwd");
   return {dq, dk, dv};
+}
+
+// First phase of the dS-materialising backward on its own: delta, then dK / dV with the
+// dS^T tiles stored into the returned workspace.  Returns {dk, dv, ws}; ws is EMPTY (and
+// nothing ran) when the dS path does not apply -- the caller then runs flash_bwd.
+std::vector<at::Tensor> flash_bwd_kv(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
+                                     const at::Tensor& v, const at::Tensor& o, const at::Tensor& lse, double scale,
+                                     bool causal, int64_t q_offset, int64_t k_offset,
+                                     const c10::optional<at::Tensor>& dk_out,
+                                     const c10::optional<at::Tensor>& dv_out) {
+  const int64_t D = q.size(3);
+  TORCH_CHECK(D == 64 || D == 128, "flash_bwd_kv: head_dim must be 64 or 128");
+  for (auto* t : {&q, &k, &v, &o, &dout}) check_qkv(*t, "flash_bwd_kv operand", D);
+  const int64_t B = q.size(0), Sq = q.size(1), H = q.size(2), Sk = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(o.sizes() == q.sizes() && dout.sizes() == q.sizes() && k.sizes() == v.sizes() && k.size(0) == B,
+              "flash_bwd_kv: shapes");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * H * Sq,
+              "flash_bwd_kv: lse [B,H,Sq] fp32");
+  TORCH_CHECK(H % Hkv == 0, "flash_bwd_kv: H must be a multiple of Hkv");
+  for (auto* t : {&k, &v, &o, &dout, &lse}) check_same_gpu(*t, q, "flash_bwd_kv operand");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  const int64_t dse = st_flash_bwd_ds_elems((int)B, (int)Sq, (int)Sk, (int)H, (int)D, causal ? 1 : 0, q_offset,
+                                            k_offset);
+  auto pick = [&](const c10::optional<at::Tensor>& t, at::IntArrayRef shape, const char* n) {
+    if (t.has_value() && t->defined()) {
+      check_qkv(*t, n, D);
+      check_same_gpu(*t, q, n);
+      TORCH_CHECK(t->sizes() == shape, n, ": wrong shape");
+      return *t;
+    }
+    return at::empty(shape, q.options());
+  };
+  auto dk = pick(dk_out, k.sizes(), "dk_out");
+  auto dv = pick(dv_out, v.sizes(), "dv_out");
+  if (dse <= 0) return {dk, dv, at::empty({0}, q.options())};
+  TORCH_CHECK(dk.strides() == dv.strides(), "flash_bwd_kv: dk_out/dv_out must share strides");
+  auto delta = at::empty({B, H, Sq}, q.options().dtype(at::kFloat));
+  int rc = st_flash_bwd_preprocess(o.data_ptr(), dout.data_ptr(), delta.data_ptr<float>(), (int)B, (int)Sq, (int)H,
+                                   (int)D, o.stride(0), o.stride(1), o.stride(2), dout.stride(0), dout.stride(1),
+                                   dout.stride(2), cur_stream());
+  ST_CHECK_RC(rc, "flash_bwd_kv preprocess");
+  const int64_t pe = st_flash_bwd_part_elems((int)B, (int)Sq, (int)Sk, (int)H, (int)Hkv, (int)D, causal ? 1 : 0);
+  at::Tensor part;
+  if (pe > 0) part = at::empty({pe}, q.options().dtype(at::kFloat));
+  auto ws = at::empty({dse}, q.options());
+  rc = st_flash_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
+                    delta.data_ptr<float>(), nullptr, dk.data_ptr(), dv.data_ptr(), (int)B, (int)Sq, (int)Sk, (int)H,
+                    (int)Hkv, (int)D, q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
+                    v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2), 0, 0, 0,
+                    dk.stride(0), dk.stride(1), dk.stride(2), (float)scale, causal ? 1 : 0, q_offset, k_offset,
+                    pe > 0 ? part.data_ptr<float>() : nullptr, ws.data_ptr(), 1, cur_stream());
+  ST_CHECK_RC(rc, "flash_bwd_kv");
+  return {dk, dv, ws};
+}
+
+// Second phase: dQ = dS K from flash_bwd_kv's workspace (on the caller's current stream).
+at::Tensor flash_bwd_q_ds(const at::Tensor& q, const at::Tensor& k, const at::Tensor& ws, double scale, bool causal,
+                          int64_t q_offset, int64_t k_offset, const c10::optional<at::Tensor>& dq_out) {
+  const int64_t D = q.size(3);
+  check_qkv(q, "q", D);
+  check_qkv(k, "k", D);
+  check_same_gpu(k, q, "k");
+  check_same_gpu(ws, q, "ws");
+  const int64_t B = q.size(0), Sq = q.size(1), H = q.size(2), Sk = k.size(1), Hkv = k.size(2);
+  const int64_t dse = st_flash_bwd_ds_elems((int)B, (int)Sq, (int)Sk, (int)H, (int)D, causal ? 1 : 0, q_offset,
+                                            k_offset);
+  TORCH_CHECK(dse > 0 && ws.numel() == dse && ws.scalar_type() == at::kBFloat16,
+              "flash_bwd_q_ds: workspace does not match this problem");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  at::Tensor dq;
+  if (dq_out.has_value() && dq_out->defined()) {
+    dq = *dq_out;
+    check_qkv(dq, "dq_out", D);
+    check_same_gpu(dq, q, "dq_out");
+    TORCH_CHECK(dq.sizes() == q.sizes(), "dq_out: wrong shape");
+  } else {
+    dq = at::empty(q.sizes(), q.options());
+  }
+  int rc = st_flash_bwd(q.data_ptr(), k.data_ptr(), k.data_ptr(), q.data_ptr(), nullptr, nullptr, dq.data_ptr(),
+                        nullptr, nullptr, (int)B, (int)Sq, (int)Sk, (int)H, (int)Hkv, (int)D, q.stride(0), q.stride(1),
+                        q.stride(2), k.stride(0), k.stride(1), k.stride(2), k.stride(0), k.stride(1), k.stride(2),
+                        q.stride(0), q.stride(1), q.stride(2), dq.stride(0), dq.stride(1), dq.stride(2), 0, 0, 0,
+                        (float)scale, causal ? 1 : 0, q_offset, k_offset, nullptr, ws.data_ptr(), 2, cur_stream());
+  ST_CHECK_RC(rc, "flash_bwd_q_ds");
+  return dq;
 }
 
 // In-place online-softmax merge of a partial attention block into a running
@@ -781,6 +866,8 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("xent_bwd_(Tensor logits, Tensor target, int vocab_start, Tensor lse, Tensor dloss, Tensor(a!) dlogits) -> ()");
   m.def("flash_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int q_offset, int k_offset) -> Tensor[]");
   m.def("flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, int q_offset, int k_offset, Tensor(a!)? dq_out=None, Tensor(b!)? dk_out=None, Tensor(c!)? dv_out=None) -> Tensor[]");
+  m.def("flash_bwd_kv(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, int q_offset, int k_offset, Tensor(a!)? dk_out=None, Tensor(b!)? dv_out=None) -> Tensor[]");
+  m.def("flash_bwd_q_ds(Tensor q, Tensor k, Tensor ws, float scale, bool causal, int q_offset, int k_offset, Tensor(a!)? dq_out=None) -> Tensor");
   m.def("wgrad_gemm_(Tensor(a!) out, Tensor dy, Tensor x, int beta, int variant=0) -> bool");
   m.def("wgrad_grouped_(Tensor(a!) out, Tensor dy, Tensor x, Tensor offs, int beta) -> bool");
   m.def("grouped_gemm(Tensor x, Tensor w, Tensor offs, bool wn) -> Tensor");
@@ -814,6 +901,8 @@ TORCH_LIBRARY_IMPL(st_amd, CUDA, m) {
   m.impl("xent_bwd_", &xent_bwd_);
   m.impl("flash_fwd", &flash_fwd);
   m.impl("flash_bwd", &flash_bwd);
+  m.impl("flash_bwd_kv", &flash_bwd_kv);
+  m.impl("flash_bwd_q_ds", &flash_bwd_q_ds);
   m.impl("lse_merge_", &lse_merge_);
   m.impl("wgrad_gemm_", &wgrad_gemm_);
   m.impl("wgrad_grouped_", &wgrad_grouped_);

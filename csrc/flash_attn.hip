@@ -1666,14 +1666,16 @@ int64_t st_flash_bwd_ds_elems(int B, int Sq, int Sk, int H, int D, int causal, i
 
 // dq / dk / dv: bf16 outputs with arbitrary (b, s, h) strides (D contiguous) so
 // they can be slices of one fused dQKV buffer.  `dsw` (st_flash_bwd_ds_elems bf16
-// elements, or null) selects the dS-materialising backward.
+// elements, or null) selects the dS-materialising backward; its `phases` can be run
+// separately (bit 0: dK/dV + the dS stores, bit 1: dQ from dS) so a caller can put the
+// HBM-bound dQ pass on another stream beside compute-bound work (ops/attention.py).
 int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse,
                  const float* delta, void* dq, void* dk, void* dv, int B, int Sq, int Sk, int H,
                  int Hkv, int D, int64_t sqb, int64_t sqs, int64_t sqh, int64_t skb, int64_t sks,
                  int64_t skh, int64_t svb, int64_t svs, int64_t svh, int64_t sdb, int64_t sds,
                  int64_t sdh, int64_t sdqb, int64_t sdqs, int64_t sdqh, int64_t sdkb, int64_t sdks,
                  int64_t sdkh, float scale, int causal, int64_t q_offset, int64_t k_offset,
-                 float* part, void* dsw, hipStream_t st) {
+                 float* part, void* dsw, int phases, hipStream_t st) {
   if (H % Hkv != 0) return -2;
   if (B == 0 || Sq == 0 || Sk == 0) return 0;
   if (!offsets_fit(Sq, sqs) || !offsets_fit(Sq, sds) || !offsets_fit(Sk, sks) || !offsets_fit(Sk, svs))
@@ -1696,36 +1698,43 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
     const int G = H / Hkv, GH = G % 4 == 0 ? 4 : (G % 2 == 0 ? 2 : 1);
     const unsigned gds = (unsigned)(((Sq + 127) / 128) * B * Hkv * (G / GH) * qsplit);
     const char* pe = std::getenv("ST_FLASH_PROBE");  // diagnostics only (tools/bench_flash_bwd_ds.py)
-    if (D == 128 && pe && std::atoi(pe) == 2) {
-      flash_bwd_dkdv_kernel<128, 2, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
-                                                             (bf16_t*)dv, nsplit, part, ds);
-      flash_bwd_dq_ds_kernel<128, 4><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
-    } else if (D == 128) {
-      flash_bwd_dkdv_kernel<128, 0, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
-                                                             (bf16_t*)dv, nsplit, part, ds);
-      if (GH == 4) flash_bwd_dq_ds_kernel<128, 4><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
-      else if (GH == 2) flash_bwd_dq_ds_kernel<128, 2><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
-      else flash_bwd_dq_ds_kernel<128, 1><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
-    } else {
-      flash_bwd_dkdv_kernel<64, 0, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
-                                                            (bf16_t*)dv, nsplit, part, ds);
-      if (GH == 4) flash_bwd_dq_ds_kernel<64, 4><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
-      else if (GH == 2) flash_bwd_dq_ds_kernel<64, 2><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
-      else flash_bwd_dq_ds_kernel<64, 1><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
+    if (phases & 1) {
+      if (D == 128 && pe && std::atoi(pe) == 2)
+        flash_bwd_dkdv_kernel<128, 2, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
+                                                               (bf16_t*)dv, nsplit, part, ds);
+      else if (D == 128)
+        flash_bwd_dkdv_kernel<128, 0, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
+                                                               (bf16_t*)dv, nsplit, part, ds);
+      else
+        flash_bwd_dkdv_kernel<64, 0, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
+                                                              (bf16_t*)dv, nsplit, part, ds);
+      ST_HIP_CHECK(hipGetLastError());
+      if (nsplit > 1) {
+        const int64_t total8 = (int64_t)B * Hkv * Sk * (D / 8);
+        dkdv_split_reduce_kernel<<<(unsigned)((total8 + 255) / 256), 256, 0, st>>>(
+            part, nsplit, Hkv, Sk, D, total8, (bf16_t*)dk, (bf16_t*)dv, sdkb, sdks, sdkh);
+      }
     }
-    ST_HIP_CHECK(hipGetLastError());
-    if (qsplit > 1) {
-      const int64_t total8 = (int64_t)B * H * Sq * (D / 8);
-      dq_split_reduce_kernel<<<(unsigned)((total8 + 255) / 256), 256, 0, st>>>(qpart, qsplit, H, Sq, D, total8,
-                                                                               (bf16_t*)dq, sdqb, sdqs, sdqh);
-    }
-    if (nsplit > 1) {
-      const int64_t total8 = (int64_t)B * Hkv * Sk * (D / 8);
-      dkdv_split_reduce_kernel<<<(unsigned)((total8 + 255) / 256), 256, 0, st>>>(
-          part, nsplit, Hkv, Sk, D, total8, (bf16_t*)dk, (bf16_t*)dv, sdkb, sdks, sdkh);
+    if (phases & 2) {
+      if (D == 128) {
+        if (GH == 4) flash_bwd_dq_ds_kernel<128, 4><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
+        else if (GH == 2) flash_bwd_dq_ds_kernel<128, 2><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
+        else flash_bwd_dq_ds_kernel<128, 1><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
+      } else {
+        if (GH == 4) flash_bwd_dq_ds_kernel<64, 4><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
+        else if (GH == 2) flash_bwd_dq_ds_kernel<64, 2><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
+        else flash_bwd_dq_ds_kernel<64, 1><<<gds, 256, 0, st>>>(pq, ds, (bf16_t*)dq, qsplit, qpart);
+      }
+      ST_HIP_CHECK(hipGetLastError());
+      if (qsplit > 1) {
+        const int64_t total8 = (int64_t)B * H * Sq * (D / 8);
+        dq_split_reduce_kernel<<<(unsigned)((total8 + 255) / 256), 256, 0, st>>>(qpart, qsplit, H, Sq, D, total8,
+                                                                                 (bf16_t*)dq, sdqb, sdqs, sdqh);
+      }
     }
     return (int)hipGetLastError();
   }
+  if (phases != 3) return -6;  // separate phases need the dS workspace
   // the dQ kernel (and its split reduce) runs on a second stream beside dK/dV, so the
   // dispatcher fills each kernel's causal tail with the other's workgroups; joined with an
   // event before returning (same stream order for callers).  Same-process A/B at Llama-3-8B

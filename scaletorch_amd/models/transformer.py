@@ -67,10 +67,25 @@ class Attention(nn.Module):
                 position_ids: torch.Tensor | None) -> torch.Tensor:
         from .attention_backends import attention, resolve_attention_backend_name
 
-        qkv = self.qkv_proj(x)
-        B, S = qkv.shape[0], qkv.shape[1]
         H, Hkv, D = self.H, self.Hkv, self.D
         backend = resolve_attention_backend_name(mesh.cp_size() > 1)
+        link = None
+        if (backend == "flash" and not self.qk_norm and self.qkv_proj.tp == 1 and torch.is_grad_enabled()
+                and x.is_cuda and getattr(self.qkv_proj.weight, "main_grad", None) is not None
+                and os.environ.get("ST_FLASH_DQ_OVERLAP", "0") == "1"):
+            # the QKV projection's backward finishes dQ beside its own k/v GEMMs (ops.attention.DQLink);
+            # opt-in: measured 3.7 ms/step SLOWER at Llama-3-8B mbs 6 (profiles/r03/dq_overlap_ab.log)
+            link = ops.attention.DQLink(H * D)
+        self.qkv_proj._st_link = link
+        try:
+            qkv = self.qkv_proj(x)
+        finally:
+            self.qkv_proj._st_link = None
+        B, S = qkv.shape[0], qkv.shape[1]
+        if link is not None:
+            out = ops.rope_attention(qkv, cos, sin, position_ids, H, Hkv, D, causal=True, scale=self.scale,
+                                     link=link)
+            return self.out_proj(out)
         if self.qk_norm and backend == "flash" and os.environ.get("ST_FUSED_QKNORM", "1") == "1":
             # Qwen3: per-head QK-norm + RoPE fused in place on the QKV buffer (csrc/qknorm_rope.hip)
             out = ops.qknorm_rope_attention(qkv, self.q_norm.weight, self.k_norm.weight, self.q_norm.eps, cos, sin,

@@ -323,9 +323,9 @@ class _ColumnParallelFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, weight, bias, group):
+    def forward(ctx, x, weight, bias, group, link=None):
         ctx.save_for_backward(x, weight)
-        ctx.group, ctx.bias = group, bias
+        ctx.group, ctx.bias, ctx.link = group, bias, link
         if x.requires_grad:
             prepare_dgrad_weight(weight)
         return F.linear(x, weight, bias)
@@ -335,6 +335,9 @@ class _ColumnParallelFn(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1])
         x2 = x.reshape(-1, x.shape[-1])
+        link = ctx.link
+        if link is not None and link.event is not None:
+            return _ColumnParallelFn._backward_split(ctx, dy, dy2, x2, weight, link)
         pre = prefetch_wgrad(weight, dy2, x2) if ctx.needs_input_grad[1] else None  # overlaps the dgrad GEMM
         dx = dgrad(dy, weight)
         handle = None
@@ -346,7 +349,48 @@ class _ColumnParallelFn(torch.autograd.Function):
             db = accumulate_grad(ctx.bias, dy2.float().sum(0))
         if handle is not None:
             handle.wait()
-        return dx, dw, db, None
+        return dx, dw, db, None, None
+
+    @staticmethod
+    def _backward_split(ctx, dy, dy2, x2, weight, link):
+        """QKV projection backward while the attention's dQ pass still runs on a side
+        stream (ops.attention.DQLink, TP = 1): the k/v columns' data gradient and weight
+        gradient first, then wait for dQ and add the q columns' (same bf16 GEMMs and fp32
+        main_grad epilogues as the one-shot path, split at a column boundary)."""
+        from ..ops.grad import _WT_EPOCH, _grad_ready, take_fresh, wgrad_into
+
+        c = link.split
+        wt = weight._st_wt if (getattr(weight, "_st_wt_epoch", -1) == _WT_EPOCH[0] and dy.is_cuda) else None
+        if wt is not None:
+            torch.cuda.current_stream().wait_event(weight._st_wt_done)
+        mg = getattr(weight, "main_grad", None)
+        want_w = ctx.needs_input_grad[1]
+        beta = (0 if take_fresh(weight) else 1) if (want_w and mg is not None) else None
+
+        def dgrad_part(lo, hi, out=None):
+            b = wt[:, lo:hi].t() if wt is not None else weight[lo:hi]  # TN on the W^T copy's column block
+            return out.addmm_(dy2[:, lo:hi], b) if out is not None else dy2[:, lo:hi] @ b
+
+        def wgrad_part(lo, hi):
+            if beta is not None:
+                wgrad_into(mg.view(mg.shape[0], -1)[lo:hi], dy2[:, lo:hi], x2, beta)
+
+        n = dy2.shape[1]
+        dx = dgrad_part(c, n)
+        wgrad_part(c, n)
+        link.wait()  # dQ (and its inverse RoPE) landed
+        dgrad_part(0, c, out=dx)
+        wgrad_part(0, c)
+        dw = None
+        if want_w:
+            if mg is not None:
+                _grad_ready(weight)
+            else:
+                dw = dy2.t().mm(x2)
+        db = None
+        if ctx.bias is not None and ctx.needs_input_grad[2]:
+            db = accumulate_grad(ctx.bias, dy2.float().sum(0))
+        return dx.view(*dy.shape[:-1], dx.shape[-1]), dw, db, None, None
 
 
 def _sp_overlap(x: torch.Tensor) -> bool:
@@ -638,7 +682,8 @@ class ColumnParallelLinear(nn.Module):
         if self.sequence_parallel and self.tp > 1:
             y = _SPColumnParallelFn.apply(x, self.weight, self.bias, self.group)
         elif self.tp > 1 or getattr(self.weight, "main_grad", None) is not None:
-            y = _ColumnParallelFn.apply(x, self.weight, self.bias, self.group)
+            # _st_link: an attention that finishes dQ in this node's backward (ops.attention.DQLink)
+            y = _ColumnParallelFn.apply(x, self.weight, self.bias, self.group, getattr(self, "_st_link", None))
         else:
             y = F.linear(x, self.weight, self.bias)
         if self.gather_output and self.tp > 1:

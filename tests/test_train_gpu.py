@@ -382,3 +382,35 @@ def test_swiglu_linear_recompute_matches_reference(monkeypatch):
     y32.backward(dy.float())
     assert rel(y, y32) < 1e-2 and rel(gu.grad, g32.grad) < 2e-2 and rel(w.main_grad, w32.grad) < 1e-2
     assert w.grad is None
+
+
+@pytest.mark.parametrize("model_kw", [dict(), dict(num_attention_heads=2, num_key_value_heads=1)])  # D 64 / 128
+def test_dq_side_stream_overlap_matches_inline(model_kw, monkeypatch):
+    """ST_FLASH_DQ_OVERLAP: the attention backward leaves dQ = dS K (+ its inverse RoPE) to
+    a side stream and the QKV projection's backward does the k/v columns first, then waits
+    (ops.attention.DQLink).  With that side stream artificially delayed (~50 ms spin before
+    every dQ pass) training must match the inline path: a missing wait reads a stale dQ."""
+    from scaletorch_amd.ops import attention as A
+
+    orig = A._dq_stream
+
+    def delayed(dev):
+        st = orig(dev)
+        with torch.cuda.stream(st):
+            torch.cuda._sleep(100_000_000)
+        return st
+
+    def run(flag):
+        monkeypatch.setenv("ST_FLASH_DQ_OVERLAP", flag)
+        tr = _tiny_trainer(max_grad_norm=0.0, **model_kw)
+        losses = [tr.reduced_loss(tr.train_step()) for _ in range(3)]
+        tr.optimizer.sync()
+        torch.cuda.synchronize()
+        return losses, torch.cat([a.param_flat.float() for a in tr.model.arenas])
+
+    l0, p0 = run("0")
+    monkeypatch.setattr(A, "_dq_stream", delayed)
+    l1, p1 = run("1")
+    for a, b in zip(l0, l1):
+        assert abs(a - b) <= 2e-3 * abs(a), (l0, l1)
+    assert ((p0 - p1).norm() / p0.norm()).item() < 1e-3
