@@ -231,7 +231,9 @@ class DQLink:
     its backward runs that pass (and dQ's inverse RoPE) on a side stream and returns at
     once; the QKV projection's backward -- the next node, holding the same link -- computes
     the k/v columns' data and weight gradients (compute-bound GEMMs) first, then waits on
-    ``event`` and adds the q columns.  ``keep`` pins what the side stream still reads."""
+    ``event`` and adds the q columns.  ``keep`` pins what the side stream still reads.
+    Opt-in (``ST_FLASH_DQ_OVERLAP=1``): at Llama-3-8B micro-batch 6 it measured 3.7 ms per
+    step slower than the inline pass (profiles/r03/dq_overlap_ab.log)."""
 
     __slots__ = ("event", "split", "keep")
 
