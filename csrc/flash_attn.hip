@@ -232,9 +232,9 @@ ST_DEVICE void dma_barrier() {
   __syncthreads();
 }
 
-template <int D, int ROWS>
+template <int D, int ROWS, int NWAVES = 4>  // the tile is split over the workgroup's NWAVES waves
 struct DmaStager {
-  static constexpr int RB = 2 * D, BYTES = ROWS * RB, PER_WAVE = BYTES / 4, NI = PER_WAVE / 1024;
+  static constexpr int RB = 2 * D, BYTES = ROWS * RB, PER_WAVE = BYTES / NWAVES, NI = PER_WAVE / 1024;
   static_assert(NI >= 1 && PER_WAVE % 1024 == 0, "tile must be whole KiB per wave");
   uint32_t voff[NI];
   uint32_t stride_bytes;
@@ -349,36 +349,42 @@ ST_DEVICE int ds_off(int k, int qh, int u, int s, int h) {
 }
 
 // ============================================================== forward
-template <int D, bool XCD = true>  // XCD: XCD-aware workgroup order (ST_FLASH_XCD=0 -> off, A/B)
-__global__ __launch_bounds__(256, 2) void flash_fwd_kernel(AttnParams p, bf16_t* __restrict__ o,
-                                                           int64_t sob, int64_t sos, int64_t soh,
-                                                           float* __restrict__ lse) {
+// XCD: XCD-aware workgroup order (ST_FLASH_XCD=0 -> off, A/B).  HP: query heads per
+// workgroup -- HP = 2 puts two heads of one GQA group in an 8-wave workgroup (waves
+// 4s .. 4s+3 = head s), so every K / V tile is DMA'd into LDS once for both.
+template <int D, bool XCD = true, int HP = 1>
+__global__ __launch_bounds__(256 * HP, 2 / HP) void flash_fwd_kernel(AttnParams p, bf16_t* __restrict__ o,
+                                                                     int64_t sob, int64_t sos, int64_t soh,
+                                                                     float* __restrict__ lse) {
   constexpr int BM = 128, BN = 64, NKK = D / 16, NDT = D / 32;
   constexpr int TB = BN * D * 2;
   __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];  // K0 K1 V0 V1
   lds_t* smem = (lds_t*)smem_raw;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, h = lane >> 5;
-  const int BH = p.B * p.H, nqt = (p.Sq + BM - 1) / BM, id = blockIdx.x;
+  const int wq = wid & 3;  // this wave's 32-query slice of the tile
+  const int nqt = (p.Sq + BM - 1) / BM, id = blockIdx.x;
   int rank, b, hq;
-  const int G = p.H / p.Hkv, BHk = p.B * p.Hkv;
+  const int G = p.H / p.Hkv, BHk = p.B * p.Hkv, NG = G / HP;  // NG head groups per kv head
   if (XCD && BHk % 8 == 0) {
     // XCD-aware order (T1): the dispatcher deals workgroups round-robin to the 8 XCDs, so
     // XCD x = id % 8 takes every (batch, kv head) pair with index = x mod 8, all G query
     // heads of each: the K / V tiles its workgroups stream are shared by G concurrent
     // workgroups in that XCD's L2 instead of one per XCD.  Heaviest query tiles first.
-    const int j = id >> 3, per_rank = (BHk >> 3) * G, rem = j % per_rank;
+    const int j = id >> 3, per_rank = (BHk >> 3) * NG, rem = j % per_rank;
     rank = j / per_rank;
-    const int bhk = (id & 7) + 8 * (rem / G);
+    const int bhk = (id & 7) + 8 * (rem / NG);
     b = bhk / p.Hkv;
-    hq = (bhk % p.Hkv) * G + rem % G;
+    hq = (bhk % p.Hkv) * G + (rem % NG) * HP;
   } else {
-    rank = id / BH;
-    b = (id % BH) / p.H;
-    hq = id % p.H;
+    const int BHG = p.B * p.H / HP;
+    rank = id / BHG;
+    b = (id % BHG) / (p.H / HP);
+    hq = (id % (p.H / HP)) * HP;
   }
+  hq += wid >> 2;
   const int qt = p.causal ? nqt - 1 - rank : rank;
   const int hk = hq / G;
-  const int q0 = qt * BM, my_q = q0 + wid * 32 + r;
+  const int q0 = qt * BM, my_q = q0 + wq * 32 + r;
 
   const rsrc_t rq = make_rsrc(p.q + (int64_t)b * p.sqb + (int64_t)hq * p.sqh, p.Sq, p.sqs, D);
   const rsrc_t rk = make_rsrc(p.k + (int64_t)b * p.skb + (int64_t)hk * p.skh, p.Sk, p.sks, D);
@@ -399,7 +405,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(AttnParams p, bf16_t*
 
   LdsAddr<D> la;
   la.init(lane);
-  DmaStager<D, BN> sk, sv;
+  DmaStager<D, BN, 4 * HP> sk, sv;
   sk.init(wid, lane, p.sks);
   sv.init(wid, lane, p.svs);
 
@@ -1571,9 +1577,21 @@ int st_flash_fwd(const void* q, const void* k, const void* v, void* o, float* ls
   const int pp = ppe ? std::atoi(ppe) : 0;
   const char* xe = std::getenv("ST_FLASH_XCD");  // XCD-aware workgroup order (default on)
   const bool xcd = !xe || std::atoi(xe) != 0;
+  // ST_FLASH_FWD_HP=2: two query heads per workgroup sharing each K/V tile in LDS.  Measured
+  // equal to one head per workgroup once the XCD-aware order shares K/V in L2 (B6 S4096:
+  // 0.852 vs 0.853 ms, profiles/r03/flash_pmc.md), so one head stays the default.
+  const char* he = std::getenv("ST_FLASH_FWD_HP");
+  const bool hp2 = (H / Hkv) % 2 == 0 && he && std::atoi(he) == 2;
   if (D == 128 && pp) {
     const unsigned grid2 = (unsigned)(((Sq + 255) / 256) * B * H);
     flash_fwd_pp_kernel<128><<<grid2, 512, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
+  } else if (hp2) {
+    const unsigned grid2 = grid / 2;
+    if (D == 128 && xcd) flash_fwd_kernel<128, true, 2><<<grid2, 512, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
+    else if (D == 128) flash_fwd_kernel<128, false, 2><<<grid2, 512, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
+    else if (D == 64 && xcd) flash_fwd_kernel<64, true, 2><<<grid2, 512, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
+    else if (D == 64) flash_fwd_kernel<64, false, 2><<<grid2, 512, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
+    else return -3;
   } else if (D == 128 && xcd)
     flash_fwd_kernel<128, true><<<grid, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
   else if (D == 128)

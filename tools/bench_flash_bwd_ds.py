@@ -50,11 +50,13 @@ for rnd in range(5):
         best[name] = min(best.get(name, 1e9), s.elapsed_time(e) / 5)
 
 
-# forward at the same shape: XCD-aware workgroup order on / off (ST_FLASH_XCD), interleaved
+# forward at the same shape, interleaved: 2 query heads per workgroup (opt-in), 1 head
+# (default), 1 head without the XCD-aware order (ST_FLASH_FWD_HP, ST_FLASH_XCD)
 fwd = {}
 for rnd in range(5):
-    for xcd in ("1", "0"):
-        os.environ["ST_FLASH_XCD"] = xcd
+    for xcd in ("1", "h1", "0"):
+        os.environ["ST_FLASH_XCD"] = "0" if xcd == "0" else "1"
+        os.environ["ST_FLASH_FWD_HP"] = "2" if xcd == "1" else "1"
         ops.flash_attn_fwd(q, k, v, scale, True)
         torch.cuda.synchronize()
         fs, fe = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -64,8 +66,8 @@ for rnd in range(5):
         fe.record()
         fe.synchronize()
         fwd[xcd] = min(fwd.get(xcd, 1e9), fs.elapsed_time(fe) / 5)
-os.environ["ST_FLASH_XCD"] = "1"
-fwd_ms = fwd["1"]
+os.environ["ST_FLASH_XCD"], os.environ["ST_FLASH_FWD_HP"] = "1", "1"
+fwd_ms = fwd["h1"]
 
 
 def rel(a, b):
@@ -73,7 +75,7 @@ def rel(a, b):
 
 
 res = {"shape": [B, S, H, Hkv, D], "fwd_ms": round(fwd_ms, 4), "fwd_tflops": round(fl_fwd / fwd_ms / 1e9, 1),
-       "fwd_ms_xcd_off": round(fwd["0"], 4),
+       "fwd_ms_2heads": round(fwd["1"], 4), "fwd_ms_xcd_off": round(fwd["0"], 4),
        "bwd_ms": {k2: round(v2, 4) for k2, v2 in best.items()},
        "tflops_5matmul": {k2: round(2.5 * fl_fwd / v2 / 1e9, 1) for k2, v2 in best.items()},
        "rel_diff": {n: rel(a, b) for n, a, b in zip(("dq", "dk", "dv"), grads["ds"], grads["recompute"])}}
