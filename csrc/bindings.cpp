@@ -42,11 +42,12 @@ int st_flash_fwd(const void* q, const void* k, const void* v, void* o, float* ls
                  int64_t skb, int64_t sks, int64_t skh, int64_t svb, int64_t svs, int64_t svh,
                  int64_t sob, int64_t sos, int64_t soh, float scale, int causal, int64_t q_offset,
                  int64_t k_offset, hipStream_t st);
-int st_flash_bwd_preprocess(const void* o, const void* dout, float* delta, int B, int S, int H,
+int st_flash_bwd_preprocess(const void* o, const void* dout, const float* lse, float* delta, float* nlse2,
+                            int B, int S, int H,
                             int D, int64_t sob, int64_t sos, int64_t soh, int64_t sdb, int64_t sds,
                             int64_t sdh, hipStream_t st);
 int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse,
-                 const float* delta, void* dq, void* dk, void* dv, int B, int Sq, int Sk,
+                 const float* delta, const float* nlse2, void* dq, void* dk, void* dv, int B, int Sq, int Sk,
                  int H, int Hkv, int D, int64_t sqb, int64_t sqs, int64_t sqh, int64_t skb,
                  int64_t sks, int64_t skh, int64_t svb, int64_t svs, int64_t svh, int64_t sdb,
                  int64_t sds, int64_t sdh, int64_t sdqb, int64_t sdqs, int64_t sdqh, int64_t sdkb,
@@ -705,8 +706,9 @@ std::vector<at::Tensor> flash_bwd(const at::Tensor& dout, const at::Tensor& q, c
   for (auto* t : {&k, &v, &o, &dout, &lse}) check_same_gpu(*t, q, "flash_bwd operand");
   c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   auto delta = at::empty({B, H, Sq}, q.options().dtype(at::kFloat));
-  int rc = st_flash_bwd_preprocess(o.data_ptr(), dout.data_ptr(), delta.data_ptr<float>(), (int)B,
-                                   (int)Sq, (int)H, (int)D, o.stride(0), o.stride(1), o.stride(2),
+  auto nlse2 = at::empty({B, H, Sq}, q.options().dtype(at::kFloat));
+  int rc = st_flash_bwd_preprocess(o.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+                                   nlse2.data_ptr<float>(), (int)B, (int)Sq, (int)H, (int)D, o.stride(0), o.stride(1), o.stride(2),
                                    dout.stride(0), dout.stride(1), dout.stride(2), cur_stream());
   ST_CHECK_RC(rc, "flash_bwd_preprocess");
   auto pick = [&](const c10::optional<at::Tensor>& t, at::IntArrayRef shape, const char* n) {
@@ -732,7 +734,8 @@ std::vector<at::Tensor> flash_bwd(const at::Tensor& dout, const at::Tensor& q, c
   at::Tensor dsw;
   if (dse > 0) dsw = at::empty({dse}, q.options());
   rc = st_flash_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
-                    delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), (int)B, (int)Sq, (int)Sk, (int)H, (int)Hkv, (int)D, q.stride(0), q.stride(1),
+                    delta.data_ptr<float>(), nlse2.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
+                    (int)B, (int)Sq, (int)Sk, (int)H, (int)Hkv, (int)D, q.stride(0), q.stride(1),
                     q.stride(2), k.stride(0), k.stride(1), k.stride(2), v.stride(0), v.stride(1),
                     v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2), dq.stride(0),
                     dq.stride(1), dq.stride(2), dk.stride(0), dk.stride(1), dk.stride(2),
@@ -778,7 +781,9 @@ std::vector<at::Tensor> flash_bwd_kv(const at::Tensor& dout, const at::Tensor& q
   if (dse <= 0) return {dk, dv, at::empty({0}, q.options())};
   TORCH_CHECK(dk.strides() == dv.strides(), "flash_bwd_kv: dk_out/dv_out must share strides");
   auto delta = at::empty({B, H, Sq}, q.options().dtype(at::kFloat));
-  int rc = st_flash_bwd_preprocess(o.data_ptr(), dout.data_ptr(), delta.data_ptr<float>(), (int)B, (int)Sq, (int)H,
+  auto nlse2 = at::empty({B, H, Sq}, q.options().dtype(at::kFloat));
+  int rc = st_flash_bwd_preprocess(o.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+                                   nlse2.data_ptr<float>(), (int)B, (int)Sq, (int)H,
                                    (int)D, o.stride(0), o.stride(1), o.stride(2), dout.stride(0), dout.stride(1),
                                    dout.stride(2), cur_stream());
   ST_CHECK_RC(rc, "flash_bwd_kv preprocess");
@@ -787,7 +792,8 @@ std::vector<at::Tensor> flash_bwd_kv(const at::Tensor& dout, const at::Tensor& q
   if (pe > 0) part = at::empty({pe}, q.options().dtype(at::kFloat));
   auto ws = at::empty({dse}, q.options());
   rc = st_flash_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
-                    delta.data_ptr<float>(), nullptr, dk.data_ptr(), dv.data_ptr(), (int)B, (int)Sq, (int)Sk, (int)H,
+                    delta.data_ptr<float>(), nlse2.data_ptr<float>(), nullptr, dk.data_ptr(), dv.data_ptr(), (int)B,
+                    (int)Sq, (int)Sk, (int)H,
                     (int)Hkv, (int)D, q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
                     v.stride(0), v.stride(1), v.stride(2), dout.stride(0), dout.stride(1), dout.stride(2), 0, 0, 0,
                     dk.stride(0), dk.stride(1), dk.stride(2), (float)scale, causal ? 1 : 0, q_offset, k_offset,
@@ -819,7 +825,7 @@ at::Tensor flash_bwd_q_ds(const at::Tensor& q, const at::Tensor& k, const at::Te
   } else {
     dq = at::empty(q.sizes(), q.options());
   }
-  int rc = st_flash_bwd(q.data_ptr(), k.data_ptr(), k.data_ptr(), q.data_ptr(), nullptr, nullptr, dq.data_ptr(),
+  int rc = st_flash_bwd(q.data_ptr(), k.data_ptr(), k.data_ptr(), q.data_ptr(), nullptr, nullptr, nullptr, dq.data_ptr(),
                         nullptr, nullptr, (int)B, (int)Sq, (int)Sk, (int)H, (int)Hkv, (int)D, q.stride(0), q.stride(1),
                         q.stride(2), k.stride(0), k.stride(1), k.stride(2), k.stride(0), k.stride(1), k.stride(2),
                         q.stride(0), q.stride(1), q.stride(2), dq.stride(0), dq.stride(1), dq.stride(2), 0, 0, 0,

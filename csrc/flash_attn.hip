@@ -726,11 +726,16 @@ __global__ __launch_bounds__(512, 1) void flash_fwd_pp_kernel(AttnParams p, bf16
 }
 
 // ============================================================== backward: delta
+// Per query row: ndelta = -rowsum(dO * O) and nlse2 = -lse * log2(e), the two row
+// constants of the backward in the form the dK/dV kernel consumes without VALU work:
+// -delta seeds the dP accumulator (dP - delta comes out of the MFMA chain) and
+// P = exp2(S c2 + nlse2) is one fma + exp per element.
 template <int D>
 __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __restrict__ o,
                                                             const bf16_t* __restrict__ dout,
-                                                            float* __restrict__ delta, int B, int S,
-                                                            int H, int64_t sob, int64_t sos,
+                                                            const float* __restrict__ lse,
+                                                            float* __restrict__ delta, float* __restrict__ nlse2,
+                                                            int B, int S, int H, int64_t sob, int64_t sos,
                                                             int64_t soh, int64_t sdb, int64_t sds,
                                                             int64_t sdh) {
   constexpr int NCH = D / 8;  // lanes per row
@@ -753,7 +758,11 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
   }
 #pragma unroll
   for (int w = NCH / 2; w > 0; w >>= 1) acc += __shfl_xor(acc, w, 64);
-  if (row < nrows && ch == 0) delta[((int64_t)b * H + hh) * S + s] = acc;
+  if (row < nrows && ch == 0) {
+    const int64_t li = ((int64_t)b * H + hh) * S + s;
+    delta[li] = -acc;
+    nlse2[li] = -lse[li] * kLog2e;
+  }
 }
 
 // ============================================================== backward: dQ
@@ -796,7 +805,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
   }
   const int64_t li = ((int64_t)b * p.H + hq) * p.Sq + my_q;
   const float lse2 = my_q < p.Sq ? lse[li] * kLog2e : 0.f;
-  const float dlt = my_q < p.Sq ? delta[li] : 0.f;
+  const float dlt = my_q < p.Sq ? -delta[li] : 0.f;  // the pre kernel stores -delta
   // register fragments resident before the DMA pipeline starts: hipcc's own
   // vmcnt bookkeeping for these loads otherwise lands inside the loop, where
   // (the asm DMAs being invisible to it) a small vmcnt would wait for them
@@ -1085,19 +1094,20 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_ds_kernel(AttnParams p, c
 // lse, delta), so dK/dV of the kv head are summed in registers and written
 // once as bf16.  Rows past Sq read as zero with lse = +inf => P = dS = 0.
 // dS softmax slice of one accumulator row group (4 registers: query rows
-// rowo .. rowo+3 of the block, this lane's key): P = exp2(S c2 - lse2) (masked
-// past the causal diagonal), dS = P (dP - delta); P overwrites S in place
+// rowo .. rowo+3 of the block, this lane's key): P = exp2(S c2 + nlse2) (masked
+// past the causal diagonal), dS = P (dP - delta) where the dP accumulator was seeded
+// with -delta (dp_seed); P overwrites S in place.  fma + exp + mul per element.
 template <bool MASK>
 ST_DEVICE void dkdv_softmax4(f32x16& s, f32x16& dp, const lds_t* st, int BQ, int rowo, int gq, float c2, int thr) {
-  const f32x4 L = *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * rowo) * kLog2e;
-  const f32x4 Dl = *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * (BQ + rowo));
+  (void)BQ;
+  const f32x4 L = *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * rowo);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int i = 4 * gq + j;
-    float pv = fast_exp2(fmaf(s[i], c2, -L[j]));
+    float pv = fast_exp2(fmaf(s[i], c2, L[j]));
     if (MASK && acc_row0(i) < thr) pv = 0.f;
     s[i] = pv;
-    dp[i] = pv * (dp[i] - Dl[j]);
+    dp[i] = pv * dp[i];
   }
 }
 
@@ -1108,7 +1118,7 @@ ST_DEVICE void dkdv_softmax4(f32x16& s, f32x16& dp, const lds_t* st, int BQ, int
 template <int D, int PROBE = 0, bool WDS = false>
 __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
     AttnParams p, const bf16_t* __restrict__ dout, int64_t sdb, int64_t sds, int64_t sdh,
-    const float* __restrict__ lse, const float* __restrict__ delta, bf16_t* __restrict__ dk,
+    const float* __restrict__ nlse2, const float* __restrict__ delta, bf16_t* __restrict__ dk,
     bf16_t* __restrict__ dv, int nsplit, float* __restrict__ part, bf16_t* __restrict__ dsw) {
   constexpr int BKW = 128, BQ = 64, NKK = D / 16, NDT = D / 32;
   constexpr int TB = BQ * D * 2;
@@ -1199,7 +1209,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
     sd.load(make_rsrc(dout + (int64_t)b * sdb + (int64_t)hq * sdh, p.Sq, sds, D), smem + (NB + buf) * TB, qb * BQ);
     if (wid < 2) {
       const int64_t row = ((int64_t)b * p.H + hq) * p.Sq;
-      lds_dma4(make_rsrc_f32((wid == 0 ? lse : delta) + row, p.Sq),
+      lds_dma4(make_rsrc_f32((wid == 0 ? nlse2 : delta) + row, p.Sq),
                (lds_t*)(stats + buf * 2 * BQ + wid * BQ), (uint32_t)((qb * BQ + lane) * 4));
     }
   };
@@ -1297,7 +1307,18 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
         }
       }
       f32x16 s[2], dp[2];
-      s[0] = s[1] = dp[0] = dp[1] = zero16();
+      s[0] = s[1] = zero16();
+      // dP accumulators seeded with -delta of their query rows (registers 4g .. 4g+3 of half
+      // u = rows 32u + 8g + 4h .. +3): the MFMA chain then yields dP - delta directly
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const f32x4 nd =
+              *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * (BQ + 32 * u + 8 * g4 + 4 * h));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dp[u][4 * g4 + j] = nd[j];
+        }
       bfx8 qa[2][NKK], da[2][NKK];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -1605,17 +1626,18 @@ int st_flash_fwd(const void* q, const void* k, const void* v, void* o, float* ls
   return (int)hipGetLastError();
 }
 
-int st_flash_bwd_preprocess(const void* o, const void* dout, float* delta, int B, int S, int H,
+int st_flash_bwd_preprocess(const void* o, const void* dout, const float* lse, float* delta, float* nlse2,
+                            int B, int S, int H,
                             int D, int64_t sob, int64_t sos, int64_t soh, int64_t sdb, int64_t sds,
                             int64_t sdh, hipStream_t st) {
   const int64_t threads = (int64_t)B * S * H * (D / 8);
   if (threads == 0) return 0;
   const unsigned blocks = (unsigned)((threads + 255) / 256);
   if (D == 128)
-    flash_bwd_pre_kernel<128><<<blocks, 256, 0, st>>>((const bf16_t*)o, (const bf16_t*)dout, delta, B,
+    flash_bwd_pre_kernel<128><<<blocks, 256, 0, st>>>((const bf16_t*)o, (const bf16_t*)dout, lse, delta, nlse2, B,
                                                       S, H, sob, sos, soh, sdb, sds, sdh);
   else if (D == 64)
-    flash_bwd_pre_kernel<64><<<blocks, 256, 0, st>>>((const bf16_t*)o, (const bf16_t*)dout, delta, B, S,
+    flash_bwd_pre_kernel<64><<<blocks, 256, 0, st>>>((const bf16_t*)o, (const bf16_t*)dout, lse, delta, nlse2, B, S,
                                                      H, sob, sos, soh, sdb, sds, sdh);
   else
     return -3;
@@ -1688,7 +1710,7 @@ int64_t st_flash_bwd_ds_elems(int B, int Sq, int Sk, int H, int D, int causal, i
 // separately (bit 0: dK/dV + the dS stores, bit 1: dQ from dS) so a caller can put the
 // HBM-bound dQ pass on another stream beside compute-bound work (ops/attention.py).
 int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse,
-                 const float* delta, void* dq, void* dk, void* dv, int B, int Sq, int Sk, int H,
+                 const float* delta, const float* nlse2, void* dq, void* dk, void* dv, int B, int Sq, int Sk, int H,
                  int Hkv, int D, int64_t sqb, int64_t sqs, int64_t sqh, int64_t skb, int64_t sks,
                  int64_t skh, int64_t svb, int64_t svs, int64_t svh, int64_t sdb, int64_t sds,
                  int64_t sdh, int64_t sdqb, int64_t sdqs, int64_t sdqh, int64_t sdkb, int64_t sdks,
@@ -1718,13 +1740,13 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
     const char* pe = std::getenv("ST_FLASH_PROBE");  // diagnostics only (tools/bench_flash_bwd_ds.py)
     if (phases & 1) {
       if (D == 128 && pe && std::atoi(pe) == 2)
-        flash_bwd_dkdv_kernel<128, 2, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
+        flash_bwd_dkdv_kernel<128, 2, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, nlse2, delta, (bf16_t*)dk,
                                                                (bf16_t*)dv, nsplit, part, ds);
       else if (D == 128)
-        flash_bwd_dkdv_kernel<128, 0, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
+        flash_bwd_dkdv_kernel<128, 0, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, nlse2, delta, (bf16_t*)dk,
                                                                (bf16_t*)dv, nsplit, part, ds);
       else
-        flash_bwd_dkdv_kernel<64, 0, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
+        flash_bwd_dkdv_kernel<64, 0, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, nlse2, delta, (bf16_t*)dk,
                                                               (bf16_t*)dv, nsplit, part, ds);
       ST_HIP_CHECK(hipGetLastError());
       if (nsplit > 1) {
@@ -1783,16 +1805,16 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
     const char* pe = std::getenv("ST_FLASH_PROBE");  // diagnostics only (tools/probe_flash.py)
     if (pe && std::atoi(pe) == 1) {
       flash_bwd_dq_kernel<128, 1><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq, qsplit, qpart);
-      flash_bwd_dkdv_kernel<128, 1><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
+      flash_bwd_dkdv_kernel<128, 1><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, nlse2, delta, (bf16_t*)dk,
                                                    (bf16_t*)dv, nsplit, part, nullptr);
     } else {
       flash_bwd_dq_kernel<128><<<gq, 256, 0, sq>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq, qsplit, qpart);
-      flash_bwd_dkdv_kernel<128><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
+      flash_bwd_dkdv_kernel<128><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, nlse2, delta, (bf16_t*)dk,
                                                    (bf16_t*)dv, nsplit, part, nullptr);
     }
   } else if (D == 64) {
     flash_bwd_dq_kernel<64><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq, qsplit, qpart);
-    flash_bwd_dkdv_kernel<64><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dk,
+    flash_bwd_dkdv_kernel<64><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, nlse2, delta, (bf16_t*)dk,
                                                   (bf16_t*)dv, nsplit, part, nullptr);
   } else {
     return -3;
