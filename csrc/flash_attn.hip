@@ -1093,21 +1093,32 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_ds_kernel(AttnParams p, c
 // query head of the GQA group x query blocks of 64 rows staged in LDS (Q, dO,
 // lse, delta), so dK/dV of the kv head are summed in registers and written
 // once as bf16.  Rows past Sq read as zero with lse = +inf => P = dS = 0.
+// the 4 nlse2 values of query rows `rowo` .. +3 (LDS stats slot)
+ST_DEVICE f32x4 dkdv_ldL(const lds_t* st, int rowo) {
+  return *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * rowo);
+}
 // dS softmax slice of one accumulator row group (4 registers: query rows
-// rowo .. rowo+3 of the block, this lane's key): P = exp2(S c2 + nlse2) (masked
-// past the causal diagonal), dS = P (dP - delta) where the dP accumulator was seeded
-// with -delta (dp_seed); P overwrites S in place.  fma + exp + mul per element.
-template <bool MASK>
-ST_DEVICE void dkdv_softmax4(f32x16& s, f32x16& dp, const lds_t* st, int BQ, int rowo, int gq, float c2, int thr) {
-  (void)BQ;
-  const f32x4 L = *reinterpret_cast<const f32x4 __attribute__((address_space(3)))*>(st + 4 * rowo);
+// 8 gq + 4h .. +3 of the half, this lane's key): P = exp2(S c2 + nlse2), dS = P (dP - delta)
+// where the dP accumulator was seeded with -delta; P overwrites S in place.  fma + exp +
+// mul per element, straight-line (the causal mask is applied afterwards, dkdv_mask).
+ST_DEVICE void dkdv_softmax4(f32x16& s, f32x16& dp, const f32x4& L, int gq, float c2) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int i = 4 * gq + j;
-    float pv = fast_exp2(fmaf(s[i], c2, L[j]));
-    if (MASK && acc_row0(i) < thr) pv = 0.f;
+    const float pv = fast_exp2(fmaf(s[i], c2, L[j]));
     s[i] = pv;
     dp[i] = pv * dp[i];
+  }
+}
+// causal diagonal: zero P and dS of the future keys of one 32-query half (register i holds
+// half-row acc_row0(i) + 4h; thr = this lane's key - the half's first query - 4h).  A select,
+// so an overflowed exp2 of a masked score leaves nothing behind.
+ST_DEVICE void dkdv_mask(f32x16& s, f32x16& dp, int thr) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const bool m = acc_row0(i) < thr;
+    s[i] = m ? 0.f : s[i];
+    dp[i] = m ? 0.f : dp[i];
   }
 }
 
@@ -1149,7 +1160,9 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
   // vmcnt bookkeeping for these loads otherwise lands inside the loop, where
   // (the asm DMAs being invisible to it) a small vmcnt would wait for them
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  const int64_t kg = p.k_offset + my_k;
+  const int64_t kg = p.k_offset + my_k, kgw = p.k_offset + k0 + 32 * __builtin_amdgcn_readfirstlane(wid);
+  // kgw: the wave's first key, read into an SGPR so the causal mask test is a scalar branch
+  // (not an exec-mask region cutting the MFMA / softmax interleave apart)
   const float c2 = p.scale * kLog2e;
 
   // query blocks that can see any key of this tile; from qb_full on, every
@@ -1273,7 +1286,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
     const lds_t* st = (const lds_t*)(stats + BUF * 2 * BQ);
     const int64_t qstart = p.q_offset + (int64_t)qb_c * BQ;  // global index of the block's row 0
     // this wave's keys vs this query block: skip when every key is in the future
-    const bool dead = p.causal && (kg - r > qstart + BQ - 1);
+    const bool dead = p.causal && (kgw > qstart + BQ - 1);
     // this wave's dS^T tile: region of (b, q-head), byte offset of the tile's 64-query half
     const rsrc_t ds_rs = make_rsrc(dsw + ((int64_t)b * p.H + hk * G + g_c) * ds_per_bh * kDsTile,
                                    (int)(ds_per_bh * 64), 128, 128);
@@ -1297,7 +1310,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
       // software-pipelined within the wave (one wave per SIMD: nothing else fills
       // the MFMA pipe while the softmax VALU runs): half 0's softmax is issued
       // between half 1's S/dP MFMAs, half 1's between half 0's dV/dK MFMAs
-      const bool need_mask = p.causal && (kg - r + 31 > qstart);
+      const bool need_mask = p.causal && (kgw + 31 > qstart);
       int thr[2] = {0, 0};
       if (need_mask) {
 #pragma unroll
@@ -1308,6 +1321,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
       }
       f32x16 s[2], dp[2];
       s[0] = s[1] = zero16();
+
       // dP accumulators seeded with -delta of their query rows (registers 4g .. 4g+3 of half
       // u = rows 32u + 8g + 4h .. +3): the MFMA chain then yields dP - delta directly
 #pragma unroll
@@ -1320,6 +1334,9 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
           for (int j = 0; j < 4; ++j) dp[u][4 * g4 + j] = nd[j];
         }
       bfx8 qa[2][NKK], da[2][NKK];
+      // nlse2 of the next softmax row group, read two MFMAs ahead of its use (read right
+      // before it, the wait for it also waited for the operand reads queued in between)
+      f32x4 Lc;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         qa[u][0] = la.rowf(qt, u, 0);
@@ -1332,6 +1349,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
             qa[u][kk + 2] = la.rowf(qt, u, kk + 2);
             da[u][kk + 2] = la.rowf(dt_, u, kk + 2);
           }
+          if (u == 0 && kk == NKK - 1) Lc = dkdv_ldL(st, 4 * h);
           __builtin_amdgcn_sched_barrier(0);
           s[u] = mfma(qa[u][kk], kf[kk], s[u]);
           dp[u] = mfma(da[u][kk], vf[kk], dp[u]);
@@ -1339,13 +1357,14 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
 #pragma unroll
             for (int gq = 0; gq < 4; ++gq)  // the 4 row groups of half 0 spread over the k-steps
               if (gq * NKK / 4 == kk) {
-                // wave-uniform branch: only blocks on the causal diagonal pay for the mask
-                if (need_mask) dkdv_softmax4<true>(s[0], dp[0], st, BQ, 8 * gq + 4 * h, gq, c2, thr[0]);
-                else dkdv_softmax4<false>(s[0], dp[0], st, BQ, 8 * gq + 4 * h, gq, c2, 0);
+                dkdv_softmax4(s[0], dp[0], Lc, gq, c2);
+                Lc = dkdv_ldL(st, gq < 3 ? 8 * (gq + 1) + 4 * h : 32 + 4 * h);  // half 1's group 0 last
               }
           }
         }
       }
+      // wave-uniform (scalar) branch: only blocks on the causal diagonal pay for the mask
+      if (need_mask) dkdv_mask(s[0], dp[0], thr[0]);
       bfx8 pf[2][2], gf[2][2];
       pf[0][0] = acc_frag(s[0], 0);
       pf[0][1] = acc_frag(s[0], 1);
@@ -1377,6 +1396,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
         __builtin_amdgcn_sched_barrier(0);
         const int dt = gi % NDT, u = gi / NDT;
         if (gi == NDT) {
+          if (need_mask) dkdv_mask(s[1], dp[1], thr[1]);
           pf[1][0] = acc_frag(s[1], 0);
           pf[1][1] = acc_frag(s[1], 1);
           gf[1][0] = acc_frag(dp[1], 0);
@@ -1391,8 +1411,8 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
 #pragma unroll
           for (int gq = 0; gq < 4; ++gq)  // half 1's row groups spread over half 0's dt groups
             if (gq * NDT / 4 == dt) {
-              if (need_mask) dkdv_softmax4<true>(s[1], dp[1], st, BQ, 32 + 8 * gq + 4 * h, gq, c2, thr[1]);
-              else dkdv_softmax4<false>(s[1], dp[1], st, BQ, 32 + 8 * gq + 4 * h, gq, c2, 0);
+              dkdv_softmax4(s[1], dp[1], Lc, gq, c2);
+              if (gq < 3) Lc = dkdv_ldL(st, 32 + 8 * (gq + 1) + 4 * h);
             }
         }
       }
