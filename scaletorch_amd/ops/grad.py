@@ -58,6 +58,10 @@ def prepare_dgrad_weight(w: torch.Tensor) -> None:
         return
     if getattr(w, "_st_wt_epoch", -1) == _WT_EPOCH[0]:
         return
+    if os.environ.get("ST_DGRAD_WT_PROBE_STALE") == "1" and getattr(w, "_st_wt", None) is not None:
+        # timing probe only (WRONG gradients): reuse the previous step's W^T, no transpose
+        w._st_wt_epoch = _WT_EPOCH[0]
+        return
     buf = getattr(w, "_st_wt", None)
     if buf is None or buf.shape != (w.shape[1], w.shape[0]):
         buf = torch.empty(w.shape[1], w.shape[0], dtype=w.dtype, device=w.device)
