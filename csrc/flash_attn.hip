@@ -34,10 +34,17 @@
 //   * online softmax in base 2 with raw v_exp_f32; the O rescale is deferred
 //     until the running max grows by 2^8 (T13) and decided wave-uniformly.
 //   * only the diagonal / tail blocks evaluate the causal mask.
-//   * backward = delta = rowsum(dO*O); dQ kernel (per 128-query tile, iterating
-//     key blocks); dK/dV kernel (per 128-key tile of one kv head, iterating
-//     every query head of its GQA group x query blocks, so dK/dV are summed in
-//     registers) -- no atomics, no partial buffers, bitwise deterministic.
+//   * backward = preprocess (-delta = -rowsum(dO*O) and -lse*log2e per query row);
+//     dK/dV kernel (per 128-key tile of one kv head, iterating every query head of
+//     its GQA group x query blocks, so dK/dV are summed in registers).  Default
+//     (ST_FLASH_BWD_DS=1): the dK/dV kernel also stores the dS it holds as bf16
+//     dS^T tiles (raw MFMA fragment layout, compact causal workspace) and
+//     dQ = dS K is a streaming kernel sharing each K tile over 4 query heads --
+//     5 MFMA products instead of 7.  Otherwise a dQ kernel (per 128-query tile)
+//     recomputes S and dP.  No atomics, no partial buffers, bitwise deterministic.
+//   * dK/dV softmax per element: exp2(fma(S, c2, nlse2)) and one multiply (the dP
+//     chain is seeded with -delta); the causal mask is a scalar branch applied
+//     after the softmax, only on diagonal blocks.
 //   * causal: workgroups are numbered heaviest-first so the dispatcher's
 //     greedy fill is a longest-job-first schedule.
 #include <cstdlib>
