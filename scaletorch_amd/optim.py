@@ -27,6 +27,8 @@ from __future__ import annotations
 
 import math
 
+import os
+
 import torch
 
 from .dist import collectives as C
@@ -95,6 +97,11 @@ class _ArenaOptimizer(torch.optim.Optimizer):
     def grad_norm(self, mp_group=None) -> torch.Tensor:
         """Global L2 norm of the gradients (device scalar, fp32)."""
         self._zero_unwritten()
+        if os.environ.get("ST_NORM_PROBE_SKIP") == "1":
+            # timing probe only (no clipping, norm reported as 0): what the norm passes cost
+            for a in self.arenas:
+                a.sq_count = 0
+            return torch.zeros(1, dtype=torch.float32, device=self.arenas[0].grad_flat.device)
         pre = [a.take_sumsq() for a in self.arenas]
         if pre and all(x is not None for x in pre) and C.get_world_size() <= 1:
             total = pre[0].clone()  # accumulated on the side stream during backward
