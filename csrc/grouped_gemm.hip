@@ -33,6 +33,11 @@
 
 #include "common.h"
 
+// timing probes only (variant builds, wrong results): 1 = no wait for the DMA, 2 = no DMA
+#ifndef ST_GMM_PROBE
+#define ST_GMM_PROBE 0
+#endif
+
 using namespace st;
 
 namespace {
@@ -215,10 +220,14 @@ __global__ __launch_bounds__(NT, 1) void grouped_gemm_kernel(const bf16_t* __res
   dma(0, 0);
   auto tile = [&](auto bufc, int kt) {
     constexpr int BUF = decltype(bufc)::value;
+#if ST_GMM_PROBE == 0
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+#if ST_GMM_PROBE != 2
     if (kt + 1 < KT) dma(BUF ^ 1, kt + 1);
+#endif
     const lds_t* stg = smem + BUF * Gm::STAGE;
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
