@@ -92,6 +92,7 @@ struct Geo {
   static constexpr int A_PIECES = A_BYTES / 1024, PIECES = STAGE / 1024;
   static constexpr int NDMA = PIECES / 8;
   static_assert(PIECES % 8 == 0, "stage must split evenly over 8 waves");
+  static_assert(NDMA % 2 == 0, "SPREAD issues half of a wave's pieces per 32-k sub-step");
 };
 
 // first g with tile_end[g] > s (tile_end = inclusive prefix of per-group M-tile counts)
@@ -104,7 +105,7 @@ ST_DEVICE int find_group(const int* __restrict__ tile_end, int G, int s) {
   return lo;
 }
 
-template <int BN, bool WN>
+template <int BN, bool WN, bool SPREAD = false>
 __global__ __launch_bounds__(NT, 1) void grouped_gemm_kernel(const bf16_t* __restrict__ X, int64_t ldx,
                                                              const bf16_t* __restrict__ W, int64_t ldw,
                                                              int64_t strideW, bf16_t* __restrict__ Y, int64_t ldy,
@@ -171,12 +172,14 @@ __global__ __launch_bounds__(NT, 1) void grouped_gemm_kernel(const bf16_t* __res
   }
   const uint32_t dma_base =
       __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem + (uint32_t)(wid * Gm::NDMA * 1024));
-  auto dma = [&](int buf, int kt) {
+  auto dma_piece = [&](int buf, int kt, int i) {
     const uint32_t kx = (uint32_t)(kt * BK * 2);             // row images: k along the row
     const uint32_t kw = WN ? (uint32_t)(kt * BK) * sW : kx;  // column image: k = row
+    lds_dma16(isA[i] ? rsX : rsW, dma_base + buf * Gm::STAGE + i * 1024, voff[i] + (isA[i] ? kx : kw));
+  };
+  auto dma = [&](int buf, int kt) {
 #pragma unroll
-    for (int i = 0; i < Gm::NDMA; ++i)
-      lds_dma16(isA[i] ? rsX : rsW, dma_base + buf * Gm::STAGE + i * 1024, voff[i] + (isA[i] ? kx : kw));
+    for (int i = 0; i < Gm::NDMA; ++i) dma_piece(buf, kt, i);
   };
 
   // ---- fragment read plan (16x16x32, natural k order: lane group gq holds k 8gq..8gq+7
@@ -225,8 +228,9 @@ __global__ __launch_bounds__(NT, 1) void grouped_gemm_kernel(const bf16_t* __res
 #endif
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    const bool more = kt + 1 < KT;
 #if ST_GMM_PROBE != 2
-    if (kt + 1 < KT) dma(BUF ^ 1, kt + 1);
+    if (!SPREAD && more) dma(BUF ^ 1, kt + 1);
 #endif
     const lds_t* stg = smem + BUF * Gm::STAGE;
 #pragma unroll
@@ -240,11 +244,24 @@ __global__ __launch_bounds__(NT, 1) void grouped_gemm_kernel(const bf16_t* __res
 #pragma unroll
       for (int i = 0; i < Gm::FM; ++i) af[i] = lds_b128(stg + aoff[i][st]);
       __builtin_amdgcn_s_setprio(1);
+      // SPREAD: the next tile's DMA pieces go out one at a time between this sub-step's MFMAs
+      // (NP per sub-step, evenly spaced) instead of in one burst after the barrier
+      constexpr int NM = Gm::FM * Gm::FN, NP = Gm::NDMA / 2;
 #pragma unroll
       for (int i = 0; i < Gm::FM; ++i)
 #pragma unroll
-        for (int j = 0; j < Gm::FN; ++j)
+        for (int j = 0; j < Gm::FN; ++j) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+          if constexpr (SPREAD) {
+#pragma unroll
+            for (int q = 0; q < NP; ++q)
+              if (i * Gm::FN + j == (q * NM) / NP + NM / (2 * NP) && ST_GMM_PROBE != 2) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (more) dma_piece(BUF ^ 1, kt + 1, st * NP + q);
+                __builtin_amdgcn_sched_barrier(0);
+              }
+          }
+        }
       __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("" ::: "memory");
@@ -297,9 +314,18 @@ int st_grouped_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, int6
   // dense shape (profiles/r03/grouped_gemm_order_ab.log): slot-major stays the default
   const char* oe = std::getenv("ST_GMM_ORDER");
   const int order = oe ? std::atoi(oe) : 0;
-#define LAUNCH(BNV, WNV)                                                                                   \
-  grouped_gemm_kernel<BNV, WNV><<<(unsigned)grid, NT, 0, st>>>(x, ldx, w, ldw, strideW, y, ldy, offs, tile_end, \
-                                                               G, N, K, order)
+  // ST_GMM_DMA_SPREAD=1: next-tile DMA pieces interleaved with the MFMAs (A/B)
+  const char* se = std::getenv("ST_GMM_DMA_SPREAD");
+  const bool spread = se && std::atoi(se) == 1;
+#define LAUNCH(BNV, WNV)                                                                                        \
+  do {                                                                                                          \
+    if (spread)                                                                                                 \
+      grouped_gemm_kernel<BNV, WNV, true><<<(unsigned)grid, NT, 0, st>>>(x, ldx, w, ldw, strideW, y, ldy, offs, \
+                                                                         tile_end, G, N, K, order);             \
+    else                                                                                                        \
+      grouped_gemm_kernel<BNV, WNV, false><<<(unsigned)grid, NT, 0, st>>>(x, ldx, w, ldw, strideW, y, ldy,      \
+                                                                          offs, tile_end, G, N, K, order);      \
+  } while (0)
   if (bn == 256) {
     if (wn) LAUNCH(256, true); else LAUNCH(256, false);
   } else {
