@@ -66,13 +66,38 @@ LAYOUTS = {
 }
 
 
-def _visible_gpus() -> int:
-    """Devices this process may use.  ``torch.cuda.device_count()`` counts the HIP
-    devices without creating a context on them (no GPU initialisation), so the
-    parent stays GPU-free and may start the ranks as children."""
-    import torch
+def _tp_transport() -> dict:
+    """TP transport the trainer chose (tensor_parallel.select_tp_transport) + its self-test."""
+    from scaletorch_amd.parallel.tensor_parallel import TRANSPORT
 
-    return torch.cuda.device_count()
+    return dict(TRANSPORT)
+
+
+def _visible_gpus() -> int:
+    """GPUs this process may use, counted WITHOUT the HIP runtime (so the parent that
+    starts the ranks never initialises a GPU): the KFD topology nodes that have SIMDs
+    (GPU agents; CPU nodes report simd_count 0), narrowed by the visible-devices
+    variables.  Falls back to torch.cuda.device_count() (hipGetDeviceCount, which does
+    initialise HIP in this process) only when the topology is unreadable."""
+    import glob
+
+    n = 0
+    for props in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+        try:
+            with open(props) as f:
+                kv = dict(line.split(None, 1) for line in f if line.strip())
+            n += int(kv.get("simd_count", "0").strip()) > 0
+        except (OSError, ValueError):
+            continue
+    if n == 0:
+        import torch
+
+        return torch.cuda.device_count()
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
 
 
 def _self_launch(n: int, argv: list[str], backend: str) -> int:
@@ -260,6 +285,9 @@ def main() -> int:
     fpt = flops_per_token(n_params, cfg.num_hidden_layers, cfg.num_attention_heads, cfg.head_dim, args.seq_len)
     fpt_causal = flops_per_token(n_params, cfg.num_hidden_layers, cfg.num_attention_heads, cfg.head_dim,
                                  args.seq_len, causal=True)
+    # strict: GEMM parameters only (no input-embedding gather) and causal attention FLOPs
+    fpt_strict = flops_per_token(cfg.matmul_params(), cfg.num_hidden_layers, cfg.num_attention_heads, cfg.head_dim,
+                                 args.seq_len, causal=True)
     peak = get_theoretical_flops()
     per_gpu = tok_s / world
     mfu = per_gpu * fpt / peak * 100
@@ -289,6 +317,9 @@ def main() -> int:
         "tokens_per_s_per_gpu": round(per_gpu, 1),
         "mfu_pct": round(mfu, 2),
         "mfu_pct_causal_flops": round(per_gpu * fpt_causal / peak * 100, 2),
+        "mfu_pct_strict": round(per_gpu * fpt_strict / peak * 100, 2),
+        "mfu_basis": "mfu_pct: 6N + 12LHdS per token, N incl. the input embedding (reference misc.py:136-174); "
+                     "mfu_pct_strict: N without the input-embedding gather, causal attention (6LHdS)",
         "peak_flops": peak,
         "baseline_tok_s_per_gpu": BASELINE_TOK_S_PER_GPU,
         "vs_baseline_basis": "context only: per-GPU tok/s over the reference's Qwen3-8B TP2-DP4 S2048 row on "
@@ -298,6 +329,7 @@ def main() -> int:
         "max_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1) if dev.type == "cuda" else 0.0,
         "comm_mb_per_step_rank0": comm,  # bytes handed to each collective per step on rank 0 (dist/trace.py)
         "moe_dispatch": moe_info,
+        "tp_transport": _tp_transport() if args.tp > 1 else None,
         "dist_world_size": dist.get_world_size() if dist.is_initialized() else 1,
         "backend": (("rccl" if a.backend == "nccl" else a.backend) if dist.is_initialized() else "none"),
         "collective_ranks_seen": ranks_seen,

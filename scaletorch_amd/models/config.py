@@ -80,6 +80,13 @@ class ModelConfig:
             total += self.vocab_size * h
         return total
 
+    def matmul_params(self, active: bool = True) -> int:
+        """Parameters that take part in a GEMM per token: ``active_params`` minus the input
+        embedding table, a gather (kept when tied: the same matrix is the LM head GEMM).
+        6x this (+ causal attention) is the strict model-FLOP count (bench ``mfu_pct_strict``)."""
+        n = self.active_params() if active else self.num_params()
+        return n if self.tie_word_embeddings else n - self.vocab_size * self.hidden_size
+
     def active_params(self) -> int:
         """Parameters touched per token (MoE: top-k experts only)."""
         if not self.is_moe:

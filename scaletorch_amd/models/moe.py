@@ -282,19 +282,39 @@ class MoERouter(nn.Module):
         return topw, topi, aux
 
 
+def _gmm_fallback(x: torch.Tensor, w: torch.Tensor, offs: torch.Tensor, wn: bool) -> torch.Tensor:
+    """``torch._grouped_mm`` when it runs here, else one GEMM per expert (one host read
+    of the offsets).  Rows past ``offs[-1]`` come back zero."""
+    wt = w if wn else w.transpose(-2, -1)
+    if _grouped_mm_available():
+        return torch._grouped_mm(x, wt, offs=offs)
+    ends = offs.tolist()
+    y = x.new_zeros(x.shape[0], wt.shape[2])
+    start = 0
+    for g, end in enumerate(ends):
+        if end > start:
+            y[start:end] = x[start:end] @ wt[g]
+        start = end
+    return y
+
+
 def _gmm(x: torch.Tensor, w: torch.Tensor, offs: torch.Tensor, wn: bool) -> torch.Tensor:
     """Per-expert ``x[rows of g] @ (w[g] if wn else w[g]^T)`` with device offsets: ONE launch
-    of csrc/grouped_gemm.hip (``ST_MOE_HIP_GMM=0``, or a shape it does not tile, falls back
-    to ``torch._grouped_mm``, which on ROCm runs a GEMM per expert)."""
+    of csrc/grouped_gemm.hip.  ``ST_MOE_HIP_GMM=0``, or a shape the kernel does not tile
+    (K not a whole number of 64-wide K tiles, N not of 128-wide N tiles, operands past
+    the kernel's 32-bit buffer offsets -- the binding then returns None), falls back to
+    ``_gmm_fallback``."""
     from ..ops import _lib
 
     K = x.shape[1]
     N = w.shape[2] if wn else w.shape[1]
     if (os.environ.get("ST_MOE_HIP_GMM", "1") == "1" and _lib.use_native(x) and x.dtype == torch.bfloat16
-            and x.stride(1) == 1 and x.stride(0) % 8 == 0 and w.is_contiguous() and K % 32 == 0 and N % 128 == 0
+            and x.stride(1) == 1 and x.stride(0) % 8 == 0 and w.is_contiguous() and K % 64 == 0 and N % 128 == 0
             and x.shape[0] > 0):
-        return _lib.ops().grouped_gemm(x, w, offs, wn)
-    return torch._grouped_mm(x, w if wn else w.transpose(-2, -1), offs=offs)
+        y = _lib.ops().grouped_gemm(x, w, offs, wn)
+        if y is not None:
+            return y
+    return _gmm_fallback(x, w, offs, wn)
 
 
 class _ExpertFFNFn(torch.autograd.Function):

@@ -274,3 +274,154 @@ def simulate_channels(P: int, V: int, M: int, depth: int = 2) -> None:
     for r in range(P):
         if len(steps[r]) != 2 * T:
             raise AssertionError(f"rank {r}: {len(steps[r])} compute steps, expected {2 * T}")
+
+
+# ---------------------------------------------------------------------------
+# Stream-level replay of the engine (pipeline_parallel.PipelineEngine) on RCCL
+# ---------------------------------------------------------------------------
+def channel_layout(kind: str, sender: int, receiver: int, P: int):
+    """Communicator of a message in the engine's layout: one 2-rank communicator per
+    directed stage pair (mesh.ProcessGroupManager._pp_channels)."""
+    return (kind, sender, receiver)
+
+
+def shared_layout(kind: str, sender: int, receiver: int, P: int):
+    """The round-3 layout: one whole-pipeline communicator per direction (plus the
+    interleaved ring seam on two more) -- a middle stage's activation receive and
+    its activation send share one RCCL stream."""
+    seam = (kind == "fwd" and sender == P - 1) or (kind == "bwd" and sender == 0)
+    return (kind, "seam" if seam else "pipe")
+
+
+def engine_programs(P: int, V: int, M: int, schedule: str = "1f1b", depth: int = 2, layout=channel_layout):
+    """Per-rank event lists in the engine's HOST issue order:
+    ("post", comm, peer, key) an irecv, ("send", comm, peer, key) an isend,
+    ("wait", key) the compute stream waiting for a received message.  Message keys
+    are (kind, receiving rank, receiver's step / micro-batch)."""
+    progs = []
+    for r in range(P):
+        ev = []
+        if schedule == "interleaved":
+            sched = build_schedule(P, V, M, r)
+            order = {"fwd": [], "bwd": []}
+            for a in sched:
+                if isinstance(a, Exchange):
+                    for kd, k in a.recv:
+                        order[kd].append(k)
+            src = {"fwd": (r - 1) % P, "bwd": (r + 1) % P}
+        else:
+            order = {"fwd": list(range(M)) if r > 0 else [], "bwd": list(range(M)) if r < P - 1 else []}
+            src = {"fwd": r - 1, "bwd": r + 1}
+        posted = {"fwd": 0, "bwd": 0}
+
+        def fill(kd):
+            while posted[kd] < len(order[kd]) and posted[kd] - taken[kd] < depth:
+                k = order[kd][posted[kd]]
+                ev.append(("post", layout(kd, src[kd], r, P), src[kd], (kd, r, k)))
+                posted[kd] += 1
+
+        taken = {"fwd": 0, "bwd": 0}
+
+        def take(kd):
+            taken[kd] += 1
+            fill(kd)
+
+        def send(kd, dst, k):
+            ev.append(("send", layout(kd, r, dst, P), dst, (kd, dst, k)))
+
+        fill("fwd")
+        fill("bwd")
+        if schedule == "interleaved":
+            for a in build_schedule(P, V, M, r):
+                if isinstance(a, Exchange):
+                    for kd, k in a.send:
+                        dst, key = _peer_and_key(P, r, kd, k, True)
+                        send(kd, dst, key[1])
+                    for kd, _k in a.recv:
+                        take(kd)
+                    continue
+                kind, k = a
+                if kind == "F" and not (r == 0 and fwd_chunk(k, P, V) == 0):
+                    ev.append(("wait", ("fwd", r, k)))
+                if kind == "B" and not (r == P - 1 and bwd_chunk(k, P, V) == V - 1):
+                    ev.append(("wait", ("bwd", r, k)))
+        else:
+            def fwd(m):
+                if r > 0:
+                    take("fwd")
+                    ev.append(("wait", ("fwd", r, m)))
+                if r < P - 1:
+                    send("fwd", r + 1, m)
+
+            def bwd(m):
+                if r < P - 1:
+                    take("bwd")
+                    ev.append(("wait", ("bwd", r, m)))
+                if r > 0:
+                    send("bwd", r - 1, m)
+
+            if schedule == "afab":
+                for m in range(M):
+                    fwd(m)
+                for m in range(M):
+                    bwd(m)
+            else:
+                warm = min(P - r - 1, M)
+                for m in range(warm):
+                    fwd(m)
+                for j in range(M - warm):
+                    fwd(warm + j)
+                    bwd(j)
+                for j in range(M - warm, M):
+                    bwd(j)
+        progs.append(ev)
+    return progs
+
+
+def simulate_streams(progs) -> None:
+    """Replay per-rank programs under RCCL semantics: the host never blocks; the
+    compute stream runs the program in order and stalls at a "wait" until that
+    message has arrived; every p2p op is enqueued on the stream of (rank, its
+    communicator) and becomes runnable once the compute stream has reached its issue
+    point (ProcessGroupNCCL fences the comm stream on the current stream); each such
+    stream runs its ops strictly in order, and a send and its receive complete
+    together when both are at the heads of their streams.  Raises on a deadlock or
+    on two heads of one communicator that pair up in the wrong order."""
+    P = len(progs)
+    cpos = [0] * P
+    queues: dict = {}
+    arrived = set()
+    while True:
+        progressed = False
+        for r in range(P):
+            while cpos[r] < len(progs[r]):
+                e = progs[r][cpos[r]]
+                if e[0] == "wait":
+                    if e[1] not in arrived:
+                        break
+                else:
+                    queues.setdefault((r, e[1]), []).append(e)
+                cpos[r] += 1
+                progressed = True
+        for (r, comm), q in list(queues.items()):
+            while q:
+                op, _, peer, key = q[0]
+                if op != "send":
+                    break
+                pq = queues.get((peer, comm))
+                if not pq:
+                    break
+                pop, _, ppeer, pkey = pq[0]
+                if pop != "post" or ppeer != r:
+                    break
+                if pkey != key:
+                    raise AssertionError(f"communicator {comm}: send {key} meets receive {pkey}")
+                q.pop(0)
+                pq.pop(0)
+                arrived.add(key)
+                progressed = True
+        if all(cpos[r] == len(progs[r]) for r in range(P)) and not any(queues.values()):
+            return
+        if not progressed:
+            heads = {k: q[0] for k, q in queues.items() if q}
+            raise AssertionError(f"p2p stream deadlock: compute at {cpos}, stream heads {heads}")

@@ -111,19 +111,49 @@ class ProcessGroupManager:
             cache[key] = groups
         return cache[key][lists.index(mine)], mine
 
+    def _pp_channels(self) -> dict:
+        """{(kind, i): communicator or None} for every directed pipeline channel this
+        rank is an end of (created collectively, same order on every rank)."""
+        P = self.sizes["pp"]
+        if P == 1:
+            return {}
+        import itertools
+
+        fixed = [a for a in AXES if a != "pp"]
+        out = {}
+        for kind in ("fwd", "bwd"):
+            for i in range(P):
+                a, b = (i, (i + 1) % P) if kind == "fwd" else ((i + 1) % P, i)  # (sender, receiver)
+                for combo in itertools.product(*[range(self.sizes[x]) for x in fixed]):
+                    fc = dict(zip(fixed, combo))
+                    ranks = [int(self.grid[tuple(s if x == "pp" else fc[x] for x in AXES)]) for s in (a, b)]
+                    g = None
+                    if self._create_groups:
+                        g = C.new_group(ranks=sorted(ranks))
+                        self._all_groups.append(g)
+                    if self.global_rank in ranks:
+                        out[(kind, i)] = g
+        return out
+
+    def pp_channel(self, kind: str, i: int):
+        """Communicator of directed pipeline channel (kind, i mod P); the whole-pipeline
+        group when groups are not created (single-process simulation)."""
+        return self.pp_channels.get((kind, i % self.pp_world_size)) or self.pp_group
+
     def _build(self) -> None:
         self.tp_group, self.tp_group_ids = self._family(("tp",))
         self.cp_group, self.cp_group_ids = self._family(("cp",))
         self.pp_group, self.pp_group_ids = self._family(("pp",))
-        # pipeline gradients travel on their own communicator: each direction is then a
-        # FIFO of its own, so a receive posted ahead (activations) can never sit in front
-        # of a send the peer is waiting for (gradients) -- parallel/pipeline_parallel.py
-        self.pp_bwd_group, _ = self._family(("pp",), channel="pp_bwd")
-        # the interleaved schedule's ring seam (last stage -> first stage activations, first
-        # -> last gradients) on two more: at pp = 2 the seam pair is the SAME pair as the
-        # forward one, and sharing its communicator would put both directions in one queue
-        self.pp_seam_group, _ = self._family(("pp",), channel="pp_seam")
-        self.pp_seam_bwd_group, _ = self._family(("pp",), channel="pp_seam_bwd")
+        # pipeline p2p: ONE 2-rank communicator per directed channel -- activations
+        # stage i -> i+1 on ("fwd", i), gradients stage i+1 -> i on ("bwd", i), the
+        # interleaved ring seam being i = P-1.  A batched p2p op (batch_isend_irecv) runs
+        # on its communicator's single RCCL stream; on a whole-pipeline communicator a
+        # middle stage's receive posted ahead from r-1 would queue in front of its send
+        # to r+1 and close a wait cycle at pp >= 3 (parallel/interleaved.py
+        # ``simulate_streams`` replays both layouts).  Each stream here carries one
+        # direction between one pair of ranks, so a posted receive only ever waits for
+        # its own sender.
+        self.pp_channels = self._pp_channels()
         self.ep_group, self.ep_group_ids = self._family(("ep",))
         self.dp_group, self.dp_group_ids = self._family(("dp",))
         self.cp_dp_group, self.cp_dp_group_ids = self._family(("dp", "cp"))

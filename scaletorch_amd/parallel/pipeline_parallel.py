@@ -8,8 +8,9 @@ Differences:
   norm + LM head on the last;
 * every exchange is non-blocking, and receives are POSTED AHEAD: activations
   travel on the pipeline communicator and gradients on a second one
-  (``mesh.pp_bwd_group``), so each direction between two stages is its own FIFO
-  and a receive posted early can never block a send the peer is waiting for.
+  (every directed stage pair has its own 2-rank communicator, ``mesh.pp_channel``),
+  so each direction between two stages is its own RCCL stream and a receive
+  posted early can never block a send the peer is waiting for.
   The engine keeps the next micro-batch's receive in flight in each direction
   (``_Mailbox``, depth 2) and waits (a stream wait on RCCL) right before the
   data is used, so the transfer runs under the current micro-batch's forward /
@@ -59,40 +60,23 @@ def wait_sends() -> None:
 
 def _p2p(send_fwd=None, send_bwd=None, recv_fwd_shape=None, recv_bwd_shape=None, dtype=torch.bfloat16,
          device=None):
-    """One grouped exchange with the neighbouring stages; returns (recv_fwd, recv_bwd).
+    """One exchange with the neighbouring stages; returns (recv_fwd, recv_bwd).
 
-    Groups with a receive are joined before returning (the caller consumes the data
-    next); send-only groups are left in flight (``wait_sends``)."""
+    Each op runs on its directed channel's communicator (``mesh.pp_channel``).
+    Receives are joined before returning (the caller consumes the data next);
+    sends are left in flight (``wait_sends``)."""
     pg = mesh.pgm
-    group = pg.pp_group
-    ops, rf, rb = [], None, None
+    r = pg.pp_rank
+    rf = rb = None
     if send_fwd is not None and pg.pp_next_rank is not None:
-        ops.append(dist.P2POp(dist.isend, send_fwd.contiguous(), pg.pp_next_rank, group))
-        _STATS["send_forward"] += 1
-        trace.record("pp.send_forward", send_fwd, peer=pg.pp_next_rank)
+        _send(send_fwd, pg.pp_next_rank, pg.pp_channel("fwd", r), "forward")
     if send_bwd is not None and pg.pp_prev_rank is not None:
-        ops.append(dist.P2POp(dist.isend, send_bwd.contiguous(), pg.pp_prev_rank, group))
-        _STATS["send_backward"] += 1
-        trace.record("pp.send_backward", send_bwd, peer=pg.pp_prev_rank)
+        _send(send_bwd, pg.pp_prev_rank, pg.pp_channel("bwd", r - 1), "backward")
     if recv_fwd_shape is not None and pg.pp_prev_rank is not None:
-        rf = torch.empty(recv_fwd_shape, dtype=dtype, device=device)
-        ops.append(dist.P2POp(dist.irecv, rf, pg.pp_prev_rank, group))
-        _STATS["recv_forward"] += 1
-        trace.record("pp.recv_forward", rf, peer=pg.pp_prev_rank)
-    if recv_bwd_shape is not None and pg.pp_next_rank is not None:
-        rb = torch.empty(recv_bwd_shape, dtype=dtype, device=device)
-        ops.append(dist.P2POp(dist.irecv, rb, pg.pp_next_rank, group))
-        _STATS["recv_backward"] += 1
-        trace.record("pp.recv_backward", rb, peer=pg.pp_next_rank)
-    if ops:
-        works = dist.batch_isend_irecv(ops)
-        if rf is None and rb is None:
-            _INFLIGHT.append((works, [op.tensor for op in ops]))
-        else:
-            for w in works:
-                w.wait()
-    if rf is not None:
+        rf = _Recv(recv_fwd_shape, dtype, device, pg.pp_prev_rank, pg.pp_channel("fwd", r - 1), "forward").get()
         rf.requires_grad_(True)
+    if recv_bwd_shape is not None and pg.pp_next_rank is not None:
+        rb = _Recv(recv_bwd_shape, dtype, device, pg.pp_next_rank, pg.pp_channel("bwd", r), "backward").get()
     return rf, rb
 
 
@@ -220,18 +204,20 @@ class PipelineEngine:
         return x.grad if x is not None else None
 
     def _mailboxes(self, num_micro: int):
-        """(activation mailbox or None, gradient mailbox or None) of this stage."""
+        """(activation mailbox or None, gradient mailbox or None, forward-send channel,
+        gradient-send channel) of this stage; every channel is its own 2-rank
+        communicator (mesh.ProcessGroupManager._pp_channels)."""
         pg = mesh.pgm
-        bwd_group = getattr(pg, "pp_bwd_group", None) or pg.pp_group
+        r = pg.pp_rank
         rf = None if self._first else _Mailbox(num_micro, self.tensor_shape, self.dtype, self.device,
-                                               pg.pp_prev_rank, pg.pp_group, "forward")
+                                               pg.pp_prev_rank, pg.pp_channel("fwd", r - 1), "forward")
         rb = None if self._last else _Mailbox(num_micro, self.tensor_shape, self.dtype, self.device,
-                                              pg.pp_next_rank, bwd_group, "backward")
-        return rf, rb, bwd_group
+                                              pg.pp_next_rank, pg.pp_channel("bwd", r), "backward")
+        return rf, rb, pg.pp_channel("fwd", r), pg.pp_channel("bwd", r - 1)
 
     def train_step_afab(self, data_iter, num_micro: int) -> torch.Tensor:
         pg = mesh.pgm
-        rf, rb, bwd_group = self._mailboxes(num_micro)
+        rf, rb, fwd_out, bwd_out = self._mailboxes(num_micro)
         ins, outs = deque(), deque()
         loss_sum = torch.zeros((), dtype=torch.float32, device=self.device)
         for _ in range(num_micro):
@@ -239,7 +225,7 @@ class PipelineEngine:
             batch = next(data_iter)
             y = self._forward(batch, x, num_micro)
             if not self._last:
-                _send(y.detach(), pg.pp_next_rank, pg.pp_group, "forward")
+                _send(y.detach(), pg.pp_next_rank, fwd_out, "forward")
             else:
                 loss_sum += y.detach().float()
             ins.append(x)
@@ -249,7 +235,7 @@ class PipelineEngine:
             x, y = ins.popleft(), outs.popleft()
             dx = self._backward(x, y, dy, last_backward=(i == num_micro - 1))
             if not self._first:
-                _send(dx, pg.pp_prev_rank, bwd_group, "backward")
+                _send(dx, pg.pp_prev_rank, bwd_out, "backward")
         wait_sends()
         return loss_sum
 
@@ -260,7 +246,7 @@ class PipelineEngine:
         pg = mesh.pgm
         warmup = min(pg.pp_world_size - pg.pp_rank - 1, num_micro)
         steady = num_micro - warmup
-        rf, rb, bwd_group = self._mailboxes(num_micro)
+        rf, rb, fwd_out, bwd_out = self._mailboxes(num_micro)
         ins, outs = deque(), deque()
         loss_sum = torch.zeros((), dtype=torch.float32, device=self.device)
         n_bwd = 0
@@ -271,7 +257,7 @@ class PipelineEngine:
             if self._last:
                 loss_sum.add_(y.detach().float())
             else:
-                _send(y.detach(), pg.pp_next_rank, pg.pp_group, "forward")
+                _send(y.detach(), pg.pp_next_rank, fwd_out, "forward")
             ins.append(x)
             outs.append(y)
 
@@ -282,7 +268,7 @@ class PipelineEngine:
             n_bwd += 1
             dx = self._backward(xo, yo, dy, last_backward=(n_bwd == num_micro))
             if not self._first:
-                _send(dx, pg.pp_prev_rank, bwd_group, "backward")
+                _send(dx, pg.pp_prev_rank, bwd_out, "backward")
 
         for _ in range(warmup):
             fwd()
@@ -308,17 +294,11 @@ class PipelineEngine:
         P, r, V, M = pg.pp_world_size, pg.pp_rank, self.virtual_stages, num_micro
         ring = pg.pp_group_ids
         nxt, prv = ring[(r + 1) % P], ring[(r - 1) % P]
-        # one communicator per (direction, seam): every channel carries ONE direction
-        # between ONE pair of ranks, so a receive posted ahead only ever waits for its
-        # own sender (interleaved.simulate_channels replays this model)
-        group = pg.pp_group
-        bwd_group = getattr(pg, "pp_bwd_group", None) or group
-        seam_group = getattr(pg, "pp_seam_group", None) or group
-        seam_bwd_group = getattr(pg, "pp_seam_bwd_group", None) or bwd_group
-        fwd_out = seam_group if r == P - 1 else group        # our forward sends
-        fwd_in = seam_group if r == 0 else group             # our forward receives
-        bwd_out = seam_bwd_group if r == 0 else bwd_group    # our gradient sends
-        bwd_in = seam_bwd_group if r == P - 1 else bwd_group  # our gradient receives
+        # one 2-rank communicator per directed channel (mesh._pp_channels): every RCCL
+        # stream carries ONE direction between ONE pair of ranks, so a receive posted
+        # ahead only ever waits for its own sender (interleaved.simulate_streams)
+        fwd_out, fwd_in = pg.pp_channel("fwd", r), pg.pp_channel("fwd", r - 1)
+        bwd_out, bwd_in = pg.pp_channel("bwd", r - 1), pg.pp_channel("bwd", r)
         batches: list = []
 
         def batch(m):

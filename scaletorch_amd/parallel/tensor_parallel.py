@@ -53,6 +53,7 @@ def set_tp_comm(kind: str) -> None:
     if kind not in ("rccl", "xgmi"):
         raise ValueError(f"tp_comm must be rccl or xgmi, got {kind!r}")
     _TP_COMM = kind
+    TRANSPORT["tp"] = kind
 
 
 _PAIR: list = [None]  # dist/xgmi.PairPath of a 2-rank TP group (multipath SP collectives)
@@ -65,6 +66,82 @@ def setup_tp_pair_path(group) -> None:
     from ..dist.xgmi import setup_pair_path
 
     _PAIR[0] = setup_pair_path(group)
+
+
+TRANSPORT: dict = {"tp": "rccl", "selftest": None}  # chosen TP transport (bench JSON reports it)
+
+
+def select_tp_transport(group, requested: str = "auto", probe_mb: int = 64) -> str:
+    """Pick the TP transport at start-up; collective over the WORLD (every rank calls it).
+
+    ``requested`` "rccl" / "xgmi" are taken as given.  "auto": for a 2-rank TP group on
+    one node, set up the 7-link pair path (dist/xgmi.py ``setup_pair_path``) and
+    self-test it against RCCL on the TP group -- a ``probe_mb`` MiB all-gather and
+    reduce-scatter must match RCCL (AG bitwise, RS within one bf16 rounding), no xGMI
+    wait may time out, and the pair path must be faster than RCCL on both.  The
+    verdict is MIN-reduced over the world, so every rank takes the same path; any
+    failure falls back to RCCL.  Reference transport: RCCL/NCCL only
+    (scaletorch/parallel/sequence_parallel/sp_comms.py:31-94)."""
+    import torch.distributed as dist
+
+    if requested in ("rccl", "xgmi"):
+        set_tp_comm(requested)
+        if requested == "xgmi" and _ws(group) == 2:
+            setup_tp_pair_path(group)
+        TRANSPORT["tp"] = requested
+        return requested
+    if requested != "auto":
+        raise ValueError(f"tp_comm must be auto, rccl or xgmi, got {requested!r}")
+    ok, info = 0, {}
+    if _ws(group) == 2 and torch.cuda.is_available():
+        try:
+            setup_tp_pair_path(group)
+            pair = _PAIR[0]
+            if pair is not None:
+                ok, info = _pair_selftest(pair, group, probe_mb)
+        except Exception as e:  # noqa: BLE001 -- fall back, but every rank still joins the vote
+            ok, info = 0, {"error": repr(e)[:200]}
+    flag = torch.tensor([ok], dtype=torch.int32, device="cuda" if torch.cuda.is_available() else "cpu")
+    if dist.is_initialized():
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    choice = "xgmi" if int(flag.item()) == 1 else "rccl"
+    set_tp_comm(choice)
+    if choice == "rccl":
+        _PAIR[0] = None
+    TRANSPORT.update(tp=choice, selftest=info)
+    return choice
+
+
+def _pair_selftest(pair, group, probe_mb: int):
+    """(1 if the pair path is correct and faster than RCCL else 0, timings)."""
+    n = (probe_mb << 20) // 2
+    r = C.get_rank(group)
+    g = torch.Generator(device="cuda").manual_seed(1234 + r)
+    x = torch.randn(n // 2, device="cuda", dtype=torch.bfloat16, generator=g)
+    big = torch.randn(n, device="cuda", dtype=torch.bfloat16, generator=g)
+
+    def timed(fn, iters=5):
+        fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            out = fn()
+        e.record()
+        e.synchronize()
+        return out, s.elapsed_time(e) / iters
+
+    ag_x, t_ag_x = timed(lambda: pair.all_gather(x))
+    ag_r, t_ag_r = timed(lambda: C.all_gather(x, group=group))
+    rs_x, t_rs_x = timed(lambda: pair.reduce_scatter(big))
+    rs_r, t_rs_r = timed(lambda: C.reduce_scatter(big, group=group))
+    pair.comm.check()
+    same_ag = bool(torch.equal(ag_x, ag_r))
+    err_rs = float(((rs_x.float() - rs_r.float()).abs() / (rs_r.float().abs() + 1e-3)).max())
+    info = {"probe_mb": probe_mb, "ag_ms": [round(t_ag_x, 3), round(t_ag_r, 3)],
+            "rs_ms": [round(t_rs_x, 3), round(t_rs_r, 3)], "ag_bitwise": same_ag, "rs_max_rel_err": round(err_rs, 5)}
+    good = same_ag and err_rs < 1e-2 and t_ag_x < t_ag_r and t_rs_x < t_rs_r
+    return (1 if good else 0), info
 
 
 class _StreamWork:
@@ -236,14 +313,14 @@ def _reduce_scatter_seq(x: torch.Tensor, group) -> torch.Tensor:
 
 
 def _gather_seq_async(x: torch.Tensor, group):
-    """Issue the sequence all-gather; returns ``finish() -> [B, S, ...]`` (waits on first call)."""
+    """Issue the sequence all-gather; returns ``finish() -> [B, S, ...]`` (waits on first call).
+    RCCL async, or the xGMI pair path on its comm side stream (``_sp_gather_async``)."""
     ws = _ws(group)
     if ws == 1:
         return lambda: x
-    _trace("sp.all_gather", x, ws)
     B = x.shape[0]
     xt = x[0].contiguous() if B == 1 else x.transpose(0, 1).contiguous()
-    out, work = C.all_gather(xt, group=group, async_op=True)
+    out, work = _sp_gather_async(xt, group)
 
     def finish():
         work.wait()
@@ -256,10 +333,9 @@ def _reduce_scatter_seq_async(x: torch.Tensor, group):
     ws = _ws(group)
     if ws == 1:
         return lambda: x
-    _trace("sp.reduce_scatter", x, ws)
     B = x.shape[0]
     xt = x[0].contiguous() if B == 1 else x.transpose(0, 1).contiguous()
-    out, work = C.reduce_scatter(xt, group=group, async_op=True)
+    out, work = _sp_reduce_scatter_async(xt, group)
 
     def finish():
         work.wait()
@@ -394,10 +470,11 @@ class _ColumnParallelFn(torch.autograd.Function):
 
 
 def _sp_overlap(x: torch.Tensor) -> bool:
-    """Pipelined SP forward (ST_SP_OVERLAP=0: one blocking collective + one GEMM, A/B)."""
+    """Pipelined SP forward (ST_SP_OVERLAP=0: one blocking collective + one GEMM, A/B).
+    Composes with the xGMI pair path: its collectives run on a comm side stream."""
     import os
 
-    return _TP_COMM != "xgmi" and os.environ.get("ST_SP_OVERLAP", "1") == "1"
+    return os.environ.get("ST_SP_OVERLAP", "1") == "1"
 
 
 def _sp_chunks(Sp: int, tokens: int) -> int:
@@ -415,13 +492,103 @@ def _rows_gemm(x2: torch.Tensor, weight: torch.Tensor, out: torch.Tensor) -> Non
     torch.matmul(x2, weight.t(), out=out)
 
 
+def _bmm_into(x3: torch.Tensor, b2: torch.Tensor, out3: torch.Tensor) -> None:
+    """``out3[b] = x3[b] @ b2`` for every batch element in ONE strided-batched GEMM.
+
+    ``x3`` [B, M, K] and ``out3`` [B, M, N] may be row blocks of larger tensors
+    (batch stride != M * row stride: a sequence slice of [B, S, .]); ``b2`` [K, N]
+    is shared (batch stride 0).  hipBLASLt takes those strides as they are, so the
+    sequence-parallel pieces run as one [B*M, K] x [K, N] product instead of B
+    separate [M, K] GEMMs (with B = 4 and M = 1024 those were 48-tile launches on
+    256 CUs, profiles/r04/sp_gemm_split.json)."""
+    B = x3.shape[0]
+    if B == 1:
+        torch.matmul(x3[0], b2, out=out3[0])
+        return
+    torch.bmm(x3, b2.unsqueeze(0).expand(B, -1, -1), out=out3)
+
+
+def _dgrad_b2(weight: torch.Tensor) -> torch.Tensor:
+    """[out, in] right operand of dX = dY W: the TN view of the current W^T copy when
+    one exists (ops/grad.py ``prepare_dgrad_weight``), else the weight itself."""
+    from ..ops.grad import _WT_EPOCH
+
+    if getattr(weight, "_st_wt_epoch", -1) == _WT_EPOCH[0] and weight.is_cuda:
+        torch.cuda.current_stream().wait_event(weight._st_wt_done)
+        return weight._st_wt.t()
+    return weight
+
+
+def _sp_gather_async(part: torch.Tensor, group):
+    """Issue the all-gather of one SP sub-chunk ([B, Sc, h] -> [ws*B, Sc, h], rank-major);
+    returns (buffer, work).  Over the xGMI pair path (tp = 2, --tp_comm xgmi) it runs on
+    the comm side stream, so it overlaps the GEMMs exactly like the RCCL one."""
+    ws = _ws(group)
+    pair = _pair_for(group, part.numel(), part)
+    if pair is not None:
+        st, ready = _comm_stream(part.device)
+        with torch.cuda.stream(st):
+            st.wait_event(ready)
+            out = pair.all_gather(part)
+        part.record_stream(st)
+        out.record_stream(torch.cuda.current_stream())
+        return out, _StreamWork(st)
+    _trace("sp.all_gather", part, ws)
+    return C.all_gather(part, group=group, async_op=True)
+
+
+def _sp_reduce_scatter_async(buf: torch.Tensor, group):
+    """Issue the reduce-scatter of one SP sub-chunk ([ws*B, Sc, o] -> [B, Sc, o]);
+    returns (output, work) -- xGMI pair path on the comm side stream, else RCCL."""
+    ws = _ws(group)
+    pair = _pair_for(group, buf.numel() // 2, buf)
+    if pair is not None:
+        st, ready = _comm_stream(buf.device)
+        with torch.cuda.stream(st):
+            st.wait_event(ready)
+            out = pair.reduce_scatter(buf)
+        buf.record_stream(st)
+        out.record_stream(torch.cuda.current_stream())
+        return out, _StreamWork(st)
+    _trace("sp.reduce_scatter", buf, ws)
+    return C.reduce_scatter(buf, group=group, async_op=True)
+
+
+def _pair_for(group, n_elems: int, t: torch.Tensor):
+    """The 2-rank xGMI multipath transport for this SP message, or None (RCCL)."""
+    if not t.is_cuda or _ws(group) != 2 or _xgmi_comm(group) is None:
+        return None
+    pair = _PAIR[0]
+    if pair is None or not pair.fits(n_elems, t):
+        return None
+    from ..dist import trace
+
+    trace.record("sp.pair", t, group_size=2, transport="xgmi-pair")
+    return pair
+
+
+_COMM_STREAMS: dict = {}
+
+
+def _comm_stream(device: torch.device):
+    """(side stream of the xGMI SP collectives, event of the current stream's position):
+    the collective starts once the producer of its input has finished."""
+    st = _COMM_STREAMS.get(device.index)
+    if st is None:
+        st = _COMM_STREAMS[device.index] = torch.cuda.Stream(device=device)
+    ready = torch.cuda.Event()
+    ready.record()
+    return st, ready
+
+
 def _sp_column_forward(x_shard: torch.Tensor, weight: torch.Tensor, group) -> torch.Tensor:
     """y[B, S, out] = all_gather_seq(x_shard) W^T with the gather hidden behind GEMMs:
     the sequence all-gathers are issued first (async, in ``c`` sub-chunks), the rows of
     this rank's OWN shard are multiplied while they are in flight, then each sub-chunk's
-    peer rows as soon as that sub-chunk has landed.  Every GEMM writes its rows of y in
-    place (no assembly copy).  Reference: AllGatherFromSequenceParallelRegion + a
-    column linear, scaletorch/parallel/sequence_parallel/sp_comms.py:31-61 (serialised)."""
+    peer rows as soon as that sub-chunk has landed.  Every GEMM is ONE strided-batched
+    product over all B sequences writing its rows of y in place (no assembly copy).
+    Reference: AllGatherFromSequenceParallelRegion + a column linear,
+    scaletorch/parallel/sequence_parallel/sp_comms.py:31-61 (serialised)."""
     ws, r = _ws(group), C.get_rank(group)
     B, Sp, _ = x_shard.shape
     c = _sp_chunks(Sp, B * Sp * ws)
@@ -431,17 +598,15 @@ def _sp_column_forward(x_shard: torch.Tensor, weight: torch.Tensor, group) -> to
     for q in range(c):
         part = xs[:, q * Sc:(q + 1) * Sc]
         part = part.contiguous() if (c > 1 and B > 1) else part
-        _trace("sp.all_gather", part, ws)
-        gathers.append(C.all_gather(part, group=group, async_op=True))  # [ws*B, Sc, h], rank-major
+        gathers.append(_sp_gather_async(part, group))  # [ws*B, Sc, h], rank-major
     y = torch.empty(B, Sp * ws, weight.shape[0], dtype=x_shard.dtype, device=x_shard.device)
-    for b in range(B):  # own rows: no communication needed
-        _rows_gemm(xs[b], weight, y[b, r * Sp:(r + 1) * Sp])
+    wt = weight.t()
+    _bmm_into(xs, wt, y[:, r * Sp:(r + 1) * Sp])  # own rows: no communication needed
     for q, (buf, work) in enumerate(gathers):
         work.wait()
         for j in range(ws):
             if j != r:
-                for b in range(B):
-                    _rows_gemm(buf[j * B + b], weight, y[b, j * Sp + q * Sc: j * Sp + (q + 1) * Sc])
+                _bmm_into(buf[j * B:(j + 1) * B], wt, y[:, j * Sp + q * Sc: j * Sp + (q + 1) * Sc])
     return y
 
 
@@ -511,14 +676,13 @@ class _SPRowParallelFn(torch.autograd.Function):
         Sc = Sp // c
         out_f = weight.shape[0]
         x = x.contiguous()
+        wt = weight.t()
         pending = []
         for q in range(c):
             buf = torch.empty(ws * B, Sc, out_f, dtype=x.dtype, device=x.device)
-            for j in range(ws):
-                for b in range(B):
-                    _rows_gemm(x[b, j * Sp + q * Sc: j * Sp + (q + 1) * Sc], weight, buf[j * B + b])
-            _trace("sp.reduce_scatter", buf, ws)
-            pending.append(C.reduce_scatter(buf, group=group, async_op=True))  # -> [B, Sc, out]
+            for j in range(ws):  # every sequence's rows of (peer j, sub-chunk q): one batched GEMM
+                _bmm_into(x[:, j * Sp + q * Sc: j * Sp + (q + 1) * Sc], wt, buf[j * B:(j + 1) * B])
+            pending.append(_sp_reduce_scatter_async(buf, group))  # -> [B, Sc, out]
         if c == 1:
             out, work = pending[0]
             work.wait()
@@ -537,19 +701,17 @@ class _SPRowParallelFn(torch.autograd.Function):
         B, Sp, out_f = dy.shape
         S = Sp * ws
         dys = dy.contiguous()
-        _trace("sp.all_gather", dys, ws)
-        buf, work = C.all_gather(dys, group=group, async_op=True)  # [ws*B, Sp, out], rank-major
+        buf, work = _sp_gather_async(dys, group)  # [ws*B, Sp, out], rank-major
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(B, S, weight.shape[1], dtype=dy.dtype, device=dy.device)
-            for b in range(B):  # own rows under the gather
-                dgrad_into(dys[b], weight, dx[b, r * Sp:(r + 1) * Sp])
+            b2 = _dgrad_b2(weight)
+            _bmm_into(dys, b2, dx[:, r * Sp:(r + 1) * Sp])  # own rows under the gather
         work.wait()
         if dx is not None:
             for j in range(ws):
                 if j != r:
-                    for b in range(B):
-                        dgrad_into(buf[j * B + b], weight, dx[b, j * Sp:(j + 1) * Sp])
+                    _bmm_into(buf[j * B:(j + 1) * B], b2, dx[:, j * Sp:(j + 1) * Sp])
         dw = None
         if ctx.needs_input_grad[1]:
             if B == 1:

@@ -64,7 +64,7 @@ class ParallelArguments:
     backend: str = field(default="nccl", metadata={"help": "nccl (=RCCL) | gloo | hccl (maps to nccl)"})
     sequence_parallel: bool = field(default=False, metadata={"help": "Megatron-SP over the TP group"})
     cp_zigzag: bool = field(default=True, metadata={"help": "zig-zag load-balanced CP chunks"})
-    tp_comm: str = field(default="rccl", metadata={"help": "TP all-reduce transport: rccl | xgmi (custom one-/two-shot over IPC peer memory, dist/xgmi.py)"})
+    tp_comm: str = field(default="auto", metadata={"help": "TP transport: auto (tp = 2 on one node: self-test the 7-link xGMI pair path against RCCL at start-up and keep the faster correct one; else RCCL) | rccl | xgmi (custom one-/two-shot all-reduce + pair all-gather / reduce-scatter over IPC peer memory, dist/xgmi.py)"})
     cp_comm: str = field(default="auto", metadata={"help": "CP transport: auto (= allgather: RCCL drives all 7 xGMI links) | allgather (overlapped K/V all-gather) | ring (p2p rotation overlapped with block compute) | ulysses (head all-to-all)"})
     layer_distribution: str | None = field(default=None, metadata={"help": "comma list of layers per PP stage"})
     moe_capacity_factor: float = field(default=0.0, metadata={
@@ -93,6 +93,8 @@ class ParallelArguments:
             if getattr(self, "gradient_accumulation_steps", 1) % self.pipeline_parallel_size:
                 raise ValueError("interleaved 1F1B needs gradient_accumulation_steps divisible by "
                                  "pipeline_parallel_size")
+        if self.tp_comm not in {"auto", "rccl", "xgmi"}:
+            raise ValueError(f"tp_comm must be auto, rccl or xgmi, got {self.tp_comm}")
         if self.ep_comm not in {"rccl", "xgmi"}:
             raise ValueError(f"ep_comm must be rccl or xgmi, got {self.ep_comm}")
         if self.moe_capacity_factor < 0 or self.moe_ep_chunks < 1:

@@ -57,12 +57,14 @@ class Trainer:
 
                 debug.enable(timeout_s=a.timeout_s)
         if a.tensor_parallel_size > 1:
-            from ..parallel.tensor_parallel import set_tp_comm, setup_tp_pair_path
+            from ..parallel.tensor_parallel import select_tp_transport, set_tp_comm
 
-            set_tp_comm(a.tp_comm)
-            if (a.tp_comm == "xgmi" and a.tensor_parallel_size == 2 and a.backend == "nccl"
-                    and torch.cuda.is_available() and not a.use_cpu):
-                setup_tp_pair_path(mesh.tp_group())  # collective over the world, before any model code
+            if torch.cuda.is_available() and not a.use_cpu and (a.backend == "nccl" or a.tp_comm == "xgmi"):
+                # collective over the world, before any model code: "auto" self-tests the
+                # 7-link pair path for tp = 2 against RCCL and keeps the faster correct one
+                select_tp_transport(mesh.tp_group(), a.tp_comm)
+            else:
+                set_tp_comm("rccl" if a.tp_comm == "auto" else a.tp_comm)
         from ..models.attention_backends import set_use_flash_attention
         from ..models.moe import set_moe_dispatch
 
@@ -318,7 +320,9 @@ class Trainer:
         """Raise if a custom xGMI collective timed out since the last check (its
         outputs are invalid); called at logging steps by tools/train.py and at the
         end of bench.py so the job exits non-zero instead of training on garbage."""
-        if self.args.tp_comm == "xgmi":
+        from ..parallel.tensor_parallel import TRANSPORT
+
+        if TRANSPORT["tp"] == "xgmi":
             from ..parallel.tensor_parallel import check_xgmi
 
             check_xgmi()

@@ -60,22 +60,41 @@ def _to_cpu(obj):
 
 
 _DONE = "complete_rank_world_size={}_{}"
+_STARTED = "started_rank_world_size={}_{}"
+
+
+def _has_markers(step_dir: str) -> bool:
+    return bool(glob.glob(os.path.join(step_dir, "complete_rank_world_size=*"))
+                or glob.glob(os.path.join(step_dir, "started_rank_world_size=*")))
 
 
 def is_complete(step_dir: str) -> bool:
     """Every rank of the job that wrote ``step_dir`` finished its files: each rank
-    drops ``complete_rank_world_size={r}_{W}`` after its own writes (incl. ZeRO-1
-    optimizer shards); a directory from a crash mid-save lacks some markers."""
+    drops ``started_rank_world_size={r}_{W}`` BEFORE its first file and
+    ``complete_rank_world_size={r}_{W}`` after its last one (incl. ZeRO-1 optimizer
+    shards); a directory from a crash mid-save lacks some completion markers.
+
+    A directory with neither kind of marker predates them (legacy layout).  It
+    counts as complete only with ``ST_CKPT_ACCEPT_UNMARKED=1`` (the default) AND
+    when no sibling step directory carries markers: next to marked directories an
+    unmarked one can only be a crash of the current code before its first
+    marker, so the newest marked complete directory wins."""
     marks = glob.glob(os.path.join(step_dir, "complete_rank_world_size=*"))
     if not marks:
-        # written before completion markers existed: treat as complete (legacy layout),
-        # visibly, instead of silently restarting from step 0 next to it
-        if os.environ.get("ST_CKPT_ACCEPT_UNMARKED", "1") == "1":
-            logger.warning("checkpoint %s has no completion markers (legacy layout); treating it as complete "
-                           "(ST_CKPT_ACCEPT_UNMARKED=0 skips such directories)", step_dir)
-            return True
-        logger.warning("skipping checkpoint %s: no completion markers", step_dir)
-        return False
+        if glob.glob(os.path.join(step_dir, "started_rank_world_size=*")):
+            return False  # a save began and never finished
+        if os.environ.get("ST_CKPT_ACCEPT_UNMARKED", "1") != "1":
+            logger.warning("skipping checkpoint %s: no completion markers", step_dir)
+            return False
+        parent = os.path.dirname(os.path.abspath(step_dir))
+        for sib in glob.glob(os.path.join(parent, "*")):
+            if os.path.basename(sib).isdigit() and os.path.abspath(sib) != os.path.abspath(step_dir) \
+                    and _has_markers(sib):
+                logger.warning("skipping unmarked checkpoint %s: sibling %s has completion markers", step_dir, sib)
+                return False
+        logger.warning("checkpoint %s has no completion markers (legacy layout); treating it as complete "
+                       "(ST_CKPT_ACCEPT_UNMARKED=0 skips such directories)", step_dir)
+        return True
     worlds = {m.rsplit("_", 1)[-1] for m in marks}
     if len(worlds) != 1:
         return False
@@ -126,6 +145,10 @@ class CheckpointManager:
         sched = _to_cpu(lr_scheduler.state_dict()) if (lr_scheduler is not None and writer) else None
         self.wait()
         done = os.path.join(out_dir, _DONE.format(C.get_rank(), C.get_world_size()))
+        # before any file of this rank lands: a crash from here on leaves a directory
+        # that is_complete() recognises as a partial save
+        with open(os.path.join(out_dir, _STARTED.format(C.get_rank(), C.get_world_size())), "w") as f:
+            f.write("started\n")
 
         def _write():
             for pth, obj in writes:

@@ -76,6 +76,31 @@ def test_unmarked_legacy_checkpoint_is_accepted_visibly(tmp_path, monkeypatch):
     assert latest_checkpoint(str(tmp_path)) is None
 
 
+def test_zero_marker_crash_falls_back_to_marked_checkpoint(tmp_path):
+    """A crash mid-save before any rank wrote its completion marker: with the
+    save-started sentinel the directory is recognised as partial, and even without
+    it (a crash before the sentinel existed) an unmarked directory next to marked
+    ones is never preferred over the newest complete marked one."""
+    from scaletorch_amd.utils.checkpoint import is_complete, latest_checkpoint
+
+    w = "weights_tp_rank_world_size=0_1_pp_rank_world_size=0_1.pth"
+    d2 = tmp_path / "2"
+    d2.mkdir()
+    (d2 / w).write_bytes(b"x")
+    for r in (0, 1):
+        (d2 / f"started_rank_world_size={r}_2").write_text("started\n")
+        (d2 / f"complete_rank_world_size={r}_2").write_text("ok\n")
+    d4 = tmp_path / "4"  # crash after rank 0's first file, no completion marker at all
+    d4.mkdir()
+    (d4 / w).write_bytes(b"x")
+    (d4 / "started_rank_world_size=0_2").write_text("started\n")
+    assert not is_complete(str(d4))
+    assert latest_checkpoint(str(tmp_path)).endswith("/2")
+    (d4 / "started_rank_world_size=0_2").unlink()  # no sentinel either: the sibling decides
+    assert not is_complete(str(d4))
+    assert latest_checkpoint(str(tmp_path)).endswith("/2")
+
+
 def _resume_corrupt_worker(rank, world, work_dir):
     import torch
 

@@ -162,6 +162,17 @@ def test_interleaved_1f1b_parity(pp, v, ga, extra):
     _compare(ref, res)
 
 
+@pytest.mark.parametrize("engine", ["1f1b", "afab"])
+def test_pp3_parity(engine):
+    """Three pipeline stages (a middle stage that both receives and sends in each
+    direction) on per-channel communicators equal the single-process step."""
+    ref = _reference("tiny-llama", 4, num_hidden_layers=3)
+    res = run_workers(_worker, 3, "tiny-llama", dict(pipeline_parallel_size=3, micro_batch_size=1,
+                                                     gradient_accumulation_steps=4, num_hidden_layers=3,
+                                                     pipeline_parallel_engine=engine))
+    _compare(ref, res)
+
+
 def test_interleaved_schedules_deadlock_free_with_posted_receives():
     """The engine's model (pipeline_parallel.py): one communicator per direction and ring
     seam, receives posted 1-3 ahead, sends issued after their compute step -- every
@@ -173,6 +184,57 @@ def test_interleaved_schedules_deadlock_free_with_posted_receives():
             for M in (P, 2 * P, 4 * P):
                 for depth in (1, 2, 3):
                     I.simulate_channels(P, V, M, depth)
+
+
+def test_pipeline_engine_streams_deadlock_free_on_rccl_layout():
+    """Stream-level replay of the engine's host issue order under RCCL semantics (one
+    ordered stream per rank per communicator, comm streams fenced on compute): with one
+    2-rank communicator per directed stage pair (the mesh layout) AFAB, 1F1B and
+    interleaved 1F1B complete for P 2-8 and depth 1-3; the round-3 layout (one
+    whole-pipeline communicator per direction) deadlocks at P >= 3 with receives
+    posted two ahead, which the replay must detect."""
+    from scaletorch_amd.parallel import interleaved as I
+
+    for sched in ("afab", "1f1b", "interleaved"):
+        for P in (2, 3, 4, 8):
+            for V in ((1, 2, 3) if sched == "interleaved" else (1,)):
+                for M in (P, 2 * P, 4 * P):
+                    for depth in (1, 2, 3):
+                        I.simulate_streams(I.engine_programs(P, V, M, sched, depth, I.channel_layout))
+    for sched in ("1f1b", "interleaved"):
+        with pytest.raises(AssertionError, match="deadlock"):
+            I.simulate_streams(I.engine_programs(3, 1, 6, sched, 2, I.shared_layout))
+    I.simulate_streams(I.engine_programs(2, 1, 4, "1f1b", 2, I.shared_layout))  # pp = 2 was safe
+
+
+def test_mesh_pp_channels_are_two_rank_directed():
+    """Every pipeline channel a rank holds is a distinct 2-rank group of (sender,
+    receiver) stages, fwd i: i -> i+1 and bwd i: i+1 -> i (mod P)."""
+    from unittest import mock
+
+    from scaletorch_amd.parallel.mesh import ProcessGroupManager
+
+    made = []
+
+    def fake_new_group(ranks):
+        made.append(tuple(ranks))
+        return ("g", len(made), tuple(ranks))
+
+    for P, dp, tp in ((3, 2, 2), (2, 1, 1), (4, 1, 2)):
+        world = P * dp * tp
+        for rank in range(world):
+            made.clear()
+            with mock.patch("scaletorch_amd.dist.collectives.is_distributed", return_value=True), \
+                    mock.patch("scaletorch_amd.dist.collectives.new_group", side_effect=fake_new_group):
+                pg = ProcessGroupManager(tp_size=tp, pp_size=P, dp_size=dp, rank=rank, world_size=world)
+            chans = pg.pp_channels
+            r = pg.pp_rank
+            assert set(chans) == {("fwd", r), ("fwd", (r - 1) % P), ("bwd", r), ("bwd", (r - 1) % P)}
+            assert len(set(chans.values())) == 4
+            for (kind, i), g in chans.items():
+                assert len(g[2]) == 2 and rank in g[2]
+                send_stage, recv_stage = (i, (i + 1) % P) if kind == "fwd" else ((i + 1) % P, i)
+                assert sorted((x // tp) % P for x in g[2]) == sorted((send_stage, recv_stage))
 
 
 def test_interleaved_schedules_are_deadlock_free():
