@@ -58,11 +58,11 @@ LAYOUTS = {
     # long context: 32K tokens over 8 CP ranks (4K local), zig-zag chunks, GQA-sized K/V
     "cp8_32k": dict(cp=-1, seq_len=32768, micro_batch_size=1),
     # Mixtral 8x7B: one expert per GPU (EP carved out of DP), dense weights ZeRO-1 over DP x EP;
-    # static-capacity dispatch (2x the mean rows per rank pair: no host sync per layer; at 1.25x
-    # the random-init router overflowed 5 % of the rows, profiles/r03/rehearsal) in 2 chunks, each
-    # chunk's all-to-all overlapping the other's expert GEMMs; dropped rows are reported
-    "mixtral_ep8": dict(model="mixtral-8x7b", ep=-1, micro_batch_size=2, moe_capacity_factor=2.0,
-                        moe_ep_chunks=2),
+    # DROPLESS dispatch with the routing counts on the device (models/moe.py): exchange buffers
+    # sized by the worst case ep*T*min(k, E/ep) rows, so nothing is dropped and -- over the xGMI
+    # push exchange -- no count is read by the host.  mbs 1 x GA 2 (the R_max buffers of mbs 2
+    # would not fit in 288 GB: utils/memory.py), the same 8192 tokens per GPU per step
+    "mixtral_ep8": dict(model="mixtral-8x7b", ep=-1, micro_batch_size=1, grad_acc=2, moe_capacity_factor=0.0),
 }
 
 
@@ -209,7 +209,8 @@ def main() -> int:
                                zero1=args.zero >= 1 and dp * args.cp * args.ep > 1, sequence_parallel=args.sp,
                                gradient_checkpointing=(args.recompute if args.gc else False),
                                grad_reduce_dtype=args.grad_reduce_dtype,
-                               fused_head_chunk=args.head_chunk if args.fused_head else 0)
+                               fused_head_chunk=args.head_chunk if args.fused_head else 0,
+                               moe_dropless=args.moe_capacity_factor == 0 and args.ep > 1)
     if int(os.environ.get("RANK", "0")) == 0:
         print(f"[bench] layout {args.layout}: {args.model} tp{args.tp} pp{args.pp} cp{args.cp} ep{args.ep} dp{dp} "
               f"mbs{args.micro_batch_size} ga{ga} seq{args.seq_len}; HBM estimate {est.summary()}",
@@ -273,11 +274,16 @@ def main() -> int:
     final_loss = tr.reduced_loss(loss)
     tr.health_check()
     moe_info = None
-    if tr.model_config.is_moe:  # capacity dispatch: rows dropped in the last step (read after the timing)
-        drops = [m.dropped_rows for m in tr.raw_model.modules() if getattr(m, "dropped_rows", None) is not None]
-        moe_info = {"capacity_factor": args.moe_capacity_factor, "ep_chunks": args.moe_ep_chunks,
-                    "dropped_rows_last_step": int(sum(int(d) for d in drops)) if drops else 0}
+    if tr.model_config.is_moe:  # EP dispatch counters of the last step (device values, read after the timing)
+        layers = [m for m in tr.raw_model.modules() if getattr(m, "dropped_rows", None) is not None]
+        sent = [m.ep_rows_sent for m in layers if getattr(m, "ep_rows_sent", None) is not None]
+        from scaletorch_amd.models.moe import EP_TRANSPORT
 
+        moe_info = {"capacity_factor": args.moe_capacity_factor, "ep_chunks": args.moe_ep_chunks,
+                    "dispatch": "capacity" if args.moe_capacity_factor > 0 else "dropless",
+                    "dropped_rows_last_step": int(sum(int(m.dropped_rows) for m in layers)) if layers else 0,
+                    "rows_sent_off_rank_last_micro_batch": int(sum(int(x) for x in sent)) if sent else None,
+                    "ep_transport": dict(EP_TRANSPORT) if args.ep > 1 else None}
     tokens_per_step = tr.tokens_per_step  # global: dp*ep*mbs*ga*seq
     tok_s = tokens_per_step * args.steps / elapsed
     cfg = tr.model_config

@@ -24,8 +24,8 @@ int st_rmsnorm_bwd_nwaves(int rows);
 int st_rope_inplace(void* x, const float* cos_t, const float* sin_t, const int64_t* pos, int B,
                     int S, int NH, int D, int64_t sB, int64_t sS, int64_t sH, int pos_offset,
                     int backward, int64_t max_pos, hipStream_t st);
-int st_swiglu_fwd(const void* gu, void* out, int64_t N, int64_t I, hipStream_t st);
-int st_swiglu_bwd(const void* dout, const void* gu, void* dgu, int64_t N, int64_t I,
+int st_swiglu_fwd(const void* gu, void* out, int64_t N, int64_t I, const int* nvalid, hipStream_t st);
+int st_swiglu_bwd(const void* dout, const void* gu, void* dgu, int64_t N, int64_t I, const int* nvalid,
                   hipStream_t st);
 int st_adamw_step(float* master, float* m, float* v, const void* g, int g_is_bf16, void* p,
                   const float* clip, int64_t n, float lr, float b1, float b2, float eps, float wd,
@@ -65,6 +65,9 @@ int64_t st_grouped_gemm_slots(int T, int G);
 int st_grouped_gemm_bm();
 int st_grouped_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t strideW, void* Y, int64_t ldy,
                     const int* offs, const int* tile_end, int T, int G, int N, int K, int wn, hipStream_t st);
+int st_grouped_gemm_ex(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t strideW, void* Y,
+                       int64_t ldy, const int* offs, const int* tile_end, int T, int G, int N, int K, int wn,
+                       int epi, void* Y2, int64_t ld2, hipStream_t st);
 int st_xgmi_header_bytes();
 int st_xgmi_max_ranks();
 int64_t st_xgmi_create(int rank, int world, int64_t cap, int64_t epoch_base);
@@ -80,6 +83,12 @@ int st_xgmi_collective_sim(const int64_t* ids, const void* const* ins, void* con
 int st_xgmi_all_reduce_sim(const int64_t* ids, const void* const* ins, void* const* outs, int world, int64_t n,
                            int dtype, int mode, int blocks, hipStream_t st);
 int st_xgmi_error(int64_t id);
+int st_xgmi_ep_exchange(int64_t id, const void* in, void* out, const int* M, int E, int El, int64_t row_elems,
+                        int64_t in_rows, int64_t out_rows, int64_t area_rows_needed, int dtype, int dir, int blocks,
+                        hipStream_t st);
+int st_xgmi_ep_exchange_sim(const int64_t* ids, const void* const* ins, void* const* outs, const int* M, int world,
+                            int E, int El, int64_t row_elems, int64_t in_rows, int64_t out_rows,
+                            int64_t area_rows_needed, int dtype, int dir, int blocks, hipStream_t st);
 int st_xgmi_set_timeout(int64_t id, double seconds);
 int st_xgmi_world(int64_t id);
 int st_xgmi_destroy(int64_t id);
@@ -212,7 +221,15 @@ void rope_(at::Tensor x, const at::Tensor& cos_t, const at::Tensor& sin_t,
 }
 
 // ---------------------------------------------------------------- SwiGLU
-at::Tensor swiglu_fwd(const at::Tensor& gu) {
+// nvalid (optional int32 device scalar view, e.g. offs[-1:]): rows at or past it are skipped
+static const int* nvalid_ptr(const c10::optional<at::Tensor>& nv, const at::Tensor& ref) {
+  if (!nv.has_value() || !nv->defined()) return nullptr;
+  TORCH_CHECK(nv->scalar_type() == at::kInt && nv->numel() >= 1 && nv->is_cuda() && nv->device() == ref.device(),
+              "swiglu: nvalid must be an int32 tensor on the same GPU");
+  return nv->data_ptr<int>();
+}
+
+at::Tensor swiglu_fwd(const at::Tensor& gu, const c10::optional<at::Tensor>& nvalid) {
   check_bf16_cuda(gu, "gate_up");
   TORCH_CHECK(gu.is_contiguous() && gu.size(-1) % 16 == 0, "swiglu: [.., 2I] contiguous, I%8==0");
   const int64_t I = gu.size(-1) / 2, N = gu.numel() / gu.size(-1);
@@ -220,12 +237,12 @@ at::Tensor swiglu_fwd(const at::Tensor& gu) {
   sizes.back() = I;
   c10::hip::HIPGuardMasqueradingAsCUDA g(gu.device());
   auto out = at::empty(sizes, gu.options());
-  int rc = st_swiglu_fwd(gu.data_ptr(), out.data_ptr(), N, I, cur_stream());
+  int rc = st_swiglu_fwd(gu.data_ptr(), out.data_ptr(), N, I, nvalid_ptr(nvalid, gu), cur_stream());
   ST_CHECK_RC(rc, "swiglu_fwd");
   return out;
 }
 
-at::Tensor swiglu_bwd(const at::Tensor& dout, const at::Tensor& gu) {
+at::Tensor swiglu_bwd(const at::Tensor& dout, const at::Tensor& gu, const c10::optional<at::Tensor>& nvalid) {
   check_bf16_cuda(dout, "dout");
   check_bf16_cuda(gu, "gate_up");
   TORCH_CHECK(gu.is_contiguous() && dout.is_contiguous(), "swiglu_bwd: contiguous inputs");
@@ -233,7 +250,8 @@ at::Tensor swiglu_bwd(const at::Tensor& dout, const at::Tensor& gu) {
   TORCH_CHECK(dout.numel() == N * I, "swiglu_bwd: dout shape");
   c10::hip::HIPGuardMasqueradingAsCUDA g(gu.device());
   auto dgu = at::empty_like(gu);
-  int rc = st_swiglu_bwd(dout.data_ptr(), gu.data_ptr(), dgu.data_ptr(), N, I, cur_stream());
+  int rc = st_swiglu_bwd(dout.data_ptr(), gu.data_ptr(), dgu.data_ptr(), N, I, nvalid_ptr(nvalid, gu),
+                         cur_stream());
   ST_CHECK_RC(rc, "swiglu_bwd");
   return dgu;
 }
@@ -423,6 +441,64 @@ at::Tensor grouped_gemm(const at::Tensor& x, const at::Tensor& w, const at::Tens
   return y;
 }
 
+// Grouped gate|up GEMM with the SwiGLU epilogue: w [G, 2I, K]; returns {gu [T, 2I], a [T, I]}
+// (rows past offs[G-1] unwritten), or {} when the kernel does not take the shape.
+std::vector<at::Tensor> grouped_gemm_swiglu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& offs) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "w");
+  check_same_gpu(w, x, "w");
+  check_same_gpu(offs, x, "offs");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 3 && w.size(2) == x.size(1) && w.size(1) % 2 == 0,
+              "grouped_gemm_swiglu: x [T, K], w [G, 2I, K]");
+  TORCH_CHECK(offs.scalar_type() == at::kInt && offs.dim() == 1 && offs.is_contiguous() && offs.size(0) == w.size(0),
+              "grouped_gemm_swiglu: offs int32 [G]");
+  const int64_t T = x.size(0), K = x.size(1), G = w.size(0), N = w.size(1), I = N / 2;
+  if (x.stride(1) != 1 || !w.is_contiguous() || T == 0 || T > INT32_MAX) return {};
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  const int bm = st_grouped_gemm_bm();
+  at::Tensor counts = at::diff(offs, 1, 0, at::zeros({1}, offs.options()));
+  at::Tensor tile_end = at::cumsum(at::floor_divide(counts + (bm - 1), bm), 0, at::kInt);
+  at::Tensor gu = at::empty({T, N}, x.options());
+  at::Tensor a = at::empty({T, I}, x.options());
+  int rc = st_grouped_gemm_ex(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(1), w.stride(0), gu.data_ptr(), N,
+                              offs.data_ptr<int>(), tile_end.data_ptr<int>(), (int)T, (int)G, (int)N, (int)K, 0, 1,
+                              a.data_ptr(), I, cur_stream());
+  if (rc == -2) return {};
+  ST_CHECK_RC(rc, "grouped_gemm_swiglu");
+  return {gu, a};
+}
+
+// Down-projection data gradient with the SwiGLU backward epilogue: w [G, K=h, I]
+// (dy @ w[g]), gu [T, 2I] saved by the forward; returns dgu [T, 2I] (undefined when the
+// kernel does not take the shape).
+at::Tensor grouped_gemm_dswiglu(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& offs,
+                                const at::Tensor& gu) {
+  check_bf16_cuda(dy, "dy");
+  check_bf16_cuda(w, "w");
+  check_bf16_cuda(gu, "gu");
+  check_same_gpu(w, dy, "w");
+  check_same_gpu(gu, dy, "gu");
+  check_same_gpu(offs, dy, "offs");
+  TORCH_CHECK(dy.dim() == 2 && w.dim() == 3 && w.size(1) == dy.size(1), "grouped_gemm_dswiglu: dy [T, K], w [G, K, I]");
+  const int64_t T = dy.size(0), K = dy.size(1), G = w.size(0), I = w.size(2);
+  TORCH_CHECK(gu.dim() == 2 && gu.size(0) == T && gu.size(1) == 2 * I && gu.is_contiguous(),
+              "grouped_gemm_dswiglu: gu [T, 2I] contiguous");
+  TORCH_CHECK(offs.scalar_type() == at::kInt && offs.dim() == 1 && offs.is_contiguous() && offs.size(0) == G,
+              "grouped_gemm_dswiglu: offs int32 [G]");
+  if (dy.stride(1) != 1 || !w.is_contiguous() || T == 0 || T > INT32_MAX) return at::Tensor();
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
+  const int bm = st_grouped_gemm_bm();
+  at::Tensor counts = at::diff(offs, 1, 0, at::zeros({1}, offs.options()));
+  at::Tensor tile_end = at::cumsum(at::floor_divide(counts + (bm - 1), bm), 0, at::kInt);
+  at::Tensor dgu = at::empty({T, 2 * I}, dy.options());
+  int rc = st_grouped_gemm_ex(dy.data_ptr(), dy.stride(0), w.data_ptr(), w.stride(1), w.stride(0), dgu.data_ptr(),
+                              2 * I, offs.data_ptr<int>(), tile_end.data_ptr<int>(), (int)T, (int)G, (int)I, (int)K,
+                              1, 2, gu.data_ptr(), 2 * I, cur_stream());
+  if (rc == -2) return at::Tensor();
+  ST_CHECK_RC(rc, "grouped_gemm_dswiglu");
+  return dgu;
+}
+
 // ---------------------------------------------------------------- xGMI all-reduce
 // Stateful helpers around csrc/xgmi_allreduce.hip (catch-all kernels: most take no tensor).
 int64_t xgmi_create(int64_t rank, int64_t world, int64_t cap, int64_t epoch_base) {
@@ -533,6 +609,53 @@ void xgmi_all_reduce_sim(std::vector<int64_t> ids, std::vector<at::Tensor> ins, 
                                   ins[0].scalar_type() == at::kBFloat16 ? 0 : 1, (int)mode, (int)blocks,
                                   cur_stream());
   TORCH_CHECK(rc == 0, "xgmi_all_reduce_sim failed (", rc, ")");
+}
+// Expert-parallel exchange with device counts M [world, E] int32 (csrc/xgmi_allreduce.hip):
+// dir 0 dispatch (in: this rank's rows sorted by global expert -> out: its experts' rows,
+// expert-major, out.size(0) = the host bound R_max), dir 1 combine (the reverse).
+static void check_ep_args(const at::Tensor& inp, const at::Tensor& out, const at::Tensor& M, int64_t world) {
+  TORCH_CHECK(inp.is_cuda() && out.is_cuda() && inp.device() == out.device(), "xgmi_ep_exchange: GPU tensors");
+  TORCH_CHECK(inp.dim() == 2 && out.dim() == 2 && inp.size(1) == out.size(1) && inp.is_contiguous() &&
+                  out.is_contiguous() && inp.scalar_type() == out.scalar_type(),
+              "xgmi_ep_exchange: contiguous [rows, h] in / out of one dtype");
+  TORCH_CHECK(inp.scalar_type() == at::kBFloat16 || inp.scalar_type() == at::kFloat, "xgmi: bf16 or fp32");
+  TORCH_CHECK(inp.size(1) % 8 == 0, "xgmi_ep_exchange: row width must be a multiple of 8");
+  TORCH_CHECK(M.is_cuda() && M.device() == inp.device() && M.scalar_type() == at::kInt && M.dim() == 2 &&
+                  M.size(0) == world && M.is_contiguous(),
+              "xgmi_ep_exchange: M int32 [world, E] on the same GPU");
+  TORCH_CHECK(inp.data_ptr() != out.data_ptr(), "xgmi_ep_exchange: out-of-place only");
+}
+void xgmi_ep_exchange(int64_t id, const at::Tensor& inp, at::Tensor out, const at::Tensor& M, int64_t El,
+                      int64_t dir, int64_t area_rows, int64_t blocks) {
+  const int world = st_xgmi_world(id);
+  TORCH_CHECK(world > 0, "xgmi: unknown communicator");
+  check_ep_args(inp, out, M, world);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(inp.device());
+  int rc = st_xgmi_ep_exchange(id, inp.data_ptr(), out.data_ptr(), M.data_ptr<int>(), (int)M.size(1), (int)El,
+                               inp.size(1), inp.size(0), out.size(0), area_rows,
+                               inp.scalar_type() == at::kBFloat16 ? 0 : 1, (int)dir, (int)blocks, cur_stream());
+  TORCH_CHECK(rc == 0, "xgmi_ep_exchange failed (", rc, "): E = El x world <= 256, rows must fit the buffer");
+}
+void xgmi_ep_exchange_sim(std::vector<int64_t> ids, std::vector<at::Tensor> ins, std::vector<at::Tensor> outs,
+                          const at::Tensor& M, int64_t El, int64_t dir, int64_t area_rows, int64_t blocks) {
+  const size_t w = ids.size();
+  TORCH_CHECK(w >= 1 && ins.size() == w && outs.size() == w, "xgmi_ep_exchange_sim: one in/out per rank");
+  std::vector<const void*> ip(w);
+  std::vector<void*> op(w);
+  for (size_t r = 0; r < w; ++r) {
+    check_ep_args(ins[r], outs[r], M, (int64_t)w);
+    TORCH_CHECK(ins[r].sizes() == ins[0].sizes() && outs[r].sizes() == outs[0].sizes() &&
+                    ins[r].scalar_type() == ins[0].scalar_type() && ins[r].device() == ins[0].device(),
+                "xgmi_ep_exchange_sim: matching tensors on every rank");
+    ip[r] = ins[r].data_ptr();
+    op[r] = outs[r].data_ptr();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(ins[0].device());
+  int rc = st_xgmi_ep_exchange_sim(ids.data(), ip.data(), op.data(), M.data_ptr<int>(), (int)w, (int)M.size(1),
+                                   (int)El, ins[0].size(1), ins[0].size(0), outs[0].size(0), area_rows,
+                                   ins[0].scalar_type() == at::kBFloat16 ? 0 : 1, (int)dir, (int)blocks,
+                                   cur_stream());
+  TORCH_CHECK(rc == 0, "xgmi_ep_exchange_sim failed (", rc, ")");
 }
 int64_t xgmi_error(int64_t id) { return st_xgmi_error(id); }
 void xgmi_destroy(int64_t id) { st_xgmi_destroy(id); }
@@ -862,8 +985,8 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor? residual, Tensor weight, float eps) -> Tensor[]");
   m.def("rmsnorm_bwd(Tensor dy, Tensor s, Tensor weight, Tensor rstd, Tensor? dres, Tensor(a!) dw_accum) -> Tensor");
   m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, Tensor? pos, int pos_offset, bool backward) -> ()");
-  m.def("swiglu_fwd(Tensor gate_up) -> Tensor");
-  m.def("swiglu_bwd(Tensor dout, Tensor gate_up) -> Tensor");
+  m.def("swiglu_fwd(Tensor gate_up, Tensor? nvalid=None) -> Tensor");
+  m.def("swiglu_bwd(Tensor dout, Tensor gate_up, Tensor? nvalid=None) -> Tensor");
   m.def("adamw_step_(Tensor(a!) master, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor grad, Tensor(d!)? param, Tensor? clip_coef, float lr, float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
   m.def("sumsq_(Tensor g, Tensor(a!) out) -> ()");
   m.def("transpose_(Tensor src, Tensor(a!) dst) -> ()");
@@ -877,6 +1000,8 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("wgrad_gemm_(Tensor(a!) out, Tensor dy, Tensor x, int beta, int variant=0) -> bool");
   m.def("wgrad_grouped_(Tensor(a!) out, Tensor dy, Tensor x, Tensor offs, int beta) -> bool");
   m.def("grouped_gemm(Tensor x, Tensor w, Tensor offs, bool wn) -> Tensor");
+  m.def("grouped_gemm_swiglu(Tensor x, Tensor w, Tensor offs) -> Tensor[]");
+  m.def("grouped_gemm_dswiglu(Tensor dy, Tensor w, Tensor offs, Tensor gu) -> Tensor");
   m.def("xgmi_create(int rank, int world, int cap, int epoch_base) -> int", &xgmi_create);
   m.def("xgmi_handle(int id) -> Tensor", &xgmi_handle);
   m.def("xgmi_open(int id, int r, Tensor handle) -> ()", &xgmi_open);
@@ -886,6 +1011,10 @@ TORCH_LIBRARY(st_amd, m) {
         &xgmi_all_reduce_sim);
   m.def("xgmi_pair(int id, Tensor inp, Tensor(a!) out, int mode, int partner, int blocks) -> ()", &xgmi_pair);
   m.def("xgmi_error(int id) -> int", &xgmi_error);
+  m.def("xgmi_ep_exchange(int id, Tensor inp, Tensor(a!) out, Tensor M, int El, int dir, int area_rows, int blocks) -> ()",
+        &xgmi_ep_exchange);
+  m.def("xgmi_ep_exchange_sim(int[] ids, Tensor[] ins, Tensor(a!)[] outs, Tensor M, int El, int dir, int area_rows, int blocks) -> ()",
+        &xgmi_ep_exchange_sim);
   m.def("xgmi_set_timeout(int id, float seconds) -> ()", &xgmi_set_timeout);
   m.def("xgmi_destroy(int id) -> ()", &xgmi_destroy);
   m.def("qknorm_rope_fwd_(Tensor(a!) qkv, Tensor wq, Tensor wk, Tensor cos, Tensor sin, Tensor? pos, int H, int Hkv, float eps) -> Tensor[]");
@@ -913,6 +1042,8 @@ TORCH_LIBRARY_IMPL(st_amd, CUDA, m) {
   m.impl("wgrad_gemm_", &wgrad_gemm_);
   m.impl("wgrad_grouped_", &wgrad_grouped_);
   m.impl("grouped_gemm", &grouped_gemm);
+  m.impl("grouped_gemm_swiglu", &grouped_gemm_swiglu);
+  m.impl("grouped_gemm_dswiglu", &grouped_gemm_dswiglu);
   m.impl("qknorm_rope_fwd_", &qknorm_rope_fwd_);
   m.impl("qknorm_rope_bwd_", &qknorm_rope_bwd_);
 }

@@ -105,13 +105,26 @@ ST_DEVICE int find_group(const int* __restrict__ tile_end, int G, int s) {
   return lo;
 }
 
-template <int BN, bool WN, bool SPREAD = false>
+// EPI (epilogue): 0 = Y = X op(W);
+//   1 = SwiGLU forward (WT, BN = 256): W[g] = [gate rows 0..I | up rows I..2I]; N-tile t
+//       computes gate columns [128 t, 128 t + 128) AND the matching up columns (the B
+//       image's rows are drawn from both halves: wave w's 64 columns = 32 gate + the 32
+//       up columns of the same features, so gate and up of one feature meet in ONE
+//       lane's registers); writes gu (Y, [rows, 2I]) for the backward and
+//       a = silu(gate) * up (Y2, [rows, I]) straight from the fp32 accumulators;
+//   2 = SwiGLU backward (WN): the tile is da = dY W_down[g] ([rows, I]); the epilogue
+//       reads gate / up from gu (Y2, [rows, 2I]) and writes dgu = [d gate | d up] (Y,
+//       [rows, 2I]) -- the separate swiglu_bwd pass and the da round-trip disappear.
+template <int BN, bool WN, bool SPREAD = false, int EPI = 0>
 __global__ __launch_bounds__(NT, 1) void grouped_gemm_kernel(const bf16_t* __restrict__ X, int64_t ldx,
                                                              const bf16_t* __restrict__ W, int64_t ldw,
                                                              int64_t strideW, bf16_t* __restrict__ Y, int64_t ldy,
                                                              const int* __restrict__ offs,
                                                              const int* __restrict__ tile_end, int G, int N,
-                                                             int K, int order) {
+                                                             int K, int order, bf16_t* __restrict__ Y2,
+                                                             int64_t ld2, int I) {
+  static_assert(EPI != 1 || (BN == 256 && !WN), "SwiGLU forward epilogue: WT layout, 256-wide tiles");
+  static_assert(EPI != 2 || WN, "SwiGLU backward epilogue: WN layout");
   using Gm = Geo<BN, WN>;
   __shared__ __attribute__((aligned(16))) char smem_raw[2 * Gm::STAGE];
   lds_t* smem = (lds_t*)smem_raw;
@@ -147,9 +160,10 @@ __global__ __launch_bounds__(NT, 1) void grouped_gemm_kernel(const bf16_t* __res
   // row, so DMA of rows past it (next group / past T) reads zeros
   const bf16_t* xb = X + (int64_t)row0 * ldx;
   const i32x4 rsX = make_rsrc(xb, (uint32_t)(((int64_t)(rows - 1) * ldx + K) * 2));
-  const bf16_t* wb = W + (int64_t)g * strideW + (WN ? (int64_t)n0 : (int64_t)n0 * ldw);
-  const i32x4 rsW = make_rsrc(wb, (uint32_t)(WN ? ((int64_t)(K - 1) * ldw + BN) * 2
-                                               : ((int64_t)(BN - 1) * ldw + K) * 2));
+  const bf16_t* wb = W + (int64_t)g * strideW + (EPI == 1 ? 0 : (WN ? (int64_t)n0 : (int64_t)n0 * ldw));
+  const i32x4 rsW = make_rsrc(wb, (uint32_t)(EPI == 1 ? ((int64_t)(N - 1) * ldw + K) * 2
+                                            : WN ? ((int64_t)(K - 1) * ldw + BN) * 2
+                                                 : ((int64_t)(BN - 1) * ldw + K) * 2));
   const uint32_t sX = (uint32_t)(ldx * 2), sW = (uint32_t)(ldw * 2);
 
   // ---- DMA plan: every 1-KiB piece is 8 rows x 128 B (8 rows of 64 k, or 8 k-rows of 64
@@ -163,7 +177,12 @@ __global__ __launch_bounds__(NT, 1) void grouped_gemm_kernel(const bf16_t* __res
     const int q = isA[i] ? p : p - Gm::A_PIECES;
     const int pr = q * 8 + (lane >> 3), pc = lane & 7;  // row of the image, physical 16-B chunk
     if (isA[i] || !WN) {
-      voff[i] = (uint32_t)pr * (isA[i] ? sX : sW) + (uint32_t)((pc ^ rsw(pr)) * 16);
+      int src = pr;  // EPI 1: image row pr -> gate / up row of the weight (see the EPI note)
+      if (EPI == 1 && !isA[i]) {
+        const int wb64 = pr >> 6, w = pr & 63;
+        src = (w < 32 ? 0 : I) + 128 * nt + 32 * wb64 + (w & 31);
+      }
+      voff[i] = (uint32_t)src * (isA[i] ? sX : sW) + (uint32_t)((pc ^ rsw(pr)) * 16);
     } else {  // column image: block cb = q / 8, k-row kr, logical 32-B slot
       const int cb = q >> 3, kr = (q & 7) * 8 + (lane >> 3);
       const int logical = (((pc >> 1) ^ csw(kr)) << 1) | (pc & 1);
@@ -273,17 +292,61 @@ __global__ __launch_bounds__(NT, 1) void grouped_gemm_kernel(const bf16_t* __res
 
   // ---- epilogue: 16x16 C/D row = 4 (lane>>4) + reg (M), column = lane & 15 (N); rows past
   // the group's end are not stored
-  bf16_t* yb = Y + (int64_t)row0 * ldy + n0 + bnn + (lane & 15);
+  if constexpr (EPI == 1) {
+    static_assert(Gm::FN == 4, "32 gate + 32 up columns per wave");
+    const int cb = 128 * nt + 32 * wn + (lane & 15);  // gate feature of fragment 0
+    bf16_t* gub = Y + (int64_t)row0 * ldy;
+    bf16_t* ab = Y2 + (int64_t)row0 * ld2;
 #pragma unroll
-  for (int i = 0; i < Gm::FM; ++i)
+    for (int i = 0; i < Gm::FM; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = am + 16 * i + 4 * gq + r;
-      if (m < rows) {
+      for (int r = 0; r < 4; ++r) {
+        const int m = am + 16 * i + 4 * gq + r;
+        if (m < rows) {
 #pragma unroll
-        for (int j = 0; j < Gm::FN; ++j) yb[(int64_t)m * ldy + 16 * j] = f2bf(acc[i][j][r]);
+          for (int j = 0; j < 2; ++j) {
+            const float gv = acc[i][j][r], uv = acc[i][j + 2][r];
+            const int c = cb + 16 * j;
+            gub[(int64_t)m * ldy + c] = f2bf(gv);
+            gub[(int64_t)m * ldy + I + c] = f2bf(uv);
+            ab[(int64_t)m * ld2 + c] = f2bf(silu(gv) * uv);
+          }
+        }
       }
-    }
+  } else if constexpr (EPI == 2) {
+    const int cb = n0 + bnn + (lane & 15);
+    const bf16_t* gub = Y2 + (int64_t)row0 * ld2;
+    bf16_t* db = Y + (int64_t)row0 * ldy;
+#pragma unroll
+    for (int i = 0; i < Gm::FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = am + 16 * i + 4 * gq + r;
+        if (m < rows) {
+#pragma unroll
+          for (int j = 0; j < Gm::FN; ++j) {
+            const int c = cb + 16 * j;
+            const float gv = bf2f(gub[(int64_t)m * ld2 + c]), uv = bf2f(gub[(int64_t)m * ld2 + I + c]);
+            const float d = acc[i][j][r];
+            const float sg = 1.f / (1.f + __expf(-gv)), sl = gv * sg;
+            db[(int64_t)m * ldy + c] = f2bf(d * uv * (sg + sl * (1.f - sg)));
+            db[(int64_t)m * ldy + I + c] = f2bf(d * sl);
+          }
+        }
+      }
+  } else {
+    bf16_t* yb = Y + (int64_t)row0 * ldy + n0 + bnn + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < Gm::FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = am + 16 * i + 4 * gq + r;
+        if (m < rows) {
+#pragma unroll
+          for (int j = 0; j < Gm::FN; ++j) yb[(int64_t)m * ldy + 16 * j] = f2bf(acc[i][j][r]);
+        }
+      }
+  }
 }
 
 }  // namespace
@@ -296,43 +359,69 @@ int st_grouped_gemm_bm() { return BM; }
 
 // Y[T, N] (bf16, rows of each group) = X[T, K] @ (wn ? W[g] : W[g]^T); W[g] is [K][N] when
 // wn, else [N][K].  offs / tile_end: int32 [G] device (tile_end = inclusive prefix of
-// ceil(n_g / 256)).  0 on success, -2 unsupported shape.
-int st_grouped_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t strideW, void* Y, int64_t ldy,
-                    const int* offs, const int* tile_end, int T, int G, int N, int K, int wn, hipStream_t st) {
+// ceil(n_g / 256)).  epi 1: SwiGLU forward (wn = 0, N = 2I, I % 128 == 0): Y = gu [T, 2I],
+// Y2 = a [T, I]; epi 2: SwiGLU backward (wn = 1, N = I): Y = dgu [T, 2I], Y2 = gu [T, 2I]
+// (read).  0 on success, -2 unsupported shape.
+int st_grouped_gemm_ex(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t strideW, void* Y,
+                       int64_t ldy, const int* offs, const int* tile_end, int T, int G, int N, int K, int wn,
+                       int epi, void* Y2, int64_t ld2, hipStream_t st) {
   if (T <= 0 || G <= 0 || N <= 0 || K <= 0) return -2;
   if (K % BK || N % 128) return -2;  // K: whole 64-k tiles
-  if (ldx % 8 || ldw % 8 || ldy % 8 || ldx < K || ldy < N || (wn ? ldw < N : ldw < K)) return -2;
+  if (ldx % 8 || ldw % 8 || ldy % 8 || ldx < K || (wn ? ldw < N : ldw < K)) return -2;
   if (((uintptr_t)X | (uintptr_t)W | (uintptr_t)Y) % 16) return -2;
   if (((int64_t)(T + BM) * ldx) * 2 >= (int64_t)1 << 32) return -2;  // 32-bit buffer offsets
   if ((wn ? (int64_t)K * ldw : (int64_t)N * ldw) * 2 >= (int64_t)1 << 32) return -2;
+  int I = 0;
+  if (epi == 0) {
+    if (ldy < N) return -2;
+  } else if (epi == 1) {
+    I = N / 2;
+    if (wn || N % 256 || I % 128 || !Y2 || ldy < N || ld2 < I || ld2 % 8) return -2;
+  } else if (epi == 2) {
+    I = N;
+    if (!wn || !Y2 || ldy < 2 * I || ld2 < 2 * I || ld2 % 8) return -2;
+  } else {
+    return -2;
+  }
   const int bn = (N % 256 == 0) ? 256 : 128;
   const int64_t grid = st_grouped_gemm_slots(T, G) * (N / bn);
   if (grid >= (1LL << 31)) return -2;
   const bf16_t *x = (const bf16_t*)X, *w = (const bf16_t*)W;
   bf16_t* y = (bf16_t*)Y;
+  bf16_t* y2 = (bf16_t*)Y2;
   // 1: XCD-grouped tile order -- measured 2-19 % SLOWER than slot-major on every MoE and
   // dense shape (profiles/r03/grouped_gemm_order_ab.log): slot-major stays the default
   const char* oe = std::getenv("ST_GMM_ORDER");
   const int order = oe ? std::atoi(oe) : 0;
   // ST_GMM_DMA_SPREAD=1: next-tile DMA pieces interleaved with the MFMAs (A/B)
   const char* se = std::getenv("ST_GMM_DMA_SPREAD");
-  const bool spread = se && std::atoi(se) == 1;
-#define LAUNCH(BNV, WNV)                                                                                        \
-  do {                                                                                                          \
-    if (spread)                                                                                                 \
-      grouped_gemm_kernel<BNV, WNV, true><<<(unsigned)grid, NT, 0, st>>>(x, ldx, w, ldw, strideW, y, ldy, offs, \
-                                                                         tile_end, G, N, K, order);             \
-    else                                                                                                        \
-      grouped_gemm_kernel<BNV, WNV, false><<<(unsigned)grid, NT, 0, st>>>(x, ldx, w, ldw, strideW, y, ldy,      \
-                                                                          offs, tile_end, G, N, K, order);      \
+  const bool spread = se && std::atoi(se) == 1 && epi == 0;
+#define ARGS x, ldx, w, ldw, strideW, y, ldy, offs, tile_end, G, N, K, order, y2, ld2, I
+#define LAUNCH(BNV, WNV)                                                                         \
+  do {                                                                                           \
+    if (spread)                                                                                  \
+      grouped_gemm_kernel<BNV, WNV, true, 0><<<(unsigned)grid, NT, 0, st>>>(ARGS);               \
+    else                                                                                         \
+      grouped_gemm_kernel<BNV, WNV, false, 0><<<(unsigned)grid, NT, 0, st>>>(ARGS);              \
   } while (0)
-  if (bn == 256) {
+  if (epi == 1) {
+    grouped_gemm_kernel<256, false, false, 1><<<(unsigned)grid, NT, 0, st>>>(ARGS);
+  } else if (epi == 2) {
+    if (bn == 256) grouped_gemm_kernel<256, true, false, 2><<<(unsigned)grid, NT, 0, st>>>(ARGS);
+    else grouped_gemm_kernel<128, true, false, 2><<<(unsigned)grid, NT, 0, st>>>(ARGS);
+  } else if (bn == 256) {
     if (wn) LAUNCH(256, true); else LAUNCH(256, false);
   } else {
     if (wn) LAUNCH(128, true); else LAUNCH(128, false);
   }
 #undef LAUNCH
+#undef ARGS
   return (int)hipGetLastError();
+}
+
+int st_grouped_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t strideW, void* Y, int64_t ldy,
+                    const int* offs, const int* tile_end, int T, int G, int N, int K, int wn, hipStream_t st) {
+  return st_grouped_gemm_ex(X, ldx, W, ldw, strideW, Y, ldy, offs, tile_end, T, G, N, K, wn, 0, nullptr, 0, st);
 }
 
 }  // extern "C"

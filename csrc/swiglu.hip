@@ -19,7 +19,8 @@ namespace {
 template <int U>
 __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16_t* __restrict__ gu,
                                                           bf16_t* __restrict__ out, int64_t I8,
-                                                          int64_t N) {
+                                                          int64_t N, const int* __restrict__ nvalid) {
+  if (nvalid) N = min(N, (int64_t)max(0, *nvalid));  // rows past the device count: not touched
   const int64_t c0 = (int64_t)blockIdx.x * (256 * U) + threadIdx.x;
   for (int64_t row = blockIdx.y; row < N; row += gridDim.y) {
     const bf16_t* gp = gu + row * (I8 * 16);
@@ -51,7 +52,8 @@ template <int U>
 __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restrict__ dout,
                                                           const bf16_t* __restrict__ gu,
                                                           bf16_t* __restrict__ dgu, int64_t I8,
-                                                          int64_t N) {
+                                                          int64_t N, const int* __restrict__ nvalid) {
+  if (nvalid) N = min(N, (int64_t)max(0, *nvalid));
   const int64_t c0 = (int64_t)blockIdx.x * (256 * U) + threadIdx.x;
   for (int64_t row = blockIdx.y; row < N; row += gridDim.y) {
     const int64_t base = row * (I8 * 16);
@@ -122,19 +124,21 @@ inline int pick_u(int64_t I8) {
 
 }  // namespace
 
-extern "C" int st_swiglu_fwd(const void* gu, void* out, int64_t N, int64_t I, hipStream_t st) {
+// nvalid (may be null): device int32 row count -- rows at or past it are skipped (the
+// R_max-row expert buffers of the dropless EP dispatch, models/moe.py)
+extern "C" int st_swiglu_fwd(const void* gu, void* out, int64_t N, int64_t I, const int* nvalid, hipStream_t st) {
   if (I % 8 != 0) return -2;
   const int64_t I8 = I / 8;
   if (N == 0 || I8 == 0) return 0;
-  ST_SWIGLU_DISPATCH(swiglu_fwd_kernel, (const bf16_t*)gu, (bf16_t*)out, I8, N)
+  ST_SWIGLU_DISPATCH(swiglu_fwd_kernel, (const bf16_t*)gu, (bf16_t*)out, I8, N, nvalid)
   return (int)hipGetLastError();
 }
 
 extern "C" int st_swiglu_bwd(const void* dout, const void* gu, void* dgu, int64_t N, int64_t I,
-                             hipStream_t st) {
+                             const int* nvalid, hipStream_t st) {
   if (I % 8 != 0) return -2;
   const int64_t I8 = I / 8;
   if (N == 0 || I8 == 0) return 0;
-  ST_SWIGLU_DISPATCH(swiglu_bwd_kernel, (const bf16_t*)dout, (const bf16_t*)gu, (bf16_t*)dgu, I8, N)
+  ST_SWIGLU_DISPATCH(swiglu_bwd_kernel, (const bf16_t*)dout, (const bf16_t*)gu, (bf16_t*)dgu, I8, N, nvalid)
   return (int)hipGetLastError();
 }

@@ -473,6 +473,157 @@ __global__ __launch_bounds__(kThreads) void pair_reducescatter_kernel(Peers P, J
   }
 }
 
+
+// ---- expert-parallel token exchange with DEVICE-SIDE counts (dropless, no host sync).
+// M[s][g] = rows source rank s routes to global expert g (identical on every rank: the
+// [E] count rows are all-gathered first).  Source s holds its rows sorted by global
+// expert ("sorted" layout, P[s][g] = first row of expert g); owner d = g / El holds its
+// local experts' rows EXPERT-MAJOR: expert g's rows = [from source 0 | source 1 | ...],
+// i.e. row (s, i) of expert g sits at q(s, i) = EO[g] + SO[s][g] + (i - P[s][g]) with
+// EO[g] = rows of the owner's earlier experts, SO[s][g] = rows of g from sources < s.
+// dir 0 (dispatch): sorted rows of every source -> expert-major rows of every owner.
+// dir 1 (combine): the reverse.  Block b of every rank moves the rows of block b of each
+// SOURCE's sorted range (a fixed split of that source's rows), so after the per-block
+// handshake block b reads exactly what the peers' block b wrote.  Every index is checked
+// against the area / output sizes the host passed: a count that would overflow sets
+// the error word (2) and is skipped, never written out of bounds.
+constexpr int kMaxExperts = 256;
+struct EpArgs {
+  const int* M;      // [world, E] int32, device
+  int E, El, row8, dir;
+  int64_t in_rows;    // rows of `in`
+  int64_t out_rows;   // rows of `out`
+  int64_t area_rows;  // rows one data area holds
+};
+
+ST_DEVICE int ep_find(const int* Ps, int E, int i) {  // g with Ps[g] <= i < Ps[g + 1]
+  int lo = 0, hi = E - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (Ps[mid] <= i) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void ep_exchange_kernel(Peers P, Jobs J, int world, EpArgs A, int64_t cap,
+                                                               uint32_t epoch) {
+  __shared__ int sP[kMaxRanks][kMaxExperts + 1];
+  __shared__ int sSO[kMaxRanks][kMaxExperts];
+  __shared__ int sEO[kMaxExperts];
+  const Job& jb = J.j[blockIdx.y];
+  const int me = jb.rank;
+  const T* __restrict__ in = (const T*)jb.in;
+  T* __restrict__ out = (T*)jb.out;
+  const int parity = epoch & 1;
+  const int E = A.E, El = A.El, row8 = A.row8;
+  for (int x = threadIdx.x; x < world * E; x += blockDim.x) sSO[x / E][x % E] = max(0, A.M[x]);
+  __syncthreads();
+  if (threadIdx.x < (unsigned)world) {  // P: per-source prefix over experts
+    const int s = threadIdx.x;
+    int acc = 0;
+    for (int g = 0; g < E; ++g) {
+      sP[s][g] = acc;
+      acc += sSO[s][g];
+    }
+    sP[s][E] = acc;
+  }
+  __syncthreads();
+  for (int g = threadIdx.x; g < E; g += blockDim.x) {  // SO: per-expert prefix over sources
+    int acc = 0;
+    for (int s = 0; s < world; ++s) {
+      const int m = sSO[s][g];
+      sSO[s][g] = acc;
+      acc += m;
+    }
+    sEO[g] = acc;  // total rows of expert g (turned into EO below)
+  }
+  __syncthreads();
+  if (threadIdx.x < (unsigned)world) {  // EO: per-owner prefix over its local experts
+    const int d = threadIdx.x;
+    int acc = 0;
+    for (int e = 0; e < El; ++e) {
+      const int tot = sEO[d * El + e];
+      sEO[d * El + e] = acc;
+      acc += tot;
+    }
+  }
+  __syncthreads();
+  const int64_t rowb = (int64_t)row8;  // 8-element vectors per row
+  // block b's share of source s's sorted rows
+  auto range = [&](int s, int64_t& lo, int64_t& hi) {
+    const int64_t Ts = sP[s][E];
+    const int64_t per = (Ts + gridDim.x - 1) / gridDim.x;
+    lo = min(Ts, (int64_t)blockIdx.x * per);
+    hi = min(Ts, lo + per);
+  };
+  auto qpos = [&](int s, int64_t i, int g) -> int64_t { return (int64_t)sEO[g] + sSO[s][g] + (i - sP[s][g]); };
+  const rsrc_t mine = buf_rsrc(P.buf[me], cap);
+  if (A.dir == 0) {
+    // phase 1, as a source: push my block's sorted rows to their owners' areas (expert-major slots)
+    int64_t lo, hi;
+    range(me, lo, hi);
+    for (int64_t v = threadIdx.x; v < (hi - lo) * rowb; v += blockDim.x) {
+      const int64_t i = lo + v / rowb, c = v % rowb;
+      const int g = ep_find(sP[me], E, (int)i);
+      const int64_t q = qpos(me, i, g);
+      if (q >= A.area_rows || i >= A.in_rows) {
+        atomicExch(jb.err, 2);
+        continue;
+      }
+      put8<T>(buf_rsrc(P.buf[g / El], cap), area_off<T>(0, parity, cap, q * rowb + c), in + (i * rowb + c) * 8);
+    }
+    if (!block_barrier(P, me, world, 0, epoch, jb.err, jb.timeout)) return;
+    // phase 2, as the owner: copy out the rows block b of every source wrote into my area
+    for (int s = 0; s < world; ++s) {
+      int64_t a, z;
+      range(s, a, z);
+      a = max(a, (int64_t)sP[s][me * El]);
+      z = min(z, (int64_t)sP[s][(me + 1) * El]);
+      for (int64_t v = threadIdx.x; v < max((int64_t)0, z - a) * rowb; v += blockDim.x) {
+        const int64_t i = a + v / rowb, c = v % rowb;
+        const int64_t q = qpos(s, i, ep_find(sP[s], E, (int)i));
+        if (q >= A.out_rows || q >= A.area_rows) {
+          atomicExch(jb.err, 2);
+          continue;
+        }
+        get8<T>(mine, area_off<T>(0, parity, cap, q * rowb + c), out + (q * rowb + c) * 8);
+      }
+    }
+  } else {
+    // phase 1, as the owner: send every source its rows of my experts (expert-major in -> its sorted slots)
+    for (int s = 0; s < world; ++s) {
+      int64_t a, z;
+      range(s, a, z);
+      a = max(a, (int64_t)sP[s][me * El]);
+      z = min(z, (int64_t)sP[s][(me + 1) * El]);
+      const rsrc_t dst = buf_rsrc(P.buf[s], cap);
+      for (int64_t v = threadIdx.x; v < max((int64_t)0, z - a) * rowb; v += blockDim.x) {
+        const int64_t i = a + v / rowb, c = v % rowb;
+        const int64_t q = qpos(s, i, ep_find(sP[s], E, (int)i));
+        if (i >= A.area_rows || q >= A.in_rows) {
+          atomicExch(jb.err, 2);
+          continue;
+        }
+        put8<T>(dst, area_off<T>(0, parity, cap, i * rowb + c), in + (q * rowb + c) * 8);
+      }
+    }
+    if (!block_barrier(P, me, world, 0, epoch, jb.err, jb.timeout)) return;
+    // phase 2, as a source: my block's sorted rows have arrived in my area
+    int64_t lo, hi;
+    range(me, lo, hi);
+    for (int64_t v = threadIdx.x; v < (hi - lo) * rowb; v += blockDim.x) {
+      const int64_t i = lo + v / rowb, c = v % rowb;
+      if (i >= A.out_rows || i >= A.area_rows) {
+        atomicExch(jb.err, 2);
+        continue;
+      }
+      get8<T>(mine, area_off<T>(0, parity, cap, i * rowb + c), out + (i * rowb + c) * 8);
+    }
+  }
+}
+
 struct Comm {
   int rank = 0, world = 1;
   int64_t cap = 0;  // bytes per data area
@@ -641,6 +792,62 @@ int st_xgmi_pair(int64_t id, const void* in, void* out, int64_t n, int dtype, in
   Jobs J{};
   J.j[0] = Job{in, out, c->rank, c->err, c->timeout, partner};
   return launch(c->peers, J, 1, c->world, n, c->cap, dtype, mode, blocks, ++c->epoch, st);
+}
+
+
+// Expert-parallel exchange (dispatch dir 0 / combine dir 1) with device counts M
+// ([world, E] int32, the same tensor content on every rank); rows of row_elems
+// elements; `in_rows` / `out_rows` = rows of in / out (every rank's, in the simulation); `area_rows_needed` = the most
+// rows one data area must hold (host bound: dispatch R_max, combine this rank's rows).
+int st_xgmi_ep_exchange(int64_t id, const void* in, void* out, const int* M, int E, int El, int64_t row_elems,
+                        int64_t in_rows, int64_t out_rows, int64_t area_rows_needed, int dtype, int dir, int blocks,
+                        hipStream_t st) {
+  Comm* c = get(id);
+  if (!c || E < 1 || E > kMaxExperts || El < 1 || E != El * c->world || row_elems % 8 || (dir != 0 && dir != 1))
+    return -2;
+  const int64_t elt = dtype == 0 ? 2 : 4;
+  const int64_t rowbytes = row_elems * elt;
+  if (area_rows_needed * rowbytes > c->cap || ((uintptr_t)in | (uintptr_t)out) % 16) return -2;
+  for (int r = 0; r < c->world; ++r)
+    if (!c->peers.buf[r]) return -3;
+  if (blocks <= 0 || blocks > kMaxBlocks) blocks = kMaxBlocks;
+  Jobs J{};
+  J.j[0] = Job{in, out, c->rank, c->err, c->timeout};
+  EpArgs A{M, E, El, (int)(row_elems / 8), dir, in_rows, out_rows, c->cap / rowbytes};
+  const dim3 grid(blocks, 1);
+  const uint32_t epoch = ++c->epoch;
+  if (dtype == 0) ep_exchange_kernel<bf16_t><<<grid, kThreads, 0, st>>>(c->peers, J, c->world, A, c->cap, epoch);
+  else ep_exchange_kernel<float><<<grid, kThreads, 0, st>>>(c->peers, J, c->world, A, c->cap, epoch);
+  return (int)hipGetLastError();
+}
+
+// Simulation of the exchange across ids[0..world) in ONE launch (rank = blockIdx.y).
+int st_xgmi_ep_exchange_sim(const int64_t* ids, const void* const* ins, void* const* outs, const int* M, int world,
+                            int E, int El, int64_t row_elems, int64_t in_rows, int64_t out_rows,
+                            int64_t area_rows_needed, int dtype, int dir, int blocks, hipStream_t st) {
+  if (world < 1 || world > kMaxRanks || E < 1 || E > kMaxExperts || El < 1 || E != El * world || row_elems % 8 ||
+      (dir != 0 && dir != 1))
+    return -2;
+  Comm* c0 = get(ids[0]);
+  if (!c0 || c0->world != world) return -2;
+  const int64_t elt = dtype == 0 ? 2 : 4;
+  const int64_t rowbytes = row_elems * elt;
+  if (area_rows_needed * rowbytes > c0->cap) return -2;
+  if (blocks <= 0 || blocks > kMaxBlocks) blocks = kMaxBlocks;
+  Jobs J{};
+  uint32_t epoch = 0;
+  for (int r = 0; r < world; ++r) {
+    Comm* c = get(ids[r]);
+    if (!c || c->rank != r || c->world != world || c->cap != c0->cap) return -2;
+    if (((uintptr_t)ins[r] | (uintptr_t)outs[r]) % 16) return -2;
+    J.j[r] = Job{ins[r], outs[r], r, c->err, c->timeout};
+    epoch = ++c->epoch;
+  }
+  EpArgs A{M, E, El, (int)(row_elems / 8), dir, in_rows, out_rows, c0->cap / rowbytes};
+  const dim3 grid(blocks, world);
+  if (dtype == 0) ep_exchange_kernel<bf16_t><<<grid, kThreads, 0, st>>>(c0->peers, J, world, A, c0->cap, epoch);
+  else ep_exchange_kernel<float><<<grid, kThreads, 0, st>>>(c0->peers, J, world, A, c0->cap, epoch);
+  return (int)hipGetLastError();
 }
 
 int st_xgmi_world(int64_t id) {

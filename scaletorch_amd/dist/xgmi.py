@@ -94,7 +94,8 @@ class XgmiAllReduce:
             raise ValueError("xgmi all-reduce spans at most the 8 GPUs of one node")
         where = [None] * self.world
         dist.all_gather_object(where, (socket.gethostname(), torch.cuda.current_device()), group=group)
-        if len({h for h, _ in where}) != 1 or len({d for _, d in where}) != self.world:
+        shared_ok = os.environ.get("ST_GPU_OVERSUBSCRIBE", "0") == "1"  # 1-GPU multi-rank rehearsals / tests
+        if len({h for h, _ in where}) != 1 or (len({d for _, d in where}) != self.world and not shared_ok):
             raise ValueError(f"xgmi all-reduce needs one GPU per rank on one node, got {where}")
         self.id = int(_ops().xgmi_create(self.rank, self.world, self.cap, self._next_base()))
         _ops().xgmi_set_timeout(self.id, self.timeout_s)
@@ -175,6 +176,42 @@ class XgmiAllReduce:
         _ops().xgmi_all_reduce(self.id, t, out, _MODES["all_to_all"],
                                _blocks_for(t.numel() * t.element_size() // self.world))
         return out
+
+    # ---- expert-parallel exchange with device-side counts (dropless, no host sync)
+    def ep_counts(self, counts: torch.Tensor) -> torch.Tensor:
+        """All-gather this rank's per-expert row counts (int32 [E], device) into the
+        [world, E] matrix every rank needs for the exchange -- a bitwise copy through the
+        all-gather kernel (int32 viewed as fp32, padded to 8 words)."""
+        E = counts.numel()
+        E8 = (E + 7) // 8 * 8
+        src = torch.zeros(E8, dtype=torch.int32, device=counts.device)
+        src[:E] = counts.to(torch.int32)
+        out = torch.empty(self.world * E8, dtype=torch.int32, device=counts.device)
+        _ops().xgmi_all_reduce(self.id, src.view(torch.float32), out.view(torch.float32), _MODES["all_gather"],
+                               _blocks_for(E8 * 4))
+        return out.view(self.world, E8)[:, :E].contiguous()
+
+    def ep_fits(self, rows: int, t: torch.Tensor) -> bool:
+        """``rows`` rows of ``t``'s width fit one data area (the host bound of an exchange)."""
+        return (t.is_cuda and t.dtype in (torch.bfloat16, torch.float32) and t.dim() == 2 and t.shape[1] % 8 == 0
+                and rows * t.shape[1] * t.element_size() <= self.cap)
+
+    def ep_exchange(self, x: torch.Tensor, M: torch.Tensor, El: int, direction: int, out_rows: int,
+                    area_rows: int) -> torch.Tensor:
+        """Dispatch (direction 0: ``x`` = this rank's rows sorted by global expert ->
+        [out_rows, h] of its local experts' rows, expert-major, the first sum(M[:, mine])
+        rows valid) or combine (direction 1: the reverse, out_rows = this rank's sorted
+        rows).  ``M`` [world, E] int32 device counts (``ep_counts``); ``area_rows`` the
+        host bound of rows landing in one rank's buffer.  No host sync."""
+        out = torch.empty(out_rows, x.shape[1], dtype=x.dtype, device=x.device)
+        _ops().xgmi_ep_exchange(self.id, x.contiguous(), out, M, El, direction, area_rows, 0)
+        return out
+
+    @staticmethod
+    def ep_exchange_sim(comms, xs, M, El: int, direction: int, out_rows: int, area_rows: int):
+        outs = [torch.empty(out_rows, x.shape[1], dtype=x.dtype, device=x.device) for x in xs]
+        _ops().xgmi_ep_exchange_sim([c.id for c in comms], xs, outs, M, El, direction, area_rows, 0)
+        return outs
 
     def _pair_ok(self, n_elems: int, t: torch.Tensor) -> bool:
         # a relay holds a path's share of the message in a slot of cap / 8 bytes

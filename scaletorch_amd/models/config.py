@@ -166,6 +166,15 @@ _REGISTRY: dict[str, dict] = {
                      moe_intermediate_size=128, num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2,
                      head_dim=64, max_position_embeddings=1024, rms_norm_eps=1e-6, rope_theta=1000000.0,
                      qk_norm=True, num_experts=8, num_experts_per_tok=2, init="normal"),
+    # 8 query / 8 KV heads: every TP size of the reference's 8-device table (scripts/bench_reference_rows_8gpu.py --smoke)
+    "tiny-qwen3-8h": dict(model_type="qwen3", vocab_size=512, hidden_size=256, intermediate_size=512,
+                          num_hidden_layers=2, num_attention_heads=8, num_key_value_heads=8, head_dim=32,
+                          max_position_embeddings=1024, rms_norm_eps=1e-6, rope_theta=1000000.0,
+                          tie_word_embeddings=True, qk_norm=True, init="normal"),
+    "tiny-moe-8h": dict(model_type="qwen3_moe", vocab_size=512, hidden_size=256, intermediate_size=512,
+                        moe_intermediate_size=128, num_hidden_layers=2, num_attention_heads=8, num_key_value_heads=8,
+                        head_dim=32, max_position_embeddings=1024, rms_norm_eps=1e-6, rope_theta=1000000.0,
+                        qk_norm=True, num_experts=8, num_experts_per_tok=2, init="normal"),
     "tiny-mixtral": dict(model_type="mixtral", vocab_size=512, hidden_size=256, intermediate_size=256,
                          num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2,
                          max_position_embeddings=1024, rms_norm_eps=1e-5, rope_theta=1000000.0,

@@ -204,6 +204,214 @@ def capacity_receive_order(recv_kept: torch.Tensor, cap: int):
     return order, offs
 
 
+# ---------------------------------------------------------------- dropless exchange, device counts
+# Every EP rank all-gathers its per-expert row counts into M [ep, E] (device, int32).
+# From M alone each rank knows where every row goes: source s holds its rows sorted
+# by global expert (P[s][g] = first row of expert g), owner d = g // El receives its
+# experts' rows EXPERT-MAJOR (expert g = [rows from source 0 | source 1 | ...]), row
+# (s, i) of expert g landing at q = EO[g] + SO[s][g] + (i - P[s][g]).  The exchange
+# buffers are sized by the host bound R_max = ep * T_max * min(k, El) rows (every
+# token routes at most min(k, El) rows to one owner), so nothing is ever dropped and
+# no count is read by the host: on one node the push kernel
+# (csrc/xgmi_allreduce.hip ``ep_exchange_kernel``) places the rows straight at q in
+# the owner's buffer; elsewhere RCCL moves them with exact splits after one host read
+# of M per layer.  The grouped GEMMs run on the R_max-row buffer with device offsets,
+# so only the real rows cost FLOPs.  Reference: dispatch_tokens / gather_tokens,
+# scaletorch/parallel/expert_parallel/ep_comms.py:41-171 (host-synced splits, three
+# all-to-alls, no autograd).
+_ROWS_BOUND: dict = {}
+
+
+def ep_rows_bound(T: int, group) -> int:
+    """Largest local token count over the EP group (one host sync per distinct T)."""
+    key = (id(group), int(T))
+    if key not in _ROWS_BOUND:
+        t = torch.tensor([int(T)], dtype=torch.int64,
+                         device="cuda" if (torch.cuda.is_available() and _group_on_gpu(group)) else "cpu")
+        if C.get_world_size(group) > 1:
+            C.all_reduce(t, op="max", group=group)
+        _ROWS_BOUND[key] = int(t.item())
+    return _ROWS_BOUND[key]
+
+
+def _group_on_gpu(group) -> bool:
+    import torch.distributed as dist
+
+    try:
+        return dist.get_backend(group) == "nccl"
+    except (RuntimeError, ValueError, AttributeError):
+        return False
+
+
+def ep_owner_positions(M: torch.Tensor, El: int, owner: int, rows: int) -> torch.Tensor:
+    """Expert-major position q of every row ``owner`` receives, in ARRIVAL order (source
+    0's rows of the owner's experts in expert order, then source 1's, ...); ``rows`` =
+    their number (host).  Device only."""
+    Ml = M.long()
+    ep, E = Ml.shape
+    blk = Ml[:, owner * El:(owner + 1) * El]                        # [s, e] block sizes
+    SO = torch.cumsum(Ml, 0) - Ml                                   # rows of g from sources < s
+    tot = blk.sum(0)                                                # [e]
+    EO = torch.cumsum(tot, 0) - tot                                 # owner's expert offsets
+    base = (EO[None, :] + SO[:, owner * El:(owner + 1) * El]).reshape(-1)
+    sizes = blk.reshape(-1)
+    start = torch.cumsum(sizes, 0) - sizes
+    rep = torch.repeat_interleave(torch.arange(ep * El, device=M.device), sizes, output_size=rows)
+    return base[rep] + (torch.arange(rows, device=M.device) - start[rep])
+
+
+def ep_exchange_reference(xs: list, M: torch.Tensor, El: int, direction: int, out_rows: int) -> list:
+    """All ranks' exchange in ONE process (tests): ``xs[r]`` = rank r's input.  Direction
+    0: rank r's sorted rows -> every owner's expert-major rows (``out_rows`` per owner,
+    the tail past the received rows zero); 1: the reverse (each source gets its own
+    sum(M[s]) rows; ``out_rows`` unused).  Built from explicit per-row loops over M, independent of the position
+    formula it checks."""
+    Mh = M.to("cpu", torch.int64)
+    ep, E = Mh.shape
+    rows = [out_rows] * ep if direction == 0 else [int(Mh[s].sum()) for s in range(ep)]
+    outs = [xs[0].new_zeros(rows[r], xs[0].shape[1]) for r in range(ep)]
+    # expert-major slot lists per owner: for each local expert, sources in order
+    for d in range(ep):
+        slot = 0
+        for e in range(El):
+            g = d * El + e
+            for s in range(ep):
+                first = int(Mh[s, :g].sum())
+                for j in range(int(Mh[s, g])):
+                    if direction == 0:
+                        outs[d][slot] = xs[s][first + j]
+                    else:
+                        outs[s][first + j] = xs[d][slot]
+                    slot += 1
+    return outs
+
+
+def _ep_exchange_rccl(x: torch.Tensor, M: torch.Tensor, El: int, direction: int, out_rows: int, group):
+    """The exchange over RCCL / gloo: exact splits from ONE host read of M (the
+    dispatch and combine of a layer reuse it through autograd), same layouts as the
+    push kernel."""
+    ep = M.shape[0]
+    me = C.get_rank(group)
+    Mh = M.detach().to("cpu", torch.int64)
+    rows_to = Mh.view(ep, ep, El).sum(2)  # [source, owner]
+    R = int(rows_to[:, me].sum())
+    q = ep_owner_positions(M.to(x.device), El, me, R)
+    if direction == 0:
+        r = C.all_to_all(x.contiguous(), group=group, output_split_sizes=rows_to[:, me].tolist(),
+                         input_split_sizes=rows_to[me].tolist())
+        out = x.new_zeros(out_rows, x.shape[1]) if _ZERO_PAD[0] else x.new_empty(out_rows, x.shape[1])
+        out.index_copy_(0, q, r)
+        return out
+    out = C.all_to_all(x.index_select(0, q), group=group, output_split_sizes=rows_to[me].tolist(),
+                       input_split_sizes=rows_to[:, me].tolist())
+    if out.shape[0] != out_rows:
+        raise RuntimeError(f"EP combine returned {out.shape[0]} rows, expected {out_rows}")
+    return out
+
+
+_ZERO_PAD = [os.environ.get("ST_MOE_ZERO_PAD", "0") == "1"]  # zero the unused tail of R_max buffers (debug)
+
+
+def _ep_exchange(x, M, El, direction, out_rows, area_rows, group, comm):
+    trace.record("ep.exchange" if direction == 0 else "ep.exchange_back", x, group_size=C.get_world_size(group),
+                 transport="xgmi" if comm is not None else "rccl")
+    if comm is not None:
+        out = comm.ep_exchange(x, M, El, direction, out_rows, area_rows)
+        if _ZERO_PAD[0] and direction == 0:  # rows past the received ones hold stale data
+            valid = M[:, C.get_rank(group) * El:(C.get_rank(group) + 1) * El].sum()
+            out.masked_fill_((torch.arange(out_rows, device=out.device) >= valid)[:, None], 0)
+        return out
+    return _ep_exchange_rccl(x, M, El, direction, out_rows, group)
+
+
+class _EPExchange(torch.autograd.Function):
+    """Dispatch (direction 0: sorted rows -> owners' expert-major rows) or combine
+    (direction 1); backward is the other direction with the same counts."""
+
+    @staticmethod
+    def forward(ctx, x, M, El, direction, out_rows, bounds, group, comm):
+        ctx.save_for_backward(M)
+        ctx.meta = (El, direction, x.shape[0], bounds, group, comm)
+        area = bounds[0] if direction == 0 else bounds[1]
+        return _ep_exchange(x, M, El, direction, out_rows, area, group, comm)
+
+    @staticmethod
+    def backward(ctx, g):
+        (M,) = ctx.saved_tensors
+        El, direction, in_rows, bounds, group, comm = ctx.meta
+        rev = 1 - direction
+        area = bounds[0] if rev == 0 else bounds[1]
+        return (_ep_exchange(g.contiguous(), M, El, rev, in_rows, area, group, comm),
+                None, None, None, None, None, None, None)
+
+
+def ep_counts_matrix(counts: torch.Tensor, group, comm=None) -> torch.Tensor:
+    """[ep, E] int32 routing counts of every EP rank (device all-gather, no host sync)."""
+    c = counts.to(torch.int32).contiguous()
+    if comm is not None:
+        return comm.ep_counts(c)
+    return C.all_gather(c, group=group).view(C.get_world_size(group), -1)
+
+
+def ep_comm_for(group):
+    """The EP group's xGMI communicator when the push exchange is enabled, else None."""
+    return _EP_XGMI.get(id(group)) if _DISPATCH["comm"] == "xgmi" else None
+
+
+def select_ep_transport(group, requested: str = "auto") -> str:
+    """Collective over the EP group at start-up.  "auto": set up the xGMI communicator
+    (one node, one GPU per rank) and self-test the push exchange against the RCCL
+    exchange on random routing (bitwise equal both ways); the MIN-reduced verdict picks
+    xgmi or rccl for every rank.  Sets the dispatch transport and returns it."""
+    if requested == "rccl" or C.get_world_size(group) <= 1:
+        _DISPATCH["comm"] = "rccl"
+        return "rccl"
+    ok = 0
+    info: dict = {}
+    try:
+        setup_ep_xgmi(group)
+        comm = _EP_XGMI.get(id(group))
+        if comm is not None:
+            ok, info = _ep_selftest(comm, group)
+    except Exception as e:  # noqa: BLE001 -- every rank still joins the vote
+        ok, info = 0, {"error": repr(e)[:200]}
+        if requested == "xgmi":
+            raise
+    flag = torch.tensor([ok], dtype=torch.int32, device="cuda" if _group_on_gpu(group) else "cpu")
+    C.all_reduce(flag, op="min", group=group)
+    choice = "xgmi" if int(flag.item()) == 1 else "rccl"
+    if requested == "xgmi" and choice != "xgmi":
+        raise RuntimeError(f"ep_comm xgmi requested but the push exchange self-test failed: {info}")
+    _DISPATCH["comm"] = choice
+    EP_TRANSPORT.update(ep=choice, selftest=info)
+    return choice
+
+
+EP_TRANSPORT: dict = {"ep": "rccl", "selftest": None}
+
+
+def _ep_selftest(comm, group):
+    ep = C.get_world_size(group)
+    El, T, k, h = 2, 96, 2, 64
+    E = El * ep
+    g = torch.Generator(device="cuda").manual_seed(77 + C.get_rank(group))
+    topi = torch.stack([torch.randperm(E, generator=g, device="cuda")[:k] for _ in range(T)])
+    counts = torch.bincount(topi.reshape(-1), minlength=E).to(torch.int32)
+    x = torch.randn(T * k, h, device="cuda", dtype=torch.bfloat16, generator=g)
+    M = ep_counts_matrix(counts, group, comm)
+    M_ref = ep_counts_matrix(counts, group, None)
+    R_max, Tk = ep * T * min(k, El), T * k
+    a = comm.ep_exchange(x, M, El, 0, R_max, R_max)
+    b = _ep_exchange_rccl(x, M, El, 0, R_max, group)
+    valid = int(M[:, C.get_rank(group) * El:(C.get_rank(group) + 1) * El].sum())
+    back_a = comm.ep_exchange(a, M, El, 1, Tk, Tk)
+    back_b = _ep_exchange_rccl(b, M, El, 1, Tk, group)
+    comm.check()
+    ok = bool(torch.equal(M, M_ref) and torch.equal(a[:valid], b[:valid]) and torch.equal(back_a, back_b)
+              and torch.equal(back_a, x))
+    return (1 if ok else 0), {"rows": valid, "bitwise": ok}
+
+
 _GMM_OK: bool | None = None
 
 
@@ -317,6 +525,41 @@ def _gmm(x: torch.Tensor, w: torch.Tensor, offs: torch.Tensor, wn: bool) -> torc
     return _gmm_fallback(x, w, offs, wn)
 
 
+def _gmm_swiglu(x: torch.Tensor, w_gu: torch.Tensor, offs: torch.Tensor):
+    """(gu, a = silu(gate) * up) of the grouped gate|up GEMM: ONE launch with the SwiGLU
+    in the epilogue (csrc/grouped_gemm.hip EPI 1) when the kernel takes the shape
+    (I % 128 == 0), else the GEMM and a separate SwiGLU pass (valid rows only)."""
+    from ..ops import _lib
+
+    K, N = x.shape[1], w_gu.shape[1]
+    if (os.environ.get("ST_MOE_FUSED_SWIGLU", "1") == "1" and _lib.use_native(x) and x.dtype == torch.bfloat16
+            and x.stride(1) == 1 and x.stride(0) % 8 == 0 and w_gu.is_contiguous() and K % 64 == 0
+            and N % 256 == 0 and x.shape[0] > 0):
+        out = _lib.ops().grouped_gemm_swiglu(x, w_gu, offs)
+        if out:
+            return out[0], out[1]
+    gu = _gmm(x, w_gu, offs, wn=False)
+    if gu.is_cuda and _lib.use_native(gu):
+        return gu, _lib.ops().swiglu_fwd(gu, offs[-1:])
+    return gu, ops.swiglu(gu)
+
+
+def _gmm_dswiglu(dy: torch.Tensor, w_dn: torch.Tensor, offs: torch.Tensor, gu: torch.Tensor) -> torch.Tensor:
+    """dgu = SwiGLU-backward(dy @ w_dn[g], gu): the down projection's data-gradient GEMM with
+    the SwiGLU backward in its epilogue (EPI 2), else GEMM + swiglu_bwd (valid rows)."""
+    from ..ops import _lib
+
+    K, I = dy.shape[1], w_dn.shape[2]
+    if (os.environ.get("ST_MOE_FUSED_SWIGLU", "1") == "1" and _lib.use_native(dy) and dy.dtype == torch.bfloat16
+            and dy.stride(1) == 1 and dy.stride(0) % 8 == 0 and w_dn.is_contiguous() and K % 64 == 0
+            and I % 128 == 0 and dy.shape[0] > 0 and gu.is_contiguous()):
+        dgu = _lib.ops().grouped_gemm_dswiglu(dy, w_dn, offs, gu)
+        if dgu is not None:
+            return dgu
+    da = _gmm(dy, w_dn, offs, wn=True)
+    return _lib.ops().swiglu_bwd(da.contiguous(), gu, offs[-1:])
+
+
 class _ExpertFFNFn(torch.autograd.Function):
     """Grouped expert SwiGLU FFN: forward and data-gradient GEMMs are one launch each over
     all local experts (``_gmm``, csrc/grouped_gemm.hip), and the weight gradients are
@@ -332,10 +575,13 @@ class _ExpertFFNFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, offs, w_gu, w_dn):
-        gu = _gmm(x, w_gu, offs, wn=False)
-        a = ops.swiglu(gu)
+        gu, a = _gmm_swiglu(x, w_gu, offs)
         y = _gmm(a, w_dn, offs, wn=False)
-        ctx.save_for_backward(x, gu, a, offs)
+        # padded buffers (dropless EP: R_max rows, the real ones counted on the device):
+        # keep only gu and recompute a over the valid rows in backward
+        ctx.keep_a = os.environ.get("ST_MOE_SAVE_ACT", "auto") == "1" or (
+            os.environ.get("ST_MOE_SAVE_ACT", "auto") == "auto" and not getattr(x, "_st_padded", False))
+        ctx.save_for_backward(x, gu, a if ctx.keep_a else None, offs)
         ctx.w_gu, ctx.w_dn = w_gu, w_dn
         return y
 
@@ -347,8 +593,9 @@ class _ExpertFFNFn(torch.autograd.Function):
         x, gu, a, offs = ctx.saved_tensors
         w_gu, w_dn = ctx.w_gu, ctx.w_dn
         dy = dy.contiguous()
-        da = _gmm(dy, w_dn, offs, wn=True)
-        dgu = _lib.ops().swiglu_bwd(da.contiguous(), gu)
+        if a is None:
+            a = _lib.ops().swiglu_fwd(gu, offs[-1:])  # valid rows only
+        dgu = _gmm_dswiglu(dy, w_dn, offs, gu)
         dx = _gmm(dgu, w_gu, offs, wn=True)
         counts = None
         for w, dout, inp in ((w_dn, dy, a), (w_gu, dgu, x)):
@@ -405,17 +652,20 @@ class MoEExperts(nn.Module):
             dn.normal_(0.0, self.init_std, generator=keyed_generator(key and key + ".down", dev))
             self.w_down.copy_(dn[e0:e0 + self.num_local].chunk(self.tp, 2)[self.tp_rank])
 
-    def forward(self, x: torch.Tensor, counts) -> torch.Tensor:
-        """x: rows grouped by local expert (``counts[e]`` rows each; list or device tensor).
+    def forward(self, x: torch.Tensor, counts=None, offs: torch.Tensor | None = None) -> torch.Tensor:
+        """x: rows grouped by local expert (``counts[e]`` rows each -- list or device
+        tensor -- or the inclusive device prefix ``offs``); rows past the last expert's
+        (capacity / R_max padding) are not computed: their output is undefined on the
+        grouped-GEMM path and zero (still connected) on the per-expert path.
 
-        GPU: two grouped GEMMs over all local experts (``torch._grouped_mm`` with
-        device-side group offsets -> hipBLASLt grouped kernels): no per-expert
-        launches and no host read of the routing counts.  CPU / fallback: one GEMM
-        pair per expert."""
+        GPU: two grouped GEMMs over all local experts (csrc/grouped_gemm.hip, device
+        offsets): no per-expert launches and no host read of the routing counts.
+        CPU / fallback: one GEMM pair per expert."""
         if x.is_cuda and _grouped_mm_available() and x.dtype == torch.bfloat16:
-            if not isinstance(counts, torch.Tensor):
-                counts = torch.tensor(counts, dtype=torch.int32)
-            offs = torch.cumsum(counts.to(device=x.device, dtype=torch.int32), 0, dtype=torch.int32)
+            if offs is None:
+                if not isinstance(counts, torch.Tensor):
+                    counts = torch.tensor(counts, dtype=torch.int32)
+                offs = torch.cumsum(counts.to(device=x.device, dtype=torch.int32), 0, dtype=torch.int32)
             if x.shape[0] == 0:
                 return self._empty(x)
             mg_gu, mg_dn = (getattr(w, "main_grad", None) for w in (self.w_gate_up, self.w_down))
@@ -425,6 +675,8 @@ class MoEExperts(nn.Module):
                 return _ExpertFFNFn.apply(x.contiguous(), offs, self.w_gate_up, self.w_down)
             gu = torch._grouped_mm(x.contiguous(), self.w_gate_up.transpose(-2, -1), offs=offs)
             return torch._grouped_mm(ops.swiglu(gu), self.w_down.transpose(-2, -1), offs=offs)
+        if counts is None:
+            counts = torch.diff(offs.long(), prepend=offs.new_zeros(1, dtype=torch.long))
         if isinstance(counts, torch.Tensor):
             counts = counts.tolist()
         outs = []
@@ -436,7 +688,7 @@ class MoEExperts(nn.Module):
             gu = torch.matmul(xe, self.w_gate_up[e].t())
             outs.append(torch.matmul(ops.swiglu(gu), self.w_down[e].t()))
             off += n
-        if off < x.shape[0]:  # capacity padding rows past the last expert: zero output, connected
+        if off < x.shape[0]:  # padding rows past the last expert: zero output, connected
             outs.append(x[off:] * 0)
         if not outs:
             return self._empty(x)
@@ -506,25 +758,36 @@ class MoELayer(nn.Module):
             return self._tp_reduce(out, tp_group)
         # stable sort of the T*k (token, slot) entries by global expert + row gather
         perm = ops.moe.permutation(topi, self.num_experts)
-        counts = perm.counts
         xs = ops.moe.gather_rows(x2, perm)  # rows sorted by global expert
         if self.ep == 1:
-            y = self.experts(xs, counts)  # device counts: no host sync on the grouped-GEMM path
+            y = self.experts(xs, perm.counts)  # device counts: no host sync on the grouped-GEMM path
         else:
-            group = mesh.pgm.ep_group
-            # counts per (dest rank, local expert); exchange the full matrix once
-            send_mat = counts.view(self.ep, self.num_local)
-            recv_mat = C.all_to_all(send_mat.contiguous(), group=group)  # [src, local expert]
-            mats = torch.stack([send_mat.sum(1), recv_mat.sum(1)]).cpu()  # the ONE host sync per layer
-            send_splits, recv_splits = mats[0].tolist(), mats[1].tolist()
-            xr = all_to_all_rows(xs, recv_splits, send_splits, group)  # rows grouped [src][expert]
-            # src-major -> expert-major order, computed on device from the count matrix
-            order = expert_major_order(recv_mat, sum(recv_splits))
-            ye = self.experts(xr.index_select(0, order), recv_mat.sum(0))
-            yr = ye.index_select(0, torch.argsort(order))  # back to [src][expert] for the return trip
-            y = all_to_all_rows(yr, send_splits, recv_splits, group)
+            y = self._forward_ep_dropless(xs, perm.counts)
         out = ops.moe.combine(y, topw, perm).view(shape)
         return self._tp_reduce(out, tp_group)
+
+    def _forward_ep_dropless(self, xs: torch.Tensor, counts: torch.Tensor) -> torch.Tensor:
+        """Dropless expert parallelism with device-side counts (see ``ep_owner_positions``):
+        one count all-gather, one dispatch exchange, the grouped expert GEMMs over the
+        R_max-row buffer (device offsets), one combine exchange.  No host read of the
+        routing on the xGMI transport; one per layer (the splits) on RCCL."""
+        group = mesh.pgm.ep_group
+        ep, El, k = self.ep, self.num_local, self.top_k
+        comm = ep_comm_for(group)
+        Tk = xs.shape[0]
+        T_max = ep_rows_bound(Tk // k, group)
+        R_max, Tk_max = ep * T_max * min(k, El), T_max * k
+        if comm is not None and not (comm.ep_fits(R_max, xs) and comm.ep_fits(Tk_max, xs)):
+            comm = None  # buffers too small for this shape: RCCL exchange
+        M = ep_counts_matrix(counts, group, comm)
+        mine = M[:, self.ep_rank * El:(self.ep_rank + 1) * El]
+        offs = torch.cumsum(mine.sum(0), 0, dtype=torch.int32)  # grouped-GEMM offsets (device)
+        xe = _EPExchange.apply(xs, M, El, 0, R_max, (R_max, Tk_max), group, comm)
+        xe._st_padded = True  # R_max rows, the first offs[-1] real: the FFN recomputes a over those
+        ye = self.experts(xe, offs=offs)
+        self.dropped_rows = xs.new_zeros((), dtype=torch.int64)  # dropless by construction
+        self.ep_rows_sent = Tk - mine[self.ep_rank].sum()  # rows that left this rank (device)
+        return _EPExchange.apply(ye, M, El, 1, Tk, (R_max, Tk_max), group, comm)
 
     def _tp_reduce(self, out: torch.Tensor, tp_group) -> torch.Tensor:
         # expert down-projections are TP partial sums: reduce once, after the combine

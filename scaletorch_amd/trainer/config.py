@@ -68,12 +68,13 @@ class ParallelArguments:
     cp_comm: str = field(default="auto", metadata={"help": "CP transport: auto (= allgather: RCCL drives all 7 xGMI links) | allgather (overlapped K/V all-gather) | ring (p2p rotation overlapped with block compute) | ulysses (head all-to-all)"})
     layer_distribution: str | None = field(default=None, metadata={"help": "comma list of layers per PP stage"})
     moe_capacity_factor: float = field(default=0.0, metadata={
-        "help": "EP dispatch: 0 = dropless (exact splits: one host read of the routing counts per MoE layer); "
-                "> 0 = static per-(source, destination) capacity ceil(f * T * k / ep) rows: no host sync, rows "
-                "past the capacity are dropped (counted in the layer's dropped_rows)"})
-    ep_comm: str = field(default="rccl", metadata={
-        "help": "EP all-to-all transport of the capacity dispatch: rccl | xgmi (push all-to-all over IPC peer "
-                "memory, dist/xgmi.py; falls back to RCCL for messages it does not take)"})
+        "help": "EP dispatch: 0 = dropless (exchange buffers sized by the worst case ep*T*min(k, E/ep) rows, "
+                "routing counts stay on the device; over xGMI no host sync at all, over RCCL one host read "
+                "of the count matrix per layer for the splits); > 0 = static per-(source, destination) "
+                "capacity ceil(f * T * k / ep) rows: rows past it are dropped (counted in dropped_rows)"})
+    ep_comm: str = field(default="auto", metadata={
+        "help": "EP transport: auto (one node: self-test the xGMI push exchange against RCCL at start-up and "
+                "keep it when it matches) | rccl | xgmi (push into IPC peer memory, dist/xgmi.py)"})
     moe_ep_chunks: int = field(default=1, metadata={
         "help": "EP dispatch pipelining (capacity mode): the tokens are dispatched in this many chunks, each "
                 "chunk's all-to-all overlapping the previous chunk's expert GEMMs"})
@@ -95,8 +96,8 @@ class ParallelArguments:
                                  "pipeline_parallel_size")
         if self.tp_comm not in {"auto", "rccl", "xgmi"}:
             raise ValueError(f"tp_comm must be auto, rccl or xgmi, got {self.tp_comm}")
-        if self.ep_comm not in {"rccl", "xgmi"}:
-            raise ValueError(f"ep_comm must be rccl or xgmi, got {self.ep_comm}")
+        if self.ep_comm not in {"auto", "rccl", "xgmi"}:
+            raise ValueError(f"ep_comm must be auto, rccl or xgmi, got {self.ep_comm}")
         if self.moe_capacity_factor < 0 or self.moe_ep_chunks < 1:
             raise ValueError("moe_capacity_factor must be >= 0 and moe_ep_chunks >= 1")
         if self.backend not in {"nccl", "gloo", "hccl"}:

@@ -68,12 +68,14 @@ class Trainer:
         from ..models.attention_backends import set_use_flash_attention
         from ..models.moe import set_moe_dispatch
 
-        set_moe_dispatch(a.moe_capacity_factor, a.moe_ep_chunks, a.ep_comm)
-        if (a.ep_comm == "xgmi" and a.expert_parallel_size > 1 and a.backend == "nccl" and torch.cuda.is_available()
-                and not a.use_cpu):
-            from ..models.moe import setup_ep_xgmi
+        set_moe_dispatch(a.moe_capacity_factor, a.moe_ep_chunks, "rccl" if a.ep_comm == "auto" else a.ep_comm)
+        if a.expert_parallel_size > 1 and torch.cuda.is_available() and not a.use_cpu and a.ep_comm != "rccl" \
+                and (a.backend == "nccl" or os.environ.get("ST_GPU_OVERSUBSCRIBE", "0") == "1"):
+            from ..models.moe import select_ep_transport
 
-            setup_ep_xgmi(mesh.pgm.ep_group)  # collective over each EP group, at start-up
+            # collective over each EP group, at start-up: "auto" self-tests the xGMI push
+            # exchange (dropless, device counts) against RCCL and keeps it when it matches
+            select_ep_transport(mesh.pgm.ep_group, a.ep_comm)
 
         set_use_flash_attention(a.use_flash_attention)
         if a.context_parallel_size > 1:

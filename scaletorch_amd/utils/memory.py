@@ -52,11 +52,15 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
                          micro_batch: int = 1, seq_len: int = 4096, grad_acc: int = 1, zero1: bool = False,
                          sequence_parallel: bool = False, gradient_checkpointing: bool = False,
                          pp_engine: str = "1f1b", grad_reduce_dtype: str = "bf16",
-                         fused_head_chunk: int = 0, recompute_swiglu: bool | None = None) -> MemoryEstimate:
+                         fused_head_chunk: int = 0, recompute_swiglu: bool | None = None,
+                         moe_dropless: bool = False) -> MemoryEstimate:
     """Worst-rank estimate (first pipeline stage for activations, largest stage for weights).
 
     ``fused_head_chunk`` > 0: the fused chunked LM head (ops/fused_head.py) -- one
-    chunk of logits and dX instead of the logits and their gradient."""
+    chunk of logits and dX instead of the logits and their gradient.
+    ``moe_dropless`` (EP > 1, models/moe.py dropless exchange): each MoE layer keeps its
+    expert input and gate|up output at the host bound R_max = ep * T * min(k, E/ep) rows
+    (the SwiGLU output is recomputed in backward), plus the sorted rows of the combine."""
     h, d = cfg.hidden_size, cfg.head_dim
     H, Hkv = cfg.num_attention_heads, cfg.num_key_value_heads
     L = cfg.num_hidden_layers
@@ -90,6 +94,14 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
         recompute_swiglu = os.environ.get("ST_MLP_RECOMPUTE_ACT", "0") == "1"
     mlp_b = _ACT_MLP - (_ACT_SWIGLU if (recompute_swiglu and tp == 1 and not cfg.is_moe) else 0)
     per_layer = _ACT_ATTN * h + mlp_b * h * k_eff * cfg.intermediate_size / (3.5 * h)
+    moe_extra = 0.0  # bytes per MoE layer outside the per-token model (dropless R_max buffers)
+    if cfg.is_moe and ep > 1 and moe_dropless:
+        k = cfg.num_experts_per_tok
+        per_layer = _ACT_ATTN * h
+        t_micro = micro_batch * seq_len / cp
+        r_max = ep * t_micro * min(k, cfg.num_experts // ep)
+        moe_extra = (r_max * (2 * h + 4 * cfg.moe_intermediate_size / tp) + t_micro * k * 4 * h) * (
+            tokens / t_micro)
     if tp > 1:
         per_layer = per_layer / tp if sequence_parallel else 8 * h + (per_layer - 8 * h) / tp
     if gradient_checkpointing == "selective":  # attention activations kept, norm + MLP recomputed
@@ -100,6 +112,7 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
         act = tokens * (2 * h * layers) + tokens * per_layer
     else:
         act = tokens * per_layer * layers
+    act += moe_extra * sum(1 for i in range(layers) if cfg.layer_is_moe(i))
     head_tokens = micro_batch * seq_len / cp
     if fused_head_chunk:
         # one chunk of logits + dX (the head's dW goes straight into main_grad)

@@ -87,3 +87,29 @@ def test_bench_mismatched_world_fails():
     out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1"], cwd=ROOT, env=env,
                          capture_output=True, text=True, timeout=300)
     assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr, out.stderr[-2000:]
+
+
+@pytest.mark.slow
+def test_reference_8gpu_table_replay_smoke(tmp_path):
+    """scripts/bench_reference_rows_8gpu.py replays BASELINE.md §2 row by row: every row
+    maps to an 8-rank layout, and a world-8 CPU/gloo smoke (tiny models, results
+    invalid) of the reference's distinct mixed layouts -- TP4-PP2, TP2-CP2-DP2,
+    EP2-TP4 -- runs end to end and writes one JSONL line per row with the reference's
+    tok/s/GPU next to ours."""
+    import json
+    import subprocess
+    import sys
+
+    script = os.path.join(ROOT, "scripts", "bench_reference_rows_8gpu.py")
+    listing = subprocess.run([sys.executable, script, "--list"], capture_output=True, text=True, check=True)
+    assert len(listing.stdout.split()) == 52  # every published row of BASELINE.md §2
+    out = tmp_path / "rows.jsonl"
+    pat = "qwen3-8b-tp4-pp2|qwen3-8b-tp2-cp2-dp2|a3b-ep2-tp4-mbs1-ga1-s2048$"
+    p = subprocess.run([sys.executable, script, "--smoke", "--filter", pat, "--steps", "1", "--warmup", "1",
+                        "--out", str(out)], capture_output=True, text=True, timeout=900)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    recs = [json.loads(line) for line in out.read_text().splitlines()]
+    assert {r["layout"] for r in recs} == {"tp4-pp2", "tp2-cp2-dp2", "ep2-tp4"}
+    for r in recs:
+        assert r["rc"] == 0 and r["ours"]["n_gpus"] == 8 and r["reference_tok_s_per_gpu"] > 0
+        assert r["ours"]["config"]["parallelism"].startswith("dp")

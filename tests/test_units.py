@@ -527,3 +527,40 @@ def test_moe_capacity_plan_simulated_exchange():
         sent_from = torch.full((rows,), -1)
         sent_from[plan.send_idx[plan.send_valid]] = flat[plan.send_valid]
         assert torch.equal(got, sent_from)
+
+
+def test_ep_owner_positions_match_bruteforce_layout():
+    """Dropless EP exchange layout (models/moe.py): the device position formula
+    (``ep_owner_positions``) places every received row where the per-row reference
+    puts it, and dispatch followed by combine is the identity, for random routing
+    with empty experts and uneven token counts."""
+    import torch
+
+    from scaletorch_amd.models.moe import ep_exchange_reference, ep_owner_positions
+
+    g = torch.Generator().manual_seed(5)
+    for ep, El, k in ((2, 2, 2), (4, 1, 2), (4, 3, 2), (8, 2, 4)):
+        E = ep * El
+        T = [int(torch.randint(3, 20, (1,), generator=g)) for _ in range(ep)]
+        xs, M = [], torch.zeros(ep, E, dtype=torch.int32)
+        for s in range(ep):
+            if s == 1:  # rank 1 never routes to expert 0
+                topi = torch.stack([torch.randperm(E - 1, generator=g)[:k] + 1 for _ in range(T[s])])
+            else:
+                topi = torch.stack([torch.randperm(E, generator=g)[:k] for _ in range(T[s])])
+            M[s] = torch.bincount(topi.reshape(-1), minlength=E).to(torch.int32)
+            xs.append(torch.randn(T[s] * k, 8, generator=g))
+        R_max = ep * max(T) * min(k, El)
+        got = ep_exchange_reference(xs, M, El, 0, R_max)
+        for d in range(ep):
+            R = int(M[:, d * El:(d + 1) * El].sum())
+            assert R <= R_max
+            q = ep_owner_positions(M, El, d, R)
+            arrival = torch.cat([xs[s][int(M[s, :d * El].sum()):int(M[s, :(d + 1) * El].sum())] for s in range(ep)])
+            placed = torch.zeros(R_max, 8)
+            placed[q] = arrival
+            assert torch.equal(placed, got[d]), (ep, El, d)
+            assert sorted(q.tolist()) == list(range(R))  # a permutation of the first R rows
+        backs = ep_exchange_reference(got, M, El, 1, 0)
+        for s in range(ep):
+            assert torch.equal(backs[s], xs[s])

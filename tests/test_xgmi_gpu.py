@@ -102,6 +102,29 @@ def _ipc_worker(rank, world, port, q):
             comm.check()
             lo, hi = min(rank, partner), max(rank, partner)
             res.append(bool((y[:2048] == lo).all() and (y[2048:] == hi).all()))
+        # dropless EP push exchange with device counts over real IPC mappings
+        from scaletorch_amd.models.moe import ep_exchange_reference
+
+        El, k, T, h = 2, 2, 32, 64
+        E = El * world
+        g = torch.Generator().manual_seed(3)  # same seed on every rank: the same global routing
+        M = torch.zeros(world, E, dtype=torch.int32)
+        xs = []
+        for s in range(world):
+            topi = torch.stack([torch.randperm(E, generator=g)[:k] for _ in range(T)])
+            M[s] = torch.bincount(topi.reshape(-1), minlength=E).to(torch.int32)
+            xs.append(torch.randn(T * k, h, generator=g).to(torch.bfloat16))
+        R_max = world * T * min(k, El)
+        Md = M.cuda()
+        counts_all = comm.ep_counts(M[rank].cuda())  # the count all-gather over IPC
+        out = comm.ep_exchange(xs[rank].cuda(), Md, El, 0, R_max, R_max)
+        back = comm.ep_exchange(out, Md, El, 1, T * k, T * k)
+        torch.cuda.synchronize()
+        comm.check()
+        ref = ep_exchange_reference(xs, M, El, 0, R_max)
+        R = int(M[:, rank * El:(rank + 1) * El].sum())
+        res.append(bool(torch.equal(counts_all.cpu(), M) and torch.equal(out[:R].cpu(), ref[rank][:R])
+                        and torch.equal(back.cpu(), xs[rank])))
         q.put((rank, "ok", res))
         comm.close()
     except Exception as e:  # noqa: BLE001
@@ -237,6 +260,70 @@ def test_xgmi_pair_multipath_simulated(world, dtype, n):
                 me = 0 if r == lo else 1
                 ref = (big[lo][me * n:(me + 1) * n].float() + big[hi][me * n:(me + 1) * n].float()).to(dtype)
                 assert torch.equal(rs[r], ref)
+    finally:
+        for c in comms:
+            c.close()
+
+
+@pytest.mark.parametrize("world,El,k", [(2, 2, 2), (4, 1, 2), (8, 1, 2), (8, 16, 8)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_xgmi_ep_exchange_simulated(world, El, k, dtype):
+    """Dropless EP push exchange with device counts (ep_exchange_kernel): dispatch places
+    every source's rows expert-major in the owners' buffers exactly like the per-row
+    reference (models/moe.py ep_exchange_reference), bitwise; combine returns them to the
+    sources' sorted order; skewed routing (a hot expert) and an empty expert included;
+    the error word stays clear."""
+    from scaletorch_amd.models.moe import ep_exchange_reference
+
+    assert _lib.load(), _lib.load_error()
+    E, T, h = world * El, 64, 128
+    R_max = world * T * min(k, El)
+    comms = XgmiAllReduce.simulate(world, max_bytes=R_max * h * 4 + 4096)
+    try:
+        g = torch.Generator().manual_seed(11)
+        for trial in range(3):
+            M = torch.zeros(world, E, dtype=torch.int32)
+            for s in range(world):
+                w = torch.ones(E)
+                w[0] = 0.0 if trial == 1 else 1.0          # expert 0 empty in trial 1
+                if trial == 2:
+                    w[E - 1] = 50.0                         # a hot expert in trial 2
+                topi = torch.stack([torch.multinomial(w, k, replacement=False, generator=g) for _ in range(T)])
+                M[s] = torch.bincount(topi.reshape(-1), minlength=E).to(torch.int32)
+            xs = [torch.randn(T * k, h, generator=g).to(dtype).cuda() for _ in range(world)]
+            Md = M.cuda()
+            outs = XgmiAllReduce.ep_exchange_sim(comms, xs, Md, El, 0, R_max, R_max)
+            torch.cuda.synchronize()
+            for c in comms:
+                assert int(_lib.ops().xgmi_error(c.id)) == 0
+            ref = ep_exchange_reference([x.cpu() for x in xs], M, El, 0, R_max)
+            for d in range(world):
+                R = int(M[:, d * El:(d + 1) * El].sum())
+                assert torch.equal(outs[d][:R].cpu(), ref[d][:R]), (trial, d)
+            back = XgmiAllReduce.ep_exchange_sim(comms, outs, Md, El, 1, T * k, T * k)
+            torch.cuda.synchronize()
+            for c in comms:
+                assert int(_lib.ops().xgmi_error(c.id)) == 0
+            for s in range(world):
+                assert torch.equal(back[s], xs[s]), (trial, s)
+    finally:
+        for c in comms:
+            c.close()
+
+
+def test_xgmi_ep_exchange_rejects_overflow_without_writing():
+    """Counts claiming more rows than the host bound: the kernel sets the error word and
+    skips those rows instead of writing past the buffers (no fault)."""
+    assert _lib.load(), _lib.load_error()
+    world, El, T, h = 2, 1, 16, 64
+    comms = XgmiAllReduce.simulate(world, max_bytes=1 << 20)
+    try:
+        M = torch.tensor([[2 * T, 0], [0, 2 * T]], dtype=torch.int32, device="cuda")  # > the 16 input rows
+        xs = [torch.randn(T, h, device="cuda", dtype=torch.bfloat16) for _ in range(world)]
+        outs = XgmiAllReduce.ep_exchange_sim(comms, xs, M, El, 0, T, T)
+        torch.cuda.synchronize()
+        assert int(_lib.ops().xgmi_error(comms[0].id)) == 2
+        assert outs[0].shape == (T, h)
     finally:
         for c in comms:
             c.close()
