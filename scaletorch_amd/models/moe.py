@@ -222,16 +222,21 @@ def capacity_receive_order(recv_kept: torch.Tensor, cap: int):
 _ROWS_BOUND: dict = {}
 
 
-def ep_rows_bound(T: int, group) -> int:
-    """Largest local token count over the EP group (one host sync per distinct T)."""
+def ep_rows_range(T: int, group) -> tuple[int, int]:
+    """(smallest, largest) local token count over the EP group (one host sync per distinct T)."""
     key = (id(group), int(T))
     if key not in _ROWS_BOUND:
-        t = torch.tensor([int(T)], dtype=torch.int64,
+        t = torch.tensor([int(T), -int(T)], dtype=torch.int64,
                          device="cuda" if (torch.cuda.is_available() and _group_on_gpu(group)) else "cpu")
         if C.get_world_size(group) > 1:
             C.all_reduce(t, op="max", group=group)
-        _ROWS_BOUND[key] = int(t.item())
+        _ROWS_BOUND[key] = (-int(t[1].item()), int(t[0].item()))
     return _ROWS_BOUND[key]
+
+
+def ep_rows_bound(T: int, group) -> int:
+    """Largest local token count over the EP group (sizes the dropless exchange buffers)."""
+    return ep_rows_range(T, group)[1]
 
 
 def _group_on_gpu(group) -> bool:
@@ -811,6 +816,10 @@ class MoELayer(nn.Module):
         group = mesh.pgm.ep_group
         ep, k = self.ep, self.top_k
         T = x2.shape[0]
+        lo, hi = ep_rows_range(T, group)
+        if lo != hi:  # the static buffers assume one token count on every EP rank (raised on every rank)
+            raise ValueError(f"capacity EP dispatch needs the same token count on every EP rank (got {lo}..{hi}); "
+                             "use the dropless dispatch (--moe_capacity_factor 0)")
         nch = max(1, min(_DISPATCH["chunks"], T))
         cf = _DISPATCH["capacity_factor"]
         bounds = [T * c // nch for c in range(nch + 1)]

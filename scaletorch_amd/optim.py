@@ -195,6 +195,9 @@ class ArenaAdamW(_ArenaOptimizer):
         st = self.side_stream
         if self.clip_coef is not None:
             self.clip_coef.record_stream(st)
+        # timing probe only (WRONG training: the weights never change): ST_OPT_PROBE_SKIP=1
+        # skips every update kernel, so an A/B prices what the side-stream AdamW costs the step
+        skip = os.environ.get("ST_OPT_PROBE_SKIP") == "1"
         with torch.cuda.stream(st):
             st.wait_event(ev)
             for g, a in zip(self.param_groups, self.arenas):
@@ -202,7 +205,7 @@ class ArenaAdamW(_ArenaOptimizer):
                 for b in reversed(a.buckets):
                     lo, hi, so = b.shard_lo, b.shard_hi, b.state_lo
                     n = hi - lo
-                    if n:
+                    if n and not skip:
                         _lib.ops().adamw_step_(a.master[so: so + n], a.exp_avg[so: so + n],
                                                a.exp_avg_sq[so: so + n], a.grad_flat[lo:hi],
                                                a.param_flat[lo:hi], self.clip_coef, lr, b1, b2, eps, wd, t)

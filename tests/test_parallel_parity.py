@@ -471,3 +471,50 @@ def test_every_weight_read_waits_for_its_bucket(model, world, kw):
     without calling their owning module, racing the side-stream optimizer update)."""
     for missing in run_workers(_cover_worker, world, model, kw):
         assert missing == [], missing
+
+
+def _dropless_uneven_worker(rank, world):
+    """EP=2 MoE layer on a rank-dependent token count vs the same layer with every expert
+    local (ep = 1 math, built from the same full weights)."""
+    import torch.distributed as dist
+
+    from scaletorch_amd.models.config import get_model_config
+    from scaletorch_amd.models.moe import MoELayer
+    from scaletorch_amd.parallel import mesh
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = get_model_config("tiny-moe")
+    torch.manual_seed(0)
+    ref_layer = MoELayer(cfg).float()  # ep = 1: all 8 experts here (mesh not installed yet)
+    mesh.setup_process_group_manager(ep_size=world)
+    layer = MoELayer(cfg).float()
+    with torch.no_grad():
+        layer.router.gate.weight.copy_(ref_layer.router.gate.weight)
+        El = layer.num_local
+        layer.experts.w_gate_up.copy_(ref_layer.experts.w_gate_up[rank * El:(rank + 1) * El])
+        layer.experts.w_down.copy_(ref_layer.experts.w_down[rank * El:(rank + 1) * El])
+    T = 5 + 7 * rank  # different token counts on the two ranks
+    g = torch.Generator().manual_seed(100 + rank)
+    x = torch.randn(1, T, cfg.hidden_size, generator=g)
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    ya = layer(xa)
+    yb = ref_layer(xb)
+    ya.square().sum().backward()
+    yb.square().sum().backward()
+    gw = ref_layer.experts.w_gate_up.grad.clone()
+    dist.all_reduce(gw)  # every rank's tokens reach the owner's experts: sum the per-rank references
+    gw = gw[rank * El:(rank + 1) * El]
+    return (ya.detach(), yb.detach(), xa.grad, xb.grad, layer.experts.w_gate_up.grad, gw,
+            int(layer.dropped_rows))
+
+
+def test_moe_dropless_uneven_token_counts():
+    """Dropless EP dispatch with device counts when EP ranks hold DIFFERENT token counts
+    (ragged batches): outputs, input gradients and expert weight gradients equal the
+    all-experts-local computation; nothing is dropped."""
+    res = run_workers(_dropless_uneven_worker, 2)
+    for ya, yb, ga, gb, wa, wb, dropped in res:
+        torch.testing.assert_close(ya, yb, atol=1e-5, rtol=1e-4)
+        torch.testing.assert_close(ga, gb, atol=1e-5, rtol=1e-4)
+        torch.testing.assert_close(wa, wb, atol=1e-5, rtol=1e-4)
+        assert dropped == 0
