@@ -200,9 +200,35 @@ def accumulate_grad(param: torch.Tensor, grad: torch.Tensor):
     return None
 
 
+def _one_t_ok(dy2d: torch.Tensor, x2d: torch.Tensor) -> bool:
+    T = dy2d.shape[0]
+    return (T % 64 == 0 and dy2d.shape[1] % 64 == 0 and x2d.shape[1] % 64 == 0 and dy2d.stride(1) == 1
+            and x2d.stride(1) == 1 and dy2d.stride(0) % 8 == 0 and x2d.stride(0) % 8 == 0
+            and dy2d.data_ptr() % 16 == 0 and x2d.data_ptr() % 16 == 0)
+
+
+def _wgrad_one_t(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, beta: int) -> None:
+    """out = beta out + dY^T X with the SMALLER operand first transposed to token-contiguous
+    (csrc/transpose.hip, ~5.5 TB/s), so hipBLASLt reads one operand K-contiguous: on the
+    gate|up shape (dY 28672 wide, X 4096) 1390 vs 1292 TF/s for the HIP kernel, transpose
+    included (profiles/r03/wgrad_layouts.log).  Picked per shape by ``_wgrad_pick``."""
+    from . import _lib
+
+    T = dy2d.shape[0]
+    if x2d.shape[1] <= dy2d.shape[1]:
+        xt = torch.empty(x2d.shape[1], T, dtype=x2d.dtype, device=x2d.device)
+        _lib.ops().transpose_(x2d, xt)
+        torch.ops.aten.addmm.dtype_out(out, dy2d.t(), xt.t(), torch.float32, beta=beta, alpha=1, out=out)
+    else:
+        dyt = torch.empty(dy2d.shape[1], T, dtype=dy2d.dtype, device=dy2d.device)
+        _lib.ops().transpose_(dy2d, dyt)
+        torch.ops.aten.addmm.dtype_out(out, dyt, x2d, torch.float32, beta=beta, alpha=1, out=out)
+
+
 def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> int:
     """First call per (shape, strides): time the two HIP kernels (1: 4-stage ring,
-    2: 8-phase ping-pong, csrc/wgrad_gemm.hip; each with and without the tail split) against the hipBLASLt fp32-epilogue
+    2: 8-phase ping-pong, csrc/wgrad_gemm.hip; each with and without the tail split), 3: hipBLASLt
+    on the smaller operand transposed to token-contiguous (``_wgrad_one_t``), against the hipBLASLt fp32-epilogue
     GEMM on a scratch output (5 rounds x 2 calls, same stream, interleaved) and keep
     the fastest -- 0 = hipBLASLt.  On gfx950 none wins every projection shape
     (tools/probe_wgrad.py: the 8-phase kernel +3-13 % on out/down, -1-2 % on
@@ -225,6 +251,8 @@ def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> int:
     if not arms:
         _WGRAD_CHOICE[key] = 0
         return 0
+    if _one_t_ok(dy2d, x2d):  # 3: hipBLASLt on the smaller operand made token-contiguous (transpose timed in)
+        arms[3] = lambda: _wgrad_one_t(scratch, dy2d, x2d, 1)
 
     def blas():
         torch.ops.aten.addmm.dtype_out(scratch, dy2d.t(), x2d, torch.float32, beta=1, alpha=1, out=scratch)
@@ -326,12 +354,15 @@ def wgrad_into(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, beta: i
         from . import _lib
 
         if _lib.use_native(dy2d):
-            forced = os.environ.get("ST_WGRAD_VARIANT", "")  # 0 / 1 / 2 / 17 / 18 overrides the pick (A/B)
-            if forced in ("0", "1", "2", "17", "18"):
+            forced = os.environ.get("ST_WGRAD_VARIANT", "")  # 0 / 1 / 2 / 3 / 17 / 18 overrides the pick (A/B)
+            if forced in ("0", "1", "2", "3", "17", "18"):
                 variant = int(forced)
             elif variant is None:
                 variant = _wgrad_pick(dy2d, x2d)
-            if variant and _lib.ops().wgrad_gemm_(out, dy2d, x2d, beta, variant):
+            if variant == 3 and _one_t_ok(dy2d, x2d):
+                _wgrad_one_t(out, dy2d, x2d, beta)
+                return
+            if variant and variant != 3 and _lib.ops().wgrad_gemm_(out, dy2d, x2d, beta, variant):
                 return
     if _ADDMM_DTYPE_OK is not False and dy2d.is_cuda and os.environ.get("ST_WGRAD_FP32_GEMM", "1") == "1":
         try:

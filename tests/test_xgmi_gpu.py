@@ -19,6 +19,10 @@ from scaletorch_amd.dist.xgmi import XgmiAllReduce  # noqa: E402
 from scaletorch_amd.ops import _lib  # noqa: E402
 
 
+def rel(a: torch.Tensor, b: torch.Tensor) -> float:
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
 def _run_sim(world, n, dtype, oneshot_max):
     comms = XgmiAllReduce.simulate(world, max_bytes=4 << 20, oneshot_max=oneshot_max)
     try:
@@ -327,3 +331,53 @@ def test_xgmi_ep_exchange_rejects_overflow_without_writing():
     finally:
         for c in comms:
             c.close()
+
+
+def _sp_train_worker(rank, world, tp_comm, seed):
+    """One SGD step of a 2-layer Llama with TP = 2 + sequence parallelism, every rank on
+    THIS GPU over gloo; tp_comm 'xgmi' routes the SP all-gathers / reduce-scatters over the
+    IPC pair path on its comm side stream (overlapped with the batched SP GEMMs) and the
+    TP all-reduces over the xGMI communicator."""
+    os.environ.update(ST_GPU_OVERSUBSCRIBE="1", ST_XGMI_TIMEOUT_S="30")
+    from scaletorch_amd.parallel import tensor_parallel as TP
+    from scaletorch_amd.trainer.config import ScaleTorchArguments
+    from scaletorch_amd.trainer.engine import Trainer
+
+    a = ScaleTorchArguments(model_name_or_path="tiny-llama", synthetic_data=True, sequence_length=512,
+                            backend="gloo", dtype="bfloat16", tensor_parallel_size=world, sequence_parallel=True,
+                            micro_batch_size=4, tp_comm=tp_comm, optimizer_type="sgd", learning_rate=0.5,
+                            lr_scheduler_type="constant", max_grad_norm=None, total_train_steps=2, seed=seed)
+    tr = Trainer(a, build_data=False)
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randint(0, tr.model_config.vocab_size, (4, 513), generator=g)
+    pos = torch.arange(512).unsqueeze(0).expand(4, -1).contiguous()
+    batch = {"input_ids": ids[:, :-1].contiguous(), "target_ids": ids[:, 1:].contiguous(), "position_ids": pos,
+             "hidden_states": None}
+    tr.data = iter([batch] * 4)
+    losses = [tr.reduced_loss(tr.train_step()) for _ in range(2)]
+    torch.cuda.synchronize()
+    tr.health_check()
+    sd = {k: v.detach().float().cpu() for k, v in tr.raw_model.reference_state_dict().items()
+          if "decoder_layers.1" in k}
+    return losses, sd, TP.TRANSPORT["tp"], TP._PAIR[0] is not None
+
+
+def test_sp_decoder_layers_pair_path_matches_gloo_same_gpu():
+    """tp = 2 sequence-parallel training step over the xGMI pair path (2 processes, real IPC
+    on one GPU) equals the same step over gloo within bf16 tolerance: losses of two steps
+    and the updated weights of the second decoder layer."""
+    from tests.dist_harness import run_workers
+
+    try:
+        ref = run_workers(_sp_train_worker, 2, "rccl", 3, timeout=300)
+        got = run_workers(_sp_train_worker, 2, "xgmi", 3, timeout=300)
+    except RuntimeError as e:
+        if "IPC" in str(e) or "hipIpc" in str(e):
+            pytest.skip(f"IPC on a shared GPU unsupported here: {e}")
+        raise
+    for (l_ref, sd_ref, tr_ref, _), (l_got, sd_got, tr_got, pair) in zip(ref, got):
+        assert tr_ref == "rccl" and tr_got == "xgmi" and pair
+        for a, b in zip(l_ref, l_got):
+            assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (l_ref, l_got)
+        for k in sd_ref:
+            assert rel(sd_got[k], sd_ref[k]) < 2e-2, k
