@@ -120,6 +120,11 @@ class _CPAttnFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        """Two phases per chunk (csrc/flash_attn.hip's dS-materialising backward): first
+        every chunk's dK/dV pass (dS tiles stored), then the dK/dV reduce-scatter is issued
+        ASYNC and the chunks' dQ passes (dQ = dS K, HBM-bound) run while it is in flight;
+        it is joined only at the very end.  (Shapes the dS path does not take run the
+        one-shot backward in phase 1.)"""
         q, kv_g, out = ctx.saved_tensors[:3]
         lses = ctx.saved_tensors[3:]
         H, Hkv, D, scale, zigzag, chunks, S = ctx.meta
@@ -130,23 +135,46 @@ class _CPAttnFn(torch.autograd.Function):
         dout = dout.contiguous()
         order = sorted(range(len(chunks)), key=lambda i: -(chunks[i][2] + chunks[i][1]))  # widest prefix first
         covered = 0
+        pending_dq = []  # (chunk, workspace) whose dQ pass runs under the reduce-scatter
+        native = _lib.use_native(q)
         for i in order:
             off, n, g0 = chunks[i]
             kend = g0 + n
             args = (dout[:, off: off + n], q[:, off: off + n], k_full[:, :kend], v_full[:, :kend],
                     out[:, off: off + n].contiguous(), lses[i], scale, True, g0, 0)
-            if covered == 0:
+            first = covered == 0
+            if first:
                 dkv[:, kend:].zero_()
-                ops.flash_attn_bwd(*args, dq=dq[:, off: off + n], dk=dkv[:, :kend, :Hkv], dv=dkv[:, :kend, Hkv:])
                 covered = kend
-            else:
-                dq_c, dk_c, dv_c = ops.flash_attn_bwd(*args, dq=dq[:, off: off + n])
+            ws = None
+            if native:
+                dk_c, dv_c, ws = _lib.ops().flash_bwd_kv(*args, dkv[:, :kend, :Hkv] if first else None,
+                                                         dkv[:, :kend, Hkv:] if first else None)
+                if ws.numel():
+                    pending_dq.append((i, ws))
+                else:
+                    ws = None
+            if ws is None:  # one-shot backward (dQ now)
+                if first:
+                    ops.flash_attn_bwd(*args, dq=dq[:, off: off + n], dk=dkv[:, :kend, :Hkv],
+                                       dv=dkv[:, :kend, Hkv:])
+                    continue
+                _, dk_c, dv_c = ops.flash_attn_bwd(*args, dq=dq[:, off: off + n])
+            if not first:
                 dkv[:, :kend, :Hkv] += dk_c
                 dkv[:, :kend, Hkv:] += dv_c
         if zigzag:
             dkv = dkv.index_select(1, _inverse(_global_order_index(S, cp, q.device)))  # back to rank order
-        dkv_local = _reduce_scatter_seq_dim1(dkv.contiguous(), group)
-        return dq, dkv_local.contiguous(), None, None, None, None, None
+        xt = dkv.transpose(0, 1).contiguous()
+        trace.record("cp.dkv_reduce_scatter", xt, group_size=cp, overlapped=bool(pending_dq))
+        rs, work = C.reduce_scatter(xt, group=group, async_op=True)
+        for i, ws in pending_dq:  # dQ passes under the reduce-scatter
+            off, n, g0 = chunks[i]
+            _lib.ops().flash_bwd_q_ds(q[:, off: off + n], k_full[:, :g0 + n], ws, scale, True, g0, 0,
+                                      dq[:, off: off + n])
+        if work is not None:
+            work.wait()
+        return dq, rs.transpose(0, 1).contiguous(), None, None, None, None, None
 
 
 def _chunks_of(rank: int, S: int, cp: int, s: int, zigzag: bool):
