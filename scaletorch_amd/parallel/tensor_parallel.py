@@ -492,20 +492,33 @@ def _rows_gemm(x2: torch.Tensor, weight: torch.Tensor, out: torch.Tensor) -> Non
     torch.matmul(x2, weight.t(), out=out)
 
 
-def _bmm_into(x3: torch.Tensor, b2: torch.Tensor, out3: torch.Tensor) -> None:
-    """``out3[b] = x3[b] @ b2`` for every batch element in ONE strided-batched GEMM.
+def _bmm_into(x3: torch.Tensor, b2: torch.Tensor, out3: torch.Tensor, mode: str | None = None) -> None:
+    """``out3[b] = x3[b] @ b2`` for every batch element; ``x3`` [B, M, K] and ``out3`` [B, M, N]
+    may be sequence slices of larger [B, S, .] tensors (batch stride != M * row stride).
 
-    ``x3`` [B, M, K] and ``out3`` [B, M, N] may be row blocks of larger tensors
-    (batch stride != M * row stride: a sequence slice of [B, S, .]); ``b2`` [K, N]
-    is shared (batch stride 0).  hipBLASLt takes those strides as they are, so the
-    sequence-parallel pieces run as one [B*M, K] x [K, N] product instead of B
-    separate [M, K] GEMMs (with B = 4 and M = 1024 those were 48-tile launches on
-    256 CUs, profiles/r04/sp_gemm_split.json)."""
-    B = x3.shape[0]
+    ``fold`` (default): ONE [B*M, K] x [K, N] GEMM -- the input slice is gathered into a
+    contiguous buffer when it is strided, the output written in place when contiguous,
+    else through one strided copy; ``loop``: one 2-D GEMM per batch element straight
+    on the strided views (the round-3 form).  ``tools/bench_sp_gemm.py`` times both
+    against the unsplit GEMM at the tp2pp2dp2 shapes (profiles/r04/).  Only plain 2-D
+    GEMMs are issued: a strided-batched torch.bmm with a stride-0 weight and a strided
+    output faulted on ROCm 7 here (illegal address), so it is not used."""
+    import os
+
+    B, M, K = x3.shape
     if B == 1:
         torch.matmul(x3[0], b2, out=out3[0])
         return
-    torch.bmm(x3, b2.unsqueeze(0).expand(B, -1, -1), out=out3)
+    mode = mode or os.environ.get("ST_SP_GEMM", "fold")
+    if mode == "loop":
+        for b in range(B):
+            torch.matmul(x3[b], b2, out=out3[b])
+        return
+    x2 = x3.reshape(B * M, K)
+    if out3.is_contiguous():
+        torch.matmul(x2, b2, out=out3.view(B * M, out3.shape[-1]))
+    else:
+        out3.copy_(torch.matmul(x2, b2).view(B, M, out3.shape[-1]))
 
 
 def _dgrad_b2(weight: torch.Tensor) -> torch.Tensor:
