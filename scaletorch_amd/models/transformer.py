@@ -111,12 +111,19 @@ class MLP(nn.Module):
         self.gate_up_proj = FusedColumnParallelLinear(cfg.hidden_size, [I, I], ["gate_proj", "up_proj"],
                                                       sequence_parallel=sequence_parallel, **init)
         self.down_proj = RowParallelLinear(I, cfg.hidden_size, sequence_parallel=sequence_parallel, **init)
+        # the fused SP MLP path reads both weights directly (DataParallel bucket waits)
+        self._st_reads = (self.gate_up_proj, self.down_proj)
 
     def reset_parameters(self) -> None:
         self.gate_up_proj.reset_parameters()
         self.down_proj.reset_parameters()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        from ..parallel.tensor_parallel import sp_mlp_applies, sp_mlp
+
+        if sp_mlp_applies(self, x):
+            # the whole SP MLP in the gathered row layout (tensor_parallel._SPMLPFn)
+            return sp_mlp(x, self.gate_up_proj.weight, self.down_proj.weight, self.gate_up_proj.group)
         return self.down_proj(self.gate_up_proj(x), act="swiglu")
 
 

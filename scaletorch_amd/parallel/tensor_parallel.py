@@ -664,6 +664,156 @@ class _SPColumnParallelFn(torch.autograd.Function):
         return scatter(), dw, db, None
 
 
+def _swiglu_fwd(gu: torch.Tensor) -> torch.Tensor:
+    from ..ops import _lib
+
+    if gu.is_cuda and _lib.use_native(gu) and gu.dtype == torch.bfloat16:
+        return _lib.ops().swiglu_fwd(gu.contiguous())
+    g, u = gu.chunk(2, dim=-1)
+    return F.silu(g) * u
+
+
+def _swiglu_bwd(da: torch.Tensor, gu: torch.Tensor) -> torch.Tensor:
+    from ..ops import _lib
+
+    if gu.is_cuda and _lib.use_native(gu) and gu.dtype == torch.bfloat16:
+        return _lib.ops().swiglu_bwd(da.contiguous(), gu.contiguous())
+    g, u = gu.float().chunk(2, dim=-1)
+    sg = torch.sigmoid(g)
+    d = da.float()
+    return torch.cat([d * u * (sg + g * sg * (1 - sg)), d * g * sg], dim=-1).to(gu.dtype)
+
+
+def _peer_ranges(ws: int, r: int) -> list[tuple[int, int]]:
+    """Contiguous ranges of peer ranks (everyone but r): at most two."""
+    return [(a, b) for a, b in ((0, r), (r + 1, ws)) if b > a]
+
+
+def _wgrad_pieces(weight: torch.Tensor, pieces) -> torch.Tensor | None:
+    """dW = sum_p dy_p^T x_p straight into ``weight.main_grad`` (the first piece overwrites a
+    fresh accumulator, the rest add; ONE grad-ready signal), or returned for autograd."""
+    from ..ops.grad import _grad_ready, take_fresh, wgrad_into
+
+    mg = getattr(weight, "main_grad", None)
+    if mg is None:
+        dw = None
+        for dy2, x2 in pieces:
+            p = dy2.t().mm(x2)
+            dw = p if dw is None else dw + p
+        return dw
+    fresh = take_fresh(weight)
+    m2 = mg.view(mg.shape[0], -1)
+    for i, (dy2, x2) in enumerate(pieces):
+        wgrad_into(m2, dy2, x2, 0 if (fresh and i == 0) else 1)
+    _grad_ready(weight)
+    return None
+
+
+class _SPMLPFn(torch.autograd.Function):
+    """The whole sequence-parallel SwiGLU MLP (gate|up column GEMM -> SwiGLU -> down row
+    GEMM) in the GATHERED layout: the intermediate rows are kept in the order the
+    sequence all-gather delivers them, [sub-chunk q][rank j][sequence b][Sc rows],
+    instead of [b][S].  Every GEMM piece is then one contiguous 2-D product over all B
+    sequences -- the gate|up rows of (q, j) land in one block, the down projection of
+    sub-chunk q is ONE [ws*B*Sc] GEMM that writes its reduce-scatter buffer directly --
+    with no strided writes, no per-sequence loops and no layout copies; only the [B, Sp]
+    shard at the ends is in sequence order.  The gather of sub-chunk q+1 and the
+    reduce-scatter of sub-chunk q overlap the GEMMs (RCCL async, or the xGMI pair path on
+    its comm side stream).  Backward re-gathers x and gathers dY per sub-chunk (same
+    layout), runs dgrad -> SwiGLU backward -> dgrad per sub-chunk with each dX
+    reduce-scatter in flight under the next, and accumulates both weight gradients over
+    the sub-chunks into main_grad.  Reference: the Llama MLP with
+    AllGather/ReduceScatterFromSequenceParallelRegion around it,
+    scaletorch/models/llama.py:236-249, scaletorch/parallel/sequence_parallel/sp_comms.py:31-94."""
+
+    @staticmethod
+    def forward(ctx, x_shard, w_gu, w_dn, group):
+        ws, r = _ws(group), C.get_rank(group)
+        B, Sp, h = x_shard.shape
+        c = _sp_chunks(Sp, B * Sp * ws)
+        Sc = Sp // c
+        n2, I = w_gu.shape[0], w_dn.shape[1]
+        if x_shard.requires_grad:
+            prepare_dgrad_weight(w_gu)
+            prepare_dgrad_weight(w_dn)
+        xs = x_shard.contiguous()
+        parts = [xs[:, q * Sc:(q + 1) * Sc].contiguous() if c > 1 else xs for q in range(c)]
+        gathers = [_sp_gather_async(p, group) for p in parts]  # [ws*B, Sc, h] each, rank-major
+        gu = torch.empty(c, ws, B * Sc, n2, dtype=xs.dtype, device=xs.device)
+        wgu_t, wdn_t = w_gu.t(), w_dn.t()
+        for q in range(c):  # own rows while the gathers are in flight
+            torch.matmul(parts[q].view(B * Sc, h), wgu_t, out=gu[q, r])
+        y = torch.empty(B, Sp, h, dtype=xs.dtype, device=xs.device)
+        scatters, acts = [], []
+        for q, (buf, work) in enumerate(gathers):
+            work.wait()
+            for j0, j1 in _peer_ranges(ws, r):
+                torch.matmul(buf[j0 * B:j1 * B].reshape(-1, h), wgu_t, out=gu[q, j0:j1].view(-1, n2))
+            a_q = _swiglu_fwd(gu[q]).view(-1, I)  # [ws*B*Sc, I]: kept for the down weight gradient
+            acts.append(a_q)
+            rs_in = torch.matmul(a_q, wdn_t).view(ws * B, Sc, h)
+            scatters.append(_sp_reduce_scatter_async(rs_in, group))  # -> [B, Sc, h]
+        for q, (out, work) in enumerate(scatters):
+            work.wait()
+            y[:, q * Sc:(q + 1) * Sc] = out
+        ctx.save_for_backward(xs, gu, w_gu, w_dn, *acts)
+        ctx.group, ctx.c = group, c
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xs, gu, w_gu, w_dn = ctx.saved_tensors[:4]
+        acts = ctx.saved_tensors[4:]
+        group, c = ctx.group, ctx.c
+        ws = _ws(group)
+        B, Sp, h = xs.shape
+        Sc = Sp // c
+        n2, I = w_gu.shape[0], w_dn.shape[1]
+        dys = dy.contiguous()
+        dgathers = [_sp_gather_async(dys[:, q * Sc:(q + 1) * Sc].contiguous() if c > 1 else dys, group)
+                    for q in range(c)]
+        xgathers = [_sp_gather_async(xs[:, q * Sc:(q + 1) * Sc].contiguous() if c > 1 else xs, group)
+                    for q in range(c)]
+        b_dn, b_gu = _dgrad_b2(w_dn), _dgrad_b2(w_gu)  # [h, I] and [2I, h] right operands
+        dx = torch.empty(B, Sp, h, dtype=dys.dtype, device=dys.device)
+        scatters, dn_pieces, dgus = [], [], []
+        for q, (dbuf, work) in enumerate(dgathers):
+            work.wait()
+            dY = dbuf.reshape(-1, h)
+            da = torch.matmul(dY, b_dn)  # [ws*B*Sc, I]
+            dgu_q = _swiglu_bwd(da, gu[q].view(-1, n2))
+            dgus.append(dgu_q)
+            dn_pieces.append((dY, acts[q]))
+            dxf = torch.matmul(dgu_q, b_gu).view(ws * B, Sc, h)
+            scatters.append(_sp_reduce_scatter_async(dxf, group))
+        dw_dn = _wgrad_pieces(w_dn, dn_pieces) if ctx.needs_input_grad[2] else None
+        gu_pieces = []
+        for q, (xbuf, work) in enumerate(xgathers):
+            work.wait()
+            gu_pieces.append((dgus[q], xbuf.reshape(-1, h)))
+        dw_gu = _wgrad_pieces(w_gu, gu_pieces) if ctx.needs_input_grad[1] else None
+        for q, (out, work) in enumerate(scatters):
+            work.wait()
+            dx[:, q * Sc:(q + 1) * Sc] = out
+        return dx, dw_gu, dw_dn, None
+
+
+def sp_mlp_applies(mlp, x: torch.Tensor) -> bool:
+    """The gathered-layout SP MLP takes this call: TP > 1 with sequence parallelism,
+    bias-free projections, a [B, Sp, h] shard, training with gradients
+    (``ST_SP_MLP=0``: the per-projection SP path, A/B)."""
+    import os
+
+    gu, dn = mlp.gate_up_proj, mlp.down_proj
+    return (gu.tp > 1 and gu.sequence_parallel and dn.sequence_parallel and gu.bias is None and dn.bias is None
+            and x.dim() == 3 and torch.is_grad_enabled() and os.environ.get("ST_SP_MLP", "1") == "1"
+            and _sp_overlap(x))
+
+
+def sp_mlp(x_shard: torch.Tensor, w_gu: torch.Tensor, w_dn: torch.Tensor, group) -> torch.Tensor:
+    return _SPMLPFn.apply(x_shard, w_gu, w_dn, group)
+
+
 class _SPRowParallelFn(torch.autograd.Function):
     """Sequence-parallel row linear: y_shard = reduce_scatter_seq(x W^T), pipelined.
 

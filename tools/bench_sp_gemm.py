@@ -113,6 +113,35 @@ def main() -> int:
         out[name]["per_element_vs_unsplit"] = round(t["unsplit"] / t["per_element"], 3)
         out[name]["rel_err_fold_vs_loop"] = err
         print(name, json.dumps(out[name]), flush=True)
+    # the SP MLP in the gathered layout (tensor_parallel._SPMLPFn): every piece is a contiguous
+    # 2-D GEMM -- gate|up over [B*Sc] rows per (q, own / peer block), down over [ws*B*Sc] per q
+    I2, Il = 2 * I // ws, I // ws
+    wgu = torch.randn(I2, h, device=dev, dtype=torch.bfloat16) * 0.02
+    wdn = torch.randn(h, Il, device=dev, dtype=torch.bfloat16) * 0.02
+    xg = torch.randn(c, ws, B * Sc, h, device=dev, dtype=torch.bfloat16)
+    gu = torch.empty(c, ws, B * Sc, I2, device=dev, dtype=torch.bfloat16)
+    a = torch.randn(c, ws * B * Sc, Il, device=dev, dtype=torch.bfloat16)
+    rs = torch.empty(c, ws * B * Sc, h, device=dev, dtype=torch.bfloat16)
+    xf = xg.view(-1, h)
+    guf = torch.empty(B * S, I2, device=dev, dtype=torch.bfloat16)
+    af = a.view(-1, Il)
+    yf = torch.empty(B * S, h, device=dev, dtype=torch.bfloat16)
+
+    def mlp_pieces():
+        for q in range(c):
+            torch.matmul(xg[q, 0], wgu.t(), out=gu[q, 0])            # own rows
+            torch.matmul(xg[q, 1:].reshape(-1, h), wgu.t(), out=gu[q, 1:].view(-1, I2))  # peers
+            torch.matmul(a[q], wdn.t(), out=rs[q])                    # down: one GEMM per sub-chunk
+
+    def mlp_unsplit():
+        torch.matmul(xf, wgu.t(), out=guf)
+        torch.matmul(af, wdn.t(), out=yf)
+
+    flops = 2.0 * B * S * h * (I2 + Il)
+    t = {"unsplit": _time(mlp_unsplit), "gathered_layout": _time(mlp_pieces)}
+    out["mlp_gathered_layout"] = {k + "_tflops": round(flops / v / 1e9, 1) for k, v in t.items()}
+    out["mlp_gathered_layout"]["pieces_vs_unsplit"] = round(t["unsplit"] / t["gathered_layout"], 3)
+    print("mlp_gathered_layout", json.dumps(out["mlp_gathered_layout"]), flush=True)
     print(json.dumps(out, indent=1))
     return 0
 
