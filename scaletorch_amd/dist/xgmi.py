@@ -59,6 +59,13 @@ def _blocks_for(nbytes: int) -> int:
     return int(min(256, max(8, nbytes // (64 << 10))))
 
 
+def _ep_blocks(area_rows: int, x: torch.Tensor, world: int) -> int:
+    """Workgroups of an EP exchange: sized by the HOST bound of the rows moved (identical on
+    every rank -- the per-block handshake pairs block b of every rank), one per ~64 KiB of
+    a rank's share, 8..256; every block of every rank must be co-resident for the barrier."""
+    return _blocks_for(area_rows * x.shape[1] * x.element_size() // max(1, world))
+
+
 _MODES = {"oneshot": 0, "twoshot": 1, "all_gather": 2, "reduce_scatter": 3, "all_to_all": 4,
           "pair_all_gather": 5, "pair_reduce_scatter": 6}
 
@@ -204,13 +211,15 @@ class XgmiAllReduce:
         rows).  ``M`` [world, E] int32 device counts (``ep_counts``); ``area_rows`` the
         host bound of rows landing in one rank's buffer.  No host sync."""
         out = torch.empty(out_rows, x.shape[1], dtype=x.dtype, device=x.device)
-        _ops().xgmi_ep_exchange(self.id, x.contiguous(), out, M, El, direction, area_rows, 0)
+        _ops().xgmi_ep_exchange(self.id, x.contiguous(), out, M, El, direction, area_rows,
+                                _ep_blocks(area_rows, x, self.world))
         return out
 
     @staticmethod
     def ep_exchange_sim(comms, xs, M, El: int, direction: int, out_rows: int, area_rows: int):
         outs = [torch.empty(out_rows, x.shape[1], dtype=x.dtype, device=x.device) for x in xs]
-        _ops().xgmi_ep_exchange_sim([c.id for c in comms], xs, outs, M, El, direction, area_rows, 0)
+        _ops().xgmi_ep_exchange_sim([c.id for c in comms], xs, outs, M, El, direction, area_rows,
+                                    _ep_blocks(area_rows, xs[0], len(comms)))
         return outs
 
     def _pair_ok(self, n_elems: int, t: torch.Tensor) -> bool:
