@@ -561,18 +561,24 @@ __global__ __launch_bounds__(kThreads) void ep_exchange_kernel(Peers P, Jobs J, 
   auto qpos = [&](int s, int64_t i, int g) -> int64_t { return (int64_t)sEO[g] + sSO[s][g] + (i - sP[s][g]); };
   const rsrc_t mine = buf_rsrc(P.buf[me], cap);
   if (A.dir == 0) {
-    // phase 1, as a source: push my block's sorted rows to their owners' areas (expert-major slots)
+    // phase 1, as a source: push my block's sorted rows to their owners' areas (expert-major
+    // slots), owner by owner -- the buffer descriptor of the destination must be
+    // wave-uniform (buf_rsrc reads the base from lane 0), so one pass per owner
     int64_t lo, hi;
     range(me, lo, hi);
-    for (int64_t v = threadIdx.x; v < (hi - lo) * rowb; v += blockDim.x) {
-      const int64_t i = lo + v / rowb, c = v % rowb;
-      const int g = ep_find(sP[me], E, (int)i);
-      const int64_t q = qpos(me, i, g);
-      if (q >= A.area_rows || i >= A.in_rows) {
-        atomicExch(jb.err, 2);
-        continue;
+    for (int d = 0; d < world; ++d) {
+      const int64_t a = max(lo, (int64_t)sP[me][d * El]), z = min(hi, (int64_t)sP[me][(d + 1) * El]);
+      if (z <= a) continue;  // uniform: a, z come from LDS tables and block-uniform bounds
+      const rsrc_t dst = buf_rsrc(P.buf[d], cap);
+      for (int64_t v = threadIdx.x; v < (z - a) * rowb; v += blockDim.x) {
+        const int64_t i = a + v / rowb, c = v % rowb;
+        const int64_t q = qpos(me, i, ep_find(sP[me], E, (int)i));
+        if (q >= A.area_rows || i >= A.in_rows) {
+          atomicExch(jb.err, 2);
+          continue;
+        }
+        put8<T>(dst, area_off<T>(0, parity, cap, q * rowb + c), in + (i * rowb + c) * 8);
       }
-      put8<T>(buf_rsrc(P.buf[g / El], cap), area_off<T>(0, parity, cap, q * rowb + c), in + (i * rowb + c) * 8);
     }
     if (!block_barrier(P, me, world, 0, epoch, jb.err, jb.timeout)) return;
     // phase 2, as the owner: copy out the rows block b of every source wrote into my area
