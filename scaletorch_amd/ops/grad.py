@@ -251,7 +251,8 @@ def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> int:
     if not arms:
         _WGRAD_CHOICE[key] = 0
         return 0
-    if _one_t_ok(dy2d, x2d):  # 3: hipBLASLt on the smaller operand made token-contiguous (transpose timed in)
+    if _one_t_ok(dy2d, x2d) and os.environ.get("ST_WGRAD_ONE_T", "1") == "1":
+        # 3: hipBLASLt on the smaller operand made token-contiguous (transpose timed in)
         arms[3] = lambda: _wgrad_one_t(scratch, dy2d, x2d, 1)
 
     def blas():
