@@ -125,10 +125,8 @@ extern "C" {
 // ST_ADAMW_BLOCKS caps the grid (grid-stride loop): a small grid leaves most CUs
 // to the GEMMs of the forward pass the side-stream update overlaps (optim.py).
 static unsigned adamw_grid(int64_t n4) {
-  static const long cap = [] {
-    const char* e = std::getenv("ST_ADAMW_BLOCKS");
-    return e ? std::atol(e) : 0L;
-  }();
+  const char* e = std::getenv("ST_ADAMW_BLOCKS");  // read per launch: same-process A/B (tools/ab_step.py)
+  const long cap = e ? std::atol(e) : 0L;
   unsigned g = grid_for(n4);
   if (cap > 0 && g > (unsigned)cap) g = (unsigned)cap;
   return g;

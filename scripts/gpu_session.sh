@@ -12,6 +12,7 @@ for s in $STEPS; do
     sp_gemm) step sp_gemm 240 python tools/bench_sp_gemm.py || exit $? ;;
     newk) step new_kernels 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_kernels_gpu.py tests/test_xgmi_gpu.py -m gpu -k "swiglu_epilogue or fused_matches or ep_exchange or ipc or grouped" || exit $? ;;
     onet_ab) step onet_ab 900 python tools/ab_step.py --variants ST_WGRAD_ONE_T=1,ST_WGRAD_ONE_T=0 --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 || exit $? ;;
+    adamw_ab) step adamw_ab 900 python tools/ab_step.py --variants ST_ADAMW_BLOCKS=0,ST_ADAMW_BLOCKS=1024,ST_ADAMW_BLOCKS=256,ST_ADAMW_BLOCKS=64 --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 || exit $? ;;
     cp_reorder) step cp_reorder 240 python tools/bench_cp_reorder.py || exit $? ;;
     opt_probe) step opt_probe 900 python tools/ab_step.py --variants ST_OPT_PROBE_SKIP=0,ST_OPT_PROBE_SKIP=1 --rounds 4 --steps 3 --micro_batch_size 6 --fused_head 1 || exit $? ;;
     moe) step mx_proxy 400 python bench.py --layout mixtral_ep8 --micro_batch_size 2 --grad_acc 1 --layers 4 --steps 5 --warmup 2 || exit $?
