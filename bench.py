@@ -158,6 +158,9 @@ def main() -> int:
     ap.add_argument("--layers", type=int, default=None, help="(debug only; result marked invalid)")
     ap.add_argument("--moe_capacity_factor", type=float, default=None,
                     help="EP dispatch: 0 dropless (one host read of the counts per layer), > 0 static capacity")
+    ap.add_argument("--opt_state_dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="AdamW moment dtype (bf16 = the reference's own optimizer-state precision; "
+                         "fp32 master weights either way)")
     ap.add_argument("--moe_ep_chunks", type=int, default=None, help="EP dispatch chunks (capacity mode)")
     args = ap.parse_args()
     launched = "WORLD_SIZE" in os.environ
@@ -210,7 +213,8 @@ def main() -> int:
                                gradient_checkpointing=(args.recompute if args.gc else False),
                                grad_reduce_dtype=args.grad_reduce_dtype,
                                fused_head_chunk=args.head_chunk if args.fused_head else 0,
-                               moe_dropless=args.moe_capacity_factor == 0 and args.ep > 1)
+                               moe_dropless=args.moe_capacity_factor == 0 and args.ep > 1,
+                               optimizer_state_dtype=args.opt_state_dtype)
     if int(os.environ.get("RANK", "0")) == 0:
         print(f"[bench] layout {args.layout}: {args.model} tp{args.tp} pp{args.pp} cp{args.cp} ep{args.ep} dp{dp} "
               f"mbs{args.micro_batch_size} ga{ga} seq{args.seq_len}; HBM estimate {est.summary()}",
@@ -229,6 +233,7 @@ def main() -> int:
         num_hidden_layers=args.layers, dtype="bfloat16", weight_decay=0.1, betas=(0.9, 0.95),
         zero_stage=args.zero, fused_lm_head=bool(args.fused_head), lm_head_chunk_tokens=args.head_chunk,
         moe_capacity_factor=args.moe_capacity_factor, moe_ep_chunks=args.moe_ep_chunks,
+        optimizer_state_dtype=args.opt_state_dtype,
     )
     if args.backend == "gloo" and torch.cuda.is_available():  # 1-GPU multi-rank rehearsal
         from scaletorch_amd.dist.gloo_staging import stage_gloo_cuda_p2p
@@ -319,7 +324,8 @@ def main() -> int:
                    "parallelism": par, "layout": args.layout, "sequence_parallel": args.sp, "activation_checkpointing": args.gc,
                    "virtual_pipeline": args.vpp if args.pp > 1 else 1,
                    "lm_head": f"fused, {args.head_chunk}-token chunks" if args.fused_head else "logits + CE",
-                   "grad_reduce_dtype": args.grad_reduce_dtype, "zero_stage": args.zero if dp * args.cp * args.ep > 1 else 0},
+                   "grad_reduce_dtype": args.grad_reduce_dtype, "zero_stage": args.zero if dp * args.cp * args.ep > 1 else 0,
+                   "optimizer": f"AdamW, fp32 master, {args.opt_state_dtype} moments"},
         "tokens_per_s_per_gpu": round(per_gpu, 1),
         "mfu_pct": round(mfu, 2),
         "mfu_pct_causal_flops": round(per_gpu * fpt_causal / peak * 100, 2),

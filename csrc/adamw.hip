@@ -32,15 +32,50 @@ ST_DEVICE float4 load_g4<bf16_t>(const bf16_t* g, int64_t i) {
                      __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u));
 }
 
-template <typename G>
-__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, float* __restrict__ m,
-                                                     float* __restrict__ v, const G* __restrict__ g,
+// Optimizer moments: fp32 (default) or bf16 (ST optimizer_state_dtype="bf16": the
+// reference's own state precision, torch AdamW on bf16 params; the fp32 master
+// weights stay).  bf16 moments cut the pass from 30 to 22 B/param.
+template <typename S>
+ST_DEVICE f32x4 load_s4(const S* s, int64_t i);
+template <>
+ST_DEVICE f32x4 load_s4<float>(const float* s, int64_t i) {
+  return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(s + i));
+}
+template <>
+ST_DEVICE f32x4 load_s4<bf16_t>(const bf16_t* s, int64_t i) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(s + i));
+  f32x4 r;
+  r[0] = __uint_as_float(v[0] << 16);
+  r[1] = __uint_as_float(v[0] & 0xffff0000u);
+  r[2] = __uint_as_float(v[1] << 16);
+  r[3] = __uint_as_float(v[1] & 0xffff0000u);
+  return r;
+}
+template <typename S>
+ST_DEVICE void store_s4(S* s, int64_t i, f32x4 v);
+template <>
+ST_DEVICE void store_s4<float>(float* s, int64_t i, f32x4 v) {
+  __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(s + i));
+}
+template <>
+ST_DEVICE void store_s4<bf16_t>(bf16_t* s, int64_t i, f32x4 v) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  u32x2 o;
+  o[0] = pack_bf16x2(v[0], v[1]);
+  o[1] = pack_bf16x2(v[2], v[3]);
+  __builtin_nontemporal_store(o, reinterpret_cast<u32x2*>(s + i));
+}
+
+template <typename G, typename S>
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, S* __restrict__ m,
+                                                     S* __restrict__ v, const G* __restrict__ g,
                                                      bf16_t* __restrict__ p, const float* __restrict__ clip,
                                                      int64_t n4, float lr, float b1, float b2, float eps,
                                                      float wd, float bc1, float bc2_sqrt) {
   const float cs = clip ? *clip : 1.f;
   const float step = lr / bc1, decay = 1.f - lr * wd;
-  // Two 16-B chunks per thread per iteration, all loads issued before any math
+  // Two 4-element chunks per thread per iteration, all loads issued before any math
   // (10 independent HBM streams in flight per thread); every byte is touched
   // exactly once, so loads/stores are non-temporal (no L2 pollution).
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -53,8 +88,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, 
     for (int u = 0; u < 2; ++u) {
       if (u < nv) {
         w[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(master + ii[u]));
-        mm[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(m + ii[u]));
-        vv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(v + ii[u]));
+        mm[u] = load_s4<S>(m, ii[u]);
+        vv[u] = load_s4<S>(v, ii[u]);
         gg[u] = load_g4<G>(g, ii[u]);
       }
     }
@@ -71,8 +106,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, 
         w[u][k] = w[u][k] * decay - step * mm[u][k] / denom;
       }
       __builtin_nontemporal_store(w[u], reinterpret_cast<f32x4*>(master + ii[u]));
-      __builtin_nontemporal_store(mm[u], reinterpret_cast<f32x4*>(m + ii[u]));
-      __builtin_nontemporal_store(vv[u], reinterpret_cast<f32x4*>(v + ii[u]));
+      store_s4<S>(m, ii[u], mm[u]);
+      store_s4<S>(v, ii[u], vv[u]);
       if (p) {
         uint2 o;
         o.x = pack_bf16x2(w[u][0], w[u][1]);
@@ -81,6 +116,98 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, 
       }
     }
   }
+}
+
+// AdamW over ONE 2-D weight [R, C] (a contiguous run of the arena) that ALSO writes
+// the updated bf16 weight transposed, W^T [C, R], for the data-gradient GEMM's TN
+// layout (ops/grad.py): the side-stream transpose the next forward would launch per
+// weight re-reads W (2 B/elt) in a separate pass -- here the update already holds the
+// new values in registers, so W^T costs only its 2 B/elt of writes and no launch.
+// Tile 64 x 64 per 256-thread workgroup: 16 lanes x 4 fp32 cover one 256-B row of
+// master / m / v / g (4 passes of 16 rows, all loads issued before any math); the
+// bf16 results go row-major to p and into a padded LDS tile, which is read back by
+// columns so each lane stores 16 B of W^T (8 lanes = one 128-B W^T row segment).
+constexpr int kWT = 64, kWLd = kWT + 2;
+
+template <typename G, typename S>
+__global__ __launch_bounds__(256) void adamw_wt_kernel(float* __restrict__ master, S* __restrict__ m,
+                                                        S* __restrict__ v, const G* __restrict__ g,
+                                                        bf16_t* __restrict__ p, bf16_t* __restrict__ wt,
+                                                        const float* __restrict__ clip, int R, int C, float lr,
+                                                        float b1, float b2, float eps, float wd, float bc1,
+                                                        float bc2_sqrt) {
+  __shared__ bf16_t tile[kWT * kWLd];
+  const float cs = clip ? *clip : 1.f;
+  const float step = lr / bc1, decay = 1.f - lr * wd;
+  const int tiles_c = C / kWT;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int r0 = (b / tiles_c) * kWT, c0 = (b % tiles_c) * kWT;
+  const int t = threadIdx.x;
+  const int lc = (t & 15) * 4, lr0 = t >> 4;  // 4 columns of one row; rows lr0 + 16 * pass
+  f32x4 w[4], mm[4], vv[4];
+  float4 gg[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t i = (int64_t)(r0 + lr0 + 16 * u) * C + c0 + lc;
+    w[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(master + i));
+    mm[u] = load_s4<S>(m, i);
+    vv[u] = load_s4<S>(v, i);
+    gg[u] = load_g4<G>(g, i);
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t i = (int64_t)(r0 + lr0 + 16 * u) * C + c0 + lc;
+    const float ga[4] = {gg[u].x, gg[u].y, gg[u].z, gg[u].w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gk = ga[k] * cs;
+      mm[u][k] = b1 * mm[u][k] + (1.f - b1) * gk;
+      vv[u][k] = b2 * vv[u][k] + (1.f - b2) * gk * gk;
+      const float denom = sqrtf(vv[u][k]) / bc2_sqrt + eps;
+      w[u][k] = w[u][k] * decay - step * mm[u][k] / denom;
+    }
+    __builtin_nontemporal_store(w[u], reinterpret_cast<f32x4*>(master + i));
+    store_s4<S>(m, i, mm[u]);
+    store_s4<S>(v, i, vv[u]);
+    const uint32_t lo = pack_bf16x2(w[u][0], w[u][1]), hi = pack_bf16x2(w[u][2], w[u][3]);
+    *reinterpret_cast<uint2*>(p + i) = make_uint2(lo, hi);
+    // padded LDS row (132 B): 4-B aligned only
+    uint32_t* d = reinterpret_cast<uint32_t*>(tile + (lr0 + 16 * u) * kWLd + lc);
+    d[0] = lo;
+    d[1] = hi;
+  }
+  __syncthreads();
+  const int chunk = t & 7, row = t >> 3;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int oc = row + 32 * q;  // W^T row = W column
+    BF8 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t a = tile[(chunk * 8 + 2 * j) * kWLd + oc];
+      const uint32_t c = tile[(chunk * 8 + 2 * j + 1) * kWLd + oc];
+      o.w[j] = a | (c << 16);
+    }
+    st8(wt + (int64_t)(c0 + oc) * R + r0 + chunk * 8, o);
+  }
+}
+
+template <typename S>
+int launch_adamw_wt(float* master, S* m, S* v, const void* g, int g_is_bf16, void* p, void* wt,
+                    const float* clip, int R, int C, float lr, float b1, float b2, float eps, float wd,
+                    float bc1, float bc2_sqrt, hipStream_t st) {
+  if (R % kWT || C % kWT || R <= 0 || C <= 0) return -2;
+  const int64_t blocks = (int64_t)(R / kWT) * (C / kWT);
+  if (blocks > 0x7fffffff) return -3;
+  if (g_is_bf16)
+    adamw_wt_kernel<bf16_t, S><<<(unsigned)blocks, 256, 0, st>>>(master, m, v, (const bf16_t*)g, (bf16_t*)p,
+                                                                 (bf16_t*)wt, clip, R, C, lr, b1, b2, eps, wd,
+                                                                 bc1, bc2_sqrt);
+  else
+    adamw_wt_kernel<float, S><<<(unsigned)blocks, 256, 0, st>>>(master, m, v, (const float*)g, (bf16_t*)p,
+                                                                (bf16_t*)wt, clip, R, C, lr, b1, b2, eps, wd,
+                                                                bc1, bc2_sqrt);
+  return 0;
 }
 
 // Stage 1 of the squared L2 norm: per-block partial sums (deterministic).
@@ -118,13 +245,9 @@ inline unsigned grid_for(int64_t n4) {
   return (unsigned)b;
 }
 
-}  // namespace
-
-extern "C" {
-
 // ST_ADAMW_BLOCKS caps the grid (grid-stride loop): a small grid leaves most CUs
 // to the GEMMs of the forward pass the side-stream update overlaps (optim.py).
-static unsigned adamw_grid(int64_t n4) {
+unsigned adamw_grid(int64_t n4) {
   const char* e = std::getenv("ST_ADAMW_BLOCKS");  // read per launch: same-process A/B (tools/ab_step.py)
   const long cap = e ? std::atol(e) : 0L;
   unsigned g = grid_for(n4);
@@ -132,18 +255,48 @@ static unsigned adamw_grid(int64_t n4) {
   return g;
 }
 
-int st_adamw_step(float* master, float* m, float* v, const void* g, int g_is_bf16, void* p,
-                  const float* clip, int64_t n, float lr, float b1, float b2, float eps, float wd,
-                  float bc1, float bc2_sqrt, hipStream_t st) {
+template <typename S>
+void launch_adamw(float* master, S* m, S* v, const void* g, int g_is_bf16, void* p,
+                         const float* clip, int64_t n4, float lr, float b1, float b2, float eps,
+                         float wd, float bc1, float bc2_sqrt, hipStream_t st) {
+  if (g_is_bf16)
+    adamw_kernel<bf16_t, S><<<adamw_grid(n4), 256, 0, st>>>(master, m, v, (const bf16_t*)g, (bf16_t*)p,
+                                                          clip, n4, lr, b1, b2, eps, wd, bc1, bc2_sqrt);
+  else
+    adamw_kernel<float, S><<<adamw_grid(n4), 256, 0, st>>>(master, m, v, (const float*)g, (bf16_t*)p,
+                                                         clip, n4, lr, b1, b2, eps, wd, bc1, bc2_sqrt);
+}
+
+}  // namespace
+
+extern "C" {
+
+// states_bf16: exp_avg / exp_avg_sq are bf16 arrays (else fp32)
+int st_adamw_step(float* master, void* m, void* v, int states_bf16, const void* g, int g_is_bf16,
+                  void* p, const float* clip, int64_t n, float lr, float b1, float b2, float eps,
+                  float wd, float bc1, float bc2_sqrt, hipStream_t st) {
   if (n % 4 != 0) return -2;
   const int64_t n4 = n / 4;
   if (n4 == 0) return 0;
-  if (g_is_bf16)
-    adamw_kernel<bf16_t><<<adamw_grid(n4), 256, 0, st>>>(master, m, v, (const bf16_t*)g, (bf16_t*)p,
-                                                       clip, n4, lr, b1, b2, eps, wd, bc1, bc2_sqrt);
+  if (states_bf16)
+    launch_adamw<bf16_t>(master, (bf16_t*)m, (bf16_t*)v, g, g_is_bf16, p, clip, n4, lr, b1, b2, eps, wd,
+                         bc1, bc2_sqrt, st);
   else
-    adamw_kernel<float><<<adamw_grid(n4), 256, 0, st>>>(master, m, v, (const float*)g, (bf16_t*)p,
-                                                      clip, n4, lr, b1, b2, eps, wd, bc1, bc2_sqrt);
+    launch_adamw<float>(master, (float*)m, (float*)v, g, g_is_bf16, p, clip, n4, lr, b1, b2, eps, wd, bc1,
+                        bc2_sqrt, st);
+  return (int)hipGetLastError();
+}
+
+// AdamW over one [R, C] weight run + its bf16 transpose W^T [C, R] (see adamw_wt_kernel)
+int st_adamw_wt_step(float* master, void* m, void* v, int states_bf16, const void* g, int g_is_bf16,
+                     void* p, void* wt, int R, int C, const float* clip, float lr, float b1, float b2,
+                     float eps, float wd, float bc1, float bc2_sqrt, hipStream_t st) {
+  const int rc = states_bf16
+                     ? launch_adamw_wt<bf16_t>(master, (bf16_t*)m, (bf16_t*)v, g, g_is_bf16, p, wt, clip, R, C,
+                                               lr, b1, b2, eps, wd, bc1, bc2_sqrt, st)
+                     : launch_adamw_wt<float>(master, (float*)m, (float*)v, g, g_is_bf16, p, wt, clip, R, C, lr,
+                                              b1, b2, eps, wd, bc1, bc2_sqrt, st);
+  if (rc) return rc;
   return (int)hipGetLastError();
 }
 

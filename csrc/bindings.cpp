@@ -27,9 +27,12 @@ int st_rope_inplace(void* x, const float* cos_t, const float* sin_t, const int64
 int st_swiglu_fwd(const void* gu, void* out, int64_t N, int64_t I, const int* nvalid, hipStream_t st);
 int st_swiglu_bwd(const void* dout, const void* gu, void* dgu, int64_t N, int64_t I, const int* nvalid,
                   hipStream_t st);
-int st_adamw_step(float* master, float* m, float* v, const void* g, int g_is_bf16, void* p,
-                  const float* clip, int64_t n, float lr, float b1, float b2, float eps, float wd,
-                  float bc1, float bc2_sqrt, hipStream_t st);
+int st_adamw_step(float* master, void* m, void* v, int states_bf16, const void* g, int g_is_bf16,
+                  void* p, const float* clip, int64_t n, float lr, float b1, float b2, float eps,
+                  float wd, float bc1, float bc2_sqrt, hipStream_t st);
+int st_adamw_wt_step(float* master, void* m, void* v, int states_bf16, const void* g, int g_is_bf16,
+                     void* p, void* wt, int R, int C, const float* clip, float lr, float b1, float b2,
+                     float eps, float wd, float bc1, float bc2_sqrt, hipStream_t st);
 int st_sumsq_partials();
 int st_sumsq(const void* g, int g_is_bf16, int64_t n, float* partial, float* out, hipStream_t st);
 int st_xent_fwd(const void* logits, int64_t ld, const int64_t* tgt, int64_t N, int V,
@@ -266,9 +269,10 @@ void adamw_step_(at::Tensor master, at::Tensor exp_avg, at::Tensor exp_avg_sq,
   const int64_t n = master.numel();
   TORCH_CHECK(exp_avg.numel() == n && exp_avg_sq.numel() == n && grad.numel() == n,
               "adamw: arena sizes differ");
-  TORCH_CHECK(exp_avg.scalar_type() == at::kFloat && exp_avg_sq.scalar_type() == at::kFloat &&
+  const bool sbf = exp_avg.scalar_type() == at::kBFloat16;
+  TORCH_CHECK((exp_avg.scalar_type() == at::kFloat || sbf) && exp_avg_sq.scalar_type() == exp_avg.scalar_type() &&
                   exp_avg.is_contiguous() && exp_avg_sq.is_contiguous() && grad.is_contiguous(),
-              "adamw: states must be contiguous fp32");
+              "adamw: states must be contiguous fp32 or bf16 (both the same)");
   TORCH_CHECK(grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16,
               "adamw: grad must be fp32 or bf16");
   TORCH_CHECK(n % 4 == 0, "adamw: arena length must be a multiple of 4");
@@ -291,12 +295,51 @@ void adamw_step_(at::Tensor master, at::Tensor exp_avg, at::Tensor exp_avg_sq,
   const double bc1 = 1.0 - std::pow(beta1, (double)step);
   const double bc2 = 1.0 - std::pow(beta2, (double)step);
   c10::hip::HIPGuardMasqueradingAsCUDA g(master.device());
-  int rc = st_adamw_step(master.data_ptr<float>(), exp_avg.data_ptr<float>(),
-                         exp_avg_sq.data_ptr<float>(), grad.data_ptr(),
+  int rc = st_adamw_step(master.data_ptr<float>(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
+                         sbf ? 1 : 0, grad.data_ptr(),
                          grad.scalar_type() == at::kBFloat16 ? 1 : 0, pp, cp, n, (float)lr,
                          (float)beta1, (float)beta2, (float)eps, (float)weight_decay, (float)bc1,
                          (float)std::sqrt(bc2), cur_stream());
   ST_CHECK_RC(rc, "adamw_step_");
+}
+
+// AdamW over one 2-D weight's arena run that also writes the updated bf16 weight
+// transposed into `wt` [C, R] (param is the [R, C] weight view of the arena)
+void adamw_wt_step_(at::Tensor master, at::Tensor exp_avg, at::Tensor exp_avg_sq, const at::Tensor& grad,
+                    at::Tensor param, at::Tensor wt, const c10::optional<at::Tensor>& clip_coef, double lr,
+                    double beta1, double beta2, double eps, double weight_decay, int64_t step) {
+  TORCH_CHECK(param.dim() == 2 && param.is_contiguous(), "adamw_wt: param must be a contiguous 2-D weight");
+  check_bf16_cuda(param, "param");
+  check_bf16_cuda(wt, "wt");
+  const int64_t R = param.size(0), C = param.size(1), n = R * C;
+  TORCH_CHECK(wt.dim() == 2 && wt.size(0) == C && wt.size(1) == R && wt.is_contiguous(), "adamw_wt: wt must be [C, R]");
+  TORCH_CHECK(R % 64 == 0 && C % 64 == 0 && R <= INT32_MAX && C <= INT32_MAX, "adamw_wt: R, C multiples of 64");
+  TORCH_CHECK(master.is_cuda() && master.scalar_type() == at::kFloat && master.is_contiguous() && master.numel() == n,
+              "adamw_wt: master must be contiguous fp32 of the weight's size");
+  const bool sbf = exp_avg.scalar_type() == at::kBFloat16;
+  TORCH_CHECK((exp_avg.scalar_type() == at::kFloat || sbf) && exp_avg_sq.scalar_type() == exp_avg.scalar_type() &&
+                  exp_avg.is_contiguous() && exp_avg_sq.is_contiguous() && exp_avg.numel() == n &&
+                  exp_avg_sq.numel() == n,
+              "adamw_wt: states must be contiguous fp32 or bf16 of the weight's size");
+  TORCH_CHECK((grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16) && grad.is_contiguous() &&
+                  grad.numel() == n,
+              "adamw_wt: grad must be contiguous fp32 or bf16 of the weight's size");
+  for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{&exp_avg, &exp_avg_sq, &grad, &param, &wt})
+    check_same_gpu(*t, master, "adamw_wt operand");
+  const float* cp = nullptr;
+  if (clip_coef.has_value() && clip_coef->defined()) {
+    TORCH_CHECK(clip_coef->scalar_type() == at::kFloat && clip_coef->numel() == 1, "adamw_wt: clip");
+    check_same_gpu(*clip_coef, master, "clip_coef");
+    cp = clip_coef->data_ptr<float>();
+  }
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(master.device());
+  int rc = st_adamw_wt_step(master.data_ptr<float>(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(), sbf ? 1 : 0,
+                            grad.data_ptr(), grad.scalar_type() == at::kBFloat16 ? 1 : 0, param.data_ptr(),
+                            wt.data_ptr(), (int)R, (int)C, cp, (float)lr, (float)beta1, (float)beta2, (float)eps,
+                            (float)weight_decay, (float)bc1, (float)std::sqrt(bc2), cur_stream());
+  ST_CHECK_RC(rc, "adamw_wt_step_");
 }
 
 // grad[V, H] fp32 += rows of dy[T, H] bf16 grouped by token id; sorted_ids / order from a
@@ -988,6 +1031,7 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("swiglu_fwd(Tensor gate_up, Tensor? nvalid=None) -> Tensor");
   m.def("swiglu_bwd(Tensor dout, Tensor gate_up, Tensor? nvalid=None) -> Tensor");
   m.def("adamw_step_(Tensor(a!) master, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor grad, Tensor(d!)? param, Tensor? clip_coef, float lr, float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
+  m.def("adamw_wt_step_(Tensor(a!) master, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor grad, Tensor(d!) param, Tensor(e!) wt, Tensor? clip_coef, float lr, float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
   m.def("sumsq_(Tensor g, Tensor(a!) out) -> ()");
   m.def("transpose_(Tensor src, Tensor(a!) dst) -> ()");
   m.def("embedding_bwd_(Tensor(a!) grad, Tensor dy, Tensor sorted_ids, Tensor order) -> ()");
@@ -1029,6 +1073,7 @@ TORCH_LIBRARY_IMPL(st_amd, CUDA, m) {
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("adamw_step_", &adamw_step_);
+  m.impl("adamw_wt_step_", &adamw_wt_step_);
   m.impl("sumsq_", &sumsq_);
   m.impl("transpose_", &transpose_);
   m.impl("embedding_bwd_", &embedding_bwd_);

@@ -41,6 +41,14 @@ def bump_weight_epoch() -> None:
     _WT_EPOCH[0] += 1
 
 
+def invalidate_wt(params) -> None:
+    """The weights were overwritten outside the optimizer (checkpoint / HF load): drop
+    their W^T copies, including one the fused AdamW pass left pending."""
+    for w in params:
+        w._st_wt_pending = None
+        w._st_wt_epoch = -1
+
+
 def _wt_enabled(w: torch.Tensor) -> bool:
     return (w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2 and w.shape[0] % 64 == 0
             and w.shape[1] % 64 == 0 and getattr(w, "main_grad", None) is not None
@@ -57,6 +65,14 @@ def prepare_dgrad_weight(w: torch.Tensor) -> None:
     if not _lib.use_native(w):
         return
     if getattr(w, "_st_wt_epoch", -1) == _WT_EPOCH[0]:
+        return
+    pending = getattr(w, "_st_wt_pending", None)
+    if pending is not None:
+        # the side-stream AdamW pass already wrote W^T with the updated weight
+        # (optim.py ``_step_overlapped``, csrc/adamw.hip adamw_wt_kernel): adopt it
+        w._st_wt_pending = None
+        w._st_wt_done = pending
+        w._st_wt_epoch = _WT_EPOCH[0]
         return
     if os.environ.get("ST_DGRAD_WT_PROBE_STALE") == "1" and getattr(w, "_st_wt", None) is not None:
         # timing probe only (WRONG gradients): reuse the previous step's W^T, no transpose

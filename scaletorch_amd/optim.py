@@ -4,7 +4,9 @@ Reference: ``create_optimizer`` (scaletorch/trainer/model_builder.py:103-162:
 adamw[fused] / adam / sgd(m=0.9) / lamb->adamw) and ``clip_gradients``
 (scaletorch/trainer/train_step.py:122-136, a LOCAL clip_grad_norm_).
 
-* ``ArenaAdamW``: fp32 master weights + fp32 exp_avg / exp_avg_sq per arena;
+* ``ArenaAdamW``: fp32 master weights + fp32 (or, ``state_dtype="bf16"``, bf16 --
+  the reference's own state precision: 22 instead of 30 B/param per step and
+  8 B/param less memory) exp_avg / exp_avg_sq per arena;
   on GPU one fused HIP kernel (csrc/adamw.hip) per arena updates master, m, v
   and writes the bf16 model copy -- the whole step is 1-2 launches.  The
   reference kept bf16 params AND bf16 optimizer states (no master weights).
@@ -74,8 +76,11 @@ class _ArenaOptimizer(torch.optim.Optimizer):
     def reload_masters(self) -> None:
         """Re-read the fp32 master copy from the (externally overwritten) bf16 params,
         e.g. after an HF weight import into a model whose optimizer already exists."""
+        from .ops.grad import invalidate_wt
+
         self.sync()
         for a in self.arenas:
+            invalidate_wt(a.params)
             if a.master is None:
                 continue
             a.wait_params()
@@ -162,6 +167,9 @@ class _ArenaOptimizer(torch.optim.Optimizer):
             self._load_arena_state(a, s)
 
     def _load_arena_state(self, a, s) -> None:
+        from .ops.grad import invalidate_wt
+
+        invalidate_wt(a.params)
         if s.get("master") is not None and a.master is not None:
             a.master.copy_(s["master"].to(a.master.device))
             for lo, hi, so in a.segments():
@@ -172,12 +180,13 @@ class _ArenaOptimizer(torch.optim.Optimizer):
 
 class ArenaAdamW(_ArenaOptimizer):
     def __init__(self, dp_model, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0, fused: bool = True, decoupled: bool = True):
+                 weight_decay: float = 0.0, fused: bool = True, decoupled: bool = True, state_dtype: str = "fp32"):
         super().__init__(dp_model, lr, dict(betas=tuple(betas), eps=eps, weight_decay=weight_decay))
         self.fused = fused
         self.decoupled = decoupled
+        sd = {"fp32": torch.float32, "bf16": torch.bfloat16}[state_dtype]
         for a in self.arenas:
-            a.exp_avg = torch.zeros(a.state_numel, dtype=torch.float32, device=a.param_flat.device)
+            a.exp_avg = torch.zeros(a.state_numel, dtype=sd, device=a.param_flat.device)
             a.exp_avg_sq = torch.zeros_like(a.exp_avg)
 
     def _native(self, a) -> bool:
@@ -198,6 +207,7 @@ class ArenaAdamW(_ArenaOptimizer):
         # timing probe only (WRONG training: the weights never change): ST_OPT_PROBE_SKIP=1
         # skips every update kernel, so an A/B prices what the side-stream AdamW costs the step
         skip = os.environ.get("ST_OPT_PROBE_SKIP") == "1"
+        fuse_wt = os.environ.get("ST_ADAMW_WT", "1") == "1"
         with torch.cuda.stream(st):
             st.wait_event(ev)
             for g, a in zip(self.param_groups, self.arenas):
@@ -205,10 +215,22 @@ class ArenaAdamW(_ArenaOptimizer):
                 for b in reversed(a.buckets):
                     lo, hi, so = b.shard_lo, b.shard_hi, b.state_lo
                     n = hi - lo
+                    fused = []
                     if n and not skip:
-                        _lib.ops().adamw_step_(a.master[so: so + n], a.exp_avg[so: so + n],
-                                               a.exp_avg_sq[so: so + n], a.grad_flat[lo:hi],
-                                               a.param_flat[lo:hi], self.clip_coef, lr, b1, b2, eps, wd, t)
+                        plan = self._wt_plan(a, b) if fuse_wt and not a.zero1 else [("flat", lo, hi, None)]
+                        for kind, plo, phi, w in plan:
+                            if kind == "flat":
+                                s0 = so + plo - lo
+                                _lib.ops().adamw_step_(a.master[s0: s0 + phi - plo], a.exp_avg[s0: s0 + phi - plo],
+                                                       a.exp_avg_sq[s0: s0 + phi - plo], a.grad_flat[plo:phi],
+                                                       a.param_flat[plo:phi], self.clip_coef, lr, b1, b2, eps, wd, t)
+                            else:
+                                s0 = so + plo - lo
+                                _lib.ops().adamw_wt_step_(a.master[s0: s0 + phi - plo], a.exp_avg[s0: s0 + phi - plo],
+                                                          a.exp_avg_sq[s0: s0 + phi - plo], a.grad_flat[plo:phi],
+                                                          a.param_flat[plo:phi].view(w.shape), w._st_wt,
+                                                          self.clip_coef, lr, b1, b2, eps, wd, t)
+                                fused.append(w)
                     if a.zero1:
                         trace.record("dp.all_gather", a.param_flat[b.start: b.end], group_size=a.world, arena=a.name)
                         b.ag_handle = dist.all_gather_into_tensor(a.param_flat[b.start: b.end],
@@ -217,6 +239,34 @@ class ArenaAdamW(_ArenaOptimizer):
                     else:
                         b.opt_event = torch.cuda.Event()
                         b.opt_event.record(st)
+                        for w in fused:
+                            w._st_wt_pending = b.opt_event
+
+    def _wt_plan(self, a, b) -> list:
+        """The bucket's update as launches: ("wt", lo, hi, w) for every weight that keeps a
+        W^T copy for its data-gradient GEMM (ops/grad.py) -- updated by the kernel that
+        also writes W^T -- and ("flat", lo, hi, None) for the runs between them."""
+        from .ops.grad import _wt_enabled
+
+        offs = getattr(a, "_st_off_of", None)
+        if offs is None:
+            offs = a._st_off_of = {id(p): o for p, o in zip(a.params, a.offsets)}
+        runs = []
+        for w in b.params:
+            wt = getattr(w, "_st_wt", None)
+            if wt is not None and _wt_enabled(w) and wt.shape == (w.shape[1], w.shape[0]):
+                o = offs[id(w)]
+                runs.append((o, o + w.numel(), w))
+        runs.sort(key=lambda r: r[0])
+        plan, cur = [], b.shard_lo
+        for o, e, w in runs:
+            if o > cur:
+                plan.append(("flat", cur, o, None))
+            plan.append(("wt", o, e, w))
+            cur = e
+        if cur < b.shard_hi:
+            plan.append(("flat", cur, b.shard_hi, None))
+        return plan
 
     @torch.no_grad()
     def step(self, closure=None):  # noqa: ARG002
@@ -239,8 +289,14 @@ class ArenaAdamW(_ArenaOptimizer):
                     grad = grad * self.clip_coef
                 if not self.decoupled and wd:
                     grad = grad + wd * master
+                m_st, v_st = m, v
+                if m.dtype != torch.float32:  # bf16 moments: fp32 math, one rounding per step (as the kernel)
+                    m, v = m.float(), v.float()
                 m.mul_(b1).add_(grad, alpha=1 - b1)
                 v.mul_(b2).addcmul_(grad, grad, value=1 - b2)
+                if m_st is not m:
+                    m_st.copy_(m)
+                    v_st.copy_(v)
                 bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
                 denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
                 if self.decoupled and wd:
@@ -257,6 +313,7 @@ class ArenaAdamW(_ArenaOptimizer):
 
     def _load_arena_state(self, a, s) -> None:
         super()._load_arena_state(a, s)
+        # copy_ converts: an fp32-state checkpoint resumes into bf16 states and vice versa
         a.exp_avg.copy_(s["exp_avg"].to(a.exp_avg.device))
         a.exp_avg_sq.copy_(s["exp_avg_sq"].to(a.exp_avg_sq.device))
 
@@ -322,9 +379,13 @@ class ArenaLAMB(ArenaAdamW):
             grad = a.grad_flat.float()
             if self.clip_coef is not None:
                 grad = grad * self.clip_coef
-            a.exp_avg.mul_(b1).add_(grad, alpha=1 - b1)
-            a.exp_avg_sq.mul_(b2).addcmul_(grad, grad, value=1 - b2)
-            upd = (a.exp_avg / (1 - b1 ** t)) / ((a.exp_avg_sq / (1 - b2 ** t)).sqrt() + eps)
+            m, v = a.exp_avg.float(), a.exp_avg_sq.float()
+            m.mul_(b1).add_(grad, alpha=1 - b1)
+            v.mul_(b2).addcmul_(grad, grad, value=1 - b2)
+            if m is not a.exp_avg:
+                a.exp_avg.copy_(m)
+                a.exp_avg_sq.copy_(v)
+            upd = (m / (1 - b1 ** t)) / ((v / (1 - b2 ** t)).sqrt() + eps)
             if wd:
                 upd.add_(master, alpha=wd)
             for p, o in zip(a.params, a.offsets):
@@ -338,12 +399,13 @@ class ArenaLAMB(ArenaAdamW):
 
 
 def create_optimizer(dp_model, optimizer_type: str = "adamw", lr: float = 1e-3, weight_decay: float = 0.0,
-                     betas=(0.9, 0.999), eps: float = 1e-8, use_fused_adam: bool = True):
+                     betas=(0.9, 0.999), eps: float = 1e-8, use_fused_adam: bool = True, state_dtype: str = "fp32"):
     t = optimizer_type.lower()
     if t == "adamw":
-        return ArenaAdamW(dp_model, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, fused=use_fused_adam)
+        return ArenaAdamW(dp_model, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, fused=use_fused_adam,
+                          state_dtype=state_dtype)
     if t == "adam":
-        return ArenaAdam(dp_model, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        return ArenaAdam(dp_model, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, state_dtype=state_dtype)
     if t == "sgd":
         return ArenaSGD(dp_model, lr=lr, momentum=0.9, weight_decay=weight_decay)
     if t == "lamb":

@@ -143,8 +143,13 @@ class OptimizerArguments:
     betas: list[float] = field(default_factory=lambda: [0.9, 0.999], metadata={"help": "two floats"})
     learning_rate: float = field(default=1e-3)
     adam_eps: float = field(default=1e-8)
+    optimizer_state_dtype: str = field(
+        default="fp32", metadata={"help": "AdamW exp_avg / exp_avg_sq dtype: fp32 | bf16 (the reference's own "
+                                          "state precision; fp32 master weights are kept either way)"})
 
     def __post_init__(self) -> None:
+        if self.optimizer_state_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"optimizer_state_dtype must be fp32 or bf16, got {self.optimizer_state_dtype!r}")
         if self.optimizer_type not in _VALID_OPTIMIZERS:
             raise ValueError(f"optimizer_type must be one of {sorted(_VALID_OPTIMIZERS)}, got {self.optimizer_type}")
         if self.learning_rate <= 0:

@@ -115,7 +115,8 @@ class Trainer:
         self.model = DataParallel(model, bucket_size=bucket, reduce_dtype=a.grad_reduce_dtype,
                                   zero1=a.zero_stage >= 1)
         self.optimizer = create_optimizer(self.model, a.optimizer_type, a.learning_rate, a.weight_decay,
-                                          a.betas, a.adam_eps, a.use_fused_adam)
+                                          a.betas, a.adam_eps, a.use_fused_adam,
+                                          state_dtype=a.optimizer_state_dtype)
         self.total_steps = a.total_train_steps or 1000
         self.lr_scheduler = create_lr_scheduler(self.optimizer, a.lr_scheduler_type, self.total_steps,
                                                 a.warmup_steps, a.T_max, a.eta_min, a.power, a.step_size, a.gamma,

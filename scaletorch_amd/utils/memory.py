@@ -53,7 +53,7 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
                          sequence_parallel: bool = False, gradient_checkpointing: bool = False,
                          pp_engine: str = "1f1b", grad_reduce_dtype: str = "bf16",
                          fused_head_chunk: int = 0, recompute_swiglu: bool | None = None,
-                         moe_dropless: bool = False) -> MemoryEstimate:
+                         moe_dropless: bool = False, optimizer_state_dtype: str = "fp32") -> MemoryEstimate:
     """Worst-rank estimate (first pipeline stage for activations, largest stage for weights).
 
     ``fused_head_chunk`` > 0: the fused chunked LM head (ops/fused_head.py) -- one
@@ -79,7 +79,8 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
     n = dense + expert
     dense_dp = dp * cp * ep
     expert_dp = dp * cp
-    opt = 12 * (dense / (dense_dp if zero1 else 1) + expert / (expert_dp if zero1 else 1))
+    opt_bytes = 4 + (4 if optimizer_state_dtype == "bf16" else 8)  # fp32 master + m/v
+    opt = opt_bytes * (dense / (dense_dp if zero1 else 1) + expert / (expert_dp if zero1 else 1))
     # activations of the micro-batches a rank holds at once
     tokens = micro_batch * seq_len / cp
     if pp > 1:

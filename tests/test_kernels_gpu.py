@@ -146,6 +146,57 @@ def test_adamw_and_sumsq():
     assert abs(out.item() - ref) / ref < 1e-5
 
 
+def test_adamw_bf16_moments():
+    """bf16 exp_avg / exp_avg_sq (optimizer_state_dtype="bf16"): fp32 math on the
+    widened moments, the update uses the unrounded fp32 moments, one bf16 rounding
+    (nearest-even) per stored moment -- checked against an fp32 PyTorch reference."""
+    torch.manual_seed(0)
+    n = 4096 * 33 + 8
+    master = torch.randn(n, device="cuda")
+    m = (torch.randn(n, device="cuda") * 0.01).to(torch.bfloat16)
+    v = (torch.rand(n, device="cuda") * 0.01).to(torch.bfloat16)
+    g = torch.randn(n, device="cuda")
+    p = master.to(torch.bfloat16)
+    mr, vr, wr = m.float(), v.float(), master.clone()
+    lr, b1, b2, eps, wd, t = 1e-3, 0.9, 0.95, 1e-8, 0.1, 3
+    _lib.ops().adamw_step_(master, m, v, g, p, None, lr, b1, b2, eps, wd, t)
+    mr.mul_(b1).add_(g, alpha=1 - b1)
+    vr.mul_(b2).addcmul_(g, g, value=1 - b2)
+    wr.mul_(1 - lr * wd)
+    wr.addcdiv_(mr / (1 - b1 ** t), (vr / (1 - b2 ** t)).sqrt() + eps, value=-lr)
+    assert (m.float() - mr).abs().le(mr.abs() * 2 ** -8 + 1e-30).all()
+    assert (v.float() - vr).abs().le(vr.abs() * 2 ** -8 + 1e-30).all()
+    assert (master - wr).abs().max().item() < 1e-6
+    assert rel(p, wr) < 1e-2
+
+
+@pytest.mark.parametrize("sd", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("RC", [(192, 320), (1024, 64)])
+def test_adamw_wt_matches_flat_update_and_transpose(sd, RC):
+    """The fused AdamW + W^T pass (csrc/adamw.hip adamw_wt_kernel) == the flat AdamW
+    kernel followed by a transpose, bitwise (same per-element math), for fp32 and bf16
+    moments, a non-square weight and a one-tile-wide one."""
+    torch.manual_seed(0)
+    R, C = RC
+    n = R * C
+    master = torch.randn(n, device="cuda")
+    m = (torch.randn(n, device="cuda") * 0.01).to(sd)
+    v = (torch.rand(n, device="cuda") * 0.01).to(sd)
+    g = torch.randn(n, device="cuda")
+    p = master.to(torch.bfloat16).view(R, C)
+    wt = torch.empty(C, R, device="cuda", dtype=torch.bfloat16)
+    clip = torch.tensor([0.7], device="cuda")
+    ref = [x.clone() for x in (master, m, v, p)]
+    args = (1e-3, 0.9, 0.95, 1e-8, 0.1, 5)
+    _lib.ops().adamw_step_(ref[0], ref[1], ref[2], g, ref[3].view(-1), clip, *args)
+    _lib.ops().adamw_wt_step_(master, m, v, g, p, wt, clip, *args)
+    assert torch.equal(master, ref[0]) and torch.equal(m, ref[1]) and torch.equal(v, ref[2])
+    assert torch.equal(p, ref[3])
+    assert torch.equal(wt, ref[3].t())
+    with pytest.raises(RuntimeError):
+        _lib.ops().adamw_wt_step_(master, m, v, g, p, wt.t(), clip, *args)  # wt must be [C, R] contiguous
+
+
 @pytest.mark.parametrize("V", [512, 32000])
 def test_cross_entropy(V):
     torch.manual_seed(0)

@@ -1,4 +1,5 @@
 """CPU unit tests: mesh math, config, schedulers, data, models, checkpoints, utils."""
+import itertools
 import math
 import os
 
@@ -564,3 +565,37 @@ def test_ep_owner_positions_match_bruteforce_layout():
         backs = ep_exchange_reference(got, M, El, 1, 0)
         for s in range(ep):
             assert torch.equal(backs[s], xs[s])
+
+
+def test_bf16_optimizer_moments_track_fp32(tmp_path):
+    """optimizer_state_dtype="bf16" (the reference's own AdamW state precision, fp32
+    master kept): bf16 moments, the same losses as fp32 moments to bf16 accuracy, and a
+    checkpoint written with fp32 moments resumes into bf16 moments (and back)."""
+    from scaletorch_amd.trainer.engine import Trainer
+    from scaletorch_amd.utils.checkpoint import CheckpointManager, latest_checkpoint
+
+    def run(sd):
+        torch.manual_seed(0)
+        a = ScaleTorchArguments(model_name_or_path="tiny-llama", synthetic_data=True, micro_batch_size=2,
+                                sequence_length=32, use_cpu=True, dtype="bfloat16", total_train_steps=6,
+                                optimizer_state_dtype=sd, learning_rate=1e-3, warmup_steps=0,
+                                lr_scheduler_type="constant")
+        tr = Trainer(a)
+        batch = next(tr.data)
+        tr.data = itertools.repeat(batch)
+        return tr, [float(tr.train_step()) for _ in range(5)]
+
+    tr32, l32 = run("fp32")
+    tr16, l16 = run("bf16")
+    assert all(a.exp_avg.dtype == torch.bfloat16 for a in tr16.optimizer.arenas)
+    assert l16[-1] < l16[0]
+    for x, y in zip(l32, l16):
+        assert abs(x - y) < 0.02 * abs(x)
+    cm = CheckpointManager(str(tmp_path))
+    cm.save_checkpoint(tr32.model, tr32.optimizer, 5, 320)
+    cm.wait()
+    tr16.optimizer.load_state_dict(tr32.optimizer.state_dict())
+    for a16, a32 in zip(tr16.optimizer.arenas, tr32.optimizer.arenas):
+        assert torch.equal(a16.exp_avg, a32.exp_avg.to(torch.bfloat16))
+        assert torch.equal(a16.master, a32.master)
+    assert latest_checkpoint(str(tmp_path)) is not None
