@@ -158,6 +158,9 @@ def main() -> int:
     ap.add_argument("--layers", type=int, default=None, help="(debug only; result marked invalid)")
     ap.add_argument("--moe_capacity_factor", type=float, default=None,
                     help="EP dispatch: 0 dropless (one host read of the counts per layer), > 0 static capacity")
+    ap.add_argument("--gemm_tuning", default="auto", choices=["auto", "use", "tune", "off"],
+                    help="TunableOp table for the library GEMMs (utils/gemm_tuning.py); tune: time every "
+                         "solution of each new GEMM signature in the warm-up and add it to the table")
     ap.add_argument("--opt_state_dtype", default="fp32", choices=["fp32", "bf16"],
                     help="AdamW moment dtype (bf16 = the reference's own optimizer-state precision; "
                          "fp32 master weights either way)")
@@ -233,7 +236,7 @@ def main() -> int:
         num_hidden_layers=args.layers, dtype="bfloat16", weight_decay=0.1, betas=(0.9, 0.95),
         zero_stage=args.zero, fused_lm_head=bool(args.fused_head), lm_head_chunk_tokens=args.head_chunk,
         moe_capacity_factor=args.moe_capacity_factor, moe_ep_chunks=args.moe_ep_chunks,
-        optimizer_state_dtype=args.opt_state_dtype,
+        optimizer_state_dtype=args.opt_state_dtype, gemm_tuning=args.gemm_tuning,
     )
     if args.backend == "gloo" and torch.cuda.is_available():  # 1-GPU multi-rank rehearsal
         from scaletorch_amd.dist.gloo_staging import stage_gloo_cuda_p2p
@@ -259,6 +262,12 @@ def main() -> int:
     for _ in range(args.warmup):
         loss = tr.train_step()
     sync()
+    if tr.gemm_tuning == "tune":  # tuned in the warm-up: save the table, time with lookups only
+        from scaletorch_amd.utils import gemm_tuning
+
+        if rank == 0:
+            gemm_tuning.finish()
+        torch.cuda.tunable.tuning_enable(False)
     from scaletorch_amd.dist import trace as comm_trace
 
     comm0 = comm_trace.stats()  # host-side counters only (a dict increment per collective)
@@ -325,7 +334,8 @@ def main() -> int:
                    "virtual_pipeline": args.vpp if args.pp > 1 else 1,
                    "lm_head": f"fused, {args.head_chunk}-token chunks" if args.fused_head else "logits + CE",
                    "grad_reduce_dtype": args.grad_reduce_dtype, "zero_stage": args.zero if dp * args.cp * args.ep > 1 else 0,
-                   "optimizer": f"AdamW, fp32 master, {args.opt_state_dtype} moments"},
+                   "optimizer": f"AdamW, fp32 master, {args.opt_state_dtype} moments",
+                   "gemm_tuning": tr.gemm_tuning},
         "tokens_per_s_per_gpu": round(per_gpu, 1),
         "mfu_pct": round(mfu, 2),
         "mfu_pct_causal_flops": round(per_gpu * fpt_causal / peak * 100, 2),

@@ -143,6 +143,8 @@ class OptimizerArguments:
     betas: list[float] = field(default_factory=lambda: [0.9, 0.999], metadata={"help": "two floats"})
     learning_rate: float = field(default=1e-3)
     adam_eps: float = field(default=1e-8)
+    gemm_tuning: str = field(
+        default="auto", metadata={"help": "library GEMM solutions (utils/gemm_tuning.py): auto | use | tune | off"})
     optimizer_state_dtype: str = field(
         default="fp32", metadata={"help": "AdamW exp_avg / exp_avg_sq dtype: fp32 | bf16 (the reference's own "
                                           "state precision; fp32 master weights are kept either way)"})

@@ -85,6 +85,12 @@ class Trainer:
             set_cp_comm(a.cp_comm)
         self.device = torch.device("cuda", torch.cuda.current_device()) if (torch.cuda.is_available() and not a.use_cpu) \
             else torch.device("cpu")
+        if self.device.type == "cuda":
+            from ..utils.gemm_tuning import configure as _tune_gemms
+
+            self.gemm_tuning = _tune_gemms(a.gemm_tuning)
+        else:
+            self.gemm_tuning = "off"
         self.dtype = _DTYPES[a.dtype]
         if self.device.type == "cpu" and self.dtype == torch.float16:
             self.dtype = torch.float32

@@ -6,7 +6,15 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 STEPS=${STEPS:-"tests bench"}
-step() { local name=$1 to=$2; shift 2; echo "=== $name"; timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; tail -n 4 "gpurun_out/$name.log" | cut -c1-400; echo "=== $name rc=$rc"; return $rc; }
+step() {
+  local name=$1 to=$2; shift 2; echo "=== $name"
+  # heartbeat: a slow-but-live step (the GPU test suite, a multi-process test) must not
+  # look hung to gpurun's 180-s silence check; each step's own timeout bounds real hangs
+  ( while true; do sleep 60; echo "[$name] alive $(date +%T) $(wc -l < "gpurun_out/$name.log" 2>/dev/null) lines"; done ) & local hb=$!
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?
+  kill $hb 2>/dev/null; wait $hb 2>/dev/null
+  tail -n 4 "gpurun_out/$name.log" | cut -c1-400; echo "=== $name rc=$rc"; return $rc
+}
 for s in $STEPS; do
   case $s in
     sp_gemm) step sp_gemm 240 python tools/bench_sp_gemm.py || exit $? ;;
@@ -18,12 +26,18 @@ for s in $STEPS; do
     moe) step mx_proxy 400 python bench.py --layout mixtral_ep8 --micro_batch_size 2 --grad_acc 1 --layers 4 --steps 5 --warmup 2 || exit $?
          step q3_proxy 400 python bench.py --model qwen3-30b-a3b --layers 4 --micro_batch_size 2 --steps 5 --warmup 2 || exit $? ;;
     moe_prof) step mx_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_mx -o run --output-format csv -- python bench.py --layout mixtral_ep8 --micro_batch_size 2 --grad_acc 1 --layers 4 --steps 3 --warmup 2 || exit $? ;;
-    tests) step gpu_tests 900 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests -m gpu || exit $? ;;
+    tests) step gpu_tests 1000 python -u -m pytest -x -v --timeout 330 --timeout-method thread tests -m gpu || exit $? ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 || exit $? ;;
     bench16) step bench16 600 python bench.py --steps 10 --warmup 3 --opt_state_dtype bf16 || exit $? ;;
     adamk) step adamw_kernels 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_train_gpu.py -m gpu -k "adamw or overlapped or delayed or deterministic" || exit $? ;;
     wt_ab) step wt_ab 900 python tools/ab_step.py --variants ST_ADAMW_WT=1,ST_ADAMW_WT=0 --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 || exit $? ;;
     prof) step step_prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_step -o run --output-format csv -- python bench.py --steps 3 --warmup 2 || exit $? ;;
+    rehearse) step rehearse 1000 env LAYOUTS="${LAYOUTS:-mixtral_ep8 tp2pp2dp2}" LAYOUT_TIMEOUT=400 bash scripts/rehearse_layouts_1gpu.sh || exit $? ;;
+    replay) step replay 1100 python scripts/bench_reference_rows_8gpu.py --rehearse --steps 2 --warmup 1 --timeout 300 \
+              --out gpurun_out/reference_rows_rehearsal.jsonl --filter "${REPLAY_FILTER:-.}" || exit $? ;;
+    # the table is written under gpurun_out/ (merged back) and copied into scaletorch_amd/tuning/ by hand
+    gtune) step gemm_tune 900 env ST_GEMM_TUNING_FILE=gpurun_out/gemm_gfx950.csv python bench.py --steps 1 --warmup 2 --gemm_tuning tune || exit $? ;;
+    gtune_ab) step gemm_tune_ab 900 env ST_GEMM_TUNING_FILE=gpurun_out/gemm_gfx950.csv python tools/ab_step.py --variants TUNABLE=1,TUNABLE=0 --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 --gemm_tuning use || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

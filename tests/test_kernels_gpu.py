@@ -164,8 +164,13 @@ def test_adamw_bf16_moments():
     vr.mul_(b2).addcmul_(g, g, value=1 - b2)
     wr.mul_(1 - lr * wd)
     wr.addcdiv_(mr / (1 - b1 ** t), (vr / (1 - b2 ** t)).sqrt() + eps, value=-lr)
-    assert (m.float() - mr).abs().le(mr.abs() * 2 ** -8 + 1e-30).all()
-    assert (v.float() - vr).abs().le(vr.abs() * 2 ** -8 + 1e-30).all()
+    # one nearest-even rounding: |err| <= 2^-8 |x|, plus an absolute slack for the fp32
+    # fma-vs-mul/add order (visible where b1*m and (1-b1)*g nearly cancel), and almost
+    # every element equals PyTorch's own rounding
+    for got, want in ((m, mr), (v, vr)):
+        err = (got.float() - want).abs()
+        assert err.le(want.abs() * 2 ** -8 + 1e-7).all(), (err - want.abs() * 2 ** -8).max().item()
+        assert (got == want.to(torch.bfloat16)).float().mean().item() > 0.99
     assert (master - wr).abs().max().item() < 1e-6
     assert rel(p, wr) < 1e-2
 

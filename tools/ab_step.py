@@ -25,6 +25,11 @@ def set_variant(tr, name: str, side) -> None:
     if "=" in name:
         for kv in name.split("+"):
             k, v = kv.split("=", 1)
+            if k == "TUNABLE":  # TunableOp table lookups on / off (utils/gemm_tuning.py)
+                import torch
+
+                torch.cuda.tunable.enable(v == "1")
+                continue
             os.environ[k] = v
             if k.startswith("ST_WGRAD"):  # re-run the per-shape wgrad pick under this setting
                 from scaletorch_amd.ops import grad as G
@@ -52,6 +57,8 @@ def main() -> int:
     ap.add_argument("--seq_len", type=int, default=4096)
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--fused_head", type=int, default=0, help="1: fused LM head + CE (bench.py default)")
+    ap.add_argument("--opt_state_dtype", default="fp32")
+    ap.add_argument("--gemm_tuning", default="auto")
     args = ap.parse_args()
     import torch
 
@@ -62,7 +69,8 @@ def main() -> int:
                             sequence_length=args.seq_len, total_train_steps=10_000, learning_rate=3e-4,
                             lr_scheduler_type="constant", warmup_steps=0, max_grad_norm=1.0, dtype="bfloat16",
                             num_hidden_layers=args.layers, weight_decay=0.1, betas=(0.9, 0.95),
-                            fused_lm_head=bool(args.fused_head))
+                            fused_lm_head=bool(args.fused_head), optimizer_state_dtype=args.opt_state_dtype,
+                            gemm_tuning=args.gemm_tuning)
     tr = Trainer(a)
     side = tr.model.side_stream
     variants = args.variants.split(",")

@@ -27,7 +27,7 @@ CLASSES = [  # (class, regex on the kernel name), first match wins
     ("moe_route/permute/combine", r"moe_|topk|permute|combine|gather_rows"),
     ("flash_fwd", r"flash_fwd"),
     ("flash_bwd", r"flash_bwd"),
-    ("adamw", r"adamw_kernel"),
+    ("adamw", r"adamw_kernel|adamw_wt_kernel"),
     ("grad_norm", r"sumsq_kernel|sum_partials_kernel"),
     ("rmsnorm", r"rmsnorm|colsum_kernel"),
     ("swiglu", r"swiglu"),
@@ -61,7 +61,7 @@ def main() -> int:
     else:
         c = sqlite3.connect(args.db)
         rows = c.execute("select name, start, end from kernels order by start").fetchall()
-    ad = [(s, e) for n, s, e in rows if "adamw_kernel" in n]
+    ad = [(s, e) for n, s, e in rows if "adamw_kernel" in n or "adamw_wt_kernel" in n]
     if len(ad) < args.steps + 1:
         print("not enough AdamW launches to find step boundaries", file=sys.stderr)
         return 1
