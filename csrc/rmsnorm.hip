@@ -35,24 +35,48 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
   const size_t base = (size_t)row * h;
   float v[NCH][8];
   float ss = 0.f;
+  // every load of the row is issued before the first store (hipcc otherwise keeps
+  // the residual-sum store of chunk c ahead of chunk c+1's loads: 2 loads in flight)
+  BF8 xa[NCH], ra[RES ? NCH : 1];
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int col = c * 512 + lane * 8;
     if (col < h) {
-      BF8 a = ld8(x + base + col);
-      unpack8(a, v[c]);
+      xa[c] = ld8(x + base + col);
+      if (RES) ra[RES ? c : 0] = ld8(res + base + col);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < h) {
+      unpack8(xa[c], v[c]);
       if (RES) {
         float r[8];
-        unpack8(ld8(res + base + col), r);
+        unpack8(ra[RES ? c : 0], r);
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[c][i] = bf2f(f2bf(v[c][i] + r[i]));
-        st8(sum_out + base + col, pack8(v[c]));
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) ss += v[c][i] * v[c][i];
     } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i) v[c][i] = 0.f;
+    }
+  }
+  // the weight (L2-resident) is requested before any store, so waiting for it does
+  // not also wait for the row's stores (vmcnt counts both)
+  BF8 wa[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < h) wa[c] = ld8(w + col);
+  }
+  if (RES) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < h) st8(sum_out + base + col, pack8(v[c]));
     }
   }
   ss = wave_sum(ss);
@@ -63,7 +87,7 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
     const int col = c * 512 + lane * 8;
     if (col < h) {
       float wf[8], o[8];
-      unpack8(ld8(w + col), wf);
+      unpack8(wa[c], wf);
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = v[c][i] * rs * wf[i];
       st8(y + base + col, pack8(o));
