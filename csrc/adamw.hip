@@ -67,6 +67,18 @@ ST_DEVICE void store_s4<bf16_t>(bf16_t* s, int64_t i, f32x4 v) {
   __builtin_nontemporal_store(o, reinterpret_cast<u32x2*>(s + i));
 }
 
+// One element of the AdamW update, shared by the flat and the W^T-writing kernels so
+// both compile to the same instruction sequence (explicit fmas, no contraction left to
+// the scheduler): the fused pass is bitwise equal to the flat one.
+ST_DEVICE void adam_elem(float& w, float& m, float& v, float g, float b1, float b2, float eps, float step,
+                         float decay, float bc2_sqrt) {
+#pragma clang fp contract(off)
+  m = __builtin_fmaf(b1, m, (1.f - b1) * g);
+  v = __builtin_fmaf(b2, v, ((1.f - b2) * g) * g);
+  const float denom = sqrtf(v) / bc2_sqrt + eps;
+  w = __builtin_fmaf(w, decay, -(step * (m / denom)));
+}
+
 template <typename G, typename S>
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, S* __restrict__ m,
                                                      S* __restrict__ v, const G* __restrict__ g,
@@ -99,11 +111,11 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, 
       const float ga[4] = {gg[u].x, gg[u].y, gg[u].z, gg[u].w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float gk = ga[k] * cs;
-        mm[u][k] = b1 * mm[u][k] + (1.f - b1) * gk;
-        vv[u][k] = b2 * vv[u][k] + (1.f - b2) * gk * gk;
-        const float denom = sqrtf(vv[u][k]) / bc2_sqrt + eps;
-        w[u][k] = w[u][k] * decay - step * mm[u][k] / denom;
+        float wk = w[u][k], mk = mm[u][k], vk = vv[u][k];
+        adam_elem(wk, mk, vk, ga[k] * cs, b1, b2, eps, step, decay, bc2_sqrt);
+        w[u][k] = wk;
+        mm[u][k] = mk;
+        vv[u][k] = vk;
       }
       __builtin_nontemporal_store(w[u], reinterpret_cast<f32x4*>(master + ii[u]));
       store_s4<S>(m, ii[u], mm[u]);
@@ -160,11 +172,11 @@ __global__ __launch_bounds__(256) void adamw_wt_kernel(float* __restrict__ maste
     const float ga[4] = {gg[u].x, gg[u].y, gg[u].z, gg[u].w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float gk = ga[k] * cs;
-      mm[u][k] = b1 * mm[u][k] + (1.f - b1) * gk;
-      vv[u][k] = b2 * vv[u][k] + (1.f - b2) * gk * gk;
-      const float denom = sqrtf(vv[u][k]) / bc2_sqrt + eps;
-      w[u][k] = w[u][k] * decay - step * mm[u][k] / denom;
+      float wk = w[u][k], mk = mm[u][k], vk = vv[u][k];
+      adam_elem(wk, mk, vk, ga[k] * cs, b1, b2, eps, step, decay, bc2_sqrt);
+      w[u][k] = wk;
+      mm[u][k] = mk;
+      vv[u][k] = vk;
     }
     __builtin_nontemporal_store(w[u], reinterpret_cast<f32x4*>(master + i));
     store_s4<S>(m, i, mm[u]);
