@@ -262,12 +262,11 @@ def main() -> int:
     for _ in range(args.warmup):
         loss = tr.train_step()
     sync()
-    if tr.gemm_tuning == "tune":  # tuned in the warm-up: save the table, time with lookups only
+    if tr.gemm_tuning == "tune":  # tuned in the warm-up (a tuning run's timing is not a result)
         from scaletorch_amd.utils import gemm_tuning
 
         if rank == 0:
             gemm_tuning.finish()
-        torch.cuda.tunable.tuning_enable(False)
     from scaletorch_amd.dist import trace as comm_trace
 
     comm0 = comm_trace.stats()  # host-side counters only (a dict increment per collective)

@@ -67,8 +67,9 @@ def configure(mode: str = "auto", path: str | None = None, max_tuning_ms: int = 
 
 
 def finish() -> None:
-    """Write the table after a tuning run (no-op otherwise)."""
-    if _STATE["mode"] == "tune":
+    """Write the table after a tuning run (no-op otherwise).  PyTorch builds without
+    ``torch.cuda.tunable.write_file`` write it when the process exits."""
+    if _STATE["mode"] == "tune" and hasattr(torch.cuda.tunable, "write_file"):
         torch.cuda.tunable.write_file(_STATE["file"])
 
 
