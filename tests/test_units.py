@@ -599,3 +599,39 @@ def test_bf16_optimizer_moments_track_fp32(tmp_path):
         assert torch.equal(a16.exp_avg, a32.exp_avg.to(torch.bfloat16))
         assert torch.equal(a16.master, a32.master)
     assert latest_checkpoint(str(tmp_path)) is not None
+
+
+def test_adamw_wt_plan_covers_each_bucket_once(monkeypatch):
+    """The fused AdamW + W^T plan (optim.py ``_wt_plan``): per bucket, the weights that keep
+    a W^T copy become ("wt") launches over exactly their arena runs, and the gaps between
+    them ("flat") cover the rest -- every element of the bucket exactly once, in order."""
+    from scaletorch_amd.ops import grad as G
+    from scaletorch_amd.trainer.engine import Trainer
+
+    a = ScaleTorchArguments(model_name_or_path="tiny-llama", synthetic_data=True, micro_batch_size=2,
+                            sequence_length=32, use_cpu=True, dtype="bfloat16", total_train_steps=2,
+                            bucket_size_mb=0.05)
+    tr = Trainer(a)
+    monkeypatch.setattr(G, "_wt_enabled", lambda w: w.dim() == 2 and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0)
+    marked = 0
+    for ar in tr.model.arenas:
+        for p in ar.params:
+            if G._wt_enabled(p):
+                p._st_wt = torch.empty(p.shape[1], p.shape[0], dtype=p.dtype)
+                marked += 1
+    assert marked > 0
+    nwt = 0
+    for ar in tr.model.arenas:
+        assert len(ar.buckets) > 1
+        for b in ar.buckets:
+            plan = tr.optimizer._wt_plan(ar, b)
+            cur = b.shard_lo
+            for kind, lo, hi, w in plan:
+                assert lo == cur and hi > lo
+                if kind == "wt":
+                    nwt += 1
+                    assert w.numel() == hi - lo and w._st_wt.shape == (w.shape[1], w.shape[0])
+                    assert ar.param_flat[lo:hi].data_ptr() == w.data_ptr()
+                cur = hi
+            assert cur == b.shard_hi
+    assert nwt == marked
