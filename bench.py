@@ -161,9 +161,10 @@ def main() -> int:
     ap.add_argument("--gemm_tuning", default="auto", choices=["auto", "use", "tune", "off"],
                     help="TunableOp table for the library GEMMs (utils/gemm_tuning.py); tune: time every "
                          "solution of each new GEMM signature in the warm-up and add it to the table")
-    ap.add_argument("--opt_state_dtype", default="fp32", choices=["fp32", "bf16"],
-                    help="AdamW moment dtype (bf16 = the reference's own optimizer-state precision; "
-                         "fp32 master weights either way)")
+    ap.add_argument("--opt_state_dtype", default="bf16", choices=["fp32", "bf16"],
+                    help="AdamW moment dtype: bf16 (default) = the reference's own optimizer-state precision "
+                         "(torch AdamW on its bf16 model keeps bf16 exp_avg / exp_avg_sq and NO master "
+                         "weights); ours keeps fp32 master weights either way")
     ap.add_argument("--moe_ep_chunks", type=int, default=None, help="EP dispatch chunks (capacity mode)")
     args = ap.parse_args()
     launched = "WORLD_SIZE" in os.environ
