@@ -6,7 +6,7 @@ adamw[fused] / adam / sgd(m=0.9) / lamb->adamw) and ``clip_gradients``
 
 * ``ArenaAdamW``: fp32 master weights + fp32 (or, ``state_dtype="bf16"``, bf16 --
   the reference's own state precision: 22 instead of 30 B/param per step and
-  8 B/param less memory) exp_avg / exp_avg_sq per arena;
+  4 B/param less memory) exp_avg / exp_avg_sq per arena;
   on GPU one fused HIP kernel (csrc/adamw.hip) per arena updates master, m, v
   and writes the bf16 model copy -- the whole step is 1-2 launches.  The
   reference kept bf16 params AND bf16 optimizer states (no master weights).

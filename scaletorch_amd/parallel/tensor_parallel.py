@@ -45,7 +45,6 @@ def _ws(group) -> int:
 # does not take).  One communicator per TP group, created on first use.
 _TP_COMM = "rccl"
 _XGMI: dict = {}
-_XGMI_STREAM: dict = {}
 
 
 def set_tp_comm(kind: str) -> None:
@@ -168,17 +167,12 @@ def _tp_all_reduce(x: torch.Tensor, group, async_op: bool = False):
         if comm is None:
             comm = _XGMI[key] = XgmiAllReduce(group)
         if comm.supports(x):
+            # every xGMI collective of the process runs on ONE stream (``_on_comm_stream``)
+            work = _on_comm_stream(lambda t: comm.all_reduce(t), x)[1]
             if not async_op:
-                comm.all_reduce(x)
+                work.wait()
                 return None
-            st = _XGMI_STREAM.get(x.device.index)
-            if st is None:
-                st = _XGMI_STREAM[x.device.index] = torch.cuda.Stream(device=x.device)
-            st.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(st):
-                comm.all_reduce(x)
-            x.record_stream(st)
-            return _StreamWork(st)
+            return work
     return C.all_reduce(x, group=group, async_op=async_op)
 
 
@@ -288,7 +282,7 @@ def _gather_seq(x: torch.Tensor, group) -> torch.Tensor:
     pair = _PAIR[0] if (xg is not None and ws == 2) else None
     if pair is not None and pair.fits(x.numel(), x):
         xg = pair  # multipath: direct link + 2-hop relays
-    gather = xg.all_gather if xg is not None else (lambda t: C.all_gather(t, group=group))
+    gather = _synced(xg.all_gather) if xg is not None else (lambda t: C.all_gather(t, group=group))
     if x.shape[0] == 1:
         return gather(x[0].contiguous()).unsqueeze(0)
     xt = x.transpose(0, 1).contiguous()  # [S/tp, B, ...]
@@ -305,7 +299,7 @@ def _reduce_scatter_seq(x: torch.Tensor, group) -> torch.Tensor:
     pair = _PAIR[0] if (xg is not None and ws == 2) else None
     if pair is not None and pair.fits(x.numel() // 2, x):
         xg = pair  # multipath: direct link + 2-hop relays
-    scatter = xg.reduce_scatter if xg is not None else (lambda t: C.reduce_scatter(t, group=group))
+    scatter = _synced(xg.reduce_scatter) if xg is not None else (lambda t: C.reduce_scatter(t, group=group))
     if x.shape[0] == 1:
         return scatter(x[0].contiguous()).unsqueeze(0)
     xt = x.transpose(0, 1).contiguous()
@@ -539,13 +533,7 @@ def _sp_gather_async(part: torch.Tensor, group):
     ws = _ws(group)
     pair = _pair_for(group, part.numel(), part)
     if pair is not None:
-        st, ready = _comm_stream(part.device)
-        with torch.cuda.stream(st):
-            st.wait_event(ready)
-            out = pair.all_gather(part)
-        part.record_stream(st)
-        out.record_stream(torch.cuda.current_stream())
-        return out, _StreamWork(st)
+        return _on_comm_stream(pair.all_gather, part)
     _trace("sp.all_gather", part, ws)
     return C.all_gather(part, group=group, async_op=True)
 
@@ -556,13 +544,7 @@ def _sp_reduce_scatter_async(buf: torch.Tensor, group):
     ws = _ws(group)
     pair = _pair_for(group, buf.numel() // 2, buf)
     if pair is not None:
-        st, ready = _comm_stream(buf.device)
-        with torch.cuda.stream(st):
-            st.wait_event(ready)
-            out = pair.reduce_scatter(buf)
-        buf.record_stream(st)
-        out.record_stream(torch.cuda.current_stream())
-        return out, _StreamWork(st)
+        return _on_comm_stream(pair.reduce_scatter, buf)
     _trace("sp.reduce_scatter", buf, ws)
     return C.reduce_scatter(buf, group=group, async_op=True)
 
@@ -592,6 +574,33 @@ def _comm_stream(device: torch.device):
     ready = torch.cuda.Event()
     ready.record()
     return st, ready
+
+
+def _on_comm_stream(fn, t: torch.Tensor):
+    """Run the xGMI collective ``fn(t)`` on the comm stream once the current stream has
+    produced ``t``; returns (output, work).  EVERY xGMI collective of the process (TP
+    all-reduce, SP all-gather / reduce-scatter, pair path, sync or async) goes through
+    this one stream: the IPC protocol's epoch-parity buffers assume the group's
+    collectives run one after another in issue order, which two streams would not keep
+    (an async reduce-scatter still in flight beside a synchronous all-gather issued on
+    the compute stream deadlocked the pair path)."""
+    st, ready = _comm_stream(t.device)
+    with torch.cuda.stream(st):
+        st.wait_event(ready)
+        out = fn(t)
+    t.record_stream(st)
+    if isinstance(out, torch.Tensor) and out.data_ptr() != t.data_ptr():
+        out.record_stream(torch.cuda.current_stream())
+    return out, _StreamWork(st)
+
+
+def _synced(fn):
+    """``fn`` (an xGMI collective) on the comm stream, the current stream waiting for it."""
+    def run(t):
+        out, work = _on_comm_stream(fn, t)
+        work.wait()
+        return out
+    return run
 
 
 def _sp_column_forward(x_shard: torch.Tensor, weight: torch.Tensor, group) -> torch.Tensor:

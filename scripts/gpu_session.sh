@@ -29,6 +29,8 @@ for s in $STEPS; do
     tests) step gpu_tests 1000 python -u -m pytest -x -v --timeout 330 --timeout-method thread tests -m gpu || exit $? ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 || exit $? ;;
     bench16) step bench16 600 python bench.py --steps 10 --warmup 3 --opt_state_dtype bf16 || exit $? ;;
+    mbs7) step bench_mbs7 600 python bench.py --steps 10 --warmup 3 --micro_batch_size 7 || exit $? ;;
+    mbs8) step bench_mbs8 600 env ST_HBM_HEADROOM_GB=8 python bench.py --steps 10 --warmup 3 --micro_batch_size 8 || exit $? ;;
     bench32) step bench32 600 python bench.py --steps 10 --warmup 3 --opt_state_dtype fp32 || exit $? ;;
     adamk) step adamw_kernels 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_train_gpu.py -m gpu -k "adamw or overlapped or delayed or deterministic or rmsnorm" || exit $? ;;
     wt_ab) step wt_ab 900 python tools/ab_step.py --variants ST_ADAMW_WT=1,ST_ADAMW_WT=0 --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 || exit $? ;;
