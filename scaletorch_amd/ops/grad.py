@@ -223,22 +223,30 @@ def _one_t_ok(dy2d: torch.Tensor, x2d: torch.Tensor) -> bool:
             and dy2d.data_ptr() % 16 == 0 and x2d.data_ptr() % 16 == 0)
 
 
-def _wgrad_one_t(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, beta: int) -> None:
+def _wgrad_one_t(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, beta: int, tuned: bool = False) -> None:
     """out = beta out + dY^T X with the SMALLER operand first transposed to token-contiguous
     (csrc/transpose.hip, ~5.5 TB/s), so hipBLASLt reads one operand K-contiguous: on the
     gate|up shape (dY 28672 wide, X 4096) 1390 vs 1292 TF/s for the HIP kernel, transpose
-    included (profiles/r03/wgrad_layouts.log).  Picked per shape by ``_wgrad_pick``."""
+    included (profiles/r03/wgrad_layouts.log).  ``tuned``: the GEMM runs on csrc/gemm.cpp's
+    autotuned hipBLASLt call (every heuristic candidate timed once per shape) instead of
+    PyTorch's first heuristic.  Picked per shape by ``_wgrad_pick``."""
     from . import _lib
 
     T = dy2d.shape[0]
     if x2d.shape[1] <= dy2d.shape[1]:
         xt = torch.empty(x2d.shape[1], T, dtype=x2d.dtype, device=x2d.device)
         _lib.ops().transpose_(x2d, xt)
-        torch.ops.aten.addmm.dtype_out(out, dy2d.t(), xt.t(), torch.float32, beta=beta, alpha=1, out=out)
+        if tuned:
+            _lib.ops().gemm_(out, dy2d, xt, True, True, 1.0, float(beta))
+        else:
+            torch.ops.aten.addmm.dtype_out(out, dy2d.t(), xt.t(), torch.float32, beta=beta, alpha=1, out=out)
     else:
         dyt = torch.empty(dy2d.shape[1], T, dtype=dy2d.dtype, device=dy2d.device)
         _lib.ops().transpose_(dy2d, dyt)
-        torch.ops.aten.addmm.dtype_out(out, dyt, x2d, torch.float32, beta=beta, alpha=1, out=out)
+        if tuned:
+            _lib.ops().gemm_(out, dyt, x2d, False, False, 1.0, float(beta))
+        else:
+            torch.ops.aten.addmm.dtype_out(out, dyt, x2d, torch.float32, beta=beta, alpha=1, out=out)
 
 
 def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> int:
@@ -268,8 +276,14 @@ def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> int:
         _WGRAD_CHOICE[key] = 0
         return 0
     if _one_t_ok(dy2d, x2d) and os.environ.get("ST_WGRAD_ONE_T", "1") == "1":
-        # 3: hipBLASLt on the smaller operand made token-contiguous (transpose timed in)
+        # 3: hipBLASLt on the smaller operand made token-contiguous (transpose timed in);
+        # 5: the same on the autotuned hipBLASLt call (csrc/gemm.cpp)
         arms[3] = lambda: _wgrad_one_t(scratch, dy2d, x2d, 1)
+        if os.environ.get("ST_WGRAD_TUNED", "1") == "1":
+            arms[5] = lambda: _wgrad_one_t(scratch, dy2d, x2d, 1, tuned=True)
+    if os.environ.get("ST_WGRAD_TUNED", "1") == "1":
+        # 4: the fp32-epilogue GEMM on the autotuned hipBLASLt call, operands as stored
+        arms[4] = lambda: _lib.ops().gemm_(scratch, dy2d, x2d, True, False, 1.0, 1.0)
 
     def blas():
         torch.ops.aten.addmm.dtype_out(scratch, dy2d.t(), x2d, torch.float32, beta=1, alpha=1, out=scratch)
@@ -371,15 +385,18 @@ def wgrad_into(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, beta: i
         from . import _lib
 
         if _lib.use_native(dy2d):
-            forced = os.environ.get("ST_WGRAD_VARIANT", "")  # 0 / 1 / 2 / 3 / 17 / 18 overrides the pick (A/B)
-            if forced in ("0", "1", "2", "3", "17", "18"):
+            forced = os.environ.get("ST_WGRAD_VARIANT", "")  # 0-5 / 17 / 18 overrides the pick (A/B)
+            if forced in ("0", "1", "2", "3", "4", "5", "17", "18"):
                 variant = int(forced)
             elif variant is None:
                 variant = _wgrad_pick(dy2d, x2d)
-            if variant == 3 and _one_t_ok(dy2d, x2d):
-                _wgrad_one_t(out, dy2d, x2d, beta)
+            if variant in (3, 5) and _one_t_ok(dy2d, x2d):
+                _wgrad_one_t(out, dy2d, x2d, beta, tuned=variant == 5)
                 return
-            if variant and variant != 3 and _lib.ops().wgrad_gemm_(out, dy2d, x2d, beta, variant):
+            if variant == 4:
+                _lib.ops().gemm_(out, dy2d, x2d, True, False, 1.0, float(beta))
+                return
+            if variant and variant not in (3, 4, 5) and _lib.ops().wgrad_gemm_(out, dy2d, x2d, beta, variant):
                 return
     if _ADDMM_DTYPE_OK is not False and dy2d.is_cuda and os.environ.get("ST_WGRAD_FP32_GEMM", "1") == "1":
         try:

@@ -19,6 +19,7 @@ for s in $STEPS; do
   case $s in
     sp_gemm) step sp_gemm 240 python tools/bench_sp_gemm.py || exit $? ;;
     newk) step new_kernels 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_kernels_gpu.py tests/test_xgmi_gpu.py -m gpu -k "swiglu_epilogue or fused_matches or ep_exchange or ipc or grouped" || exit $? ;;
+    tuned_ab) step wgrad_tuned_ab 900 python tools/ab_step.py --variants ST_WGRAD_TUNED=1,ST_WGRAD_TUNED=0 --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 || exit $? ;;
     onet_ab) step onet_ab 900 python tools/ab_step.py --variants ST_WGRAD_ONE_T=1,ST_WGRAD_ONE_T=0 --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 || exit $? ;;
     adamw_ab) step adamw_ab 900 python tools/ab_step.py --variants ST_ADAMW_BLOCKS=0,ST_ADAMW_BLOCKS=1024,ST_ADAMW_BLOCKS=256,ST_ADAMW_BLOCKS=64 --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 || exit $? ;;
     cp_reorder) step cp_reorder 240 python tools/bench_cp_reorder.py || exit $? ;;
@@ -26,6 +27,8 @@ for s in $STEPS; do
     moe) step mx_proxy 400 python bench.py --layout mixtral_ep8 --micro_batch_size 2 --grad_acc 1 --layers 4 --steps 5 --warmup 2 || exit $?
          step q3_proxy 400 python bench.py --model qwen3-30b-a3b --layers 4 --micro_batch_size 2 --steps 5 --warmup 2 || exit $? ;;
     moe_prof) step mx_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_mx -o run --output-format csv -- python bench.py --layout mixtral_ep8 --micro_batch_size 2 --grad_acc 1 --layers 4 --steps 3 --warmup 2 || exit $? ;;
+    sptest) step sp_pair_test 400 python -u -m pytest -x -v --timeout 330 --timeout-method thread tests/test_xgmi_gpu.py -m gpu -k sp_decoder || exit $? ;;
+    xtests) step xgmi_tests 700 python -u -m pytest -x -v --timeout 330 --timeout-method thread tests/test_xgmi_gpu.py -m gpu || exit $? ;;
     tests) step gpu_tests 1000 python -u -m pytest -x -v --timeout 330 --timeout-method thread tests -m gpu || exit $? ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 || exit $? ;;
     bench16) step bench16 600 python bench.py --steps 10 --warmup 3 --opt_state_dtype bf16 || exit $? ;;

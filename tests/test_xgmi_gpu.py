@@ -339,6 +339,10 @@ def _sp_train_worker(rank, world, tp_comm, seed):
     IPC pair path on its comm side stream (overlapped with the batched SP GEMMs) and the
     TP all-reduces over the xGMI communicator."""
     os.environ.update(ST_GPU_OVERSUBSCRIBE="1", ST_XGMI_TIMEOUT_S="30")
+    import faulthandler
+    import sys
+
+    faulthandler.dump_traceback_later(100, exit=False)  # a hang shows where each rank stands
     from scaletorch_amd.parallel import tensor_parallel as TP
     from scaletorch_amd.trainer.config import ScaleTorchArguments
     from scaletorch_amd.trainer.engine import Trainer
@@ -354,9 +358,14 @@ def _sp_train_worker(rank, world, tp_comm, seed):
     batch = {"input_ids": ids[:, :-1].contiguous(), "target_ids": ids[:, 1:].contiguous(), "position_ids": pos,
              "hidden_states": None}
     tr.data = iter([batch] * 4)
-    losses = [tr.reduced_loss(tr.train_step()) for _ in range(2)]
+    losses = []
+    for i in range(2):
+        losses.append(tr.reduced_loss(tr.train_step()))
+        print(f"[sp worker {rank} {tp_comm}] step {i} loss {losses[-1]:.4f} transport {TP.TRANSPORT['tp']}",
+              file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     tr.health_check()
+    faulthandler.cancel_dump_traceback_later()
     sd = {k: v.detach().float().cpu() for k, v in tr.raw_model.reference_state_dict().items()
           if "decoder_layers.1" in k}
     return losses, sd, TP.TRANSPORT["tp"], TP._PAIR[0] is not None
@@ -369,8 +378,8 @@ def test_sp_decoder_layers_pair_path_matches_gloo_same_gpu():
     from tests.dist_harness import run_workers
 
     try:
-        ref = run_workers(_sp_train_worker, 2, "rccl", 3, timeout=300)
-        got = run_workers(_sp_train_worker, 2, "xgmi", 3, timeout=300)
+        ref = run_workers(_sp_train_worker, 2, "rccl", 3, timeout=140)
+        got = run_workers(_sp_train_worker, 2, "xgmi", 3, timeout=140)
     except RuntimeError as e:
         if "IPC" in str(e) or "hipIpc" in str(e):
             pytest.skip(f"IPC on a shared GPU unsupported here: {e}")
