@@ -338,7 +338,9 @@ def _sp_train_worker(rank, world, tp_comm, seed):
     THIS GPU over gloo; tp_comm 'xgmi' routes the SP all-gathers / reduce-scatters over the
     IPC pair path on its comm side stream (overlapped with the batched SP GEMMs) and the
     TP all-reduces over the xGMI communicator."""
-    os.environ.update(ST_GPU_OVERSUBSCRIBE="1", ST_XGMI_TIMEOUT_S="30")
+    # 16 MiB IPC buffers: both processes share ONE GPU here, and opening a peer's
+    # 512 MiB default buffer on the same device hung in hipIpcOpenMemHandle
+    os.environ.update(ST_GPU_OVERSUBSCRIBE="1", ST_XGMI_TIMEOUT_S="30", ST_XGMI_MAX_MB="16")
     import faulthandler
     import sys
 
