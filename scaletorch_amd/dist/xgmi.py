@@ -283,9 +283,13 @@ XgmiComm = XgmiAllReduce  # the communicator carries all three collectives
 
 
 def _max_bytes_default() -> int:
+    """IPC data area of the node communicator behind the pair path (ST_XGMI_MAX_MB, 64 MiB:
+    the tp = 2 SP sub-chunks at S = 4096 are 16-32 MiB; larger messages take RCCL).  Two
+    processes sharing one GPU hung opening a peer's 512 MiB area (hipIpcOpenMemHandle);
+    16 MiB opened at once (tests/test_xgmi_gpu.py SP pair-path test)."""
     import os
 
-    return int(float(os.environ.get("ST_XGMI_MAX_MB", "512")) * (1 << 20))
+    return int(float(os.environ.get("ST_XGMI_MAX_MB", "64")) * (1 << 20))
 
 
 def node_group():

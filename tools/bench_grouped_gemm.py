@@ -58,6 +58,9 @@ def main() -> int:
             "torch_grouped_mm": lambda: torch._grouped_mm(x, w if wn else w.transpose(-2, -1), offs=offs),
             "dense_hipblaslt": lambda: torch.matmul(x, w[0] if wn else w[0].t()),
         }
+        if not wn and "gate_up" in name:  # SwiGLU epilogue: gu and a = silu(g) * u from the GEMM
+            arms["hip_grouped_swiglu_epilogue"] = lambda: _lib.ops().grouped_gemm_swiglu(x, w, offs)
+            arms["hip_grouped_then_swiglu"] = lambda: _lib.ops().swiglu_fwd(_lib.ops().grouped_gemm(x, w, offs, wn))
         if wn and G == 1:  # the TN form on a transposed weight copy (what ops/grad.py runs today)
             wt = w[0].t().contiguous()
             arms["dense_hipblaslt_TN_on_WT_copy"] = lambda: torch.nn.functional.linear(x, wt)
