@@ -27,6 +27,7 @@ for s in $STEPS; do
     moe) step mx_proxy 400 python bench.py --layout mixtral_ep8 --micro_batch_size 2 --grad_acc 1 --layers 4 --steps 5 --warmup 2 || exit $?
          step q3_proxy 400 python bench.py --model qwen3-30b-a3b --layers 4 --micro_batch_size 2 --steps 5 --warmup 2 || exit $? ;;
     moe_prof) step mx_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_mx -o run --output-format csv -- python bench.py --layout mixtral_ep8 --micro_batch_size 2 --grad_acc 1 --layers 4 --steps 3 --warmup 2 || exit $? ;;
+    gmm) step grouped_gemm_bench 300 python tools/bench_grouped_gemm.py || exit $? ;;
     dswiglu) step dense_swiglu 240 python tools/bench_dense_swiglu.py || exit $? ;;
     sptest) step sp_pair_test 400 python -u -m pytest -x -v --timeout 330 --timeout-method thread tests/test_xgmi_gpu.py -m gpu -k sp_decoder || exit $? ;;
     xtests) step xgmi_tests 700 python -u -m pytest -x -v --timeout 330 --timeout-method thread tests/test_xgmi_gpu.py -m gpu || exit $? ;;
