@@ -282,13 +282,18 @@ class XgmiAllReduce:
 XgmiComm = XgmiAllReduce  # the communicator carries all three collectives
 
 
-def _max_bytes_default() -> int:
-    """IPC data area of the node communicator behind the pair path (ST_XGMI_MAX_MB, 64 MiB:
-    the tp = 2 SP sub-chunks at S = 4096 are 16-32 MiB; larger messages take RCCL).  Two
-    processes sharing one GPU hung opening a peer's 512 MiB area (hipIpcOpenMemHandle);
-    16 MiB opened at once (tests/test_xgmi_gpu.py SP pair-path test)."""
+def _max_bytes_default(kind: str = "pair") -> int:
+    """IPC data area per rank.  ``pair``: the node communicator behind the tp = 2 pair path
+    (ST_XGMI_MAX_MB, 64 MiB: the SP sub-chunks at S = 4096 are 16-32 MiB; larger messages
+    take RCCL).  ``ep``: the dropless EP exchange (ST_XGMI_EP_MAX_MB, 512 MiB: one rank's
+    landing area at the host bound, 268 MiB for Mixtral EP 8 at 4096 tokens).  Two
+    processes sharing ONE GPU (rehearsals / tests) hung opening a peer's 512 MiB area
+    (hipIpcOpenMemHandle) while 16 MiB opened at once (tests/test_xgmi_gpu.py SP pair-path
+    test): such runs set the variables low."""
     import os
 
+    if kind == "ep":
+        return int(float(os.environ.get("ST_XGMI_EP_MAX_MB", "512")) * (1 << 20))
     return int(float(os.environ.get("ST_XGMI_MAX_MB", "64")) * (1 << 20))
 
 

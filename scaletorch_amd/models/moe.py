@@ -81,7 +81,7 @@ def setup_ep_xgmi(group) -> None:
     from ..dist.xgmi import XgmiAllReduce, _max_bytes_default
 
     if group is not None and C.get_world_size(group) > 1:
-        _EP_XGMI[id(group)] = XgmiAllReduce(group, max_bytes=_max_bytes_default())
+        _EP_XGMI[id(group)] = XgmiAllReduce(group, max_bytes=_max_bytes_default("ep"))
 
 
 def _ep_a2a(x: torch.Tensor, group, async_op: bool):
