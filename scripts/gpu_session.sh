@@ -42,7 +42,7 @@ for s in $STEPS; do
     prof) step step_prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_step -o run --output-format csv -- python bench.py --steps 3 --warmup 2 || exit $? ;;
     rehearse) step rehearse 1000 env LAYOUTS="${LAYOUTS:-mixtral_ep8 tp2pp2dp2}" LAYOUT_TIMEOUT=400 bash scripts/rehearse_layouts_1gpu.sh || exit $? ;;
     rehearse_mx) step rehearse_mx 600 env LAYOUTS=mixtral_ep8 LAYOUT_TIMEOUT=420 EXTRA="--seq_len 512" ST_XGMI_EP_MAX_MB=48 bash scripts/rehearse_layouts_1gpu.sh || exit $? ;;
-    replay) step replay 1100 python scripts/bench_reference_rows_8gpu.py --rehearse --steps 2 --warmup 1 --timeout 300 \
+    replay) step replay 1100 env ST_XGMI_EP_MAX_MB=48 python scripts/bench_reference_rows_8gpu.py --rehearse --steps 2 --warmup 1 --timeout 300 \
               --out gpurun_out/reference_rows_rehearsal.jsonl --filter "${REPLAY_FILTER:-.}" || exit $? ;;
     # the table is written under gpurun_out/ (merged back) and copied into scaletorch_amd/tuning/ by hand
     gtune) step gemm_tune 900 env ST_GEMM_TUNING_FILE=gpurun_out/gemm_gfx950.csv python bench.py --steps 1 --warmup 2 --gemm_tuning tune || exit $? ;;
