@@ -264,9 +264,18 @@ def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> int:
     if got is not None:
         return got
     M, N = dy2d.shape[1], x2d.shape[1]
-    if M * N * 4 > _TUNE_MAX_BYTES or os.environ.get("ST_WGRAD_TUNE", "1") != "1":
+    if os.environ.get("ST_WGRAD_TUNE", "1") != "1":
         _WGRAD_CHOICE[key] = 1
         return 1
+    if M * N * 4 > _TUNE_MAX_BYTES:
+        # output too large for a scratch copy (the untied LM head: 128256 x 4096 fp32 = 2.1 GB):
+        # time the arms on a column slice of dY -- the first Ms output rows -- instead
+        Ms = max(256, (_TUNE_MAX_BYTES // (N * 4)) // 256 * 256)
+        if Ms >= M or Ms * N * 4 > _TUNE_MAX_BYTES or os.environ.get("ST_WGRAD_TUNE_LARGE", "1") != "1":
+            _WGRAD_CHOICE[key] = 1
+            return 1
+        dy2d = dy2d[:, :Ms]
+        M = Ms
     scratch = torch.zeros(M, N, dtype=torch.float32, device=dy2d.device)
     # +16: the same kernel without the tail split (csrc/wgrad_gemm.hip), where the last
     # partial round of tiles is left partly idle instead of being cut into token ranges

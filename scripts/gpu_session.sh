@@ -19,6 +19,7 @@ for s in $STEPS; do
   case $s in
     sp_gemm) step sp_gemm 240 python tools/bench_sp_gemm.py || exit $? ;;
     newk) step new_kernels 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_kernels_gpu.py tests/test_xgmi_gpu.py -m gpu -k "swiglu_epilogue or fused_matches or ep_exchange or ipc or grouped" || exit $? ;;
+    large_ab) step wgrad_large_ab 900 python tools/ab_step.py --variants ST_WGRAD_TUNE_LARGE=1,ST_WGRAD_TUNE_LARGE=0 --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 || exit $? ;;
     tuned_ab) step wgrad_tuned_ab 900 python tools/ab_step.py --variants ST_WGRAD_TUNED=1,ST_WGRAD_TUNED=0 --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 || exit $? ;;
     onet_ab) step onet_ab 900 python tools/ab_step.py --variants ST_WGRAD_ONE_T=1,ST_WGRAD_ONE_T=0 --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 || exit $? ;;
     adamw_ab) step adamw_ab 900 python tools/ab_step.py --variants ST_ADAMW_BLOCKS=0,ST_ADAMW_BLOCKS=1024,ST_ADAMW_BLOCKS=256,ST_ADAMW_BLOCKS=64 --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 || exit $? ;;
@@ -34,6 +35,8 @@ for s in $STEPS; do
     tests) step gpu_tests 1000 python -u -m pytest -x -v --timeout 330 --timeout-method thread tests -m gpu || exit $? ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 || exit $? ;;
     bench16) step bench16 600 python bench.py --steps 10 --warmup 3 --opt_state_dtype bf16 || exit $? ;;
+    hc8k) step bench_hc8k 600 python bench.py --steps 10 --warmup 3 --head_chunk 8192 || exit $? ;;
+    hc12k) step bench_hc12k 600 python bench.py --steps 10 --warmup 3 --head_chunk 12288 || exit $? ;;
     mbs7) step bench_mbs7 600 python bench.py --steps 10 --warmup 3 --micro_batch_size 7 || exit $? ;;
     mbs8) step bench_mbs8 600 env ST_HBM_HEADROOM_GB=8 python bench.py --steps 10 --warmup 3 --micro_batch_size 8 || exit $? ;;
     bench32) step bench32 600 python bench.py --steps 10 --warmup 3 --opt_state_dtype fp32 || exit $? ;;
