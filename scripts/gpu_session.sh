@@ -19,6 +19,7 @@ for s in $STEPS; do
   case $s in
     sp_gemm) step sp_gemm 240 python tools/bench_sp_gemm.py || exit $? ;;
     newk) step new_kernels 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_kernels_gpu.py tests/test_xgmi_gpu.py -m gpu -k "swiglu_epilogue or fused_matches or ep_exchange or ipc or grouped" || exit $? ;;
+    wside_ab) step wgrad_side_ab 900 python tools/ab_step.py --variants ST_WGRAD_STREAM=main,ST_WGRAD_STREAM=side --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 || exit $? ;;
     large_ab) step wgrad_large_ab 900 python tools/ab_step.py --variants ST_WGRAD_TUNE_LARGE=1,ST_WGRAD_TUNE_LARGE=0 --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 || exit $? ;;
     tuned_ab) step wgrad_tuned_ab 900 python tools/ab_step.py --variants ST_WGRAD_TUNED=1,ST_WGRAD_TUNED=0 --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 || exit $? ;;
     onet_ab) step onet_ab 900 python tools/ab_step.py --variants ST_WGRAD_ONE_T=1,ST_WGRAD_ONE_T=0 --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 || exit $? ;;

@@ -291,6 +291,15 @@ def test_zero1_adamw_parity(kw):
     _compare(ref, res, atol=5e-5, rtol=5e-3)
 
 
+def test_zero1_adamw_bf16_moments_parity():
+    """bf16 AdamW moments (``optimizer_state_dtype="bf16"``, the bench default) under ZeRO-1:
+    the shard-sized bf16 states give the same 2 steps as the replicated bf16-moment run."""
+    kw = dict(data_parallel_size=2, micro_batch_size=2, zero_stage=1, bucket_size_mb=0.02)
+    ref = _reference("tiny-llama", 1, optimizer_state_dtype="bf16", **_ADAM)
+    res = run_workers(_worker, 2, "tiny-llama", dict(kw, optimizer_state_dtype="bf16", **_ADAM))
+    _compare(ref, res, atol=5e-5, rtol=5e-3)
+
+
 def test_zero1_moe_ep2_dense_sharded():
     """EP=2: the dense arena shards over DP x EP, the expert arena (world 1) does not.
     Compared with the replicated-optimizer EP=2 run (the MoE combine's fp32 summation
