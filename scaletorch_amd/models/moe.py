@@ -318,8 +318,10 @@ _ZERO_PAD = [os.environ.get("ST_MOE_ZERO_PAD", "0") == "1"]  # zero the unused t
 
 
 def _ep_exchange(x, M, El, direction, out_rows, area_rows, group, comm):
-    trace.record("ep.exchange" if direction == 0 else "ep.exchange_back", x, group_size=C.get_world_size(group),
-                 transport="xgmi" if comm is not None else "rccl")
+    # bytes counted = the rows that really travel per rank (dispatch: this rank's T*k sorted
+    # rows; combine: the T*k rows it gets back), not the R_max-row padded expert buffer
+    trace.record("ep.exchange" if direction == 0 else "ep.exchange_back", x if direction == 0 else x[:out_rows],
+                 group_size=C.get_world_size(group), transport="xgmi" if comm is not None else "rccl")
     if comm is not None:
         out = comm.ep_exchange(x, M, El, direction, out_rows, area_rows)
         if _ZERO_PAD[0] and direction == 0:  # rows past the received ones hold stale data
