@@ -30,6 +30,7 @@ for s in $STEPS; do
          step q3_proxy 400 python bench.py --model qwen3-30b-a3b --layers 4 --micro_batch_size 2 --steps 5 --warmup 2 || exit $? ;;
     moe_prof) step mx_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_mx -o run --output-format csv -- python bench.py --layout mixtral_ep8 --micro_batch_size 2 --grad_acc 1 --layers 4 --steps 3 --warmup 2 || exit $? ;;
     gmm) step grouped_gemm_bench 300 python tools/bench_grouped_gemm.py || exit $? ;;
+    rmsbwd) step rmsnorm_bwd_caps 300 bash -c 'for b in 256 512 768 1024; do ST_RMSNORM_BWD_BLOCKS=$b timeout -k 5 60 python tools/bench_rmsnorm_bwd.py || exit $?; done' || exit $? ;;
     dswiglu) step dense_swiglu 240 python tools/bench_dense_swiglu.py || exit $? ;;
     sptest) step sp_pair_test 400 python -u -m pytest -x -v --timeout 330 --timeout-method thread tests/test_xgmi_gpu.py -m gpu -k sp_decoder || exit $? ;;
     xtests) step xgmi_tests 700 python -u -m pytest -x -v --timeout 330 --timeout-method thread tests/test_xgmi_gpu.py -m gpu || exit $? ;;
@@ -48,6 +49,7 @@ for s in $STEPS; do
     rehearse_mx) step rehearse_mx 600 env LAYOUTS=mixtral_ep8 LAYOUT_TIMEOUT=420 EXTRA="--seq_len 512" ST_XGMI_EP_MAX_MB=48 bash scripts/rehearse_layouts_1gpu.sh || exit $? ;;
     flash_pmc) step flash_pmc 200 timeout -s KILL 150 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d gpurun_out/flash_pmc -o run --output-format csv -- python tools/bench_flash_bwd_ds.py || exit $? ;;
     rehearse_mx4k) step rehearse_mx4k 600 env LAYOUTS=mixtral_ep8 LAYOUT_TIMEOUT=500 ST_XGMI_EP_MAX_MB=48 bash scripts/rehearse_layouts_1gpu.sh || exit $? ;;
+    rehearse_dp) step rehearse_dp 600 env LAYOUTS=dp LAYOUT_TIMEOUT=500 bash scripts/rehearse_layouts_1gpu.sh || exit $? ;;
     replay) step replay 1100 env ST_XGMI_EP_MAX_MB=48 python scripts/bench_reference_rows_8gpu.py --rehearse --steps 2 --warmup 1 --timeout 300 \
               --out gpurun_out/reference_rows_rehearsal.jsonl --filter "${REPLAY_FILTER:-.}" || exit $? ;;
     # the table is written under gpurun_out/ (merged back) and copied into scaletorch_amd/tuning/ by hand
