@@ -28,6 +28,7 @@ for s in $STEPS; do
     opt_probe) step opt_probe 900 python tools/ab_step.py --variants ST_OPT_PROBE_SKIP=0,ST_OPT_PROBE_SKIP=1 --rounds 4 --steps 3 --micro_batch_size 6 --fused_head 1 || exit $? ;;
     moe) step mx_proxy 400 python bench.py --layout mixtral_ep8 --micro_batch_size 2 --grad_acc 1 --layers 4 --steps 5 --warmup 2 || exit $?
          step q3_proxy 400 python bench.py --model qwen3-30b-a3b --layers 4 --micro_batch_size 2 --steps 5 --warmup 2 || exit $? ;;
+    q3_prof) step q3_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_q3 -o run --output-format csv -- python bench.py --model qwen3-30b-a3b --layers 4 --micro_batch_size 2 --steps 3 --warmup 2 || exit $? ;;
     moe_prof) step mx_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_mx -o run --output-format csv -- python bench.py --layout mixtral_ep8 --micro_batch_size 2 --grad_acc 1 --layers 4 --steps 3 --warmup 2 || exit $? ;;
     gmm) step grouped_gemm_bench 300 python tools/bench_grouped_gemm.py || exit $? ;;
     rmsbwd) step rmsnorm_bwd_caps 300 bash -c 'for b in 256 512 768 1024; do ST_RMSNORM_BWD_BLOCKS=$b timeout -k 5 60 python tools/bench_rmsnorm_bwd.py || exit $?; done' || exit $? ;;
