@@ -61,7 +61,16 @@ def configure(mode: str = "auto", path: str | None = None, max_tuning_ms: int = 
         tun.set_max_tuning_duration(max_tuning_ms)
         os.makedirs(os.path.dirname(path), exist_ok=True)
     if os.path.exists(path):
-        tun.read_file(path)
+        try:
+            ok = tun.read_file(path)
+        except Exception:  # noqa: BLE001 -- a table from another stack must never stop training
+            ok = False
+        if ok is False and mode == "use":
+            # validators (PyTorch / ROCm / hipBLASLt versions, GPU arch) did not match: run the
+            # library's default heuristics rather than half-applied or mismatched solutions
+            tun.enable(False)
+            _STATE.update(mode="off", file=None)
+            return "off"
     _STATE.update(mode=mode, file=path)
     return mode
 
