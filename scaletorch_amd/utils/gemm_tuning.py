@@ -42,9 +42,10 @@ def configure(mode: str = "auto", path: str | None = None, max_tuning_ms: int = 
     path = path or os.environ.get("ST_GEMM_TUNING_FILE") or TABLE
     if mode not in ("auto", "use", "tune", "off"):
         raise ValueError(f"gemm_tuning must be auto | use | tune | off, got {mode!r}")
-    if not torch.cuda.is_available():
-        mode = "off"
-    elif mode == "auto":
+    if not torch.cuda.is_available():  # nothing to tune (and torch.cuda.tunable needs a device)
+        _STATE.update(mode="off", file=None)
+        return "off"
+    if mode == "auto":
         mode = "use" if (os.path.exists(path) and _gfx950()) else "off"
     if mode == "use" and not os.path.exists(path):
         raise FileNotFoundError(f"gemm_tuning=use but {path} does not exist (run with --gemm_tuning tune first)")

@@ -635,3 +635,17 @@ def test_adamw_wt_plan_covers_each_bucket_once(monkeypatch):
                 cur = hi
             assert cur == b.shard_hi
     assert nwt == marked
+
+
+def test_gemm_tuning_modes_cpu():
+    """utils/gemm_tuning.py: invalid modes raise; without a GPU every mode is off (the
+    committed MI355X table exists and is only read on a gfx950 device)."""
+    from scaletorch_amd.utils import gemm_tuning
+
+    assert os.path.exists(gemm_tuning.TABLE)
+    with pytest.raises(ValueError):
+        gemm_tuning.configure("sometimes")
+    if not torch.cuda.is_available():
+        for mode in ("auto", "use", "tune", "off"):
+            assert gemm_tuning.configure(mode) == "off"
+        assert gemm_tuning.state() == {"mode": "off", "entries": 0}
