@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
 // partial[block, h].  The row operands are kept packed (bf16) in registers to
 // bound VGPR use at h = 8192.  Dynamic LDS: 2 * NCH * 512 fp32, lane-major
 // (element i of lane L in chunk c at c*512 + i*64 + L: bank-conflict free).
-template <int NCH, bool DRES>
+template <int NCH, bool DRES, bool PF = false>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s, const bf16_t* __restrict__ w,
     const float* __restrict__ rstd, const bf16_t* __restrict__ dres, bf16_t* __restrict__ ds,
@@ -119,26 +119,47 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
     if (col < h) wp[c] = ld8(w + col);
     else wp[c] = BF8{{0u, 0u, 0u, 0u}};
   }
+  // PF: the operands of the wave's NEXT row are requested before this row's math and
+  // stores (ST_RMSNORM_BWD_PF=1), so loads stay in flight across the row boundary
+  // instead of each row waiting for the previous row's stores (vmcnt counts both)
+  BF8 sp[NCH], dp[NCH], rp[DRES ? NCH : 1];
+  float rs = 0.f;
+#define ST_RMS_LOAD_ROW(R, S_, D_, Q_)                                        \
+  do {                                                                        \
+    const size_t b_ = (size_t)(R) * h;                                        \
+    _Pragma("unroll") for (int c = 0; c < NCH; ++c) {                         \
+      const int col = c * 512 + lane * 8;                                     \
+      if (col < h) {                                                          \
+        S_[c] = ld8(s + b_ + col);                                            \
+        D_[c] = ld8(dy + b_ + col);                                           \
+        if (DRES) Q_[DRES ? c : 0] = ld8(dres + b_ + col);                    \
+      } else {                                                                \
+        S_[c] = BF8{{0u, 0u, 0u, 0u}};                                        \
+        D_[c] = BF8{{0u, 0u, 0u, 0u}};                                        \
+        if (DRES) Q_[DRES ? c : 0] = BF8{{0u, 0u, 0u, 0u}};                   \
+      }                                                                       \
+    }                                                                         \
+  } while (0)
+  if (PF && gw < rows) {
+    ST_RMS_LOAD_ROW(gw, sp, dp, rp);
+    rs = rstd[gw];
+  }
   for (int row = gw; row < rows; row += nw) {
     const size_t base = (size_t)row * h;
-    const float rs = rstd[row];
-    BF8 sp[NCH], dp[NCH], rp[DRES ? NCH : 1];
-    float dot = 0.f;
-    // every operand of the row (incl. the residual-stream gradient) is issued
-    // before the reduction, so a wave has 2-3 x NCH 16-byte loads in flight
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int col = c * 512 + lane * 8;
-      if (col < h) {
-        sp[c] = ld8(s + base + col);
-        dp[c] = ld8(dy + base + col);
-        if (DRES) rp[DRES ? c : 0] = ld8(dres + base + col);
-      } else {
-        sp[c] = BF8{{0u, 0u, 0u, 0u}};
-        dp[c] = BF8{{0u, 0u, 0u, 0u}};
-        if (DRES) rp[DRES ? c : 0] = BF8{{0u, 0u, 0u, 0u}};
+    BF8 sn[PF ? NCH : 1], dn[PF ? NCH : 1], rn[(PF && DRES) ? NCH : 1];
+    float rsn = 0.f;
+    if (PF) {
+      if (row + nw < rows) {
+        ST_RMS_LOAD_ROW(row + nw, sn, dn, rn);
+        rsn = rstd[row + nw];
       }
+    } else {
+      // every operand of the row (incl. the residual-stream gradient) is issued
+      // before the reduction, so a wave has 2-3 x NCH 16-byte loads in flight
+      ST_RMS_LOAD_ROW(row, sp, dp, rp);
+      rs = rstd[row];
     }
+    float dot = 0.f;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       float sv[8], dv[8], wf[8];
@@ -172,7 +193,17 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
         st8(ds + base + col, pack8(o));
       }
     }
+    if (PF) {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        sp[c] = sn[PF ? c : 0];
+        dp[c] = dn[PF ? c : 0];
+        if (DRES) rp[DRES ? c : 0] = rn[(PF && DRES) ? c : 0];
+      }
+      rs = rsn;
+    }
   }
+#undef ST_RMS_LOAD_ROW
   extern __shared__ float red_lds[];  // [2][NCH * 512]
   constexpr int kSlab = NCH * 512;
   const int wid = threadIdx.x >> 6;
@@ -290,7 +321,13 @@ int launch_bwd(const void* dy, const void* s, const void* w, const float* rstd, 
   rmsnorm_bwd_kernel<N, DRES><<<grid, block, 2 * (N) * 512 * sizeof(float), st>>>(        \
       (const bf16_t*)dy, (const bf16_t*)s, (const bf16_t*)w, rstd, (const bf16_t*)dres,     \
       (bf16_t*)ds, partial, rows, h)
-  if (nch <= 1) ST_RMS_BWD(1);
+  const char* pfe = std::getenv("ST_RMSNORM_BWD_PF");  // read per call: same-process A/B
+  const bool pf = pfe && std::atoi(pfe) == 1;
+  if (pf && nch > 4 && nch <= 8)
+    rmsnorm_bwd_kernel<8, DRES, true><<<grid, block, 2 * 8 * 512 * sizeof(float), st>>>(
+        (const bf16_t*)dy, (const bf16_t*)s, (const bf16_t*)w, rstd, (const bf16_t*)dres, (bf16_t*)ds, partial,
+        rows, h);
+  else if (nch <= 1) ST_RMS_BWD(1);
   else if (nch <= 2) ST_RMS_BWD(2);
   else if (nch <= 4) ST_RMS_BWD(4);
   else if (nch <= 8) ST_RMS_BWD(8);

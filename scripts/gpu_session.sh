@@ -32,6 +32,7 @@ for s in $STEPS; do
     moe_prof) step mx_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_mx -o run --output-format csv -- python bench.py --layout mixtral_ep8 --micro_batch_size 2 --grad_acc 1 --layers 4 --steps 3 --warmup 2 || exit $? ;;
     gmm) step grouped_gemm_bench 300 python tools/bench_grouped_gemm.py || exit $? ;;
     rmsbwd) step rmsnorm_bwd_caps 300 bash -c 'for b in 256 512 768 1024; do ST_RMSNORM_BWD_BLOCKS=$b timeout -k 5 60 python tools/bench_rmsnorm_bwd.py || exit $?; done' || exit $? ;;
+    rmspf) step rmsnorm_pf 400 bash -c 'for v in 0 1 0 1; do ST_RMSNORM_BWD_PF=$v timeout -k 5 60 python tools/bench_rmsnorm_bwd.py || exit $?; done && ST_RMSNORM_BWD_PF=1 timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_train_gpu.py -m gpu -k "rmsnorm or deterministic or native_vs_reference"' || exit $? ;;
     dswiglu) step dense_swiglu 240 python tools/bench_dense_swiglu.py || exit $? ;;
     sptest) step sp_pair_test 400 python -u -m pytest -x -v --timeout 330 --timeout-method thread tests/test_xgmi_gpu.py -m gpu -k sp_decoder || exit $? ;;
     xtests) step xgmi_tests 700 python -u -m pytest -x -v --timeout 330 --timeout-method thread tests/test_xgmi_gpu.py -m gpu || exit $? ;;

@@ -43,7 +43,8 @@ def main() -> int:
         b.synchronize()
         best = min(best, a.elapsed_time(b) / 10)
     nbytes = 4 * rows * h * 2  # dy, s, dres read + ds written (bf16)
-    print(json.dumps({"blocks_cap": os.environ.get("ST_RMSNORM_BWD_BLOCKS", "default"), "bwd_ms": round(best, 4),
+    print(json.dumps({"blocks_cap": os.environ.get("ST_RMSNORM_BWD_BLOCKS", "default"),
+                      "prefetch": os.environ.get("ST_RMSNORM_BWD_PF", "0"), "bwd_ms": round(best, 4),
                       "TBps_rows": round(nbytes / best / 1e9, 2)}))
     return 0
 
