@@ -321,8 +321,10 @@ int launch_bwd(const void* dy, const void* s, const void* w, const float* rstd, 
   rmsnorm_bwd_kernel<N, DRES><<<grid, block, 2 * (N) * 512 * sizeof(float), st>>>(        \
       (const bf16_t*)dy, (const bf16_t*)s, (const bf16_t*)w, rstd, (const bf16_t*)dres,     \
       (bf16_t*)ds, partial, rows, h)
+  // prefetching body at h <= 4096 (default on; ST_RMSNORM_BWD_PF=0 for the A/B): isolated at
+  // the bench shape 0.1776-0.1779 -> 0.1701-0.1725 ms (profiles/r04/rmsnorm_bwd_prefetch.log)
   const char* pfe = std::getenv("ST_RMSNORM_BWD_PF");  // read per call: same-process A/B
-  const bool pf = pfe && std::atoi(pfe) == 1;
+  const bool pf = !pfe || std::atoi(pfe) == 1;
   if (pf && nch > 4 && nch <= 8)
     rmsnorm_bwd_kernel<8, DRES, true><<<grid, block, 2 * 8 * 512 * sizeof(float), st>>>(
         (const bf16_t*)dy, (const bf16_t*)s, (const bf16_t*)w, rstd, (const bf16_t*)dres, (bf16_t*)ds, partial,
