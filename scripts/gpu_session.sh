@@ -56,6 +56,8 @@ for s in $STEPS; do
               --out gpurun_out/reference_rows_rehearsal.jsonl --filter "${REPLAY_FILTER:-.}" || exit $? ;;
     # the table is written under gpurun_out/ (merged back) and copied into scaletorch_amd/tuning/ by hand
     gtune) step gemm_tune 900 env ST_GEMM_TUNING_FILE=gpurun_out/gemm_gfx950.csv python bench.py --steps 1 --warmup 2 --gemm_tuning tune || exit $? ;;
+    gtune_rot) step gemm_tune_rot 900 env ST_GEMM_TUNING_FILE=gpurun_out/gemm_gfx950_rot.csv PYTORCH_TUNABLEOP_ROTATING_BUFFER_SIZE=512 PYTORCH_TUNABLEOP_MAX_TUNING_DURATION_MS=60 python bench.py --steps 1 --warmup 2 --gemm_tuning tune || exit $? ;;
+    gtune_rot_ab) step gemm_tune_rot_ab 900 env ST_GEMM_TUNING_FILE=gpurun_out/gemm_gfx950_rot.csv python tools/ab_step.py --variants TUNABLE=1,TUNABLE=0 --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 --gemm_tuning use || exit $? ;;
     gtune_ab) step gemm_tune_ab 900 python tools/ab_step.py --variants TUNABLE=1,TUNABLE=0 --rounds 3 --steps 3 --micro_batch_size 6 --fused_head 1 --gemm_tuning use || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
