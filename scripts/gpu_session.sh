@@ -41,6 +41,10 @@ for s in $STEPS; do
     bench16) step bench16 600 python bench.py --steps 10 --warmup 3 --opt_state_dtype bf16 || exit $? ;;
     hc8k) step bench_hc8k 600 python bench.py --steps 10 --warmup 3 --head_chunk 8192 || exit $? ;;
     hc12k) step bench_hc12k 600 python bench.py --steps 10 --warmup 3 --head_chunk 12288 || exit $? ;;
+    prio) step bench_prio_default 600 python bench.py --steps 10 --warmup 3 || exit $?
+          step bench_prio_high 600 env ST_COMPUTE_STREAM_PRIORITY=-1 python bench.py --steps 10 --warmup 3 || exit $?
+          step bench_prio_default2 600 python bench.py --steps 10 --warmup 3 || exit $?
+          step bench_prio_high2 600 env ST_COMPUTE_STREAM_PRIORITY=-1 python bench.py --steps 10 --warmup 3 || exit $? ;;
     mbs7) step bench_mbs7 600 python bench.py --steps 10 --warmup 3 --micro_batch_size 7 || exit $? ;;
     mbs8) step bench_mbs8 600 env ST_HBM_HEADROOM_GB=8 python bench.py --steps 10 --warmup 3 --micro_batch_size 8 || exit $? ;;
     bench32) step bench32 600 python bench.py --steps 10 --warmup 3 --opt_state_dtype fp32 || exit $? ;;
