@@ -283,18 +283,19 @@ XgmiComm = XgmiAllReduce  # the communicator carries all three collectives
 
 
 def _max_bytes_default(kind: str = "pair") -> int:
-    """IPC data area per rank.  ``pair``: the node communicator behind the tp = 2 pair path
-    (ST_XGMI_MAX_MB, 64 MiB: the SP sub-chunks at S = 4096 are 16-32 MiB; larger messages
-    take RCCL).  ``ep``: the dropless EP exchange (ST_XGMI_EP_MAX_MB, 512 MiB: one rank's
-    landing area at the host bound, 268 MiB for Mixtral EP 8 at 4096 tokens).  Two
-    processes sharing ONE GPU (rehearsals / tests) hung opening a peer's 512 MiB area
-    (hipIpcOpenMemHandle) while 16 MiB opened at once (tests/test_xgmi_gpu.py SP pair-path
-    test): such runs set the variables low."""
+    """IPC data area per rank (ST_XGMI_MAX_MB for the node communicator behind the tp = 2 pair
+    path, ST_XGMI_EP_MAX_MB for the dropless EP exchange; 512 MiB each).  The pair path's
+    relay slots are an eighth of it (``_pair_ok``), so 512 MiB takes messages up to 64 MiB
+    -- the SP sub-chunks at S = 4096 (16-32 MiB) and the start-up self-test (32 MiB); the
+    EP area holds one rank's landing rows at the host bound (268 MiB for Mixtral EP 8 at
+    4096 tokens).  Two processes sharing ONE GPU (rehearsals / tests) hung opening a peer's
+    512 MiB area (hipIpcOpenMemHandle) while 16 MiB opened at once (tests/test_xgmi_gpu.py
+    SP pair-path test): such runs set the variables low."""
     import os
 
     if kind == "ep":
         return int(float(os.environ.get("ST_XGMI_EP_MAX_MB", "512")) * (1 << 20))
-    return int(float(os.environ.get("ST_XGMI_MAX_MB", "64")) * (1 << 20))
+    return int(float(os.environ.get("ST_XGMI_MAX_MB", "512")) * (1 << 20))
 
 
 def node_group():
