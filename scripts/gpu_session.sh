@@ -56,6 +56,7 @@ for s in $STEPS; do
     flash_pmc) step flash_pmc 200 timeout -s KILL 150 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d gpurun_out/flash_pmc -o run --output-format csv -- python tools/bench_flash_bwd_ds.py || exit $? ;;
     rehearse_mx4k) step rehearse_mx4k 600 env LAYOUTS=mixtral_ep8 LAYOUT_TIMEOUT=500 ST_XGMI_EP_MAX_MB=48 bash scripts/rehearse_layouts_1gpu.sh || exit $? ;;
     rehearse_dp) step rehearse_dp 600 env LAYOUTS=dp LAYOUT_TIMEOUT=500 bash scripts/rehearse_layouts_1gpu.sh || exit $? ;;
+    gmm_pmc) step gmm_pmc 250 timeout -s KILL 200 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d gpurun_out/gmm_pmc -o run --output-format csv -- python tools/bench_grouped_gemm.py || exit $? ;;
     replay) step replay 1100 env ST_XGMI_EP_MAX_MB=48 python scripts/bench_reference_rows_8gpu.py --rehearse --steps 2 --warmup 1 --timeout 300 \
               --out gpurun_out/reference_rows_rehearsal.jsonl --filter "${REPLAY_FILTER:-.}" || exit $? ;;
     # the table is written under gpurun_out/ (merged back) and copied into scaletorch_amd/tuning/ by hand
