@@ -806,3 +806,30 @@ def test_expert_ffn_fused_matches_unfused():
             os.environ.pop("ST_MOE_FUSED_SWIGLU", None)
     for a, b in zip(res["1"], res["0"]):
         assert rel(a, b) < 2e-2
+
+
+@pytest.mark.parametrize("cp,rank", [(4, 1), (8, 3)])
+def test_cp_two_phase_backward_at_zigzag_offsets(cp, rank):
+    """The CP all-gather backward's two phases (parallel/context_parallel.py ``_CPAttnFn``):
+    per zig-zag chunk the dK/dV kernel with the dS workspace (``flash_bwd_kv``), then, while
+    the dK/dV reduce-scatter would be in flight, dQ = dS K (``flash_bwd_q_ds``) -- checked
+    per chunk at the rank's global offsets against the fp32 ``flash_bwd_ref``."""
+    from scaletorch_amd.parallel.context_parallel import zigzag_chunk_starts
+
+    torch.manual_seed(0)
+    S, H, Hkv, D = 128 * 2 * cp, 4, 2, 128
+    a, b, c = zigzag_chunk_starts(S, cp, rank)
+    kf = torch.randn(1, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    vf = torch.randn(1, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    for g0 in (a, b):
+        q = torch.randn(1, c, H, D, device="cuda", dtype=torch.bfloat16)
+        k, v = kf[:, :g0 + c], vf[:, :g0 + c]
+        out, lse = ops.flash_attn_fwd(q, k, v, scale, True, g0, 0)
+        dout = torch.randn_like(out)
+        dk, dv, ws = _lib.ops().flash_bwd_kv(dout, q, k, v, out, lse, scale, True, g0, 0, None, None)
+        assert ws.numel() > 0, "the dS path did not take the CP chunk shape"
+        dq = torch.empty_like(q)
+        _lib.ops().flash_bwd_q_ds(q, k, ws, scale, True, g0, 0, dq)
+        rq, rk, rv = ops.attention.flash_bwd_ref(dout, q, k, v, out, lse, scale, True, g0, 0)
+        assert rel(dq, rq) < 2e-2 and rel(dk, rk) < 2e-2 and rel(dv, rv) < 2e-2, g0
