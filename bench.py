@@ -73,6 +73,16 @@ def _tp_transport() -> dict:
     return dict(TRANSPORT)
 
 
+def _planned_ipc(args, mcfg) -> int:
+    """IPC areas the start-up transport self-tests may keep (utils/memory.py comm term)."""
+    if args.tp <= 1 and args.ep <= 1:
+        return 0
+    from scaletorch_amd.dist.xgmi import planned_ipc_bytes
+
+    msg = args.micro_batch_size * (args.seq_len // max(1, args.cp)) * mcfg.hidden_size * 2
+    return planned_ipc_bytes(args.tp, args.ep, msg, moe_dropless=args.moe_capacity_factor == 0 and args.ep > 1)
+
+
 def _visible_gpus() -> int:
     """GPUs this process may use, counted WITHOUT the HIP runtime (so the parent that
     starts the ranks never initialises a GPU): the KFD topology nodes that have SIMDs
@@ -218,7 +228,8 @@ def main() -> int:
                                grad_reduce_dtype=args.grad_reduce_dtype,
                                fused_head_chunk=args.head_chunk if args.fused_head else 0,
                                moe_dropless=args.moe_capacity_factor == 0 and args.ep > 1,
-                               optimizer_state_dtype=args.opt_state_dtype)
+                               optimizer_state_dtype=args.opt_state_dtype,
+                               xgmi_ipc_bytes=_planned_ipc(args, mcfg))
     if int(os.environ.get("RANK", "0")) == 0:
         print(f"[bench] layout {args.layout}: {args.model} tp{args.tp} pp{args.pp} cp{args.cp} ep{args.ep} dp{dp} "
               f"mbs{args.micro_batch_size} ga{ga} seq{args.seq_len}; HBM estimate {est.summary()}",

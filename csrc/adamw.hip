@@ -10,7 +10,12 @@
 //     written in the same pass;
 //   * the clip coefficient is read from DEVICE memory (computed from the
 //     all-reduced global norm), so clipping needs no host synchronisation;
-//   * grads may be fp32 (main_grad arena) or bf16.
+//   * grads may be fp32 (main_grad arena) or bf16;
+//   * bf16 moments are stored with STOCHASTIC rounding: a hashed 16-bit offset per
+//     (element, step, moment) is added to the fp32 bits before truncation, so the stored
+//     moment is unbiased.  Round-to-nearest froze exp_avg_sq at beta2 = 0.999, where the
+//     per-step change (0.1 %) is below bf16's half-ulp.  The hash is
+//     mirrored bit-for-bit by scaletorch_amd/optim.py ``sr_offsets``.
 #include "common.h"
 
 #include <cstdlib>
@@ -52,18 +57,41 @@ ST_DEVICE f32x4 load_s4<bf16_t>(const bf16_t* s, int64_t i) {
   r[3] = __uint_as_float(v[1] & 0xffff0000u);
   return r;
 }
+// 32-bit integer mixer (lowbias32): cheap, full avalanche; optim.py mirrors it in int64.
+ST_DEVICE uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+// key of one moment at one step (0 = m, 1 = v); the element index is its ARENA index
+// (launch base + local), so a ZeRO-1 shard rounds exactly as the replicated arena does
+ST_DEVICE uint32_t sr_key(uint32_t step, uint32_t which) {
+  return mix32((step * 0x9e3779b9u) ^ (which ? 0x85ebca6bu : 0u));
+}
+// stochastic fp32 -> bf16: add 16 random low bits, truncate; NaN / Inf keep the plain cast
+ST_DEVICE uint32_t sr_bf16(float x, int64_t idx, uint32_t key) {
+  const uint32_t u = __float_as_uint(x);
+  if ((u & 0x7f800000u) == 0x7f800000u) return f2bf(x);
+  const uint32_t r = mix32((uint32_t)idx ^ mix32((uint32_t)((uint64_t)idx >> 32) ^ key)) & 0xffffu;
+  return (u + r) >> 16;
+}
+
 template <typename S>
-ST_DEVICE void store_s4(S* s, int64_t i, f32x4 v);
+ST_DEVICE void store_s4(S* s, int64_t i, f32x4 v, uint32_t key, int64_t base);
 template <>
-ST_DEVICE void store_s4<float>(float* s, int64_t i, f32x4 v) {
+ST_DEVICE void store_s4<float>(float* s, int64_t i, f32x4 v, uint32_t, int64_t) {
   __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(s + i));
 }
 template <>
-ST_DEVICE void store_s4<bf16_t>(bf16_t* s, int64_t i, f32x4 v) {
+ST_DEVICE void store_s4<bf16_t>(bf16_t* s, int64_t i, f32x4 v, uint32_t key, int64_t base) {
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
   u32x2 o;
-  o[0] = pack_bf16x2(v[0], v[1]);
-  o[1] = pack_bf16x2(v[2], v[3]);
+  const int64_t gi = i + base;
+  o[0] = sr_bf16(v[0], gi, key) | (sr_bf16(v[1], gi + 1, key) << 16);
+  o[1] = sr_bf16(v[2], gi + 2, key) | (sr_bf16(v[3], gi + 3, key) << 16);
   __builtin_nontemporal_store(o, reinterpret_cast<u32x2*>(s + i));
 }
 
@@ -84,9 +112,11 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, 
                                                      S* __restrict__ v, const G* __restrict__ g,
                                                      bf16_t* __restrict__ p, const float* __restrict__ clip,
                                                      int64_t n4, float lr, float b1, float b2, float eps,
-                                                     float wd, float bc1, float bc2_sqrt) {
+                                                     float wd, float bc1, float bc2_sqrt, uint32_t sr_step,
+                                                     int64_t sr_base) {
   const float cs = clip ? *clip : 1.f;
   const float step = lr / bc1, decay = 1.f - lr * wd;
+  const uint32_t km = sr_key(sr_step, 0), kv = sr_key(sr_step, 1);
   // Two 4-element chunks per thread per iteration, all loads issued before any math
   // (10 independent HBM streams in flight per thread); every byte is touched
   // exactly once, so loads/stores are non-temporal (no L2 pollution).
@@ -118,8 +148,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, 
         vv[u][k] = vk;
       }
       __builtin_nontemporal_store(w[u], reinterpret_cast<f32x4*>(master + ii[u]));
-      store_s4<S>(m, ii[u], mm[u]);
-      store_s4<S>(v, ii[u], vv[u]);
+      store_s4<S>(m, ii[u], mm[u], km, sr_base);
+      store_s4<S>(v, ii[u], vv[u], kv, sr_base);
       if (p) {
         uint2 o;
         o.x = pack_bf16x2(w[u][0], w[u][1]);
@@ -147,10 +177,12 @@ __global__ __launch_bounds__(256) void adamw_wt_kernel(float* __restrict__ maste
                                                         bf16_t* __restrict__ p, bf16_t* __restrict__ wt,
                                                         const float* __restrict__ clip, int R, int C, float lr,
                                                         float b1, float b2, float eps, float wd, float bc1,
-                                                        float bc2_sqrt) {
+                                                        float bc2_sqrt, uint32_t sr_step, int64_t sr_base) {
   __shared__ bf16_t tile[kWT * kWLd];
   const float cs = clip ? *clip : 1.f;
   const float step = lr / bc1, decay = 1.f - lr * wd;
+  // same keys and element indices as the flat kernel over this weight: bitwise-equal moments
+  const uint32_t km = sr_key(sr_step, 0), kv = sr_key(sr_step, 1);
   const int tiles_c = C / kWT;
   const int b = xcd_remap(blockIdx.x, gridDim.x);
   const int r0 = (b / tiles_c) * kWT, c0 = (b % tiles_c) * kWT;
@@ -179,8 +211,8 @@ __global__ __launch_bounds__(256) void adamw_wt_kernel(float* __restrict__ maste
       vv[u][k] = vk;
     }
     __builtin_nontemporal_store(w[u], reinterpret_cast<f32x4*>(master + i));
-    store_s4<S>(m, i, mm[u]);
-    store_s4<S>(v, i, vv[u]);
+    store_s4<S>(m, i, mm[u], km, sr_base);
+    store_s4<S>(v, i, vv[u], kv, sr_base);
     const uint32_t lo = pack_bf16x2(w[u][0], w[u][1]), hi = pack_bf16x2(w[u][2], w[u][3]);
     *reinterpret_cast<uint2*>(p + i) = make_uint2(lo, hi);
     // padded LDS row (132 B): 4-B aligned only
@@ -207,18 +239,18 @@ __global__ __launch_bounds__(256) void adamw_wt_kernel(float* __restrict__ maste
 template <typename S>
 int launch_adamw_wt(float* master, S* m, S* v, const void* g, int g_is_bf16, void* p, void* wt,
                     const float* clip, int R, int C, float lr, float b1, float b2, float eps, float wd,
-                    float bc1, float bc2_sqrt, hipStream_t st) {
+                    float bc1, float bc2_sqrt, uint32_t sr_step, int64_t sr_base, hipStream_t st) {
   if (R % kWT || C % kWT || R <= 0 || C <= 0) return -2;
   const int64_t blocks = (int64_t)(R / kWT) * (C / kWT);
   if (blocks > 0x7fffffff) return -3;
   if (g_is_bf16)
     adamw_wt_kernel<bf16_t, S><<<(unsigned)blocks, 256, 0, st>>>(master, m, v, (const bf16_t*)g, (bf16_t*)p,
                                                                  (bf16_t*)wt, clip, R, C, lr, b1, b2, eps, wd,
-                                                                 bc1, bc2_sqrt);
+                                                                 bc1, bc2_sqrt, sr_step, sr_base);
   else
     adamw_wt_kernel<float, S><<<(unsigned)blocks, 256, 0, st>>>(master, m, v, (const float*)g, (bf16_t*)p,
                                                                 (bf16_t*)wt, clip, R, C, lr, b1, b2, eps, wd,
-                                                                bc1, bc2_sqrt);
+                                                                bc1, bc2_sqrt, sr_step, sr_base);
   return 0;
 }
 
@@ -270,13 +302,13 @@ unsigned adamw_grid(int64_t n4) {
 template <typename S>
 void launch_adamw(float* master, S* m, S* v, const void* g, int g_is_bf16, void* p,
                          const float* clip, int64_t n4, float lr, float b1, float b2, float eps,
-                         float wd, float bc1, float bc2_sqrt, hipStream_t st) {
+                         float wd, float bc1, float bc2_sqrt, uint32_t sr_step, int64_t sr_base, hipStream_t st) {
   if (g_is_bf16)
     adamw_kernel<bf16_t, S><<<adamw_grid(n4), 256, 0, st>>>(master, m, v, (const bf16_t*)g, (bf16_t*)p,
-                                                          clip, n4, lr, b1, b2, eps, wd, bc1, bc2_sqrt);
+                                                          clip, n4, lr, b1, b2, eps, wd, bc1, bc2_sqrt, sr_step, sr_base);
   else
     adamw_kernel<float, S><<<adamw_grid(n4), 256, 0, st>>>(master, m, v, (const float*)g, (bf16_t*)p,
-                                                         clip, n4, lr, b1, b2, eps, wd, bc1, bc2_sqrt);
+                                                         clip, n4, lr, b1, b2, eps, wd, bc1, bc2_sqrt, sr_step, sr_base);
 }
 
 }  // namespace
@@ -286,28 +318,28 @@ extern "C" {
 // states_bf16: exp_avg / exp_avg_sq are bf16 arrays (else fp32)
 int st_adamw_step(float* master, void* m, void* v, int states_bf16, const void* g, int g_is_bf16,
                   void* p, const float* clip, int64_t n, float lr, float b1, float b2, float eps,
-                  float wd, float bc1, float bc2_sqrt, hipStream_t st) {
+                  float wd, float bc1, float bc2_sqrt, uint32_t sr_step, int64_t sr_base, hipStream_t st) {
   if (n % 4 != 0) return -2;
   const int64_t n4 = n / 4;
   if (n4 == 0) return 0;
   if (states_bf16)
     launch_adamw<bf16_t>(master, (bf16_t*)m, (bf16_t*)v, g, g_is_bf16, p, clip, n4, lr, b1, b2, eps, wd,
-                         bc1, bc2_sqrt, st);
+                         bc1, bc2_sqrt, sr_step, sr_base, st);
   else
     launch_adamw<float>(master, (float*)m, (float*)v, g, g_is_bf16, p, clip, n4, lr, b1, b2, eps, wd, bc1,
-                        bc2_sqrt, st);
+                        bc2_sqrt, sr_step, sr_base, st);
   return (int)hipGetLastError();
 }
 
 // AdamW over one [R, C] weight run + its bf16 transpose W^T [C, R] (see adamw_wt_kernel)
 int st_adamw_wt_step(float* master, void* m, void* v, int states_bf16, const void* g, int g_is_bf16,
                      void* p, void* wt, int R, int C, const float* clip, float lr, float b1, float b2,
-                     float eps, float wd, float bc1, float bc2_sqrt, hipStream_t st) {
+                     float eps, float wd, float bc1, float bc2_sqrt, uint32_t sr_step, int64_t sr_base, hipStream_t st) {
   const int rc = states_bf16
                      ? launch_adamw_wt<bf16_t>(master, (bf16_t*)m, (bf16_t*)v, g, g_is_bf16, p, wt, clip, R, C,
-                                               lr, b1, b2, eps, wd, bc1, bc2_sqrt, st)
+                                               lr, b1, b2, eps, wd, bc1, bc2_sqrt, sr_step, sr_base, st)
                      : launch_adamw_wt<float>(master, (float*)m, (float*)v, g, g_is_bf16, p, wt, clip, R, C, lr,
-                                              b1, b2, eps, wd, bc1, bc2_sqrt, st);
+                                              b1, b2, eps, wd, bc1, bc2_sqrt, sr_step, sr_base, st);
   if (rc) return rc;
   return (int)hipGetLastError();
 }

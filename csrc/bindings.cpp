@@ -29,10 +29,10 @@ int st_swiglu_bwd(const void* dout, const void* gu, void* dgu, int64_t N, int64_
                   hipStream_t st);
 int st_adamw_step(float* master, void* m, void* v, int states_bf16, const void* g, int g_is_bf16,
                   void* p, const float* clip, int64_t n, float lr, float b1, float b2, float eps,
-                  float wd, float bc1, float bc2_sqrt, hipStream_t st);
+                  float wd, float bc1, float bc2_sqrt, uint32_t sr_step, int64_t sr_base, hipStream_t st);
 int st_adamw_wt_step(float* master, void* m, void* v, int states_bf16, const void* g, int g_is_bf16,
                      void* p, void* wt, int R, int C, const float* clip, float lr, float b1, float b2,
-                     float eps, float wd, float bc1, float bc2_sqrt, hipStream_t st);
+                     float eps, float wd, float bc1, float bc2_sqrt, uint32_t sr_step, int64_t sr_base, hipStream_t st);
 int st_sumsq_partials();
 int st_sumsq(const void* g, int g_is_bf16, int64_t n, float* partial, float* out, hipStream_t st);
 int st_xent_fwd(const void* logits, int64_t ld, const int64_t* tgt, int64_t N, int V,
@@ -263,7 +263,7 @@ at::Tensor swiglu_bwd(const at::Tensor& dout, const at::Tensor& gu, const c10::o
 void adamw_step_(at::Tensor master, at::Tensor exp_avg, at::Tensor exp_avg_sq,
                  const at::Tensor& grad, const c10::optional<at::Tensor>& param,
                  const c10::optional<at::Tensor>& clip_coef, double lr, double beta1, double beta2,
-                 double eps, double weight_decay, int64_t step) {
+                 double eps, double weight_decay, int64_t step, int64_t sr_base) {
   TORCH_CHECK(master.is_cuda() && master.scalar_type() == at::kFloat && master.is_contiguous(),
               "adamw: master must be contiguous fp32 on GPU");
   const int64_t n = master.numel();
@@ -299,7 +299,7 @@ void adamw_step_(at::Tensor master, at::Tensor exp_avg, at::Tensor exp_avg_sq,
                          sbf ? 1 : 0, grad.data_ptr(),
                          grad.scalar_type() == at::kBFloat16 ? 1 : 0, pp, cp, n, (float)lr,
                          (float)beta1, (float)beta2, (float)eps, (float)weight_decay, (float)bc1,
-                         (float)std::sqrt(bc2), cur_stream());
+                         (float)std::sqrt(bc2), (uint32_t)step, sr_base, cur_stream());
   ST_CHECK_RC(rc, "adamw_step_");
 }
 
@@ -307,7 +307,7 @@ void adamw_step_(at::Tensor master, at::Tensor exp_avg, at::Tensor exp_avg_sq,
 // transposed into `wt` [C, R] (param is the [R, C] weight view of the arena)
 void adamw_wt_step_(at::Tensor master, at::Tensor exp_avg, at::Tensor exp_avg_sq, const at::Tensor& grad,
                     at::Tensor param, at::Tensor wt, const c10::optional<at::Tensor>& clip_coef, double lr,
-                    double beta1, double beta2, double eps, double weight_decay, int64_t step) {
+                    double beta1, double beta2, double eps, double weight_decay, int64_t step, int64_t sr_base) {
   TORCH_CHECK(param.dim() == 2 && param.is_contiguous(), "adamw_wt: param must be a contiguous 2-D weight");
   check_bf16_cuda(param, "param");
   check_bf16_cuda(wt, "wt");
@@ -338,7 +338,7 @@ void adamw_wt_step_(at::Tensor master, at::Tensor exp_avg, at::Tensor exp_avg_sq
   int rc = st_adamw_wt_step(master.data_ptr<float>(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(), sbf ? 1 : 0,
                             grad.data_ptr(), grad.scalar_type() == at::kBFloat16 ? 1 : 0, param.data_ptr(),
                             wt.data_ptr(), (int)R, (int)C, cp, (float)lr, (float)beta1, (float)beta2, (float)eps,
-                            (float)weight_decay, (float)bc1, (float)std::sqrt(bc2), cur_stream());
+                            (float)weight_decay, (float)bc1, (float)std::sqrt(bc2), (uint32_t)step, sr_base, cur_stream());
   ST_CHECK_RC(rc, "adamw_wt_step_");
 }
 
@@ -1030,8 +1030,8 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, Tensor? pos, int pos_offset, bool backward) -> ()");
   m.def("swiglu_fwd(Tensor gate_up, Tensor? nvalid=None) -> Tensor");
   m.def("swiglu_bwd(Tensor dout, Tensor gate_up, Tensor? nvalid=None) -> Tensor");
-  m.def("adamw_step_(Tensor(a!) master, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor grad, Tensor(d!)? param, Tensor? clip_coef, float lr, float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
-  m.def("adamw_wt_step_(Tensor(a!) master, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor grad, Tensor(d!) param, Tensor(e!) wt, Tensor? clip_coef, float lr, float beta1, float beta2, float eps, float weight_decay, int step) -> ()");
+  m.def("adamw_step_(Tensor(a!) master, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor grad, Tensor(d!)? param, Tensor? clip_coef, float lr, float beta1, float beta2, float eps, float weight_decay, int step, int sr_base=0) -> ()");
+  m.def("adamw_wt_step_(Tensor(a!) master, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor grad, Tensor(d!) param, Tensor(e!) wt, Tensor? clip_coef, float lr, float beta1, float beta2, float eps, float weight_decay, int step, int sr_base=0) -> ()");
   m.def("sumsq_(Tensor g, Tensor(a!) out) -> ()");
   m.def("transpose_(Tensor src, Tensor(a!) dst) -> ()");
   m.def("embedding_bwd_(Tensor(a!) grad, Tensor dy, Tensor sorted_ids, Tensor order) -> ()");

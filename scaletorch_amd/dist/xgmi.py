@@ -298,6 +298,29 @@ def _max_bytes_default(kind: str = "pair") -> int:
     return int(float(os.environ.get("ST_XGMI_MAX_MB", "512")) * (1 << 20))
 
 
+def area_bytes(max_bytes: int) -> int:
+    """Device memory one communicator allocates (csrc/xgmi_allreduce.hip: a 16 KiB flag
+    header + 4 data areas: two collectives in flight x two epoch parities)."""
+    return 16384 + 4 * ((int(max_bytes) + 255) // 256 * 256)
+
+
+def planned_ipc_bytes(tp: int = 1, ep: int = 1, tp_msg_bytes: int | None = None,
+                      moe_dropless: bool = False) -> int:
+    """Upper bound of the IPC areas a rank holds when the start-up self-tests keep xGMI
+    (losers are closed): tp = 2 -> the node communicator of the pair path + the 2-rank one;
+    tp > 2 -> one TP-group communicator sized by the message; EP dropless -> the push area."""
+    from ..parallel.tensor_parallel import _tp_area_bytes
+
+    total = 0
+    if tp == 2:
+        total += area_bytes(_max_bytes_default()) + area_bytes(64 << 20)
+    elif tp > 2:
+        total += area_bytes(_tp_area_bytes(tp_msg_bytes))
+    if ep > 1 and moe_dropless:
+        total += area_bytes(_max_bytes_default("ep"))
+    return total
+
+
 def node_group():
     """The process group of the ranks on this node (collective over the WORLD: every rank
     creates every node's group, in the same order)."""

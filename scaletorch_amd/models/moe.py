@@ -219,19 +219,35 @@ def capacity_receive_order(recv_kept: torch.Tensor, cap: int):
 # so only the real rows cost FLOPs.  Reference: dispatch_tokens / gather_tokens,
 # scaletorch/parallel/expert_parallel/ep_comms.py:41-171 (host-synced splits, three
 # all-to-alls, no autograd).
-_ROWS_BOUND: dict = {}
+_TOKEN_BOUND: dict = {"n": None}
+
+
+def set_ep_token_bound(n: int | None) -> None:
+    """Declare the token count of every MoE call on every EP rank (the trainer: micro-batch x
+    sequence / cp -- identical on all ranks by construction, its loaders drop ragged tail
+    batches).  With it the exchange buffers are sized on the host with NO collective; without
+    it (library use, tests) every call agrees on the bound with one small all-reduce."""
+    _TOKEN_BOUND["n"] = None if n is None else int(n)
 
 
 def ep_rows_range(T: int, group) -> tuple[int, int]:
-    """(smallest, largest) local token count over the EP group (one host sync per distinct T)."""
-    key = (id(group), int(T))
-    if key not in _ROWS_BOUND:
-        t = torch.tensor([int(T), -int(T)], dtype=torch.int64,
-                         device="cuda" if (torch.cuda.is_available() and _group_on_gpu(group)) else "cpu")
-        if C.get_world_size(group) > 1:
-            C.all_reduce(t, op="max", group=group)
-        _ROWS_BOUND[key] = (-int(t[1].item()), int(t[0].item()))
-    return _ROWS_BOUND[key]
+    """(smallest, largest) local token count over the EP group.
+
+    Every rank takes the same branch on every call, so the collectives on the EP group stay
+    in step even when the token counts change between calls: with a declared bound
+    (``set_ep_token_bound``) no collective runs and the range is (T, bound) -- a local T above
+    the bound raises; otherwise ONE all-reduce per call (no cache keyed on the local T: a rank
+    whose T repeats would skip the collective its peers enter -- ADVICE r04)."""
+    n = _TOKEN_BOUND["n"]
+    if n is not None:
+        if int(T) > n:
+            raise ValueError(f"MoE call with {T} tokens exceeds the declared EP token bound {n}")
+        return int(T), n
+    t = torch.tensor([int(T), -int(T)], dtype=torch.int64,
+                     device="cuda" if (torch.cuda.is_available() and _group_on_gpu(group)) else "cpu")
+    if C.get_world_size(group) > 1:
+        C.all_reduce(t, op="max", group=group)
+    return -int(t[1].item()), int(t[0].item())
 
 
 def ep_rows_bound(T: int, group) -> int:
@@ -291,13 +307,15 @@ def ep_exchange_reference(xs: list, M: torch.Tensor, El: int, direction: int, ou
     return outs
 
 
-def _ep_exchange_rccl(x: torch.Tensor, M: torch.Tensor, El: int, direction: int, out_rows: int, group):
-    """The exchange over RCCL / gloo: exact splits from ONE host read of M (the
-    dispatch and combine of a layer reuse it through autograd), same layouts as the
-    push kernel."""
+def _ep_exchange_rccl(x: torch.Tensor, M: torch.Tensor, El: int, direction: int, out_rows: int, group,
+                      Mh: torch.Tensor | None = None):
+    """The exchange over RCCL / gloo with exact splits, same layouts as the push kernel.
+    ``Mh``: M already read to the host -- the MoE layer reads it ONCE per forward and hands
+    it to the dispatch, the combine and both backward exchanges (``_EPExchange``)."""
     ep = M.shape[0]
     me = C.get_rank(group)
-    Mh = M.detach().to("cpu", torch.int64)
+    if Mh is None:
+        Mh = M.detach().to("cpu", torch.int64)
     rows_to = Mh.view(ep, ep, El).sum(2)  # [source, owner]
     R = int(rows_to[:, me].sum())
     q = ep_owner_positions(M.to(x.device), El, me, R)
@@ -317,7 +335,7 @@ def _ep_exchange_rccl(x: torch.Tensor, M: torch.Tensor, El: int, direction: int,
 _ZERO_PAD = [os.environ.get("ST_MOE_ZERO_PAD", "0") == "1"]  # zero the unused tail of R_max buffers (debug)
 
 
-def _ep_exchange(x, M, El, direction, out_rows, area_rows, group, comm):
+def _ep_exchange(x, M, El, direction, out_rows, area_rows, group, comm, Mh=None):
     # bytes counted = the rows that really travel per rank (dispatch: this rank's T*k sorted
     # rows; combine: the T*k rows it gets back), not the R_max-row padded expert buffer
     trace.record("ep.exchange" if direction == 0 else "ep.exchange_back", x if direction == 0 else x[:out_rows],
@@ -336,20 +354,20 @@ class _EPExchange(torch.autograd.Function):
     (direction 1); backward is the other direction with the same counts."""
 
     @staticmethod
-    def forward(ctx, x, M, El, direction, out_rows, bounds, group, comm):
+    def forward(ctx, x, M, El, direction, out_rows, bounds, group, comm, Mh=None):
         ctx.save_for_backward(M)
-        ctx.meta = (El, direction, x.shape[0], bounds, group, comm)
+        ctx.meta = (El, direction, x.shape[0], bounds, group, comm, Mh)
         area = bounds[0] if direction == 0 else bounds[1]
-        return _ep_exchange(x, M, El, direction, out_rows, area, group, comm)
+        return _ep_exchange(x, M, El, direction, out_rows, area, group, comm, Mh)
 
     @staticmethod
     def backward(ctx, g):
         (M,) = ctx.saved_tensors
-        El, direction, in_rows, bounds, group, comm = ctx.meta
+        El, direction, in_rows, bounds, group, comm, Mh = ctx.meta
         rev = 1 - direction
         area = bounds[0] if rev == 0 else bounds[1]
-        return (_ep_exchange(g.contiguous(), M, El, rev, in_rows, area, group, comm),
-                None, None, None, None, None, None, None)
+        return (_ep_exchange(g.contiguous(), M, El, rev, in_rows, area, group, comm, Mh),
+                None, None, None, None, None, None, None, None)
 
 
 def ep_counts_matrix(counts: torch.Tensor, group, comm=None) -> torch.Tensor:
@@ -389,6 +407,14 @@ def select_ep_transport(group, requested: str = "auto") -> str:
     choice = "xgmi" if int(flag.item()) == 1 else "rccl"
     if requested == "xgmi" and choice != "xgmi":
         raise RuntimeError(f"ep_comm xgmi requested but the push exchange self-test failed: {info}")
+    if choice == "rccl":
+        # free the losing communicator's IPC area (kHeader + 4 x 512 MiB by default) once no
+        # peer can still be reading it
+        comm = _EP_XGMI.pop(id(group), None)
+        if comm is not None:
+            torch.cuda.synchronize()
+            C.barrier(group=group)
+            comm.close()
     _DISPATCH["comm"] = choice
     EP_TRANSPORT.update(ep=choice, selftest=info)
     return choice
@@ -787,14 +813,17 @@ class MoELayer(nn.Module):
         if comm is not None and not (comm.ep_fits(R_max, xs) and comm.ep_fits(Tk_max, xs)):
             comm = None  # buffers too small for this shape: RCCL exchange
         M = ep_counts_matrix(counts, group, comm)
+        # RCCL transport: ONE host read of the counts per layer forward, shared by the dispatch,
+        # the combine and both backward exchanges (the xGMI push exchange reads none)
+        Mh = M.detach().to("cpu", torch.int64) if comm is None else None
         mine = M[:, self.ep_rank * El:(self.ep_rank + 1) * El]
         offs = torch.cumsum(mine.sum(0), 0, dtype=torch.int32)  # grouped-GEMM offsets (device)
-        xe = _EPExchange.apply(xs, M, El, 0, R_max, (R_max, Tk_max), group, comm)
+        xe = _EPExchange.apply(xs, M, El, 0, R_max, (R_max, Tk_max), group, comm, Mh)
         xe._st_padded = True  # R_max rows, the first offs[-1] real: the FFN recomputes a over those
         ye = self.experts(xe, offs=offs)
         self.dropped_rows = xs.new_zeros((), dtype=torch.int64)  # dropless by construction
         self.ep_rows_sent = Tk - mine[self.ep_rank].sum()  # rows that left this rank (device)
-        return _EPExchange.apply(ye, M, El, 1, Tk, (R_max, Tk_max), group, comm)
+        return _EPExchange.apply(ye, M, El, 1, Tk, (R_max, Tk_max), group, comm, Mh)
 
     def _tp_reduce(self, out: torch.Tensor, tp_group) -> torch.Tensor:
         # expert down-projections are TP partial sums: reduce once, after the combine

@@ -38,6 +38,55 @@ from .dist import trace
 from .ops import _lib
 
 
+
+# ---------------------------------------------------------------- bf16 moments: stochastic rounding
+# Mirror of csrc/adamw.hip ``sr_bf16`` (bit-for-bit): a 16-bit offset hashed from (element
+# index, step, launch length, moment) is added to the fp32 bits, which are then truncated,
+# so a stored bf16 moment is an UNBIASED estimate of its fp32 value.  Round-to-nearest
+# froze exp_avg_sq at beta2 = 0.999 (its 0.1 % per-step change is below bf16's half-ulp).
+_M32 = 0xFFFFFFFF
+
+
+def _mix32_int(x: int) -> int:
+    x &= _M32
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & _M32
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & _M32
+    x ^= x >> 16
+    return x
+
+
+def _mix32(x: torch.Tensor) -> torch.Tensor:
+    """lowbias32 on an int64 tensor of uint32 values (wrapping products masked to 32 bits)."""
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    return x ^ (x >> 16)
+
+
+def sr_key(step: int, which: int) -> int:
+    """Key of one moment at one step (0 = exp_avg, 1 = exp_avg_sq)."""
+    return _mix32_int(((int(step) * 0x9E3779B9) & _M32) ^ (0x85EBCA6B if which else 0))
+
+
+def sr_round_bf16(x: torch.Tensor, key: int, base: int = 0) -> torch.Tensor:
+    """fp32 ``x`` -> bf16 by stochastic rounding, as the kernel; element i of ``x`` (flat
+    order) is arena element ``base + i`` -- the index the offset is hashed from, so a ZeRO-1
+    shard rounds exactly as the replicated arena does."""
+    xf = x.reshape(-1).float()
+    idx = torch.arange(base, base + xf.numel(), dtype=torch.int64, device=xf.device)
+    u = xf.view(torch.int32).to(torch.int64) & _M32
+    r = _mix32((idx & _M32) ^ _mix32((idx >> 32) ^ key)) & 0xFFFF
+    bits = ((u + r) >> 16) & 0xFFFF
+    out = (bits - (bits >= 0x8000).to(torch.int64) * 0x10000).to(torch.int16).view(torch.bfloat16)
+    special = (u & 0x7F800000) == 0x7F800000
+    if bool(special.any()):
+        out = torch.where(special, xf.to(torch.bfloat16), out)
+    return out
+
+
 class _ArenaOptimizer(torch.optim.Optimizer):
     """Base: per-arena optimizer state over the arena's SEGMENTS -- the whole
     arena, or under ZeRO-1 (data_parallel.GradArena ``zero1``) this rank's
@@ -223,13 +272,14 @@ class ArenaAdamW(_ArenaOptimizer):
                                 s0 = so + plo - lo
                                 _lib.ops().adamw_step_(a.master[s0: s0 + phi - plo], a.exp_avg[s0: s0 + phi - plo],
                                                        a.exp_avg_sq[s0: s0 + phi - plo], a.grad_flat[plo:phi],
-                                                       a.param_flat[plo:phi], self.clip_coef, lr, b1, b2, eps, wd, t)
+                                                       a.param_flat[plo:phi], self.clip_coef, lr, b1, b2, eps, wd, t,
+                                                       plo)
                             else:
                                 s0 = so + plo - lo
                                 _lib.ops().adamw_wt_step_(a.master[s0: s0 + phi - plo], a.exp_avg[s0: s0 + phi - plo],
                                                           a.exp_avg_sq[s0: s0 + phi - plo], a.grad_flat[plo:phi],
                                                           a.param_flat[plo:phi].view(w.shape), w._st_wt,
-                                                          self.clip_coef, lr, b1, b2, eps, wd, t)
+                                                          self.clip_coef, lr, b1, b2, eps, wd, t, plo)
                                 fused.append(w)
                     if a.zero1:
                         trace.record("dp.all_gather", a.param_flat[b.start: b.end], group_size=a.world, arena=a.name)
@@ -280,9 +330,10 @@ class ArenaAdamW(_ArenaOptimizer):
             lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
             native = (self.fused and self.decoupled and _lib.use_native(a.param_flat) and a.master is not None
                       and a.param_flat.dtype == torch.bfloat16)
-            for param, gseg, master, m, v in self._views(a, (a.exp_avg, a.exp_avg_sq)):
+            for (param, gseg, master, m, v), base in zip(self._views(a, (a.exp_avg, a.exp_avg_sq)),
+                                                         (lo for lo, _, _ in a.segments())):
                 if native:
-                    _lib.ops().adamw_step_(master, m, v, gseg, param, self.clip_coef, lr, b1, b2, eps, wd, t)
+                    _lib.ops().adamw_step_(master, m, v, gseg, param, self.clip_coef, lr, b1, b2, eps, wd, t, base)
                     continue
                 grad = gseg.float()
                 if self.clip_coef is not None:
@@ -290,13 +341,13 @@ class ArenaAdamW(_ArenaOptimizer):
                 if not self.decoupled and wd:
                     grad = grad + wd * master
                 m_st, v_st = m, v
-                if m.dtype != torch.float32:  # bf16 moments: fp32 math, one rounding per step (as the kernel)
+                if m.dtype != torch.float32:  # bf16 moments: fp32 math, one stochastic rounding per step
                     m, v = m.float(), v.float()
                 m.mul_(b1).add_(grad, alpha=1 - b1)
                 v.mul_(b2).addcmul_(grad, grad, value=1 - b2)
                 if m_st is not m:
-                    m_st.copy_(m)
-                    v_st.copy_(v)
+                    m_st.copy_(sr_round_bf16(m, sr_key(t, 0), base).view_as(m_st))
+                    v_st.copy_(sr_round_bf16(v, sr_key(t, 1), base).view_as(v_st))
                 bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
                 denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
                 if self.decoupled and wd:

@@ -136,6 +136,7 @@ class _CPAttnFn(torch.autograd.Function):
         order = sorted(range(len(chunks)), key=lambda i: -(chunks[i][2] + chunks[i][1]))  # widest prefix first
         covered = 0
         pending_dq = []  # (chunk, workspace) whose dQ pass runs under the reduce-scatter
+        pending_bytes, budget = 0, _ds_budget_bytes()
         native = _lib.use_native(q)
         for i in order:
             off, n, g0 = chunks[i]
@@ -150,11 +151,19 @@ class _CPAttnFn(torch.autograd.Function):
             if native:
                 dk_c, dv_c, ws = _lib.ops().flash_bwd_kv(*args, dkv[:, :kend, :Hkv] if first else None,
                                                          dkv[:, :kend, Hkv:] if first else None)
-                if ws.numel():
+                if ws.numel() and pending_bytes + ws.numel() * ws.element_size() > budget and pending_dq:
+                    # the kept workspaces would pass the budget: this chunk's dQ runs now and
+                    # its workspace is freed before the next chunk (peak = budget
+                    # + one chunk, not the sum over chunks)
+                    _lib.ops().flash_bwd_q_ds(q[:, off: off + n], k_full[:, :kend], ws, scale, True, g0, 0,
+                                              dq[:, off: off + n])
+                    ws = False
+                elif ws.numel():
                     pending_dq.append((i, ws))
+                    pending_bytes += ws.numel() * ws.element_size()
                 else:
                     ws = None
-            if ws is None:  # one-shot backward (dQ now)
+            if ws is None:  # one-shot backward (dQ now); ws False: dS path, dQ already done
                 if first:
                     ops.flash_attn_bwd(*args, dq=dq[:, off: off + n], dk=dkv[:, :kend, :Hkv],
                                        dv=dkv[:, :kend, Hkv:])
@@ -175,6 +184,15 @@ class _CPAttnFn(torch.autograd.Function):
         if work is not None:
             work.wait()
         return dq, rs.transpose(0, 1).contiguous(), None, None, None, None, None
+
+
+def _ds_budget_bytes() -> int:
+    """Bytes of dS workspace the CP backward may keep alive for its deferred dQ passes
+    (ST_CP_DS_BUDGET_GB, default 6 GB): the first chunk's workspace is always deferred, a
+    later one only while the total stays within the budget."""
+    import os
+
+    return int(float(os.environ.get("ST_CP_DS_BUDGET_GB", "6")) * 1e9)
 
 
 def _chunks_of(rank: int, S: int, cp: int, s: int, zigzag: bool):

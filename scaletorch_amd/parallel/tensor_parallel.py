@@ -40,19 +40,24 @@ def _ws(group) -> int:
     return C.get_world_size(group)
 
 
-# TP all-reduce transport: "rccl" (default) or "xgmi" (dist/xgmi.py: one-shot /
-# two-shot over IPC-mapped peer buffers; falls back to RCCL for messages it
-# does not take).  One communicator per TP group, created on first use.
+# TP transport: "rccl" or "xgmi" (dist/xgmi.py: one-shot / two-shot all-reduce, all-gather,
+# reduce-scatter over IPC-mapped peer buffers; messages a kernel does not take go to RCCL).
+# One communicator per TP group.  ``_TP_XGMI_OPS``: which collectives take the xGMI path --
+# the start-up self-test keeps each only where it beat RCCL at the run's real message size.
 _TP_COMM = "rccl"
 _XGMI: dict = {}
+_TP_XGMI_OPS = {"all_reduce": True, "all_gather": True, "reduce_scatter": True}
 
 
-def set_tp_comm(kind: str) -> None:
+def set_tp_comm(kind: str, ops: dict | None = None) -> None:
     global _TP_COMM
     if kind not in ("rccl", "xgmi"):
         raise ValueError(f"tp_comm must be rccl or xgmi, got {kind!r}")
     _TP_COMM = kind
+    for op in _TP_XGMI_OPS:
+        _TP_XGMI_OPS[op] = kind == "xgmi" and (ops is None or bool(ops.get(op, False)))
     TRANSPORT["tp"] = kind
+    TRANSPORT["ops"] = [op for op, on in _TP_XGMI_OPS.items() if on] if kind == "xgmi" else []
 
 
 _PAIR: list = [None]  # dist/xgmi.PairPath of a 2-rank TP group (multipath SP collectives)
@@ -67,48 +72,144 @@ def setup_tp_pair_path(group) -> None:
     _PAIR[0] = setup_pair_path(group)
 
 
-TRANSPORT: dict = {"tp": "rccl", "selftest": None}  # chosen TP transport (bench JSON reports it)
+TRANSPORT: dict = {"tp": "rccl", "ops": [], "selftest": None}  # chosen TP transport (bench JSON reports it)
 
 
-def select_tp_transport(group, requested: str = "auto", probe_mb: int = 64) -> str:
+def _tp_area_bytes(msg_bytes: int | None) -> int:
+    """IPC data area of a TP-group communicator: the run's largest TP message (the
+    all-reduce / reduce-scatter input [B, S, h] bf16) rounded up to 8 MiB, at least 16 MiB;
+    ST_XGMI_TP_MAX_MB overrides (shared-GPU rehearsals and tests set it small)."""
+    import os
+
+    env = os.environ.get("ST_XGMI_TP_MAX_MB")
+    if env:
+        return int(float(env) * (1 << 20))
+    m = int(msg_bytes or (64 << 20))
+    return max(16 << 20, -(-m // (8 << 20)) * (8 << 20))
+
+
+def _close_tp_xgmi() -> None:
+    """Release every TP-side IPC area (a losing self-test keeps no dead HBM)."""
+    for comm in list(_XGMI.values()):
+        comm.close()
+    _XGMI.clear()
+    if _PAIR[0] is not None:
+        _PAIR[0].comm.close()
+    _PAIR[0] = None
+
+
+def select_tp_transport(group, requested: str = "auto", probe_mb: int = 64, msg_bytes: int | None = None) -> str:
     """Pick the TP transport at start-up; collective over the WORLD (every rank calls it).
 
-    ``requested`` "rccl" / "xgmi" are taken as given.  "auto": for a 2-rank TP group on
-    one node, set up the 7-link pair path (dist/xgmi.py ``setup_pair_path``) and
-    self-test it against RCCL on the TP group -- a ``probe_mb`` MiB all-gather and
-    reduce-scatter must match RCCL (AG bitwise, RS within one bf16 rounding), no xGMI
-    wait may time out, and the pair path must be faster than RCCL on both.  The
-    verdict is MIN-reduced over the world, so every rank takes the same path; any
-    failure falls back to RCCL.  Reference transport: RCCL/NCCL only
-    (scaletorch/parallel/sequence_parallel/sp_comms.py:31-94)."""
+    ``requested`` "rccl" / "xgmi" are taken as given.  "auto", every TP size on one node:
+      * tp = 2: the 7-link pair path (dist/xgmi.py ``setup_pair_path``) self-tested against
+        RCCL -- a ``probe_mb`` MiB all-gather and reduce-scatter (AG bitwise, RS within one
+        bf16 rounding), kept only if faster on both;
+      * tp > 2 (4 / 8: the reference's TP4 / TP8 rows): a communicator over the TP group
+        whose all-reduce (one-shot <= 512 KiB, two-shot above), all-gather and
+        reduce-scatter are each timed against RCCL at the run's REAL message size
+        ``msg_bytes`` (the [B, S, h] activation a row-parallel linear all-reduces) --
+        all-gather bitwise equal to RCCL's, all-reduce / reduce-scatter within one bf16
+        rounding of an fp32 sum of the gathered inputs; each collective keeps xGMI only
+        where it is correct AND faster.
+    Every verdict is MIN-reduced over the world, so all ranks route identically; anything
+    that fails falls back to RCCL and the losing communicators are closed (their IPC areas
+    freed).  Reference transport: NCCL/HCCL only (tp_comms.py:117-166, :288-315;
+    sp_comms.py:31-94)."""
     import torch.distributed as dist
 
+    ws = _ws(group)
     if requested in ("rccl", "xgmi"):
         set_tp_comm(requested)
-        if requested == "xgmi" and _ws(group) == 2:
+        if requested == "xgmi" and ws == 2:
             setup_tp_pair_path(group)
-        TRANSPORT["tp"] = requested
         return requested
     if requested != "auto":
         raise ValueError(f"tp_comm must be auto, rccl or xgmi, got {requested!r}")
-    ok, info = 0, {}
-    if _ws(group) == 2 and torch.cuda.is_available():
+    names = list(_TP_XGMI_OPS)
+    flags, info = [0] * len(names), {}
+    if ws >= 2 and torch.cuda.is_available():
         try:
-            setup_tp_pair_path(group)
-            pair = _PAIR[0]
-            if pair is not None:
-                ok, info = _pair_selftest(pair, group, probe_mb)
+            if ws == 2:
+                setup_tp_pair_path(group)
+                pair = _PAIR[0]
+                if pair is not None:
+                    ok, info = _pair_selftest(pair, group, probe_mb)
+                    # the pair path carries the SP gathers / scatters; all-reduces stay on the
+                    # 2-rank communicator's kernels only when the pair path is on
+                    flags = [ok] * len(names)
+            else:
+                from ..dist.xgmi import XgmiAllReduce
+
+                comm = _XGMI[id(group)] = XgmiAllReduce(group, max_bytes=_tp_area_bytes(msg_bytes))
+                per_op, info = _tp_selftest(comm, group, msg_bytes or (probe_mb << 20))
+                flags = [per_op.get(n, 0) for n in names]
         except Exception as e:  # noqa: BLE001 -- fall back, but every rank still joins the vote
-            ok, info = 0, {"error": repr(e)[:200]}
-    flag = torch.tensor([ok], dtype=torch.int32, device="cuda" if torch.cuda.is_available() else "cpu")
+            flags, info = [0] * len(names), {"error": repr(e)[:200]}
+    flag = torch.tensor(flags, dtype=torch.int32, device="cuda" if torch.cuda.is_available() else "cpu")
     if dist.is_initialized():
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-    choice = "xgmi" if int(flag.item()) == 1 else "rccl"
-    set_tp_comm(choice)
+    voted = {n: bool(int(v)) for n, v in zip(names, flag.tolist())}
+    choice = "xgmi" if any(voted.values()) else "rccl"
     if choice == "rccl":
-        _PAIR[0] = None
-    TRANSPORT.update(tp=choice, selftest=info)
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if dist.is_initialized():
+            dist.barrier()  # no peer still reads an area we are about to free
+        _close_tp_xgmi()
+    set_tp_comm(choice, voted)
+    TRANSPORT.update(selftest=info)
     return choice
+
+
+def _tp_selftest(comm, group, msg_bytes: int):
+    """Per-collective verdicts ({op: 1 if correct and faster than RCCL else 0}, timings) of a
+    TP-group communicator at ``msg_bytes`` (capped by its area)."""
+    ws, r = _ws(group), C.get_rank(group)
+    n = max(8 * ws, min(int(msg_bytes), comm.cap) // 2 // (8 * ws) * (8 * ws))  # bf16 elements
+    g = torch.Generator(device="cuda").manual_seed(4321 + r)
+    x = torch.randn(n, device="cuda", dtype=torch.bfloat16, generator=g)
+    part = x[: n // ws].contiguous()
+
+    def timed(fn, iters=5):
+        out = fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        e.synchronize()
+        return out, s.elapsed_time(e) / iters
+
+    everyone = C.all_gather(x, group=group).view(ws, n).float()   # fp32 reference sum
+    ref = everyone.sum(0)
+    ar_x, t_ar_x = timed(lambda: comm.all_reduce(x, out=torch.empty_like(x)))
+    _, t_ar_r = timed(lambda: C.all_reduce(x.clone(), group=group))
+    ag_x, t_ag_x = timed(lambda: comm.all_gather(part))
+    ag_r, t_ag_r = timed(lambda: C.all_gather(part, group=group))
+    rs_x, t_rs_x = timed(lambda: comm.reduce_scatter(x))
+    rs_r, t_rs_r = timed(lambda: C.reduce_scatter(x, group=group))
+    comm.check()
+    tol = ref.abs() * 2.0 ** -8 + 1e-6  # one bf16 rounding of the exact (fp32) sum
+    ar_ok = bool(((ar_x.float() - ref).abs() <= tol).all())
+    chunk = n // ws
+    rs_ok = bool(((rs_x.float() - ref[r * chunk:(r + 1) * chunk]).abs() <= tol[r * chunk:(r + 1) * chunk]).all())
+    ag_ok = bool(torch.equal(ag_x, ag_r))
+    # ranks sharing ONE GPU (ST_GPU_OVERSUBSCRIBE=1: rehearsals / tests) time-slice it, so
+    # neither timing means anything there: the verdict is correctness alone
+    import os
+
+    shared = os.environ.get("ST_GPU_OVERSUBSCRIBE", "0") == "1"
+    per_op = {"all_reduce": int(ar_ok and (shared or t_ar_x < t_ar_r)),
+              "all_gather": int(ag_ok and (shared or t_ag_x < t_ag_r)),
+              "reduce_scatter": int(rs_ok and (shared or t_rs_x < t_rs_r))}
+    info = {"msg_mb": round(2 * n / (1 << 20), 2), "world": ws,
+            "ar_ms": [round(t_ar_x, 3), round(t_ar_r, 3)], "ag_ms": [round(t_ag_x, 3), round(t_ag_r, 3)],
+            "rs_ms": [round(t_rs_x, 3), round(t_rs_r, 3)],
+            "correct": {"all_reduce": ar_ok, "all_gather": ag_ok, "reduce_scatter": rs_ok}, "local": per_op,
+            "timing": "ignored (ranks share one GPU)" if shared else "xgmi kept only where faster"}
+    return per_op, info
 
 
 def _pair_selftest(pair, group, probe_mb: int):
@@ -158,27 +259,26 @@ def _tp_all_reduce(x: torch.Tensor, group, async_op: bool = False):
     """Sum over the TP group; returns a handle with ``wait()`` when ``async_op``."""
     from ..dist import trace
 
-    trace.record("tp.all_reduce", x, group_size=_ws(group), transport=_TP_COMM, overlapped=async_op)
-    if _TP_COMM == "xgmi" and x.is_cuda and group is not None:
-        from ..dist.xgmi import XgmiAllReduce
-
-        key = id(group)
-        comm = _XGMI.get(key)
-        if comm is None:
-            comm = _XGMI[key] = XgmiAllReduce(group)
-        if comm.supports(x):
-            # every xGMI collective of the process runs on ONE stream (``_on_comm_stream``)
-            work = _on_comm_stream(lambda t: comm.all_reduce(t), x)[1]
-            if not async_op:
-                work.wait()
-                return None
-            return work
+    comm = _xgmi_comm(group, "all_reduce") if x.is_cuda else None
+    trace.record("tp.all_reduce", x, group_size=_ws(group), transport="xgmi" if comm is not None else "rccl",
+                 overlapped=async_op)
+    if comm is not None and comm.supports(x):
+        # every xGMI collective of the process runs on ONE stream (``_on_comm_stream``); an
+        # async one (the column-parallel dX all-reduce) runs there under the dW GEMM
+        work = _on_comm_stream(lambda t: comm.all_reduce(t), x)[1]
+        if not async_op:
+            work.wait()
+            return None
+        return work
     return C.all_reduce(x, group=group, async_op=async_op)
 
 
-def _xgmi_comm(group):
-    """The xGMI communicator of ``group`` when --tp_comm xgmi is active (else None)."""
+def _xgmi_comm(group, op: str | None = None):
+    """The xGMI communicator of ``group`` when the xGMI TP transport is active and (``op``
+    given) that collective kept the xGMI path at start-up; else None (RCCL)."""
     if _TP_COMM != "xgmi" or group is None or _ws(group) == 1:
+        return None
+    if op is not None and not _TP_XGMI_OPS.get(op, False):
         return None
     from ..dist.xgmi import XgmiAllReduce
 
@@ -278,7 +378,7 @@ def _gather_seq(x: torch.Tensor, group) -> torch.Tensor:
     if ws == 1:
         return x
     _trace("sp.all_gather", x, ws)
-    xg = _xgmi_comm(group) if x.is_cuda else None
+    xg = _xgmi_comm(group, "all_gather") if x.is_cuda else None
     pair = _PAIR[0] if (xg is not None and ws == 2) else None
     if pair is not None and pair.fits(x.numel(), x):
         xg = pair  # multipath: direct link + 2-hop relays
@@ -295,7 +395,7 @@ def _reduce_scatter_seq(x: torch.Tensor, group) -> torch.Tensor:
     if ws == 1:
         return x
     _trace("sp.reduce_scatter", x, ws)
-    xg = _xgmi_comm(group) if x.is_cuda else None
+    xg = _xgmi_comm(group, "reduce_scatter") if x.is_cuda else None
     pair = _PAIR[0] if (xg is not None and ws == 2) else None
     if pair is not None and pair.fits(x.numel() // 2, x):
         xg = pair  # multipath: direct link + 2-hop relays
@@ -535,6 +635,9 @@ def _sp_gather_async(part: torch.Tensor, group):
     if pair is not None:
         return _on_comm_stream(pair.all_gather, part)
     _trace("sp.all_gather", part, ws)
+    xg = _xgmi_comm(group, "all_gather") if (part.is_cuda and ws > 2) else None
+    if xg is not None and xg.supports(part):  # tp 4 / 8: all 7 links, on the comm side stream
+        return _on_comm_stream(xg.all_gather, part.contiguous())
     return C.all_gather(part, group=group, async_op=True)
 
 
@@ -546,12 +649,15 @@ def _sp_reduce_scatter_async(buf: torch.Tensor, group):
     if pair is not None:
         return _on_comm_stream(pair.reduce_scatter, buf)
     _trace("sp.reduce_scatter", buf, ws)
+    xg = _xgmi_comm(group, "reduce_scatter") if (buf.is_cuda and ws > 2) else None
+    if xg is not None and buf.is_contiguous() and xg.supports(buf) and buf.shape[0] % ws == 0:
+        return _on_comm_stream(xg.reduce_scatter, buf)
     return C.reduce_scatter(buf, group=group, async_op=True)
 
 
 def _pair_for(group, n_elems: int, t: torch.Tensor):
     """The 2-rank xGMI multipath transport for this SP message, or None (RCCL)."""
-    if not t.is_cuda or _ws(group) != 2 or _xgmi_comm(group) is None:
+    if not t.is_cuda or _ws(group) != 2 or _xgmi_comm(group, "all_gather") is None:
         return None
     pair = _PAIR[0]
     if pair is None or not pair.fits(n_elems, t):

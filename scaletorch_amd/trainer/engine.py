@@ -59,16 +59,28 @@ class Trainer:
         if a.tensor_parallel_size > 1:
             from ..parallel.tensor_parallel import select_tp_transport, set_tp_comm
 
-            if torch.cuda.is_available() and not a.use_cpu and (a.backend == "nccl" or a.tp_comm == "xgmi"):
+            if torch.cuda.is_available() and not a.use_cpu and (a.backend == "nccl" or a.tp_comm == "xgmi"
+                                                                 or os.environ.get("ST_GPU_OVERSUBSCRIBE") == "1"):
                 # collective over the world, before any model code: "auto" self-tests the
                 # 7-link pair path for tp = 2 against RCCL and keeps the faster correct one
-                select_tp_transport(mesh.tp_group(), a.tp_comm)
+                msg = None
+                if a.micro_batch_size and a.sequence_length:
+                    # the row-parallel all-reduce / SP reduce-scatter input: [mbs, S/cp, h] bf16
+                    h = get_model_config(a.model_name_or_path).hidden_size
+                    msg = a.micro_batch_size * (a.sequence_length // max(1, a.context_parallel_size)) * h * 2
+                select_tp_transport(mesh.tp_group(), a.tp_comm, msg_bytes=msg)
             else:
                 set_tp_comm("rccl" if a.tp_comm == "auto" else a.tp_comm)
         from ..models.attention_backends import set_use_flash_attention
         from ..models.moe import set_moe_dispatch
 
         set_moe_dispatch(a.moe_capacity_factor, a.moe_ep_chunks, "rccl" if a.ep_comm == "auto" else a.ep_comm)
+        if a.expert_parallel_size > 1 and a.sequence_length and a.micro_batch_size:
+            from ..models.moe import set_ep_token_bound
+
+            # every micro-batch holds exactly this many tokens per rank (loaders drop ragged
+            # tails), so the EP exchange buffers need no per-call agreement
+            set_ep_token_bound(a.micro_batch_size * a.sequence_length // max(1, a.context_parallel_size))
         if a.expert_parallel_size > 1 and torch.cuda.is_available() and not a.use_cpu and a.ep_comm != "rccl" \
                 and (a.backend == "nccl" or os.environ.get("ST_GPU_OVERSUBSCRIBE", "0") == "1"):
             from ..models.moe import select_ep_transport

@@ -76,9 +76,11 @@ def is_complete(step_dir: str) -> bool:
 
     A directory with neither kind of marker predates them (legacy layout).  It
     counts as complete only with ``ST_CKPT_ACCEPT_UNMARKED=1`` (the default) AND
-    when no sibling step directory carries markers: next to marked directories an
-    unmarked one can only be a crash of the current code before its first
-    marker, so the newest marked complete directory wins."""
+    when no OLDER sibling step directory carries markers: once the current code has
+    saved (marked) step N, an unmarked step M > N can only be its crash before the
+    first marker.  Unmarked directories older than every marked one are legacy
+    saves and stay valid, so a crash during the first marked save after resuming
+    from a legacy step falls back to that step, not to step 0."""
     marks = glob.glob(os.path.join(step_dir, "complete_rank_world_size=*"))
     if not marks:
         if glob.glob(os.path.join(step_dir, "started_rank_world_size=*")):
@@ -87,10 +89,12 @@ def is_complete(step_dir: str) -> bool:
             logger.warning("skipping checkpoint %s: no completion markers", step_dir)
             return False
         parent = os.path.dirname(os.path.abspath(step_dir))
+        me = os.path.basename(os.path.abspath(step_dir))
         for sib in glob.glob(os.path.join(parent, "*")):
-            if os.path.basename(sib).isdigit() and os.path.abspath(sib) != os.path.abspath(step_dir) \
-                    and _has_markers(sib):
-                logger.warning("skipping unmarked checkpoint %s: sibling %s has completion markers", step_dir, sib)
+            b = os.path.basename(sib)
+            if b.isdigit() and me.isdigit() and int(b) < int(me) and _has_markers(sib):
+                logger.warning("skipping unmarked checkpoint %s: older sibling %s has save markers "
+                               "(a crash before this save's first marker)", step_dir, sib)
                 return False
         logger.warning("checkpoint %s has no completion markers (legacy layout); treating it as complete "
                        "(ST_CKPT_ACCEPT_UNMARKED=0 skips such directories)", step_dir)

@@ -53,7 +53,8 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
                          sequence_parallel: bool = False, gradient_checkpointing: bool = False,
                          pp_engine: str = "1f1b", grad_reduce_dtype: str = "bf16",
                          fused_head_chunk: int = 0, recompute_swiglu: bool | None = None,
-                         moe_dropless: bool = False, optimizer_state_dtype: str = "fp32") -> MemoryEstimate:
+                         moe_dropless: bool = False, optimizer_state_dtype: str = "fp32",
+                         xgmi_ipc_bytes: float = 0.0, cp_ds_budget_bytes: float | None = None) -> MemoryEstimate:
     """Worst-rank estimate (first pipeline stage for activations, largest stage for weights).
 
     ``fused_head_chunk`` > 0: the fused chunked LM head (ops/fused_head.py) -- one
@@ -121,6 +122,17 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
     else:
         logits = head_tokens * cfg.vocab_size / tp * 2 * 2  # bf16 logits + grad (last stage)
     comm = n * 2 if grad_reduce_dtype in ("bf16", "bfloat16") and dense_dp > 1 else 0.0
+    comm += xgmi_ipc_bytes
+    if cp > 1:
+        # transient dS workspace of the CP backward: one layer at a time, causal lower triangle
+        # of a zig-zag chunk pair (B * Hq * chunk * prefix, bf16) capped by the budget
+        if cp_ds_budget_bytes is None:
+            from ..parallel.context_parallel import _ds_budget_bytes
+
+            cp_ds_budget_bytes = _ds_budget_bytes()
+        s_loc = seq_len / cp
+        widest = micro_batch * (H / tp) * (s_loc / 2) * seq_len * 2  # last zig-zag chunk x its full prefix
+        act += min(cp_ds_budget_bytes, widest) + widest
     # bf16 W^T copies of the dense projection weights (TN data-gradient GEMMs, ops/grad.py)
     wt = 2 * (dense - 2 * h * layers - (h * cfg.num_experts if cfg.is_moe else 0) * layers)
     g = 1e9

@@ -51,20 +51,32 @@ def test_debug_collectives_on_a_zero1_training_step():
 
 
 def test_step_watchdog_fires_and_kicks():
+    """Load-tolerant: the deadline is 20x the kick period (a descheduled test process under
+    ``pytest -n 8`` must not read as a hang), and the firing is awaited with a bounded poll
+    instead of one fixed sleep."""
     import time
 
     from scaletorch_amd.utils.watchdog import StepWatchdog
 
     fired = []
-    wd = StepWatchdog(0.3, on_timeout=lambda info: fired.append(info), poll_s=0.05)
+    wd = StepWatchdog(2.0, on_timeout=lambda info: fired.append(info), poll_s=0.05)
     wd.start()
-    for _ in range(4):
-        time.sleep(0.1)
+    try:
+        t0 = time.monotonic()
+        for _ in range(4):
+            time.sleep(0.1)
+            wd.kick(step=1)
+        kicked_for = time.monotonic() - t0
+        if kicked_for < 1.5:  # the kicks were on time, so nothing may have fired
+            assert not fired
+        fired.clear()
         wd.kick(step=1)
-    assert not fired
-    time.sleep(0.6)
-    assert fired and "step 1" in fired[0]
-    wd.stop()
+        deadline = time.monotonic() + 20.0
+        while not fired and time.monotonic() < deadline:
+            time.sleep(0.05)
+        assert fired and "step 1" in fired[0]
+    finally:
+        wd.stop()
 
 
 def test_roctx_ranges_are_noops_without_profiling():

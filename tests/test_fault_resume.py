@@ -101,6 +101,35 @@ def test_zero_marker_crash_falls_back_to_marked_checkpoint(tmp_path):
     assert latest_checkpoint(str(tmp_path)).endswith("/2")
 
 
+def test_crash_in_first_marked_save_after_legacy_resume(tmp_path):
+    """Legacy (unmarked) steps 1000 and 2000, then the current code crashes during its
+    first save (step 2100: save-started sentinel, no completion marker): auto-resume
+    falls back to legacy step 2000 -- an OLDER marked sibling is what disqualifies an
+    unmarked directory, a newer partial one is not."""
+    from scaletorch_amd.utils.checkpoint import is_complete, latest_checkpoint
+
+    w = "weights_tp_rank_world_size=0_1_pp_rank_world_size=0_1.pth"
+    for step in (1000, 2000, 2100):
+        d = tmp_path / str(step)
+        d.mkdir()
+        (d / w).write_bytes(b"x")
+    (tmp_path / "2100" / "started_rank_world_size=0_2").write_text("started\n")
+    assert not is_complete(str(tmp_path / "2100"))
+    assert is_complete(str(tmp_path / "2000"))
+    assert latest_checkpoint(str(tmp_path)).endswith("/2000")
+    # the current code then completes 2200 and crashes in 2300 before any marker: 2300 is
+    # unmarked with an older marked sibling -> skipped; 2200 wins
+    for step in (2200, 2300):
+        d = tmp_path / str(step)
+        d.mkdir()
+        (d / w).write_bytes(b"x")
+    for r in (0, 1):
+        (tmp_path / "2200" / f"started_rank_world_size={r}_2").write_text("started\n")
+        (tmp_path / "2200" / f"complete_rank_world_size={r}_2").write_text("ok\n")
+    assert not is_complete(str(tmp_path / "2300"))
+    assert latest_checkpoint(str(tmp_path)).endswith("/2200")
+
+
 def _resume_corrupt_worker(rank, world, work_dir):
     import torch
 

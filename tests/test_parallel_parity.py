@@ -517,6 +517,51 @@ def _dropless_uneven_worker(rank, world):
             int(layer.dropped_rows))
 
 
+def _dropless_ragged_steps_worker(rank, world):
+    import torch.distributed as dist
+
+    from scaletorch_amd.models.config import get_model_config
+    from scaletorch_amd.models.moe import MoELayer
+    from scaletorch_amd.parallel import mesh
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = get_model_config("tiny-moe")
+    torch.manual_seed(0)
+    ref_layer = MoELayer(cfg).float()
+    mesh.setup_process_group_manager(ep_size=world)
+    layer = MoELayer(cfg).float()
+    with torch.no_grad():
+        layer.router.gate.weight.copy_(ref_layer.router.gate.weight)
+        El = layer.num_local
+        layer.experts.w_gate_up.copy_(ref_layer.experts.w_gate_up[rank * El:(rank + 1) * El])
+        layer.experts.w_down.copy_(ref_layer.experts.w_down[rank * El:(rank + 1) * El])
+    # one rank's token count repeats while its peer's changes (and the reverse): a bound
+    # cached on the local count would desynchronise the EP collectives here
+    counts = [[5, 5, 9, 9], [12, 20, 20, 6]][rank]
+    out = []
+    for step, T in enumerate(counts):
+        g = torch.Generator().manual_seed(1000 * step + rank)
+        x = torch.randn(1, T, cfg.hidden_size, generator=g)
+        xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+        ya, yb = layer(xa), ref_layer(xb)
+        ya.square().sum().backward()
+        yb.square().sum().backward()
+        out.append((ya.detach(), yb.detach(), xa.grad, xb.grad))
+    return out
+
+
+def test_moe_dropless_ragged_counts_across_steps():
+    """Several dropless EP forwards/backwards where each rank's token count changes between
+    calls independently of its peer's: every call agrees on the buffer bound, so the EP
+    collectives stay in step and each call matches the all-experts-local computation."""
+    res = run_workers(_dropless_ragged_steps_worker, 2)
+    for steps in res:
+        assert len(steps) == 4
+        for ya, yb, ga, gb in steps:
+            torch.testing.assert_close(ya, yb, atol=1e-5, rtol=1e-4)
+            torch.testing.assert_close(ga, gb, atol=1e-5, rtol=1e-4)
+
+
 def test_moe_dropless_uneven_token_counts():
     """Dropless EP dispatch with device counts when EP ranks hold DIFFERENT token counts
     (ragged batches): outputs, input gradients and expert weight gradients equal the

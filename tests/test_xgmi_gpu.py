@@ -392,3 +392,73 @@ def test_sp_decoder_layers_pair_path_matches_gloo_same_gpu():
             assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (l_ref, l_got)
         for k in sd_ref:
             assert rel(sd_got[k], sd_ref[k]) < 2e-2, k
+
+
+def _tp_train_worker(rank, world, tp_comm, sp, seed):
+    """Two SGD steps of a 2-layer Qwen3 (8 query / 8 KV heads) at TP = ``world`` on THIS
+    GPU over gloo, optionally with sequence parallelism.  tp_comm "auto": the start-up
+    self-test (tensor_parallel.select_tp_transport, tp > 2 branch) times the xGMI
+    all-reduce / all-gather / reduce-scatter against the process group at the run's real
+    message size and keeps each that is correct and faster; the decoder layers' row
+    all-reduces, column dX all-reduces (async, under the dW GEMM) and SP gathers /
+    scatters then run over the IPC communicator."""
+    # 4 MiB IPC areas: every process shares ONE GPU here (large areas hung in
+    # hipIpcOpenMemHandle on a shared device); the real messages are 1 MiB
+    os.environ.update(ST_GPU_OVERSUBSCRIBE="1", ST_XGMI_TIMEOUT_S="30", ST_XGMI_TP_MAX_MB="4")
+    import faulthandler
+    import sys
+
+    faulthandler.dump_traceback_later(150, exit=False)
+    from scaletorch_amd.parallel import tensor_parallel as TP
+    from scaletorch_amd.trainer.config import ScaleTorchArguments
+    from scaletorch_amd.trainer.engine import Trainer
+
+    a = ScaleTorchArguments(model_name_or_path="tiny-qwen3-8h", synthetic_data=True, sequence_length=512,
+                            backend="gloo", dtype="bfloat16", tensor_parallel_size=world, sequence_parallel=sp,
+                            micro_batch_size=4, tp_comm=tp_comm, optimizer_type="sgd", learning_rate=0.5,
+                            lr_scheduler_type="constant", max_grad_norm=None, total_train_steps=2, seed=seed)
+    tr = Trainer(a, build_data=False)
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randint(0, tr.model_config.vocab_size, (4, 513), generator=g)
+    pos = torch.arange(512).unsqueeze(0).expand(4, -1).contiguous()
+    batch = {"input_ids": ids[:, :-1].contiguous(), "target_ids": ids[:, 1:].contiguous(), "position_ids": pos,
+             "hidden_states": None}
+    tr.data = iter([batch] * 4)
+    losses = []
+    for i in range(2):
+        losses.append(tr.reduced_loss(tr.train_step()))
+        print(f"[tp worker {rank}/{world} {tp_comm} sp={sp}] step {i} loss {losses[-1]:.4f} "
+              f"transport {TP.TRANSPORT}", file=sys.stderr, flush=True)
+    torch.cuda.synchronize()
+    tr.health_check()
+    faulthandler.cancel_dump_traceback_later()
+    sd = {k: v.detach().float().cpu() for k, v in tr.raw_model.reference_state_dict().items()
+          if "decoder_layers.1" in k}
+    return losses, sd, dict(TP.TRANSPORT)
+
+
+@pytest.mark.parametrize("world,sp", [(4, False), (4, True), (8, True)])
+def test_tp_decoder_layers_xgmi_auto_matches_gloo_same_gpu(world, sp):
+    """at tp = 4 / 8 the "auto" transport self-tests the TP-group xGMI
+    communicator and, having won, carries the decoder layers' TP collectives (real IPC between
+    ``world`` processes on one GPU); two training steps equal the gloo run within bf16
+    tolerance (losses and the second layer's updated weights)."""
+    from tests.dist_harness import run_workers
+
+    try:
+        ref = run_workers(_tp_train_worker, world, "rccl", sp, 5, timeout=200)
+        got = run_workers(_tp_train_worker, world, "auto", sp, 5, timeout=200)
+    except RuntimeError as e:
+        if "IPC" in str(e) or "hipIpc" in str(e):
+            pytest.skip(f"IPC on a shared GPU unsupported here: {e}")
+        raise
+    for (l_ref, sd_ref, tr_ref), (l_got, sd_got, tr_got) in zip(ref, got):
+        assert tr_ref["tp"] == "rccl"
+        assert tr_got["tp"] == "xgmi", tr_got
+        want_ops = {"all_reduce", "all_gather", "reduce_scatter"}
+        assert set(tr_got["ops"]) == want_ops, tr_got
+        assert all(tr_got["selftest"]["correct"].values()), tr_got
+        for a, b in zip(l_ref, l_got):
+            assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (l_ref, l_got)
+        for k in sd_ref:
+            assert rel(sd_got[k], sd_ref[k]) < 2e-2, k

@@ -18,7 +18,7 @@ import torch  # noqa: E402
 
 from scaletorch_amd.ops import _lib  # noqa: E402
 
-T = 24576
+T = int(os.environ.get("WG_T", "24576"))
 SHAPES = [("qkv", 6144, 4096), ("out", 4096, 4096), ("gate_up", 28672, 4096), ("down", 4096, 14336)]
 
 
@@ -58,6 +58,14 @@ def main() -> int:
             arms["hipblaslt_one_T"] = lambda: torch.ops.aten.addmm.dtype_out(out, dyt, x, torch.float32, beta=0,
                                                                              alpha=1, out=out)
             tr = lambda: _lib.ops().transpose_(dy, dyt)  # noqa: E731
+        # both operands token-contiguous (what producer-written transposed copies would give)
+        dyt2 = dy.t().contiguous()
+        xt2 = x.t().contiguous()
+        arms["hipblaslt_TN"] = lambda: torch.ops.aten.addmm.dtype_out(out, dyt2, xt2.t(), torch.float32, beta=1,
+                                                                    alpha=1, out=out)
+        arms["tuned_TN"] = lambda: _lib.ops().gemm_(out, dyt2, xt2, False, True, 1.0, 1.0)
+        arms["tuned_TN_beta0"] = lambda: _lib.ops().gemm_(out, dyt2, xt2, False, True, 1.0, 0.0)
+        arms["ours_8phase"] = lambda: _lib.ops().wgrad_gemm_(out, dy, x, 1, 2)
         r = {}
         for arm, fn in arms.items():
             ms = min(timeit(fn) for _ in range(3))
