@@ -64,7 +64,7 @@ class ParallelArguments:
     backend: str = field(default="nccl", metadata={"help": "nccl (=RCCL) | gloo | hccl (maps to nccl)"})
     sequence_parallel: bool = field(default=False, metadata={"help": "Megatron-SP over the TP group"})
     cp_zigzag: bool = field(default=True, metadata={"help": "zig-zag load-balanced CP chunks"})
-    tp_comm: str = field(default="auto", metadata={"help": "TP transport: auto (tp = 2 on one node: self-test the 7-link xGMI pair path against RCCL at start-up and keep the faster correct one; else RCCL) | rccl | xgmi (custom one-/two-shot all-reduce + pair all-gather / reduce-scatter over IPC peer memory, dist/xgmi.py)"})
+    tp_comm: str = field(default="auto", metadata={"help": "TP transport: auto (one node: tp = 2 self-tests the 7-link xGMI pair path, tp 4 / 8 the TP-group communicator's all-reduce / all-gather / reduce-scatter at the run's real message size, each against RCCL at start-up, keeping every collective that is correct and faster) | rccl | xgmi (custom one-/two-shot all-reduce + all-gather / reduce-scatter over IPC peer memory, dist/xgmi.py)"})
     cp_comm: str = field(default="auto", metadata={"help": "CP transport: auto (= allgather: RCCL drives all 7 xGMI links) | allgather (overlapped K/V all-gather) | ring (p2p rotation overlapped with block compute) | ulysses (head all-to-all)"})
     layer_distribution: str | None = field(default=None, metadata={"help": "comma list of layers per PP stage"})
     moe_capacity_factor: float = field(default=0.0, metadata={

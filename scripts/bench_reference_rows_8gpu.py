@@ -169,7 +169,9 @@ def main() -> int:
             t0 = time.time()
             env = dict(os.environ, MASTER_ADDR="127.0.0.1")
             if a.rehearse:
-                env.update(ST_GPU_OVERSUBSCRIBE="1", OMP_NUM_THREADS="2")
+                # 8 processes time-slice ONE GPU: an xGMI collective waits for peers that are
+                # descheduled, so the 2 s production wait bound is raised
+                env.update(ST_GPU_OVERSUBSCRIBE="1", OMP_NUM_THREADS="2", ST_XGMI_TIMEOUT_S="60")
             try:
                 p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=a.timeout)
                 rc, text = p.returncode, p.stdout + p.stderr
@@ -188,6 +190,8 @@ def main() -> int:
             if rc != 0:
                 rec["tail"] = text[-2000:]
                 failures += 1
+                with open(os.path.splitext(os.path.abspath(a.out))[0] + f"_{r['name']}.log", "w") as lf:
+                    lf.write(text)  # the whole output: the failing rank's error is rarely in the tail
             f.write(json.dumps(rec) + "\n")
             f.flush()
             print(f"{r['name']}: rc={rc} ours={rec['ours_tok_s_per_gpu']} ref={r['reference_tok_s_per_gpu']}",
