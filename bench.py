@@ -79,8 +79,15 @@ def _planned_ipc(args, mcfg) -> int:
         return 0
     from scaletorch_amd.dist.xgmi import planned_ipc_bytes
 
-    msg = args.micro_batch_size * (args.seq_len // max(1, args.cp)) * mcfg.hidden_size * 2
-    return planned_ipc_bytes(args.tp, args.ep, msg, moe_dropless=args.moe_capacity_factor == 0 and args.ep > 1)
+    tokens = args.micro_batch_size * (args.seq_len // max(1, args.cp))
+    area = None
+    if args.ep > 1 and mcfg.is_moe:
+        from scaletorch_amd.models.moe import ep_area_bytes
+
+        area = ep_area_bytes(tokens, args.ep, mcfg.num_experts_per_tok, mcfg.num_experts, mcfg.hidden_size,
+                             args.moe_capacity_factor)
+    return planned_ipc_bytes(args.tp, args.ep, tokens * mcfg.hidden_size * 2,
+                             moe_dropless=args.moe_capacity_factor == 0 and args.ep > 1, ep_area=area)
 
 
 def _visible_gpus() -> int:

@@ -35,6 +35,10 @@ def record(op: str, tensor: torch.Tensor | None = None, peer=None, group_size: i
     s = _STATS[op]
     s[0] += 1
     s[1] += nbytes
+    if extra.get("transport") == "xgmi":  # which transport really carried it (per call)
+        x = _STATS[op + "@xgmi"]
+        x[0] += 1
+        x[1] += nbytes
     if _VERBOSE[0]:
         rank = os.environ.get("RANK", "0")
         shape = tuple(tensor.shape) if tensor is not None else ()

@@ -305,7 +305,7 @@ def area_bytes(max_bytes: int) -> int:
 
 
 def planned_ipc_bytes(tp: int = 1, ep: int = 1, tp_msg_bytes: int | None = None,
-                      moe_dropless: bool = False) -> int:
+                      moe_dropless: bool = False, ep_area: int | None = None) -> int:
     """Upper bound of the IPC areas a rank holds when the start-up self-tests keep xGMI
     (losers are closed): tp = 2 -> the node communicator of the pair path + the 2-rank one;
     tp > 2 -> one TP-group communicator sized by the message; EP dropless -> the push area."""
@@ -316,8 +316,11 @@ def planned_ipc_bytes(tp: int = 1, ep: int = 1, tp_msg_bytes: int | None = None,
         total += area_bytes(_max_bytes_default()) + area_bytes(64 << 20)
     elif tp > 2:
         total += area_bytes(_tp_area_bytes(tp_msg_bytes))
-    if ep > 1 and moe_dropless:
-        total += area_bytes(_max_bytes_default("ep"))
+    if ep > 1:
+        import os
+
+        use = ep_area if (ep_area and not os.environ.get("ST_XGMI_EP_MAX_MB")) else _max_bytes_default("ep")
+        total += area_bytes(use)
     return total
 
 

@@ -74,14 +74,30 @@ def set_moe_dispatch(capacity_factor: float = 0.0, chunks: int = 1, comm: str = 
     _DISPATCH.update(capacity_factor=float(capacity_factor), chunks=max(1, int(chunks)), comm=comm)
 
 
-def setup_ep_xgmi(group) -> None:
+def ep_area_bytes(tokens: int, ep: int, top_k: int, num_experts: int, hidden: int,
+                  capacity_factor: float = 0.0) -> int:
+    """IPC data area the EP exchange of a run needs: the dropless landing rows at the host
+    bound R_max = ep * T * min(k, E/ep) (or the capacity dispatch's cf * T * k rows) of
+    ``hidden`` bf16, rounded up to 8 MiB, at least 16 MiB (Mixtral EP 8 at 4,096 tokens:
+    268 MiB)."""
+    El = max(1, num_experts // max(1, ep))
+    rows = ep * tokens * min(top_k, El)
+    if capacity_factor > 0:
+        rows = max(rows, int(math.ceil(capacity_factor * tokens * top_k)))
+    need = rows * hidden * 2
+    return max(16 << 20, -(-need // (8 << 20)) * (8 << 20))
+
+
+def setup_ep_xgmi(group, area_bytes: int | None = None) -> None:
     """Create the EP group's xGMI communicator (collective over the group, at start-up):
     the capacity dispatch's equal-split all-to-alls then PUSH rows straight into the
-    peers' buffers over all 7 links (csrc/xgmi_allreduce.hip mode 4)."""
+    peers' buffers over all 7 links (csrc/xgmi_allreduce.hip mode 4).  ``area_bytes``: the
+    run's need (``ep_area_bytes``); ST_XGMI_EP_MAX_MB overrides, 512 MiB without either."""
     from ..dist.xgmi import XgmiAllReduce, _max_bytes_default
 
     if group is not None and C.get_world_size(group) > 1:
-        _EP_XGMI[id(group)] = XgmiAllReduce(group, max_bytes=_max_bytes_default("ep"))
+        size = area_bytes if (area_bytes and not os.environ.get("ST_XGMI_EP_MAX_MB")) else _max_bytes_default("ep")
+        _EP_XGMI[id(group)] = XgmiAllReduce(group, max_bytes=size)
 
 
 def _ep_a2a(x: torch.Tensor, group, async_op: bool):
@@ -383,7 +399,7 @@ def ep_comm_for(group):
     return _EP_XGMI.get(id(group)) if _DISPATCH["comm"] == "xgmi" else None
 
 
-def select_ep_transport(group, requested: str = "auto") -> str:
+def select_ep_transport(group, requested: str = "auto", area_bytes: int | None = None) -> str:
     """Collective over the EP group at start-up.  "auto": set up the xGMI communicator
     (one node, one GPU per rank) and self-test the push exchange against the RCCL
     exchange on random routing (bitwise equal both ways); the MIN-reduced verdict picks
@@ -394,7 +410,7 @@ def select_ep_transport(group, requested: str = "auto") -> str:
     ok = 0
     info: dict = {}
     try:
-        setup_ep_xgmi(group)
+        setup_ep_xgmi(group, area_bytes)
         comm = _EP_XGMI.get(id(group))
         if comm is not None:
             ok, info = _ep_selftest(comm, group)

@@ -260,9 +260,11 @@ def _tp_all_reduce(x: torch.Tensor, group, async_op: bool = False):
     from ..dist import trace
 
     comm = _xgmi_comm(group, "all_reduce") if x.is_cuda else None
+    if comm is not None and not comm.supports(x):
+        comm = None  # too large for the IPC area / unaligned: RCCL
     trace.record("tp.all_reduce", x, group_size=_ws(group), transport="xgmi" if comm is not None else "rccl",
                  overlapped=async_op)
-    if comm is not None and comm.supports(x):
+    if comm is not None:
         # every xGMI collective of the process runs on ONE stream (``_on_comm_stream``); an
         # async one (the column-parallel dX all-reduce) runs there under the dW GEMM
         work = _on_comm_stream(lambda t: comm.all_reduce(t), x)[1]
@@ -366,10 +368,10 @@ class ScatterToTensorParallelRegion(torch.autograd.Function):
         return torch.cat(C.all_gather(g.contiguous(), group=ctx.group, as_list=True), dim=-1), None
 
 
-def _trace(op: str, x: torch.Tensor, ws: int) -> None:
+def _trace(op: str, x: torch.Tensor, ws: int, transport: str | None = None) -> None:
     from ..dist import trace
 
-    trace.record(op, x, group_size=ws)
+    trace.record(op, x, group_size=ws, transport=transport)
 
 
 def _gather_seq(x: torch.Tensor, group) -> torch.Tensor:
@@ -377,11 +379,11 @@ def _gather_seq(x: torch.Tensor, group) -> torch.Tensor:
     ws = _ws(group)
     if ws == 1:
         return x
-    _trace("sp.all_gather", x, ws)
     xg = _xgmi_comm(group, "all_gather") if x.is_cuda else None
     pair = _PAIR[0] if (xg is not None and ws == 2) else None
     if pair is not None and pair.fits(x.numel(), x):
         xg = pair  # multipath: direct link + 2-hop relays
+    _trace("sp.all_gather", x, ws, "xgmi" if xg is not None and (xg is pair or xg.supports(x)) else None)
     gather = _synced(xg.all_gather) if xg is not None else (lambda t: C.all_gather(t, group=group))
     if x.shape[0] == 1:
         return gather(x[0].contiguous()).unsqueeze(0)
@@ -394,11 +396,11 @@ def _reduce_scatter_seq(x: torch.Tensor, group) -> torch.Tensor:
     ws = _ws(group)
     if ws == 1:
         return x
-    _trace("sp.reduce_scatter", x, ws)
     xg = _xgmi_comm(group, "reduce_scatter") if x.is_cuda else None
     pair = _PAIR[0] if (xg is not None and ws == 2) else None
     if pair is not None and pair.fits(x.numel() // 2, x):
         xg = pair  # multipath: direct link + 2-hop relays
+    _trace("sp.reduce_scatter", x, ws, "xgmi" if xg is not None and (xg is pair or xg.supports(x)) else None)
     scatter = _synced(xg.reduce_scatter) if xg is not None else (lambda t: C.reduce_scatter(t, group=group))
     if x.shape[0] == 1:
         return scatter(x[0].contiguous()).unsqueeze(0)
@@ -634,10 +636,11 @@ def _sp_gather_async(part: torch.Tensor, group):
     pair = _pair_for(group, part.numel(), part)
     if pair is not None:
         return _on_comm_stream(pair.all_gather, part)
-    _trace("sp.all_gather", part, ws)
     xg = _xgmi_comm(group, "all_gather") if (part.is_cuda and ws > 2) else None
     if xg is not None and xg.supports(part):  # tp 4 / 8: all 7 links, on the comm side stream
+        _trace("sp.all_gather", part, ws, "xgmi")
         return _on_comm_stream(xg.all_gather, part.contiguous())
+    _trace("sp.all_gather", part, ws)
     return C.all_gather(part, group=group, async_op=True)
 
 
@@ -648,10 +651,11 @@ def _sp_reduce_scatter_async(buf: torch.Tensor, group):
     pair = _pair_for(group, buf.numel() // 2, buf)
     if pair is not None:
         return _on_comm_stream(pair.reduce_scatter, buf)
-    _trace("sp.reduce_scatter", buf, ws)
     xg = _xgmi_comm(group, "reduce_scatter") if (buf.is_cuda and ws > 2) else None
     if xg is not None and buf.is_contiguous() and xg.supports(buf) and buf.shape[0] % ws == 0:
+        _trace("sp.reduce_scatter", buf, ws, "xgmi")
         return _on_comm_stream(xg.reduce_scatter, buf)
+    _trace("sp.reduce_scatter", buf, ws)
     return C.reduce_scatter(buf, group=group, async_op=True)
 
 

@@ -87,7 +87,16 @@ class Trainer:
 
             # collective over each EP group, at start-up: "auto" self-tests the xGMI push
             # exchange (dropless, device counts) against RCCL and keeps it when it matches
-            select_ep_transport(mesh.pgm.ep_group, a.ep_comm)
+            area = None
+            if a.sequence_length and a.micro_batch_size:
+                mc = get_model_config(a.model_name_or_path)
+                if mc.is_moe:
+                    from ..models.moe import ep_area_bytes
+
+                    area = ep_area_bytes(a.micro_batch_size * a.sequence_length // max(1, a.context_parallel_size),
+                                         a.expert_parallel_size, mc.num_experts_per_tok, mc.num_experts,
+                                         mc.hidden_size, a.moe_capacity_factor)
+            select_ep_transport(mesh.pgm.ep_group, a.ep_comm, area_bytes=area)
 
         set_use_flash_attention(a.use_flash_attention)
         if a.context_parallel_size > 1:
