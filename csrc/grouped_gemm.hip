@@ -349,6 +349,287 @@ __global__ __launch_bounds__(NT, 1) void grouped_gemm_kernel(const bf16_t* __res
   }
 }
 
+// ============================================================ 8-phase variant (BN = 256)
+// The synchronisation skeleton of csrc/wgrad_gemm.hip's wgrad8_kernel (the 256² 8-phase
+// template of cdna_hip_programming.md) on this file's operand images: 256 x 256 tile,
+// BK = 64, 8 waves as 2 (M) x 4 (N); wave (wr, wc) owns the four 64 x 32 quadrants (mq, nq)
+// at rows mq*128 + wr*64, columns nq*128 + wc*32.  Quadrant (mq, nq) reads only the X
+// half-image mq ([128 rows][64 k] row image) and the W half-image nq (row image in the WT
+// layout, [2 x 64-col blocks][64 k] column image in WN), 16 KiB each, so a K-tile is
+// consumed half-image by half-image in four phases -- (0,0) (0,1) (1,1) (1,0), reads p0 X0+W0,
+// p1 W1, p2 X1, p3 none (W0 / W1 fragments stay in registers) -- while the next tiles'
+// half-images stream into a ring of 8 slots behind them (LEAD 4, counted vmcnt, raw
+// barriers; waves 4-7 one barrier behind waves 0-3, so on every SIMD one wave reads while
+// its partner runs MFMAs).  The 2-phase kernel above waits vmcnt(0) at every K-tile.
+// EPI 1 (SwiGLU forward): W half-image 0 = gate rows, 1 = up rows of the tile's 128
+// features, so a lane holds gate (acc[.][j]) and up (acc[.][2 + j]) of the same feature.
+namespace g8 {
+constexpr int IMGB = 16384;  // one half-image: 128 rows x 64 k (or 64 k-rows x 128 cols) bf16
+constexpr int SLOTS = 8, LEAD = 4;
+}  // namespace g8
+
+template <bool WN, int EPI>
+__global__ __launch_bounds__(NT, 1) void grouped8_kernel(const bf16_t* __restrict__ X, int64_t ldx,
+                                                         const bf16_t* __restrict__ W, int64_t ldw, int64_t strideW,
+                                                         bf16_t* __restrict__ Y, int64_t ldy,
+                                                         const int* __restrict__ offs,
+                                                         const int* __restrict__ tile_end, int G, int N, int K,
+                                                         bf16_t* __restrict__ Y2, int64_t ld2, int I) {
+  using namespace g8;
+  static_assert(EPI != 1 || !WN, "SwiGLU forward epilogue: WT layout");
+  static_assert(EPI != 2 || WN, "SwiGLU backward epilogue: WN layout");
+  __shared__ __attribute__((aligned(16))) char smem_raw[SLOTS * IMGB];
+  lds_t* smem = (lds_t*)smem_raw;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = wid >> 2, wr = grp, wc = wid & 3;
+  // EPI 1: N = 2I columns of gu, one N-tile per 128 features (gate + up)
+  const int nbn = EPI == 1 ? I / 128 : N / 256;
+  const int slot = (int)blockIdx.x / nbn, nt = (int)blockIdx.x % nbn;
+  const int total_slots = tile_end[G - 1];
+  if (slot >= total_slots) return;  // uniform over the workgroup: no barrier reached yet
+  const int g = find_group(tile_end, G, slot);
+  const int first_slot = g ? tile_end[g - 1] : 0;
+  const int row0 = (g ? offs[g - 1] : 0) + (slot - first_slot) * BM;
+  const int rows = min(BM, offs[g] - row0);  // >= 1 by construction
+  const int n0 = nt * 256;
+
+  // ---- descriptors: X rows past the group's end and W rows / columns past the tile read as 0
+  const bf16_t* xb = X + (int64_t)row0 * ldx;
+  const i32x4 rsX = make_rsrc(xb, (uint32_t)(((int64_t)(rows - 1) * ldx + K) * 2));
+  const bf16_t* wb = W + (int64_t)g * strideW;
+  const i32x4 rsW = make_rsrc(wb, (uint32_t)(WN ? ((int64_t)(K - 1) * ldw + N) * 2 : ((int64_t)(N - 1) * ldw + K) * 2));
+  const uint32_t sX = (uint32_t)(ldx * 2), sW = (uint32_t)(ldw * 2);
+
+  // ---- DMA: half-image h (issue order X = 0: X0, 1: W0, 2: W1, 3: X1) of K-tile kt; wave w
+  // fills pieces 2w, 2w + 1 (1 KiB each: 8 rows x 128 B, or 8 k-rows x 128 B of a 64-col
+  // block); lane L lands at 16 L of its piece
+  uint32_t vX[2], vWr[2][2], vWc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = 2 * wid + i, pr = q * 8 + (lane >> 3), pc = lane & 7;
+    const uint32_t ch = (uint32_t)((pc ^ rsw(pr)) * 16);
+    vX[i] = (uint32_t)pr * sX + ch;
+    // WT row image of W half nq: tile columns nq*128 + pr -> weight row
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq) {
+      const int src = EPI == 1 ? (nq ? I : 0) + 128 * nt + pr : n0 + nq * 128 + pr;
+      vWr[nq][i] = (uint32_t)src * sW + ch;
+    }
+    // WN column image: block cb = q / 8, k-row kr, logical 32-B slot
+    const int cb = q >> 3, kr = (q & 7) * 8 + (lane >> 3);
+    const int logical = (((pc >> 1) ^ csw(kr)) << 1) | (pc & 1);
+    vWc[i] = (uint32_t)kr * sW + (uint32_t)((cb * 64 + logical * 8) * 2);
+  }
+  const uint32_t ldsw = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem + (uint32_t)(wid * 2048));
+  auto ring_dma = [&](auto xc, int slot_i, int kt, int piece) {
+    constexpr int Xh = decltype(xc)::value;
+    constexpr bool isX = (Xh == 0 || Xh == 3);
+    constexpr int half = (Xh == 2 || Xh == 3) ? 1 : 0;
+    uint32_t v;
+    if constexpr (isX) {
+      v = vX[piece] + (uint32_t)(half * 128) * sX + (uint32_t)(kt * BK * 2);
+    } else if constexpr (WN) {
+      v = vWc[piece] + (uint32_t)(kt * BK) * sW + (uint32_t)((n0 + half * 128) * 2);
+    } else {
+      v = vWr[half][piece] + (uint32_t)(kt * BK * 2);
+    }
+    lds_dma16(isX ? rsX : rsW, ldsw + (uint32_t)(slot_i * IMGB + piece * 1024), v);
+  };
+
+  // ---- fragment reads (16x16x32; lane group gq = lane >> 4 holds k 8gq .. 8gq+7 of a
+  // 32-k sub-step ks): A rows wr*64 + 16 i of a X half-image, B columns wc*32 + 16 j of a W one
+  const int gq = lane >> 4, rr = lane & 15;
+  int aoff[4][2], boff[2][2][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = wr * 64 + 16 * i + rr;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) aoff[i][ks] = r * 128 + 16 * ((4 * ks + gq) ^ rsw(r));
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int nn = wc * 32 + 16 * j;  // column within the half-image
+    if (WN) {
+      const int q = (lane >> 2) & 3, p = lane & 3;
+      const int kr = 8 * gq + q, sl = (nn & 63) >> 4;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        boff[j][ks][0] = (nn >> 6) * 8192 + (kr + 32 * ks) * 128 + 32 * (sl ^ csw(kr)) + 8 * p;
+        boff[j][ks][1] = boff[j][ks][0] + 4 * 128;
+      }
+    } else {
+      const int r = nn + rr;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) boff[j][ks][0] = boff[j][ks][1] = r * 128 + 16 * ((4 * ks + gq) ^ rsw(r));
+    }
+  }
+  auto read_b = [&](const lds_t* img, int j, int ks) -> bfx8 {
+    if constexpr (WN) return cat8(lds_tr(img + boff[j][ks][0]), lds_tr(img + boff[j][ks][1]));
+    else return lds_b128(img + boff[j][ks][0]);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
+  bfx8 af[4][2] = {}, b0[2][2] = {}, b1[2][2] = {};
+
+  auto bar = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+
+  const int KT = K / BK;
+  const int NH = 4 * KT;  // half-images of the whole K loop
+  // prologue: half-images 0 .. LEAD-1 (K-tile 0); 0 (X0) and 1 (W0) retired for phase 0
+#pragma unroll
+  for (int pc = 0; pc < 2; ++pc) ring_dma(I0(), 0, 0, pc);
+#pragma unroll
+  for (int pc = 0; pc < 2; ++pc) ring_dma(I1(), 1, 0, pc);
+#pragma unroll
+  for (int pc = 0; pc < 2; ++pc) ring_dma(I2(), 2, 0, pc);
+#pragma unroll
+  for (int pc = 0; pc < 2; ++pc) ring_dma(I3(), 3, 0, pc);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (LEAD - 2)) : "memory");
+  bar();
+  if (grp == 1) bar();  // the stagger: waves 4-7 run one barrier behind
+
+  auto phase = [&](auto pc, int kt) {
+    constexpr int P = decltype(pc)::value;
+    constexpr int MQ = (P == 0 || P == 1) ? 0 : 1, NQ = (P == 0 || P == 3) ? 0 : 1;
+    const int n0h = 4 * kt;
+    // slots read this phase: X0 = n0h, W0 = n0h + 1, W1 = n0h + 2, X1 = n0h + 3
+    const lds_t* ai = smem + ((n0h + (MQ ? 3 : 0)) % SLOTS) * IMGB;
+    if constexpr (P == 0 || P == 2) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) af[i][ks] = lds_b128(ai + aoff[i][ks]);
+    }
+    if constexpr (P == 0 || P == 1) {
+      const lds_t* bi = smem + ((n0h + 1 + NQ) % SLOTS) * IMGB;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bfx8 v = read_b(bi, j, ks);
+          if constexpr (NQ == 0) b0[j][ks] = v;
+          else b1[j][ks] = v;
+        }
+    }
+    // retire what the NEXT phase reads (p3 -> X0/W0 of kt+1, p0 -> W1, p1 -> X1, p2 -> none)
+    const int issue = n0h + P + LEAD;  // this phase's DMA (issued under its MFMAs)
+    if (issue <= NH) {
+      if constexpr (P == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (LEAD - 2)) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (LEAD - 3)) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();
+    if constexpr (P == 0 || P == 2) {
+#pragma unroll
+      for (int i = 2; i < 4; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) af[i][ks] = lds_b128(ai + aoff[i][ks]);
+    }
+    const int islot = issue % SLOTS, ikt = kt + (P + LEAD) / 4;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const bfx8 bv = NQ == 0 ? b0[j][ks] : b1[j][ks];
+          acc[MQ * 4 + i][NQ * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bv, acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
+        }
+      // the next half-image, one 1-KiB piece after the 4th and the 8th MFMA
+      if ((i == 0 || i == 1) && issue < NH) {
+        __builtin_amdgcn_sched_barrier(0);
+        ring_dma(std::integral_constant<int, (P + LEAD) % 4>(), islot, ikt, i);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+  };
+  for (int kt = 0; kt < KT; ++kt) {
+    phase(I0(), kt);
+    phase(I1(), kt);
+    phase(I2(), kt);
+    phase(I3(), kt);
+  }
+  if (grp == 0) bar();  // same barrier count in both groups
+
+  // ---- epilogue: acc[i][j] = rows (i >> 2)*128 + wr*64 + 16 (i & 3) + 4 gq + r, columns
+  // (j >> 1)*128 + wc*32 + 16 (j & 1) + (lane & 15) of the tile; rows past the group unstored
+  const int cl = lane & 15;
+  if constexpr (EPI == 1) {
+    bf16_t* gub = Y + (int64_t)row0 * ldy;
+    bf16_t* ab = Y2 + (int64_t)row0 * ld2;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = (i >> 2) * 128 + wr * 64 + 16 * (i & 3) + 4 * gq + r;
+        if (m < rows) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const float gv = acc[i][j][r], uv = acc[i][j + 2][r];
+            const int c = 128 * nt + wc * 32 + 16 * j + cl;
+            gub[(int64_t)m * ldy + c] = f2bf(gv);
+            gub[(int64_t)m * ldy + I + c] = f2bf(uv);
+            ab[(int64_t)m * ld2 + c] = f2bf(silu(gv) * uv);
+          }
+        }
+      }
+  } else if constexpr (EPI == 2) {
+    const bf16_t* gub = Y2 + (int64_t)row0 * ld2;
+    bf16_t* db = Y + (int64_t)row0 * ldy;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = (i >> 2) * 128 + wr * 64 + 16 * (i & 3) + 4 * gq + r;
+        if (m < rows) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int c = n0 + (j >> 1) * 128 + wc * 32 + 16 * (j & 1) + cl;
+            const float gv = bf2f(gub[(int64_t)m * ld2 + c]), uv = bf2f(gub[(int64_t)m * ld2 + I + c]);
+            const float d = acc[i][j][r];
+            const float sg = 1.f / (1.f + __expf(-gv)), sl = gv * sg;
+            db[(int64_t)m * ldy + c] = f2bf(d * uv * (sg + sl * (1.f - sg)));
+            db[(int64_t)m * ldy + I + c] = f2bf(d * sl);
+          }
+        }
+      }
+  } else {
+    bf16_t* yb = Y + (int64_t)row0 * ldy + n0 + wc * 32 + cl;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = (i >> 2) * 128 + wr * 64 + 16 * (i & 3) + 4 * gq + r;
+        if (m < rows) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) yb[(int64_t)m * ldy + (j >> 1) * 128 + 16 * (j & 1)] = f2bf(acc[i][j][r]);
+        }
+      }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -404,7 +685,16 @@ int st_grouped_gemm_ex(const void* X, int64_t ldx, const void* W, int64_t ldw, i
     else                                                                                         \
       grouped_gemm_kernel<BNV, WNV, false, 0><<<(unsigned)grid, NT, 0, st>>>(ARGS);              \
   } while (0)
-  if (epi == 1) {
+  // 8-phase kernel for 256-wide tiles (ST_GMM_8PHASE=0: the 2-phase kernel, A/B)
+  const char* p8e = std::getenv("ST_GMM_8PHASE");
+  const bool p8 = bn == 256 && !spread && !(p8e && std::atoi(p8e) == 0);
+#define ARGS8 x, ldx, w, ldw, strideW, y, ldy, offs, tile_end, G, N, K, y2, ld2, I
+  if (p8) {
+    if (epi == 1) grouped8_kernel<false, 1><<<(unsigned)grid, NT, 0, st>>>(ARGS8);
+    else if (epi == 2) grouped8_kernel<true, 2><<<(unsigned)grid, NT, 0, st>>>(ARGS8);
+    else if (wn) grouped8_kernel<true, 0><<<(unsigned)grid, NT, 0, st>>>(ARGS8);
+    else grouped8_kernel<false, 0><<<(unsigned)grid, NT, 0, st>>>(ARGS8);
+  } else if (epi == 1) {
     grouped_gemm_kernel<256, false, false, 1><<<(unsigned)grid, NT, 0, st>>>(ARGS);
   } else if (epi == 2) {
     if (bn == 256) grouped_gemm_kernel<256, true, false, 2><<<(unsigned)grid, NT, 0, st>>>(ARGS);
@@ -416,6 +706,7 @@ int st_grouped_gemm_ex(const void* X, int64_t ldx, const void* W, int64_t ldw, i
   }
 #undef LAUNCH
 #undef ARGS
+#undef ARGS8
   return (int)hipGetLastError();
 }
 

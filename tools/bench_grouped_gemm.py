@@ -53,13 +53,24 @@ def main() -> int:
         w = torch.randn((G, K, N) if wn else (G, N, K), device="cuda", dtype=torch.bfloat16) * 0.02
         offs = torch.arange(1, G + 1, device="cuda", dtype=torch.int32) * rows
         flops = 2.0 * T * K * N
+        def two_phase(fn):  # the 2-phase kernel (ST_GMM_8PHASE=0, read per launch) for the A/B
+            def run():
+                os.environ["ST_GMM_8PHASE"] = "0"
+                try:
+                    return fn()
+                finally:
+                    os.environ.pop("ST_GMM_8PHASE", None)
+            return run
+
         arms = {
             "hip_grouped": lambda: _lib.ops().grouped_gemm(x, w, offs, wn),
+            "hip_grouped_2phase": two_phase(lambda: _lib.ops().grouped_gemm(x, w, offs, wn)),
             "torch_grouped_mm": lambda: torch._grouped_mm(x, w if wn else w.transpose(-2, -1), offs=offs),
             "dense_hipblaslt": lambda: torch.matmul(x, w[0] if wn else w[0].t()),
         }
         if not wn and "gate_up" in name:  # SwiGLU epilogue: gu and a = silu(g) * u from the GEMM
             arms["hip_grouped_swiglu_epilogue"] = lambda: _lib.ops().grouped_gemm_swiglu(x, w, offs)
+            arms["hip_grouped_swiglu_epilogue_2phase"] = two_phase(lambda: _lib.ops().grouped_gemm_swiglu(x, w, offs))
             arms["hip_grouped_then_swiglu"] = lambda: _lib.ops().swiglu_fwd(_lib.ops().grouped_gemm(x, w, offs, wn))
         if wn and G == 1:  # the TN form on a transposed weight copy (what ops/grad.py runs today)
             wt = w[0].t().contiguous()
