@@ -855,7 +855,7 @@ std::vector<at::Tensor> flash_bwd(const at::Tensor& dout, const at::Tensor& q, c
                                   double scale, bool causal, int64_t q_offset, int64_t k_offset,
                                   const c10::optional<at::Tensor>& dq_out,
                                   const c10::optional<at::Tensor>& dk_out,
-                                  const c10::optional<at::Tensor>& dv_out) {
+                                  const c10::optional<at::Tensor>& dv_out, int64_t ds_mode) {
   const int64_t D = q.size(3);
   TORCH_CHECK(D == 64 || D == 128, "flash_bwd: head_dim must be 64 or 128");
   check_qkv(q, "q", D);
@@ -894,9 +894,11 @@ std::vector<at::Tensor> flash_bwd(const at::Tensor& dout, const at::Tensor& q, c
   const int64_t pe = st_flash_bwd_part_elems((int)B, (int)Sq, (int)Sk, (int)H, (int)Hkv, (int)D, causal ? 1 : 0);
   at::Tensor part;
   if (pe > 0) part = at::empty({pe}, q.options().dtype(at::kFloat));
-  // dS workspace of the dS-materialising backward (transient: freed on return)
-  const int64_t dse = st_flash_bwd_ds_elems((int)B, (int)Sq, (int)Sk, (int)H, (int)D, causal ? 1 : 0, q_offset,
-                                            k_offset);
+  // dS workspace of the dS-materialising backward (transient: freed on return); ds_mode 0
+  // forces the one-shot (recompute dQ) backward, -1 lets st_flash_bwd_ds_elems decide
+  const int64_t dse = ds_mode == 0 ? 0
+                                   : st_flash_bwd_ds_elems((int)B, (int)Sq, (int)Sk, (int)H, (int)D, causal ? 1 : 0,
+                                                           q_offset, k_offset);
   at::Tensor dsw;
   if (dse > 0) dsw = at::empty({dse}, q.options());
   rc = st_flash_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
@@ -1038,7 +1040,7 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("xent_fwd(Tensor logits, Tensor target, int vocab_start) -> Tensor[]");
   m.def("xent_bwd_(Tensor logits, Tensor target, int vocab_start, Tensor lse, Tensor dloss, Tensor(a!) dlogits) -> ()");
   m.def("flash_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int q_offset, int k_offset) -> Tensor[]");
-  m.def("flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, int q_offset, int k_offset, Tensor(a!)? dq_out=None, Tensor(b!)? dk_out=None, Tensor(c!)? dv_out=None) -> Tensor[]");
+  m.def("flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, int q_offset, int k_offset, Tensor(a!)? dq_out=None, Tensor(b!)? dk_out=None, Tensor(c!)? dv_out=None, int ds_mode=-1) -> Tensor[]");
   m.def("flash_bwd_kv(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, int q_offset, int k_offset, Tensor(a!)? dk_out=None, Tensor(b!)? dv_out=None) -> Tensor[]");
   m.def("flash_bwd_q_ds(Tensor q, Tensor k, Tensor ws, float scale, bool causal, int q_offset, int k_offset, Tensor(a!)? dq_out=None) -> Tensor");
   m.def("wgrad_gemm_(Tensor(a!) out, Tensor dy, Tensor x, int beta, int variant=0) -> bool");

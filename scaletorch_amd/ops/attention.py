@@ -131,11 +131,12 @@ def flash_attn_fwd(q, k, v, scale: float, causal: bool, q_offset: int = 0, k_off
 
 
 def flash_attn_bwd(dout, q, k, v, out, lse, scale: float, causal: bool, q_offset: int = 0,
-                   k_offset: int = 0, dq=None, dk=None, dv=None):
-    """(dq, dk, dv) for one attention block (writes into dq/dk/dv when given)."""
+                   k_offset: int = 0, dq=None, dk=None, dv=None, one_shot: bool = False):
+    """(dq, dk, dv) for one attention block (writes into dq/dk/dv when given).
+    ``one_shot``: the recompute-dQ backward even where the dS-materialising one applies."""
     if _lib.use_native(q):
         return _lib.ops().flash_bwd(dout.contiguous(), q, k, v, out, lse, scale, causal, q_offset,
-                                    k_offset, dq, dk, dv)
+                                    k_offset, dq, dk, dv, 0 if one_shot else -1)
     gq, gk, gv = flash_bwd_ref(dout, q, k, v, out, lse, scale, causal, q_offset, k_offset)
     res = []
     for g, dst, ref in ((gq, dq, q), (gk, dk, k), (gv, dv, v)):

@@ -320,6 +320,7 @@ def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> int:
 
 
 _WGRAD_SIDE: dict = {}
+_TN_PROBE_BUFS: dict = {}  # ST_WGRAD_TN_PROBE=1 timing probe: stale token-contiguous operands per shape
 
 
 def wgrad_side_stream(device: torch.device):
@@ -357,6 +358,19 @@ def accumulate_linear_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
     if pre is None and mg.dtype == torch.float32:
         pre = prefetch_wgrad(param, dy2d, x2d)
     beta = 0 if take_fresh(param) else 1
+    if os.environ.get("ST_WGRAD_TN_PROBE") == "1" and mg.dtype == torch.float32 and dy2d.is_cuda:
+        # TIMING PROBE ONLY (wrong gradients): the weight gradient as a TN GEMM on token-
+        # contiguous dY^T / X^T that cost nothing to produce (stale per-shape buffers) -- the
+        # in-step upper bound of "producers store transposed copies" 
+        from . import _lib
+
+        key = (tuple(dy2d.shape), tuple(x2d.shape), dy2d.device.index)
+        bufs = _TN_PROBE_BUFS.get(key)
+        if bufs is None:
+            bufs = _TN_PROBE_BUFS[key] = (dy2d.t().contiguous(), x2d.t().contiguous())
+        _lib.ops().gemm_(mg.view(mg.shape[0], -1), bufs[0], bufs[1], False, True, 1.0, float(beta))
+        _grad_ready(param)
+        return None
     if pre is not None:
         torch.cuda.current_stream().wait_event(pre.done)
         m2 = mg.view(mg.shape[0], -1)
