@@ -146,10 +146,7 @@ def select_tp_transport(group, requested: str = "auto", probe_mb: int = 64, msg_
                 flags = [per_op.get(n, 0) for n in names]
         except Exception as e:  # noqa: BLE001 -- fall back, but every rank still joins the vote
             flags, info = [0] * len(names), {"error": repr(e)[:200]}
-    flag = torch.tensor(flags, dtype=torch.int32, device="cuda" if torch.cuda.is_available() else "cpu")
-    if dist.is_initialized():
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-    voted = {n: bool(int(v)) for n, v in zip(names, flag.tolist())}
+    voted = _vote(names, flags)
     choice = "xgmi" if any(voted.values()) else "rccl"
     if choice == "rccl":
         if torch.cuda.is_available():
@@ -160,6 +157,18 @@ def select_tp_transport(group, requested: str = "auto", probe_mb: int = 64, msg_
     set_tp_comm(choice, voted)
     TRANSPORT.update(selftest=info)
     return choice
+
+
+def _vote(names: list, flags: list) -> dict:
+    """MIN of every rank's per-collective verdict over the world: a collective keeps the xGMI
+    path only if it passed on EVERY rank (one all-reduce; gloo-safe on CPU)."""
+    import torch.distributed as dist
+
+    on_gpu = torch.cuda.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"
+    flag = torch.tensor(flags, dtype=torch.int32, device="cuda" if on_gpu else "cpu")
+    if dist.is_initialized():
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return {n: bool(int(v)) for n, v in zip(names, flag.tolist())}
 
 
 def _tp_selftest(comm, group, msg_bytes: int):

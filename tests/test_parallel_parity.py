@@ -572,3 +572,42 @@ def test_moe_dropless_uneven_token_counts():
         torch.testing.assert_close(ga, gb, atol=1e-5, rtol=1e-4)
         torch.testing.assert_close(wa, wb, atol=1e-5, rtol=1e-4)
         assert dropped == 0
+
+
+def _tp_vote_worker(rank, world):
+    import torch.distributed as dist
+
+    from scaletorch_amd.parallel import tensor_parallel as TP
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    names = ["all_reduce", "all_gather", "reduce_scatter"]
+    # rank 2 saw its all-gather lose to RCCL; rank 3's reduce-scatter failed correctness
+    flags = [1, 0 if rank == 2 else 1, 0 if rank == 3 else 1]
+    voted = TP._vote(names, flags)
+
+    class FakeComm:
+        closed = 0
+
+        def close(self):
+            FakeComm.closed += 1
+
+    TP._XGMI[1] = FakeComm()
+    TP._XGMI[2] = FakeComm()
+    TP._close_tp_xgmi()
+    TP.set_tp_comm("xgmi" if any(voted.values()) else "rccl", voted)
+    routed = {op: TP._TP_XGMI_OPS[op] for op in names}
+    out = (voted, FakeComm.closed, len(TP._XGMI), dict(TP.TRANSPORT), routed)
+    TP.set_tp_comm("rccl")
+    return out
+
+
+def test_tp_transport_vote_is_min_over_ranks_and_losers_are_closed():
+    """tp 4 / 8 auto transport: each collective keeps xGMI only if EVERY rank's self-test
+    passed it (MIN vote), the per-collective routing follows the vote, and closing the
+    losing communicators releases every TP IPC area."""
+    res = run_workers(_tp_vote_worker, 4)
+    for voted, closed, left, transport, routed in res:
+        assert voted == {"all_reduce": True, "all_gather": False, "reduce_scatter": False}
+        assert closed == 2 and left == 0
+        assert transport["tp"] == "xgmi" and transport["ops"] == ["all_reduce"]
+        assert routed == {"all_reduce": True, "all_gather": False, "reduce_scatter": False}

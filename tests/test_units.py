@@ -695,3 +695,22 @@ def test_sr_round_bf16_is_unbiased_and_keeps_specials():
     z = sr_round_bf16(sp, 123)
     assert torch.isinf(z[0]) and z[0] > 0 and torch.isinf(z[1]) and z[1] < 0 and torch.isnan(z[2])
     assert z[3] == 0 and z[5].item() == -3.5
+
+
+def test_ep_token_bound_and_area_sizing():
+    """A declared EP token bound sizes the exchange with no collective (T above it raises);
+    the EP IPC area is the run's dropless landing rows (Mixtral EP 8 x 4096: 256 MiB)."""
+    from scaletorch_amd.models import moe
+
+    try:
+        moe.set_ep_token_bound(4096)
+        assert moe.ep_rows_range(4096, None) == (4096, 4096)
+        assert moe.ep_rows_range(1000, None) == (1000, 4096)
+        with pytest.raises(ValueError):
+            moe.ep_rows_range(5000, None)
+    finally:
+        moe.set_ep_token_bound(None)
+    assert moe.ep_area_bytes(4096, 8, 2, 8, 4096) == 256 << 20
+    assert moe.ep_area_bytes(16, 2, 2, 8, 64) == 16 << 20  # floor
+    # capacity dispatch: cf * T * k rows when that exceeds the dropless bound
+    assert moe.ep_area_bytes(4096, 2, 8, 128, 2048, capacity_factor=4.0) >= 4 * 4096 * 8 * 2048 * 2
