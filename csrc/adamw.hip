@@ -12,13 +12,15 @@
 //     all-reduced global norm), so clipping needs no host synchronisation;
 //   * grads may be fp32 (main_grad arena) or bf16;
 //   * bf16 moments are stored with STOCHASTIC rounding: a hashed 16-bit offset per
-//     (element, step, moment) is added to the fp32 bits before truncation, so the stored
+//     (element, step, moment: the two halves of one 32-bit hash) is added to the fp32
+//     bits before truncation, so the stored
 //     moment is unbiased.  Round-to-nearest froze exp_avg_sq at beta2 = 0.999, where the
 //     per-step change (0.1 %) is below bf16's half-ulp.  The hash is
 //     mirrored bit-for-bit by scaletorch_amd/optim.py ``sr_offsets``.
 #include "common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 using namespace st;
 
@@ -66,33 +68,45 @@ ST_DEVICE uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
-// key of one moment at one step (0 = m, 1 = v); the element index is its ARENA index
-// (launch base + local), so a ZeRO-1 shard rounds exactly as the replicated arena does
-ST_DEVICE uint32_t sr_key(uint32_t step, uint32_t which) {
-  return mix32((step * 0x9e3779b9u) ^ (which ? 0x85ebca6bu : 0u));
-}
+// key of one step; the element index is its ARENA index (launch base + local), so a ZeRO-1
+// shard rounds exactly as the replicated arena does
+ST_DEVICE uint32_t sr_key(uint32_t step) { return mix32(step * 0x9e3779b9u); }
+// 16 random bits for exp_avg (low half) and 16 for exp_avg_sq (high half) of element idx:
+// ONE mix per element (the high-word mix is shared by the 4 elements of a chunk)
+ST_DEVICE uint32_t sr_hash(uint32_t lo, uint32_t hi_mix) { return mix32(lo ^ hi_mix); }
 // stochastic fp32 -> bf16: add 16 random low bits, truncate; NaN / Inf keep the plain cast
-ST_DEVICE uint32_t sr_bf16(float x, int64_t idx, uint32_t key) {
+ST_DEVICE uint32_t sr_bf16(float x, uint32_t r16) {
   const uint32_t u = __float_as_uint(x);
   if ((u & 0x7f800000u) == 0x7f800000u) return f2bf(x);
-  const uint32_t r = mix32((uint32_t)idx ^ mix32((uint32_t)((uint64_t)idx >> 32) ^ key)) & 0xffffu;
-  return (u + r) >> 16;
+  return (u + r16) >> 16;
 }
 
 template <typename S>
-ST_DEVICE void store_s4(S* s, int64_t i, f32x4 v, uint32_t key, int64_t base);
+ST_DEVICE void store_s4(S* s, int64_t i, f32x4 v, const uint32_t (&r)[4]);
 template <>
-ST_DEVICE void store_s4<float>(float* s, int64_t i, f32x4 v, uint32_t, int64_t) {
+ST_DEVICE void store_s4<float>(float* s, int64_t i, f32x4 v, const uint32_t (&)[4]) {
   __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(s + i));
 }
 template <>
-ST_DEVICE void store_s4<bf16_t>(bf16_t* s, int64_t i, f32x4 v, uint32_t key, int64_t base) {
+ST_DEVICE void store_s4<bf16_t>(bf16_t* s, int64_t i, f32x4 v, const uint32_t (&r)[4]) {
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
   u32x2 o;
-  const int64_t gi = i + base;
-  o[0] = sr_bf16(v[0], gi, key) | (sr_bf16(v[1], gi + 1, key) << 16);
-  o[1] = sr_bf16(v[2], gi + 2, key) | (sr_bf16(v[3], gi + 3, key) << 16);
+  o[0] = sr_bf16(v[0], r[0]) | (sr_bf16(v[1], r[1]) << 16);
+  o[1] = sr_bf16(v[2], r[2]) | (sr_bf16(v[3], r[3]) << 16);
   __builtin_nontemporal_store(o, reinterpret_cast<u32x2*>(s + i));
+}
+// random words of the 4 elements at arena index gi (a multiple of 4: one high word)
+template <typename S>
+ST_DEVICE void sr_words(int64_t gi, uint32_t key, uint32_t (&rm)[4], uint32_t (&rv)[4]) {
+  if constexpr (std::is_same<S, bf16_t>::value) {
+    const uint32_t hm = mix32((uint32_t)((uint64_t)gi >> 32) ^ key);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t h = sr_hash((uint32_t)gi + k, hm);
+      rm[k] = h & 0xffffu;
+      rv[k] = h >> 16;
+    }
+  }
 }
 
 // One element of the AdamW update, shared by the flat and the W^T-writing kernels so
@@ -116,7 +130,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, 
                                                      int64_t sr_base) {
   const float cs = clip ? *clip : 1.f;
   const float step = lr / bc1, decay = 1.f - lr * wd;
-  const uint32_t km = sr_key(sr_step, 0), kv = sr_key(sr_step, 1);
+  const uint32_t key = sr_key(sr_step);
   // Two 4-element chunks per thread per iteration, all loads issued before any math
   // (10 independent HBM streams in flight per thread); every byte is touched
   // exactly once, so loads/stores are non-temporal (no L2 pollution).
@@ -148,8 +162,10 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, 
         vv[u][k] = vk;
       }
       __builtin_nontemporal_store(w[u], reinterpret_cast<f32x4*>(master + ii[u]));
-      store_s4<S>(m, ii[u], mm[u], km, sr_base);
-      store_s4<S>(v, ii[u], vv[u], kv, sr_base);
+      uint32_t rm[4] = {}, rv[4] = {};
+      sr_words<S>(ii[u] + sr_base, key, rm, rv);
+      store_s4<S>(m, ii[u], mm[u], rm);
+      store_s4<S>(v, ii[u], vv[u], rv);
       if (p) {
         uint2 o;
         o.x = pack_bf16x2(w[u][0], w[u][1]);
@@ -182,7 +198,7 @@ __global__ __launch_bounds__(256) void adamw_wt_kernel(float* __restrict__ maste
   const float cs = clip ? *clip : 1.f;
   const float step = lr / bc1, decay = 1.f - lr * wd;
   // same keys and element indices as the flat kernel over this weight: bitwise-equal moments
-  const uint32_t km = sr_key(sr_step, 0), kv = sr_key(sr_step, 1);
+  const uint32_t key = sr_key(sr_step);
   const int tiles_c = C / kWT;
   const int b = xcd_remap(blockIdx.x, gridDim.x);
   const int r0 = (b / tiles_c) * kWT, c0 = (b % tiles_c) * kWT;
@@ -211,8 +227,10 @@ __global__ __launch_bounds__(256) void adamw_wt_kernel(float* __restrict__ maste
       vv[u][k] = vk;
     }
     __builtin_nontemporal_store(w[u], reinterpret_cast<f32x4*>(master + i));
-    store_s4<S>(m, i, mm[u], km, sr_base);
-    store_s4<S>(v, i, vv[u], kv, sr_base);
+    uint32_t rm[4] = {}, rv[4] = {};
+    sr_words<S>(i + sr_base, key, rm, rv);
+    store_s4<S>(m, i, mm[u], rm);
+    store_s4<S>(v, i, vv[u], rv);
     const uint32_t lo = pack_bf16x2(w[u][0], w[u][1]), hi = pack_bf16x2(w[u][2], w[u][3]);
     *reinterpret_cast<uint2*>(p + i) = make_uint2(lo, hi);
     // padded LDS row (132 B): 4-B aligned only

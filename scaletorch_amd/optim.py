@@ -66,20 +66,25 @@ def _mix32(x: torch.Tensor) -> torch.Tensor:
     return x ^ (x >> 16)
 
 
-def sr_key(step: int, which: int) -> int:
-    """Key of one moment at one step (0 = exp_avg, 1 = exp_avg_sq)."""
-    return _mix32_int(((int(step) * 0x9E3779B9) & _M32) ^ (0x85EBCA6B if which else 0))
+def sr_key(step: int) -> int:
+    """Key of one optimizer step."""
+    return _mix32_int((int(step) * 0x9E3779B9) & _M32)
 
 
-def sr_round_bf16(x: torch.Tensor, key: int, base: int = 0) -> torch.Tensor:
-    """fp32 ``x`` -> bf16 by stochastic rounding, as the kernel; element i of ``x`` (flat
-    order) is arena element ``base + i`` -- the index the offset is hashed from, so a ZeRO-1
-    shard rounds exactly as the replicated arena does."""
+def sr_offsets(n: int, key: int, base: int = 0, device=None) -> tuple[torch.Tensor, torch.Tensor]:
+    """The kernel's 16-bit rounding offsets of arena elements base .. base + n - 1: (exp_avg,
+    exp_avg_sq) = (low, high) half of mix32(lo32(i) ^ mix32(hi32(i) ^ key))."""
+    idx = torch.arange(base, base + n, dtype=torch.int64, device=device)
+    h = _mix32((idx & _M32) ^ _mix32((idx >> 32) ^ key))
+    return h & 0xFFFF, h >> 16
+
+
+def sr_round_bf16(x: torch.Tensor, r16: torch.Tensor) -> torch.Tensor:
+    """fp32 ``x`` -> bf16 by stochastic rounding with per-element offsets ``r16`` (flat order),
+    bit-for-bit as csrc/adamw.hip ``sr_bf16``."""
     xf = x.reshape(-1).float()
-    idx = torch.arange(base, base + xf.numel(), dtype=torch.int64, device=xf.device)
     u = xf.view(torch.int32).to(torch.int64) & _M32
-    r = _mix32((idx & _M32) ^ _mix32((idx >> 32) ^ key)) & 0xFFFF
-    bits = ((u + r) >> 16) & 0xFFFF
+    bits = ((u + r16.reshape(-1)) >> 16) & 0xFFFF
     out = (bits - (bits >= 0x8000).to(torch.int64) * 0x10000).to(torch.int16).view(torch.bfloat16)
     special = (u & 0x7F800000) == 0x7F800000
     if bool(special.any()):
@@ -346,8 +351,9 @@ class ArenaAdamW(_ArenaOptimizer):
                 m.mul_(b1).add_(grad, alpha=1 - b1)
                 v.mul_(b2).addcmul_(grad, grad, value=1 - b2)
                 if m_st is not m:
-                    m_st.copy_(sr_round_bf16(m, sr_key(t, 0), base).view_as(m_st))
-                    v_st.copy_(sr_round_bf16(v, sr_key(t, 1), base).view_as(v_st))
+                    rm, rv = sr_offsets(m.numel(), sr_key(t), base, m.device)
+                    m_st.copy_(sr_round_bf16(m, rm).view_as(m_st))
+                    v_st.copy_(sr_round_bf16(v, rv).view_as(v_st))
                 bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
                 denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
                 if self.decoupled and wd:

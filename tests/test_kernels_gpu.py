@@ -151,7 +151,7 @@ def test_adamw_bf16_moments():
     widened moments, the update uses the unrounded fp32 moments, one STOCHASTIC bf16
     rounding per stored moment (csrc/adamw.hip sr_bf16) -- checked against an fp32
     PyTorch reference and the bit-exact torch mirror (optim.sr_round_bf16)."""
-    from scaletorch_amd.optim import sr_key, sr_round_bf16
+    from scaletorch_amd.optim import sr_key, sr_offsets, sr_round_bf16
 
     torch.manual_seed(0)
     n = 4096 * 33 + 8
@@ -169,10 +169,11 @@ def test_adamw_bf16_moments():
     wr.addcdiv_(mr / (1 - b1 ** t), (vr / (1 - b2 ** t)).sqrt() + eps, value=-lr)
     # one stochastic rounding: |err| < 1 ulp = 2^-7 |x| (+ slack for the fp32 fma-vs-mul/add
     # order where b1*m and (1-b1)*g nearly cancel); almost every element equals the mirror's
+    offsets = sr_offsets(n, sr_key(t), 0, "cuda")
     for which, (got, want) in enumerate(((m, mr), (v, vr))):
         err = (got.float() - want).abs()
         assert err.le(want.abs() * 2 ** -7 + 1e-7).all(), (err - want.abs() * 2 ** -7).max().item()
-        mirror = sr_round_bf16(want, sr_key(t, which))
+        mirror = sr_round_bf16(want, offsets[which])
         assert (got == mirror).float().mean().item() > 0.99
     assert (master - wr).abs().max().item() < 1e-6
     assert rel(p, wr) < 1e-2

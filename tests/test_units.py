@@ -654,7 +654,7 @@ def test_gemm_tuning_modes_cpu():
 def _second_moment_track(sr: bool, steps: int = 2000, n: int = 4096, b2: float = 0.999):
     """exp_avg_sq kept in bf16 (stochastic or nearest rounding, one rounding per step) vs fp32,
     over a stationary gradient stream of unit variance, starting from v = 0."""
-    from scaletorch_amd.optim import sr_key, sr_round_bf16
+    from scaletorch_amd.optim import sr_key, sr_offsets, sr_round_bf16
 
     g = torch.Generator().manual_seed(7)
     v32 = torch.zeros(n)
@@ -663,7 +663,7 @@ def _second_moment_track(sr: bool, steps: int = 2000, n: int = 4096, b2: float =
         gr = torch.randn(n, generator=g)
         v32.mul_(b2).addcmul_(gr, gr, value=1 - b2)
         w = v16.float().mul_(b2).addcmul_(gr, gr, value=1 - b2)
-        v16 = sr_round_bf16(w, sr_key(t, 1)) if sr else w.to(torch.bfloat16)
+        v16 = sr_round_bf16(w, sr_offsets(n, sr_key(t))[1]) if sr else w.to(torch.bfloat16)
     return v16.float(), v32
 
 
@@ -685,14 +685,14 @@ def test_bf16_second_moment_stochastic_rounding_tracks_fp32():
 
 
 def test_sr_round_bf16_is_unbiased_and_keeps_specials():
-    from scaletorch_amd.optim import sr_key, sr_round_bf16
+    from scaletorch_amd.optim import sr_key, sr_offsets, sr_round_bf16
 
     x = torch.full((1 << 16,), 1.0 + 2 ** -10)
-    y = sr_round_bf16(x, sr_key(3, 0)).float()
+    y = sr_round_bf16(x, sr_offsets(x.numel(), sr_key(3))[0]).float()
     assert set(y.unique().tolist()) <= {1.0, 1.0 + 2 ** -7}
     assert abs(y.mean().item() - x[0].item()) < 2e-5
     sp = torch.tensor([float("inf"), float("-inf"), float("nan"), 0.0, -0.0, -3.5])
-    z = sr_round_bf16(sp, 123)
+    z = sr_round_bf16(sp, sr_offsets(sp.numel(), 123)[1])
     assert torch.isinf(z[0]) and z[0] > 0 and torch.isinf(z[1]) and z[1] < 0 and torch.isnan(z[2])
     assert z[3] == 0 and z[5].item() == -3.5
 
