@@ -65,6 +65,8 @@ int64_t st_wgrad_ws_elems(int M, int N, int T, int variant);
 int st_wgrad_grouped(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int64_t strideC,
                      int M, int N, int G, const int* offs, int T_total, int beta, hipStream_t st);
 int64_t st_grouped_gemm_slots(int T, int G);
+int st_gemm4w(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t strideW, void* Y, int64_t ldy,
+              const int* offs, const int* tile_end, int T, int G, int N, int K, hipStream_t st);
 int st_grouped_gemm_bm();
 int st_grouped_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t strideW, void* Y, int64_t ldy,
                     const int* offs, const int* tile_end, int T, int G, int N, int K, int wn, hipStream_t st);
@@ -481,6 +483,31 @@ at::Tensor grouped_gemm(const at::Tensor& x, const at::Tensor& w, const at::Tens
                            (int)K, wn ? 1 : 0, cur_stream());
   if (rc == -2) return at::Tensor();
   ST_CHECK_RC(rc, "grouped_gemm");
+  return y;
+}
+
+// One-wave-per-SIMD TN GEMM (csrc/gemm4w.hip): y[T, N] = x[T, K] @ w[g]^T over the row ranges
+// [offs[g-1], offs[g]); w [G, N, K] (K contiguous).  Undefined tensor when the kernel does not
+// tile the shape.
+at::Tensor gemm4w(const at::Tensor& x, const at::Tensor& w, const at::Tensor& offs) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "w");
+  check_same_gpu(w, x, "w");
+  check_same_gpu(offs, x, "offs");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 3 && w.size(2) == x.size(1), "gemm4w: x [T, K], w [G, N, K]");
+  TORCH_CHECK(offs.scalar_type() == at::kInt && offs.dim() == 1 && offs.is_contiguous() && offs.size(0) == w.size(0),
+              "gemm4w: offs int32 [G]");
+  const int64_t T = x.size(0), K = x.size(1), G = w.size(0), N = w.size(1);
+  if (x.stride(1) != 1 || w.stride(2) != 1 || T == 0 || T > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
+    return at::Tensor();
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  at::Tensor counts = at::diff(offs, 1, 0, at::zeros({1}, offs.options()));
+  at::Tensor tile_end = at::cumsum(at::floor_divide(counts + 255, 256), 0, at::kInt);
+  at::Tensor y = at::empty({T, N}, x.options());
+  int rc = st_gemm4w(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(1), w.stride(0), y.data_ptr(), y.stride(0),
+                     offs.data_ptr<int>(), tile_end.data_ptr<int>(), (int)T, (int)G, (int)N, (int)K, cur_stream());
+  if (rc == -2) return at::Tensor();
+  ST_CHECK_RC(rc, "gemm4w");
   return y;
 }
 
@@ -1047,6 +1074,7 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("wgrad_grouped_(Tensor(a!) out, Tensor dy, Tensor x, Tensor offs, int beta) -> bool");
   m.def("grouped_gemm(Tensor x, Tensor w, Tensor offs, bool wn) -> Tensor");
   m.def("grouped_gemm_swiglu(Tensor x, Tensor w, Tensor offs) -> Tensor[]");
+  m.def("gemm4w(Tensor x, Tensor w, Tensor offs) -> Tensor");
   m.def("grouped_gemm_dswiglu(Tensor dy, Tensor w, Tensor offs, Tensor gu) -> Tensor");
   m.def("xgmi_create(int rank, int world, int cap, int epoch_base) -> int", &xgmi_create);
   m.def("xgmi_handle(int id) -> Tensor", &xgmi_handle);
@@ -1090,6 +1118,7 @@ TORCH_LIBRARY_IMPL(st_amd, CUDA, m) {
   m.impl("wgrad_grouped_", &wgrad_grouped_);
   m.impl("grouped_gemm", &grouped_gemm);
   m.impl("grouped_gemm_swiglu", &grouped_gemm_swiglu);
+  m.impl("gemm4w", &gemm4w);
   m.impl("grouped_gemm_dswiglu", &grouped_gemm_dswiglu);
   m.impl("qknorm_rope_fwd_", &qknorm_rope_fwd_);
   m.impl("qknorm_rope_bwd_", &qknorm_rope_bwd_);

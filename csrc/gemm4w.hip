@@ -1,0 +1,684 @@
+// Grouped / dense "TN" GEMM for gfx950 with ONE wave per SIMD and a 128 x 128 tile per wave:
+//   Y[rows of g] = X[rows of g] @ W[g]^T,  X [T][K], W[g] [N][K] (both K-contiguous)
+// (G = 1 is a plain GEMM; the data gradient dX = dY W runs in this layout on the W^T copy the
+// optimizer writes, ops/grad.py).  Reference call sites: every F.linear of the models and the
+// grouped expert matmul of scaletorch/models/npu_patch.py:94-127.
+//
+// Why another GEMM: csrc/grouped_gemm.hip's 8 waves x (128 x 64) tiles read 24 KiB of LDS per
+// wave per 64-k step; with the 64 KiB DMA fill that is 256 KiB per CU per 2,048 MFMA cycles,
+// i.e. LDS-bound at the MFMA rate (57-61 % MFMA busy measured, profiles/r04/grouped_gemm_pmc.md).
+// Here 4 waves x (128 x 128) read 128 KiB + write 64 KiB per K-step: 75 % of the LDS port at
+// full MFMA rate.  With one wave per SIMD nothing else hides a stall, so:
+//   * operands go global -> VGPR (buffer_load_dwordx4, a few issue cycles) -> ds_write_b128, not
+//     by LDS-DMA (whose ~60-cycle issue cost lands on the only wave of the SIMD); the loads of
+//     K-tile kt + 2 are issued during tile kt, written to LDS during tile kt + 1;
+//   * fragment registers are double-buffered: sub-step 0's MFMAs run while sub-step 1's
+//     fragments are read and half of the next tile's staged data written, sub-step 1's while
+//     the other half is written, the loads of the tile after it issued, and -- after the ONE
+//     barrier of the K-tile, a quarter into sub-step 1 -- the next tile's first fragments read;
+//   * 256 fp32 accumulators per lane (16x16x32 MFMA: 8 x 8 fragments), 512 registers / lane.
+// LDS images: [256 rows][64 k] bf16, 16-byte chunk c of row r at c ^ ((r >> 1) & 7): the
+// ds_read_b128 fragment reads and the ds_write_b128 fills are bank-conflict free.
+#include <cstdlib>
+#include <type_traits>
+
+#include "common.h"
+
+using namespace st;
+
+namespace {
+
+typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) char lds_t;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+constexpr int BM = 256, BN = 256, BK = 64, NT = 256;
+constexpr int IMG = BM * BK * 2;  // one operand image: 32 KiB
+constexpr int STAGE = 2 * IMG;     // A + B images of one K-tile
+
+ST_DEVICE int rsw(int r) { return (r >> 1) & 7; }
+
+ST_DEVICE rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+ST_DEVICE u32x4 gload(rsrc_t rs, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0); }
+ST_DEVICE void lds_w128(lds_t* p, u32x4 v) { *reinterpret_cast<u32x4 __attribute__((address_space(3)))*>(p) = v; }
+ST_DEVICE bfx8 lds_r128(const lds_t* p) { return *reinterpret_cast<const bfx8 __attribute__((address_space(3)))*>(p); }
+
+// first g with tile_end[g] > s
+ST_DEVICE int find_group(const int* __restrict__ tile_end, int G, int s) {
+  int lo = 0, hi = G;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (tile_end[mid] <= s) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+ST_DEVICE void fence() { __builtin_amdgcn_sched_barrier(0); }
+
+// work item of this workgroup.  gm == 0: slot-major (N-tile fastest).  gm > 0: XCD-aware --
+// each XCD walks its own contiguous range of ids, in groups of gm slots x (N-tiles) with the
+// slot fastest, so the ~32 workgroups an XCD runs at once start together on gm X tiles and
+// 32 / gm weight tiles and stream the same 64-k slices through its L2 (slot-major spreads a
+// weight tile's readers over time: each streams its own copy from the Infinity Cache / HBM).
+ST_DEVICE void tile_of(int gm, int nbn, int& slot, int& nt) {
+  if (gm <= 0) {
+    slot = (int)blockIdx.x / nbn;
+    nt = (int)blockIdx.x % nbn;
+    return;
+  }
+  const int nslots = (int)gridDim.x / nbn;
+  const int id = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+  const int per = gm * nbn, grp = id / per, in = id % per;
+  const int gsz = min(gm, nslots - grp * gm);
+  slot = grp * gm + in % gsz;
+  nt = in / gsz;
+}
+
+// PROBE (timing probes, wrong results): 1 = no fragment reads in the loop, 2 = no staging
+// (loads + LDS writes) in the loop, 3 = no barrier in the loop, 4 = MFMAs only, 5 = no LDS
+// writes (loads kept), 6 = no loads (LDS writes of stale registers kept)
+template <int EPI, int PROBE = 0, int PD = 1>
+__global__ __launch_bounds__(NT, 1) void gemm4w_kernel(const bf16_t* __restrict__ X, int64_t ldx,
+                                                       const bf16_t* __restrict__ W, int64_t ldw, int64_t strideW,
+                                                       bf16_t* __restrict__ Y, int64_t ldy,
+                                                       const int* __restrict__ offs, const int* __restrict__ tile_end,
+                                                       int G, int N, int K, int gm) {
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
+  lds_t* smem = (lds_t*)smem_raw;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wid >> 1, wn = wid & 1;  // 2 x 2 waves of 128 x 128
+  const int nbn = N / BN;
+  int slot, nt;
+  tile_of(gm, nbn, slot, nt);
+  const int total_slots = tile_end[G - 1];
+  if (slot >= total_slots) return;  // uniform over the workgroup: no barrier reached yet
+  const int g = find_group(tile_end, G, slot);
+  const int first_slot = g ? tile_end[g - 1] : 0;
+  const int row0 = (g ? offs[g - 1] : 0) + (slot - first_slot) * BM;
+  const int rows = min(BM, offs[g] - row0);
+  const int n0 = nt * BN;
+
+  // descriptors: X rows past the group's end read as zeros; W rows n0 .. n0 + 255 of W[g]
+  const rsrc_t rsX = make_rsrc(X + (int64_t)row0 * ldx, (uint32_t)(((int64_t)(rows - 1) * ldx + K) * 2));
+  const rsrc_t rsW = make_rsrc(W + (int64_t)g * strideW + (int64_t)n0 * ldw, (uint32_t)(((int64_t)(BN - 1) * ldw + K) * 2));
+
+  // global -> VGPR staging: thread t loads 16-B chunk (t & 7) of rows (t >> 3) + 32 i, i < 8,
+  // for A and for B; its LDS destination is that row's swizzled chunk
+  const int gr = t >> 3, gc = t & 7;
+  const uint32_t ga = (uint32_t)gr * (uint32_t)(ldx * 2) + (uint32_t)gc * 16;
+  const uint32_t gb = (uint32_t)gr * (uint32_t)(ldw * 2) + (uint32_t)gc * 16;
+  const uint32_t sxa = (uint32_t)(32 * ldx * 2), sxb = (uint32_t)(32 * ldw * 2);
+  const int wlds = gr * 128 + ((gc ^ rsw(gr)) * 16);  // + 32 rows * 128 B per i (same swizzle)
+  // staging registers roll: right after row i of the staged tile kt+1 is written to LDS, the
+  // same registers receive row i of tile kt+2, which is written one K-tile (64 MFMAs, ~1,000
+  // cycles) later.  (Loading tile kt+2 only after ALL of tile kt+1 was written left ~50 MFMAs
+  // for the loads and every LDS write waited on them: 1.13 vs 1.55 PF/s in the probes.)
+  // PD register sets: K-tile t is staged in set t % PD, loaded PD K-tiles before it is written
+  // (indices clamped to the last tile: the final steps re-load it into dead registers)
+  const int KT = K / BK;
+  u32x4 sa[PD][8], sb[PD][8];
+  auto load_a = [&](int p, int kt, int i) { sa[p][i] = gload(rsX, ga + i * sxa + (uint32_t)(min(kt, KT - 1) * BK * 2)); };
+  auto load_b = [&](int p, int kt, int i) { sb[p][i] = gload(rsW, gb + i * sxb + (uint32_t)(min(kt, KT - 1) * BK * 2)); };
+  auto write_a = [&](int p, lds_t* st, int i) { lds_w128(st + wlds + i * 32 * 128, sa[p][i]); };
+  auto write_b = [&](int p, lds_t* st, int i) { lds_w128(st + IMG + wlds + i * 32 * 128, sb[p][i]); };
+
+  // fragment reads: A rows wm*128 + 16 f + (lane & 15), B rows wn*128 + 16 f + (lane & 15);
+  // lane group q = lane >> 4 holds k 8q .. 8q+7 of sub-step ks (chunk 4 ks + q)
+  const int q = lane >> 4, rl = lane & 15;
+  int foff[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) foff[ks] = rl * 128 + (((4 * ks + q) ^ rsw(rl)) * 16);
+  const int abase = wm * 128 * 128, bbase = IMG + wn * 128 * 128;
+  // A fragments roll (row i's register is refilled for the next sub-step as soon as row i's 8
+  // MFMAs are issued), B fragments are double-buffered: 96 fragment VGPRs instead of 128
+  bfx8 fa[8], fb[2][8];
+  auto read_a = [&](const lds_t* st, int ks, int f) { fa[f] = lds_r128(st + abase + f * 16 * 128 + foff[ks]); };
+  auto read_b = [&](const lds_t* st, int set, int ks, int f) { fb[set][f] = lds_r128(st + bbase + f * 16 * 128 + foff[ks]); };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the 256 accumulators are pinned to the AGPR file by inline-asm MFMAs (a builtin MFMA left
+  // hipcc free to re-home them per unrolled copy: ~400 v_accvgpr moves per K-tile, 40 % MFMA busy)
+  auto mfma = [&](int set, int idx) {
+    const int i = idx >> 3, j = idx & 7;
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fa[i]), "v"(fb[set][j]));
+  };
+
+  // prologue: tile 0 staged and written, tiles 1 .. PD in flight, sub-step 0 of tile 0 read
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    load_a(0, 0, i);
+    load_b(0, 0, i);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    write_a(0, smem, i);
+    write_b(0, smem, i);
+  }
+#pragma unroll
+  for (int tt = 1; tt <= PD; ++tt)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      load_a(tt % PD, tt, i);
+      load_b(tt % PD, tt, i);
+    }
+  __syncthreads();
+#pragma unroll
+  for (int f = 0; f < 8; ++f) read_b(smem, 0, 0, f);
+#pragma unroll
+  for (int f = 0; f < 8; ++f) read_a(smem, 0, f);
+
+  auto step = [&](auto p_c, auto more_c, int kt) {
+    constexpr int P = decltype(p_c)::value;  // == (kt + 1) % PD: the set holding tile kt+1
+    constexpr bool more = decltype(more_c)::value;
+    const lds_t* cur = smem + (kt & 1) * STAGE;
+    lds_t* nxt = smem + ((kt + 1) & 1) * STAGE;
+    __builtin_amdgcn_s_setprio(1);
+    // ---- sub-step 0 (k 0..31): MFMAs on fb[0] and the rolling A fragments.  Set 1's B
+    // fragments read one per 4 MFMAs (m = 1, 5, ..); row i's A register refilled with its
+    // k 32..63 fragment right after row i's 8 MFMAs; half of the staged tile kt+1 (A rows)
+    // written to nxt (free since the previous tile's barrier), one write per 8 MFMAs, each
+    // followed by the load of the same row of tile kt+2
+#pragma unroll
+    for (int m = 0; m < 64; ++m) {
+      mfma(0, m);
+      if ((m & 7) == 1) {
+        fence();
+        if (PROBE != 1 && PROBE != 4) read_b(cur, 1, 1, m >> 3);
+        fence();
+      }
+      if ((m & 7) == 7) {
+        fence();
+        if (PROBE != 1 && PROBE != 4) read_a(cur, 1, m >> 3);
+        fence();
+      }
+      if (more && (m & 7) == 4) {
+        fence();
+        if (PROBE != 2 && PROBE != 4 && PROBE != 5) write_a(P, nxt, m >> 3);
+        if (PROBE != 2 && PROBE != 4 && PROBE != 6) load_a(P, kt + 1 + PD, m >> 3);
+        fence();
+      }
+    }
+    // ---- sub-step 1 (k 32..63): MFMAs on fb[1].  The staged B rows written (MFMAs 0-15),
+    // each followed by the load of the same row of tile kt+2 into its register, the barrier
+    // that publishes tile kt+1 (MFMA 24), then its sub-step-0 fragments read: A rows 0-2 at
+    // once, row i >= 3 after its MFMAs, B one per 4 MFMAs
+#pragma unroll
+    for (int m = 0; m < 64; ++m) {
+      mfma(1, m);
+      if (more && m < 16 && (m & 1) == 1) {
+        fence();
+        if (PROBE != 2 && PROBE != 4 && PROBE != 5) write_b(P, nxt, m >> 1);
+        if (PROBE != 2 && PROBE != 4 && PROBE != 6) load_b(P, kt + 1 + PD, m >> 1);
+        fence();
+      }
+      if (more && m == 24) {
+        fence();
+        __builtin_amdgcn_s_setprio(0);
+        if (PROBE != 3 && PROBE != 4) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+        if (PROBE != 1 && PROBE != 4) {
+          read_a(nxt, 0, 0);
+          read_a(nxt, 0, 1);
+          read_a(nxt, 0, 2);
+        }
+        fence();
+      }
+      if (more && m >= 31 && (m & 7) == 7) {
+        fence();
+        if (PROBE != 1 && PROBE != 4) read_a(nxt, 0, m >> 3);
+        fence();
+      }
+      if (more && m >= 26 && m <= 54 && (m & 3) == 2) {
+        fence();
+        if (PROBE != 1 && PROBE != 4) read_b(nxt, 0, 0, (m - 26) >> 2);
+        fence();
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  using T1 = std::true_type;
+  using F0 = std::false_type;
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1 % PD>;
+  int kt = 0;
+  if constexpr (PD == 1) {
+    for (; kt + 1 < KT; ++kt) step(S0(), T1(), kt);
+    step(S0(), F0(), kt);
+  } else {
+    for (; kt + 2 < KT; kt += 2) {
+      step(S1(), T1(), kt);
+      step(S0(), T1(), kt + 1);
+    }
+    if (kt + 1 < KT) {
+      step(S1(), T1(), kt);
+      step(S0(), F0(), kt + 1);
+    } else {
+      step(S1(), F0(), kt);
+    }
+  }
+
+  // the last MFMAs' results must land before VALU reads the AGPRs (>= 12 wait states)
+  asm volatile("s_nop 15\n\ts_nop 3" ::: "memory");
+  // ---- epilogue: acc[i][j] reg r = row wm*128 + 16 i + 4 q + r, column wn*128 + 16 j + rl
+  bf16_t* yb = Y + (int64_t)row0 * ldy + n0 + wn * 128 + rl;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = wm * 128 + 16 * i + 4 * q + r;
+      if (m < rows) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) yb[(int64_t)m * ldy + 16 * j] = f2bf(acc[i][j][r]);
+      }
+    }
+}
+
+// ---- "1 x 4" variant: each wave owns 256 rows x 64 columns.  Only X goes through LDS (written
+// once, read by all four waves); the wave's 64 weight columns are loaded straight from global
+// memory into MFMA B-operand registers (lane (rl, q) of fragment j: row 16 j + rl, 16 bytes at
+// k 8 q of the sub-step -- one buffer_load_dwordx4, no LDS round trip), NS - 1 K-tiles ahead.
+// Per CU and 64-k step: LDS 32 KiB written + 128 KiB read (vs 64 + 128), global 64 KiB (same),
+// 8 ds_write_b128 per wave instead of 16 -- the LDS store transfer was the largest single cost
+// of the 2 x 2 layout (probe 5: 1.27 -> 1.71 PF/s without it).
+// The last steps re-load / re-stage the final K-tile into free buffers (clamped indices) instead
+// of branching inside the MFMA stream.
+template <int NS, int PROBE = 0>
+__global__ __launch_bounds__(NT, 1) void gemm4b_kernel(const bf16_t* __restrict__ X, int64_t ldx,
+                                                       const bf16_t* __restrict__ W, int64_t ldw, int64_t strideW,
+                                                       bf16_t* __restrict__ Y, int64_t ldy,
+                                                       const int* __restrict__ offs, const int* __restrict__ tile_end,
+                                                       int G, int N, int K, int gm) {
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * IMG];
+  lds_t* smem = (lds_t*)smem_raw;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int nbn = N / BN;
+  int slot, nt;
+  tile_of(gm, nbn, slot, nt);
+  const int total_slots = tile_end[G - 1];
+  if (slot >= total_slots) return;  // uniform over the workgroup: no barrier reached yet
+  const int g = find_group(tile_end, G, slot);
+  const int first_slot = g ? tile_end[g - 1] : 0;
+  const int row0 = (g ? offs[g - 1] : 0) + (slot - first_slot) * BM;
+  const int rows = min(BM, offs[g] - row0);
+  const int n0 = nt * BN + wid * 64;  // this wave's columns
+
+  const rsrc_t rsX = make_rsrc(X + (int64_t)row0 * ldx, (uint32_t)(((int64_t)(rows - 1) * ldx + K) * 2));
+  const rsrc_t rsW = make_rsrc(W + (int64_t)g * strideW + (int64_t)n0 * ldw, (uint32_t)((63 * ldw + K) * 2));
+  const int KT = K / BK;
+
+  // X staging (as the 2 x 2 kernel): thread t holds chunk (t & 7) of rows (t >> 3) + 32 i
+  const int gr = t >> 3, gc = t & 7;
+  const uint32_t ga = (uint32_t)gr * (uint32_t)(ldx * 2) + (uint32_t)gc * 16;
+  const uint32_t sxa = (uint32_t)(32 * ldx * 2);
+  const int wlds = gr * 128 + ((gc ^ rsw(gr)) * 16);
+  u32x4 sa[8];
+  auto load_a = [&](int kt, int i) { sa[i] = gload(rsX, ga + i * sxa + (uint32_t)(min(kt, KT - 1) * BK * 2)); };
+  auto write_a = [&](lds_t* st, int i) { lds_w128(st + wlds + i * 32 * 128, sa[i]); };
+
+  const int q = lane >> 4, rl = lane & 15;
+  // weight fragments straight from memory: slot s holds K-tile kt = s (mod NS)
+  const uint32_t gbw = (uint32_t)rl * (uint32_t)(ldw * 2) + (uint32_t)q * 16;
+  const uint32_t sbj = (uint32_t)(16 * ldw * 2);
+  bfx8 fb[NS][2][4];
+  auto load_b = [&](int s, int kt, int ks, int j) {
+    fb[s][ks][j] = __builtin_bit_cast(bfx8, gload(rsW, gbw + j * sbj + (uint32_t)(min(kt, KT - 1) * BK * 2 + ks * 64)));
+  };
+
+  int foff[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) foff[ks] = rl * 128 + (((4 * ks + q) ^ rsw(rl)) * 16);
+  bfx8 fa[16];
+  auto read_a = [&](const lds_t* st, int ks, int i) { fa[i] = lds_r128(st + i * 16 * 128 + foff[ks]); };
+
+  f32x4 acc[16][4];
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mfma = [&](int s, int ks, int m) {
+    const int i = m >> 2, j = m & 3;
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fa[i]), "v"(fb[s][ks][j]));
+  };
+
+  // prologue: weight tiles 0 .. NS-2 in flight, X tile 0 staged + written, X tile 1 in flight
+#pragma unroll
+  for (int i = 0; i < 8; ++i) load_a(0, i);
+#pragma unroll
+  for (int s = 0; s + 1 < NS; ++s)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) load_b(s, s, e >> 2, e & 3);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) write_a(smem, i);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) load_a(1, i);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) read_a(smem, 0, i);
+
+  auto step = [&](auto s_c, int kt) {
+    constexpr int S = decltype(s_c)::value, SL = (S + NS - 1) % NS;
+    const lds_t* cur = smem + (kt & 1) * IMG;
+    lds_t* nxt = smem + ((kt + 1) & 1) * IMG;
+    __builtin_amdgcn_s_setprio(1);
+    // sub-step 0 (k 0..31): row i's register refilled with its k 32..63 fragment after its 4
+    // MFMAs; X tile kt+1 written (one row-piece per 8 MFMAs, each followed by the load of the
+    // same piece of tile kt+2); weight tile kt+NS-1 loaded into the slot tile kt-1 freed
+#pragma unroll
+    for (int m = 0; m < 64; ++m) {
+      mfma(S, 0, m);
+      if ((m & 3) == 3) {
+        fence();
+        if (PROBE != 1 && PROBE != 4) read_a(cur, 1, m >> 2);
+        fence();
+      }
+      if ((m & 7) == 5) {
+        fence();
+        if (PROBE != 2 && PROBE != 4 && PROBE != 5) write_a(nxt, m >> 3);
+        if (PROBE != 2 && PROBE != 4 && PROBE != 6) load_a(kt + 2, m >> 3);
+        fence();
+      }
+      if ((m & 7) == 1) {
+        fence();
+        if (PROBE != 2 && PROBE != 4 && PROBE != 6) load_b(SL, kt + NS - 1, (m >> 3) & 1, m >> 4);
+        fence();
+      }
+    }
+    // sub-step 1 (k 32..63): the barrier that publishes X tile kt+1 after row 3's MFMAs, then
+    // its k 0..31 fragments: rows 0-3 at once, row i >= 4 after its MFMAs
+#pragma unroll
+    for (int m = 0; m < 64; ++m) {
+      mfma(S, 1, m);
+      if (m == 15) {
+        fence();
+        __builtin_amdgcn_s_setprio(0);
+        if (PROBE != 3 && PROBE != 4) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+        if (PROBE != 1 && PROBE != 4) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) read_a(nxt, 0, i);
+        }
+        fence();
+      }
+      if (m >= 19 && (m & 3) == 3) {
+        fence();
+        if (PROBE != 1 && PROBE != 4) read_a(nxt, 0, m >> 2);
+        fence();
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  int kt = 0;
+  for (; kt + NS <= KT; kt += NS) {
+    step(std::integral_constant<int, 0>(), kt);
+    step(std::integral_constant<int, 1>(), kt + 1);
+    if constexpr (NS == 3) step(std::integral_constant<int, 2>(), kt + 2);
+  }
+  if (kt < KT) step(std::integral_constant<int, 0>(), kt);
+  if constexpr (NS == 3)
+    if (kt + 1 < KT) step(std::integral_constant<int, 1>(), kt + 1);
+
+  asm volatile("s_nop 15\n\ts_nop 3" ::: "memory");
+  // epilogue: acc[i][j] reg r = row 16 i + 4 q + r, column 16 j + rl of the wave's 64
+  bf16_t* yb = Y + (int64_t)row0 * ldy + n0 + rl;
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = 16 * i + 4 * q + r;
+      if (m < rows) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) yb[(int64_t)m * ldy + 16 * j] = f2bf(acc[i][j][r]);
+      }
+    }
+}
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved: nothing else in this kernel uses it
+// one 1-KiB LDS-DMA piece: lane L's 16 bytes land at lds_base + 16 L
+ST_DEVICE void dma16(rsrc_t rs, uint32_t lds_base, uint32_t voff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(lds_base), "v"(voff), "s"(rs)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// ---- "2 x 2, LDS-DMA" variant: the 2 x 2 kernel's per-wave tile and fragment schedule, with
+// both operands copied global -> LDS by buffer_load ... lds (no staging VGPRs, no ds_write:
+// per CU and K-tile 64 LDS instructions fewer -- 32 ds_read_b128 per wave remain).  The
+// source address carries the swizzle (lane L of piece q writes row 8 q + L / 8, physical
+// chunk L % 8, so it reads logical chunk (L % 8) ^ rsw(row)).  Two LDS stages: tile kt+1's 16
+// pieces per wave go out half right after the barrier of tile kt-1 (the buffer's last readers
+// are past it), half during sub-step 0 of tile kt; its barrier waits for them (vmcnt(0)).
+template <int EPI, int PROBE = 0>
+__global__ __launch_bounds__(NT, 1) void gemm4d_kernel(const bf16_t* __restrict__ X, int64_t ldx,
+                                                       const bf16_t* __restrict__ W, int64_t ldw, int64_t strideW,
+                                                       bf16_t* __restrict__ Y, int64_t ldy,
+                                                       const int* __restrict__ offs, const int* __restrict__ tile_end,
+                                                       int G, int N, int K, int gm) {
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
+  lds_t* smem = (lds_t*)smem_raw;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int nbn = N / BN;
+  int slot, nt;
+  tile_of(gm, nbn, slot, nt);
+  const int total_slots = tile_end[G - 1];
+  if (slot >= total_slots) return;  // uniform over the workgroup: no barrier reached yet
+  const int g = find_group(tile_end, G, slot);
+  const int first_slot = g ? tile_end[g - 1] : 0;
+  const int row0 = (g ? offs[g - 1] : 0) + (slot - first_slot) * BM;
+  const int rows = min(BM, offs[g] - row0);
+  const int n0 = nt * BN;
+  const rsrc_t rsX = make_rsrc(X + (int64_t)row0 * ldx, (uint32_t)(((int64_t)(rows - 1) * ldx + K) * 2));
+  const rsrc_t rsW = make_rsrc(W + (int64_t)g * strideW + (int64_t)n0 * ldw, (uint32_t)(((int64_t)(BN - 1) * ldw + K) * 2));
+  const int KT = K / BK;
+
+  // wave w copies pieces w*8 .. w*8+7 of each image (piece q = image rows 8q .. 8q+7)
+  uint32_t voa[8], vob[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int pr = (wid * 8 + i) * 8 + (lane >> 3), pc = lane & 7;
+    voa[i] = (uint32_t)pr * (uint32_t)(ldx * 2) + (uint32_t)((pc ^ rsw(pr)) * 16);
+    vob[i] = (uint32_t)pr * (uint32_t)(ldw * 2) + (uint32_t)((pc ^ rsw(pr)) * 16);
+  }
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem + (uint32_t)(wid * 8 * 1024));
+  auto dma_a = [&](int buf, int kt, int i) {
+    if (PROBE != 2 && PROBE != 4) dma16(rsX, lbase + buf * STAGE + i * 1024, voa[i] + (uint32_t)(kt * BK * 2));
+  };
+  auto dma_b = [&](int buf, int kt, int i) {
+    if (PROBE != 2 && PROBE != 4) dma16(rsW, lbase + buf * STAGE + IMG + i * 1024, vob[i] + (uint32_t)(kt * BK * 2));
+  };
+
+  const int q = lane >> 4, rl = lane & 15;
+  int foff[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) foff[ks] = rl * 128 + (((4 * ks + q) ^ rsw(rl)) * 16);
+  const int abase = wm * 128 * 128, bbase = IMG + wn * 128 * 128;
+  bfx8 fa[8], fb[2][8];
+  auto read_a = [&](const lds_t* st, int ks, int f) { fa[f] = lds_r128(st + abase + f * 16 * 128 + foff[ks]); };
+  auto read_b = [&](const lds_t* st, int set, int ks, int f) { fb[set][f] = lds_r128(st + bbase + f * 16 * 128 + foff[ks]); };
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mfma = [&](int set, int idx) {
+    const int i = idx >> 3, j = idx & 7;
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fa[i]), "v"(fb[set][j]));
+  };
+
+  // prologue: tile 0 copied and published; the X half of tile 1 in flight
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    dma_a(0, 0, i);
+    dma_b(0, 0, i);
+  }
+  if (KT > 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dma_a(1, 1, i);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+#pragma unroll
+  for (int f = 0; f < 8; ++f) read_b(smem, 0, 0, f);
+#pragma unroll
+  for (int f = 0; f < 8; ++f) read_a(smem, 0, f);
+
+  auto step = [&](auto more_c, auto more2_c, int kt) {
+    constexpr bool more = decltype(more_c)::value, more2 = decltype(more2_c)::value;
+    const lds_t* cur = smem + (kt & 1) * STAGE;
+    const lds_t* nxt = smem + ((kt + 1) & 1) * STAGE;
+    __builtin_amdgcn_s_setprio(1);
+    // sub-step 0: set 1's B fragments and row i's k 32..63 A fragment read as in the 2 x 2
+    // kernel; the weight half of tile kt+1 copied (one piece per 8 MFMAs)
+#pragma unroll
+    for (int m = 0; m < 64; ++m) {
+      mfma(0, m);
+      if ((m & 7) == 1) {
+        fence();
+        if (PROBE != 1 && PROBE != 4) read_b(cur, 1, 1, m >> 3);
+        fence();
+      }
+      if ((m & 7) == 7) {
+        fence();
+        if (PROBE != 1 && PROBE != 4) read_a(cur, 1, m >> 3);
+        fence();
+      }
+      if (more && (m & 7) == 4) {
+        fence();
+        dma_b((kt + 1) & 1, kt + 1, m >> 3);
+        fence();
+      }
+    }
+    // sub-step 1: barrier publishing tile kt+1 after MFMA 24 (own pieces landed, own reads of
+    // cur done), its first fragments read, and the X half of tile kt+2 copied into cur
+#pragma unroll
+    for (int m = 0; m < 64; ++m) {
+      mfma(1, m);
+      if (more && m == 24) {
+        fence();
+        __builtin_amdgcn_s_setprio(0);
+        if (PROBE != 3 && PROBE != 4) {
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+        if (PROBE != 1 && PROBE != 4) {
+          read_a(nxt, 0, 0);
+          read_a(nxt, 0, 1);
+          read_a(nxt, 0, 2);
+        }
+        fence();
+      }
+      if (more && m >= 31 && (m & 7) == 7) {
+        fence();
+        if (PROBE != 1 && PROBE != 4) read_a(nxt, 0, m >> 3);
+        fence();
+      }
+      if (more && m >= 26 && m <= 54 && (m & 3) == 2) {
+        fence();
+        if (PROBE != 1 && PROBE != 4) read_b(nxt, 0, 0, (m - 26) >> 2);
+        fence();
+      }
+      if (more2 && m >= 28 && m <= 63 && (m & 3) == 0 && m != 60) {
+        fence();
+        dma_a(kt & 1, kt + 2, (m - 28) >> 2);
+        fence();
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  using T1 = std::true_type;
+  using F0 = std::false_type;
+  int kt = 0;
+  for (; kt + 2 < KT; ++kt) step(T1(), T1(), kt);
+  if (kt + 1 < KT) step(T1(), F0(), kt++);
+  step(F0(), F0(), kt);
+
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 3" ::: "memory");
+  bf16_t* yb = Y + (int64_t)row0 * ldy + n0 + wn * 128 + rl;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = wm * 128 + 16 * i + 4 * q + r;
+      if (m < rows) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) yb[(int64_t)m * ldy + 16 * j] = f2bf(acc[i][j][r]);
+      }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+// M-tile slots for T rows in G groups (upper bound of sum_g ceil(n_g / 256)).
+int64_t st_gemm4w_slots(int T, int G) { return (int64_t)(T + BM - 1) / BM + G; }
+
+// Y[rows of g] = X[rows of g] @ W[g]^T; W[g] [N][K]; offs / tile_end int32 [G] device
+// (tile_end = inclusive prefix of ceil(n_g / 256)).  0 on success, -2 unsupported shape.
+int st_gemm4w(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t strideW, void* Y, int64_t ldy,
+              const int* offs, const int* tile_end, int T, int G, int N, int K, hipStream_t st) {
+  if (T <= 0 || G <= 0 || N <= 0 || K <= 0) return -2;
+  if (K % BK || N % BN) return -2;
+  if (ldx % 8 || ldw % 8 || ldy % 8 || ldx < K || ldw < K || ldy < N) return -2;
+  if (((uintptr_t)X | (uintptr_t)W | (uintptr_t)Y) % 16) return -2;
+  if (((int64_t)(BM + 32) * ldx) * 2 >= (int64_t)1 << 32) return -2;  // 32-bit buffer offsets per tile
+  if (((int64_t)BN * ldw) * 2 >= (int64_t)1 << 32) return -2;
+  const int64_t grid = st_gemm4w_slots(T, G) * (N / BN);
+  if (grid >= (1LL << 31)) return -2;
+  const char* pe = std::getenv("ST_GEMM4W_PROBE");  // timing probes (wrong results)
+  const int probe = pe ? std::atoi(pe) : 0;
+  const char* ke = std::getenv("ST_GEMM4W_KIND");  // 0: 2 x 2 waves, 1 / 2: 1 x 4, NS = 2 / 3
+  const int kind = ke ? std::atoi(ke) : 1;
+  const char* oe = std::getenv("ST_GEMM4W_ORDER");  // slots per XCD group (0: slot-major)
+  const int gm = oe ? std::atoi(oe) : 4;
+#define G4ARGS (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, strideW, (bf16_t*)Y, ldy, offs, tile_end, G, N, K, gm
+#define G4LAUNCH(KERN, ...)                                                            \
+  do {                                                                                 \
+    if (probe == 1) KERN, 1 __VA_ARGS__><<<(unsigned)grid, NT, 0, st>>>(G4ARGS);       \
+    else if (probe == 2) KERN, 2 __VA_ARGS__><<<(unsigned)grid, NT, 0, st>>>(G4ARGS);  \
+    else if (probe == 3) KERN, 3 __VA_ARGS__><<<(unsigned)grid, NT, 0, st>>>(G4ARGS);  \
+    else if (probe == 4) KERN, 4 __VA_ARGS__><<<(unsigned)grid, NT, 0, st>>>(G4ARGS);  \
+    else if (probe == 5) KERN, 5 __VA_ARGS__><<<(unsigned)grid, NT, 0, st>>>(G4ARGS);  \
+    else if (probe == 6) KERN, 6 __VA_ARGS__><<<(unsigned)grid, NT, 0, st>>>(G4ARGS);  \
+    else KERN, 0 __VA_ARGS__><<<(unsigned)grid, NT, 0, st>>>(G4ARGS);                  \
+  } while (0)
+  if (kind == 0) G4LAUNCH(gemm4w_kernel<0);
+  else if (kind == 3) G4LAUNCH(gemm4w_kernel<0, , 2);
+  else if (kind == 4) G4LAUNCH(gemm4d_kernel<0);
+  else if (kind == 2) G4LAUNCH(gemm4b_kernel<3);
+  else G4LAUNCH(gemm4b_kernel<2);
+#undef G4LAUNCH
+#undef G4ARGS
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"
