@@ -19,6 +19,13 @@
 //   * 256 fp32 accumulators per lane (16x16x32 MFMA: 8 x 8 fragments), 512 registers / lane.
 // LDS images: [256 rows][64 k] bf16, 16-byte chunk c of row r at c ^ ((r >> 1) & 7): the
 // ds_read_b128 fragment reads and the ds_write_b128 fills are bank-conflict free.
+//
+// STATUS: measured experiment, not on the model path (docs/PERF.md "one wave per SIMD GEMM").
+// On the dense gate|up / down / qkv shapes all variants run 1.16-1.37 PF/s; hipBLASLt's
+// MT256x256x64 kernel (the same 4-wave 128 x 128-per-wave structure) runs 1.35-1.58 on the same
+// box, and the 8-phase grouped kernel equals variant 0.  PMC (profiles/r05/gemm4w/pmc.md): 0 LDS
+// bank conflicts, L2 hit 64 % (78 % XCD-grouped, hipBLASLt 79 %) at the same ~250-cycle mean
+// L2 latency; hipBLASLt issues 32 LDS instructions per wave and K-tile (DMA fills) vs 48 here.
 #include <cstdlib>
 #include <type_traits>
 
@@ -84,7 +91,7 @@ ST_DEVICE void tile_of(int gm, int nbn, int& slot, int& nt) {
 // PROBE (timing probes, wrong results): 1 = no fragment reads in the loop, 2 = no staging
 // (loads + LDS writes) in the loop, 3 = no barrier in the loop, 4 = MFMAs only, 5 = no LDS
 // writes (loads kept), 6 = no loads (LDS writes of stale registers kept)
-template <int EPI, int PROBE = 0, int PD = 1>
+template <int EPI, int PROBE = 0>
 __global__ __launch_bounds__(NT, 1) void gemm4w_kernel(const bf16_t* __restrict__ X, int64_t ldx,
                                                        const bf16_t* __restrict__ W, int64_t ldw, int64_t strideW,
                                                        bf16_t* __restrict__ Y, int64_t ldy,
@@ -121,14 +128,13 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_kernel(const bf16_t* __restrict_
   // same registers receive row i of tile kt+2, which is written one K-tile (64 MFMAs, ~1,000
   // cycles) later.  (Loading tile kt+2 only after ALL of tile kt+1 was written left ~50 MFMAs
   // for the loads and every LDS write waited on them: 1.13 vs 1.55 PF/s in the probes.)
-  // PD register sets: K-tile t is staged in set t % PD, loaded PD K-tiles before it is written
-  // (indices clamped to the last tile: the final steps re-load it into dead registers)
+  // (a second register set, loading two K-tiles ahead, needs ~250 VGPRs and spilled)
   const int KT = K / BK;
-  u32x4 sa[PD][8], sb[PD][8];
-  auto load_a = [&](int p, int kt, int i) { sa[p][i] = gload(rsX, ga + i * sxa + (uint32_t)(min(kt, KT - 1) * BK * 2)); };
-  auto load_b = [&](int p, int kt, int i) { sb[p][i] = gload(rsW, gb + i * sxb + (uint32_t)(min(kt, KT - 1) * BK * 2)); };
-  auto write_a = [&](int p, lds_t* st, int i) { lds_w128(st + wlds + i * 32 * 128, sa[p][i]); };
-  auto write_b = [&](int p, lds_t* st, int i) { lds_w128(st + IMG + wlds + i * 32 * 128, sb[p][i]); };
+  u32x4 sa[8], sb[8];
+  auto load_a = [&](int kt, int i) { sa[i] = gload(rsX, ga + i * sxa + (uint32_t)(kt * BK * 2)); };
+  auto load_b = [&](int kt, int i) { sb[i] = gload(rsW, gb + i * sxb + (uint32_t)(kt * BK * 2)); };
+  auto write_a = [&](lds_t* st, int i) { lds_w128(st + wlds + i * 32 * 128, sa[i]); };
+  auto write_b = [&](lds_t* st, int i) { lds_w128(st + IMG + wlds + i * 32 * 128, sb[i]); };
 
   // fragment reads: A rows wm*128 + 16 f + (lane & 15), B rows wn*128 + 16 f + (lane & 15);
   // lane group q = lane >> 4 holds k 8q .. 8q+7 of sub-step ks (chunk 4 ks + q)
@@ -155,33 +161,32 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_kernel(const bf16_t* __restrict_
     asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fa[i]), "v"(fb[set][j]));
   };
 
-  // prologue: tile 0 staged and written, tiles 1 .. PD in flight, sub-step 0 of tile 0 read
+  // prologue: tile 0 staged and written, tile 1 in flight, sub-step 0 of tile 0 read
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    load_a(0, 0, i);
-    load_b(0, 0, i);
+    load_a(0, i);
+    load_b(0, i);
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    write_a(0, smem, i);
-    write_b(0, smem, i);
+    write_a(smem, i);
+    write_b(smem, i);
   }
-#pragma unroll
-  for (int tt = 1; tt <= PD; ++tt)
+  if (KT > 1) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      load_a(tt % PD, tt, i);
-      load_b(tt % PD, tt, i);
+      load_a(1, i);
+      load_b(1, i);
     }
+  }
   __syncthreads();
 #pragma unroll
   for (int f = 0; f < 8; ++f) read_b(smem, 0, 0, f);
 #pragma unroll
   for (int f = 0; f < 8; ++f) read_a(smem, 0, f);
 
-  auto step = [&](auto p_c, auto more_c, int kt) {
-    constexpr int P = decltype(p_c)::value;  // == (kt + 1) % PD: the set holding tile kt+1
-    constexpr bool more = decltype(more_c)::value;
+  auto step = [&](auto more_c, auto more2_c, int kt) {
+    constexpr bool more = decltype(more_c)::value, more2 = decltype(more2_c)::value;
     const lds_t* cur = smem + (kt & 1) * STAGE;
     lds_t* nxt = smem + ((kt + 1) & 1) * STAGE;
     __builtin_amdgcn_s_setprio(1);
@@ -205,8 +210,8 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_kernel(const bf16_t* __restrict_
       }
       if (more && (m & 7) == 4) {
         fence();
-        if (PROBE != 2 && PROBE != 4 && PROBE != 5) write_a(P, nxt, m >> 3);
-        if (PROBE != 2 && PROBE != 4 && PROBE != 6) load_a(P, kt + 1 + PD, m >> 3);
+        if (PROBE != 2 && PROBE != 4 && PROBE != 5) write_a(nxt, m >> 3);
+        if (more2 && PROBE != 2 && PROBE != 4 && PROBE != 6) load_a(kt + 2, m >> 3);
         fence();
       }
     }
@@ -219,8 +224,8 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_kernel(const bf16_t* __restrict_
       mfma(1, m);
       if (more && m < 16 && (m & 1) == 1) {
         fence();
-        if (PROBE != 2 && PROBE != 4 && PROBE != 5) write_b(P, nxt, m >> 1);
-        if (PROBE != 2 && PROBE != 4 && PROBE != 6) load_b(P, kt + 1 + PD, m >> 1);
+        if (PROBE != 2 && PROBE != 4 && PROBE != 5) write_b(nxt, m >> 1);
+        if (more2 && PROBE != 2 && PROBE != 4 && PROBE != 6) load_b(kt + 2, m >> 1);
         fence();
       }
       if (more && m == 24) {
@@ -254,24 +259,10 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_kernel(const bf16_t* __restrict_
   };
   using T1 = std::true_type;
   using F0 = std::false_type;
-  using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, 1 % PD>;
   int kt = 0;
-  if constexpr (PD == 1) {
-    for (; kt + 1 < KT; ++kt) step(S0(), T1(), kt);
-    step(S0(), F0(), kt);
-  } else {
-    for (; kt + 2 < KT; kt += 2) {
-      step(S1(), T1(), kt);
-      step(S0(), T1(), kt + 1);
-    }
-    if (kt + 1 < KT) {
-      step(S1(), T1(), kt);
-      step(S0(), F0(), kt + 1);
-    } else {
-      step(S1(), F0(), kt);
-    }
-  }
+  for (; kt + 2 < KT; ++kt) step(T1(), T1(), kt);
+  if (kt + 1 < KT) step(T1(), F0(), kt++);
+  step(F0(), F0(), kt);
 
   // the last MFMAs' results must land before VALU reads the AGPRs (>= 12 wait states)
   asm volatile("s_nop 15\n\ts_nop 3" ::: "memory");
@@ -656,10 +647,10 @@ int st_gemm4w(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t st
   if (grid >= (1LL << 31)) return -2;
   const char* pe = std::getenv("ST_GEMM4W_PROBE");  // timing probes (wrong results)
   const int probe = pe ? std::atoi(pe) : 0;
-  const char* ke = std::getenv("ST_GEMM4W_KIND");  // 0: 2 x 2 waves, 1 / 2: 1 x 4, NS = 2 / 3
-  const int kind = ke ? std::atoi(ke) : 1;
+  const char* ke = std::getenv("ST_GEMM4W_KIND");  // 0: 2 x 2 waves, 1 / 2: 1 x 4 (NS 2 / 3), 4: 2 x 2 LDS-DMA
+  const int kind = ke ? std::atoi(ke) : 0;
   const char* oe = std::getenv("ST_GEMM4W_ORDER");  // slots per XCD group (0: slot-major)
-  const int gm = oe ? std::atoi(oe) : 4;
+  const int gm = oe ? std::atoi(oe) : 0;
 #define G4ARGS (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, strideW, (bf16_t*)Y, ldy, offs, tile_end, G, N, K, gm
 #define G4LAUNCH(KERN, ...)                                                            \
   do {                                                                                 \
@@ -672,7 +663,6 @@ int st_gemm4w(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t st
     else KERN, 0 __VA_ARGS__><<<(unsigned)grid, NT, 0, st>>>(G4ARGS);                  \
   } while (0)
   if (kind == 0) G4LAUNCH(gemm4w_kernel<0);
-  else if (kind == 3) G4LAUNCH(gemm4w_kernel<0, , 2);
   else if (kind == 4) G4LAUNCH(gemm4d_kernel<0);
   else if (kind == 2) G4LAUNCH(gemm4b_kernel<3);
   else G4LAUNCH(gemm4b_kernel<2);
