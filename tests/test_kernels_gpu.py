@@ -760,6 +760,31 @@ def test_grouped_gemm_matches_per_expert(N, K, wn):
         off += n
 
 
+@pytest.mark.parametrize("kind", ["0", "1", "2", "4"])
+def test_gemm4w_variants_match_fp32(kind, monkeypatch):
+    """The one-wave-per-SIMD GEMM experiment (csrc/gemm4w.hip; docs/PERF.md round 5) in each
+    variant -- 2x2 register-staged, 1x4 direct weight fragments (2- / 3-deep), 2x2 LDS-DMA --
+    vs an fp32 per-group reference: empty / 1-row / partial / multi-tile groups, strided x,
+    K = 192 (three 64-k tiles) and K = 1024."""
+    monkeypatch.setenv("ST_GEMM4W_KIND", kind)
+    torch.manual_seed(11)
+    for K, counts in ((192, [37, 0, 300, 1, 513]), (1024, [256, 700])):
+        c = torch.tensor(counts, device="cuda", dtype=torch.int32)
+        G, T = c.numel(), int(c.sum())
+        offs = torch.cumsum(c, 0, dtype=torch.int32)
+        xb = torch.randn(T, K + 64, device="cuda", dtype=torch.bfloat16)
+        x = xb[:, 32:32 + K]
+        w = torch.randn(G, 512, K, device="cuda", dtype=torch.bfloat16)
+        y = _lib.ops().gemm4w(x, w, offs)
+        torch.cuda.synchronize()
+        off = 0
+        for e, n in enumerate(counts):
+            if n:
+                ref = x[off:off + n].float() @ w[e].float().t()
+                assert rel(y[off:off + n].float(), ref) < 1e-2, (kind, K, e, n)
+            off += n
+
+
 @pytest.mark.parametrize("I,K", [(256, 512), (384, 1024)])
 def test_grouped_gemm_swiglu_epilogues_match_fp32(I, K):
     """Grouped gate|up GEMM with the SwiGLU epilogue (EPI 1) and the down-projection
