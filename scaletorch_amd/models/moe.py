@@ -609,6 +609,30 @@ def _gmm_dswiglu(dy: torch.Tensor, w_dn: torch.Tensor, offs: torch.Tensor, gu: t
     return _lib.ops().swiglu_bwd(da.contiguous(), gu, offs[-1:])
 
 
+def _vendor_expert_gemms() -> str:
+    """``ST_MOE_VENDOR_GEMM``: ``auto`` (default) -- per-expert hipBLASLt GEMMs when the
+    routing counts are already on the host (the RCCL EP exchange reads them) and the rank
+    holds few experts with many rows each, the one-launch HIP grouped kernel otherwise;
+    ``1`` -- always (one host read of the counts per layer when they are not); ``0`` --
+    never.  Measured (``tools/bench_expert_ffn.py``): the grouped kernel wins on the 1-GPU
+    proxies by 16 % (Mixtral, 8 x 1,024 rows) and 4.4x (Qwen3-30B-A3B, 128 x 512 rows)."""
+    return os.environ.get("ST_MOE_VENDOR_GEMM", "auto")
+
+
+def _gemm_per_expert(x: torch.Tensor, w: torch.Tensor, counts: list, wn: bool, rows: int) -> torch.Tensor:
+    """``y[rows of e] = x[rows of e] @ (w[e] if wn else w[e]^T)`` as one library GEMM per
+    non-empty expert (host-known row counts); rows past the last expert are left undefined,
+    as on the grouped kernel."""
+    N = w.shape[2] if wn else w.shape[1]
+    y = x.new_empty(rows, N)
+    s = 0
+    for e, n in enumerate(counts):
+        if n:
+            torch.matmul(x[s:s + n], w[e] if wn else w[e].t(), out=y[s:s + n])
+        s += n
+    return y
+
+
 class _ExpertFFNFn(torch.autograd.Function):
     """Grouped expert SwiGLU FFN: forward and data-gradient GEMMs are one launch each over
     all local experts (``_gmm``, csrc/grouped_gemm.hip), and the weight gradients are
@@ -620,12 +644,25 @@ class _ExpertFFNFn(torch.autograd.Function):
     device offsets, so the backward neither reads the routing counts on the host nor
     loops over experts (the reference does the expert backward as one grouped op too,
     scaletorch/models/npu_patch.py:94-127).  Shapes the kernel does not tile fall back
-    to per-expert GEMMs after one host read of the counts."""
+    to per-expert GEMMs after one host read of the counts.
+
+    ``counts_host`` (a list, when the routing counts are on the host): the forward and
+    data-gradient GEMMs run as one hipBLASLt GEMM per expert instead (``_vendor_expert_gemms``);
+    the SwiGLU passes and the grouped weight-gradient kernel are shared."""
 
     @staticmethod
-    def forward(ctx, x, offs, w_gu, w_dn):
-        gu, a = _gmm_swiglu(x, w_gu, offs)
-        y = _gmm(a, w_dn, offs, wn=False)
+    def forward(ctx, x, offs, w_gu, w_dn, counts_host=None):
+        from ..ops import _lib
+
+        ctx.counts_host = counts_host
+        if counts_host is not None:
+            R = x.shape[0]
+            gu = _gemm_per_expert(x, w_gu, counts_host, False, R)
+            a = _lib.ops().swiglu_fwd(gu, offs[-1:])  # valid rows only
+            y = _gemm_per_expert(a, w_dn, counts_host, False, R)
+        else:
+            gu, a = _gmm_swiglu(x, w_gu, offs)
+            y = _gmm(a, w_dn, offs, wn=False)
         # padded buffers (dropless EP: R_max rows, the real ones counted on the device):
         # keep only gu and recompute a over the valid rows in backward
         ctx.keep_a = os.environ.get("ST_MOE_SAVE_ACT", "auto") == "1" or (
@@ -644,9 +681,15 @@ class _ExpertFFNFn(torch.autograd.Function):
         dy = dy.contiguous()
         if a is None:
             a = _lib.ops().swiglu_fwd(gu, offs[-1:])  # valid rows only
-        dgu = _gmm_dswiglu(dy, w_dn, offs, gu)
-        dx = _gmm(dgu, w_gu, offs, wn=True)
-        counts = None
+        ch = ctx.counts_host
+        if ch is not None:
+            da = _gemm_per_expert(dy, w_dn, ch, True, dy.shape[0])
+            dgu = _lib.ops().swiglu_bwd(da, gu, offs[-1:])
+            dx = _gemm_per_expert(dgu, w_gu, ch, True, dy.shape[0])
+        else:
+            dgu = _gmm_dswiglu(dy, w_dn, offs, gu)
+            dx = _gmm(dgu, w_gu, offs, wn=True)
+        counts = ch
         for w, dout, inp in ((w_dn, dy, a), (w_gu, dgu, x)):
             fresh = take_fresh(w)
             grouped = os.environ.get("ST_MOE_GROUPED_WGRAD", "1") == "1"  # 0: per-expert launches (A/B)
@@ -662,7 +705,7 @@ class _ExpertFFNFn(torch.autograd.Function):
                         w.main_grad[e].zero_()
                     off += n
             _grad_ready(w)
-        return dx, None, None, None
+        return dx, None, None, None, None
 
 
 class MoEExperts(nn.Module):
@@ -701,14 +744,16 @@ class MoEExperts(nn.Module):
             dn.normal_(0.0, self.init_std, generator=keyed_generator(key and key + ".down", dev))
             self.w_down.copy_(dn[e0:e0 + self.num_local].chunk(self.tp, 2)[self.tp_rank])
 
-    def forward(self, x: torch.Tensor, counts=None, offs: torch.Tensor | None = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, counts=None, offs: torch.Tensor | None = None,
+                counts_host: list | None = None) -> torch.Tensor:
         """x: rows grouped by local expert (``counts[e]`` rows each -- list or device
         tensor -- or the inclusive device prefix ``offs``); rows past the last expert's
         (capacity / R_max padding) are not computed: their output is undefined on the
         grouped-GEMM path and zero (still connected) on the per-expert path.
 
         GPU: two grouped GEMMs over all local experts (csrc/grouped_gemm.hip, device
-        offsets): no per-expert launches and no host read of the routing counts.
+        offsets): no per-expert launches and no host read of the routing counts; with
+        ``counts_host`` (or ``ST_MOE_VENDOR_GEMM=1``) one hipBLASLt GEMM per expert instead.
         CPU / fallback: one GEMM pair per expert."""
         if x.is_cuda and _grouped_mm_available() and x.dtype == torch.bfloat16:
             if offs is None:
@@ -721,7 +766,12 @@ class MoEExperts(nn.Module):
             if (torch.is_grad_enabled() and mg_gu is not None and mg_dn is not None
                     and mg_gu.dtype == torch.float32 and mg_dn.dtype == torch.float32 and self.inter % 8 == 0
                     and os.environ.get("ST_MOE_FP32_WGRAD", "1") == "1"):
-                return _ExpertFFNFn.apply(x.contiguous(), offs, self.w_gate_up, self.w_down)
+                mode = _vendor_expert_gemms()
+                if mode == "0":
+                    counts_host = None
+                elif mode == "1" and counts_host is None:
+                    counts_host = torch.diff(offs, prepend=offs.new_zeros(1)).tolist()  # one host read
+                return _ExpertFFNFn.apply(x.contiguous(), offs, self.w_gate_up, self.w_down, counts_host)
             gu = torch._grouped_mm(x.contiguous(), self.w_gate_up.transpose(-2, -1), offs=offs)
             return torch._grouped_mm(ops.swiglu(gu), self.w_down.transpose(-2, -1), offs=offs)
         if counts is None:
@@ -836,7 +886,14 @@ class MoELayer(nn.Module):
         offs = torch.cumsum(mine.sum(0), 0, dtype=torch.int32)  # grouped-GEMM offsets (device)
         xe = _EPExchange.apply(xs, M, El, 0, R_max, (R_max, Tk_max), group, comm, Mh)
         xe._st_padded = True  # R_max rows, the first offs[-1] real: the FFN recomputes a over those
-        ye = self.experts(xe, offs=offs)
+        # the RCCL exchange already holds the counts on the host: per-expert library GEMMs where
+        # they beat the grouped kernel -- few local experts with many rows each (Mixtral EP 8:
+        # one expert x 8,192 rows, 6.9 vs 7.4 ms fwd+bwd; at 16 x 4,096 or 8 x 1,024 rows the
+        # grouped kernel wins, tools/bench_expert_ffn.py, profiles/r05/expert_ffn_ab.log)
+        ch = Mh[:, self.ep_rank * El:(self.ep_rank + 1) * El].sum(0).tolist() if Mh is not None else None
+        if ch is not None and _vendor_expert_gemms() == "auto" and not (El <= 4 and sum(ch) >= 4096 * El):
+            ch = None
+        ye = self.experts(xe, offs=offs, counts_host=ch)
         self.dropped_rows = xs.new_zeros((), dtype=torch.int64)  # dropless by construction
         self.ep_rows_sent = Tk - mine[self.ep_rank].sum()  # rows that left this rank (device)
         return _EPExchange.apply(ye, M, El, 1, Tk, (R_max, Tk_max), group, comm, Mh)

@@ -858,6 +858,35 @@ def test_expert_ffn_fused_matches_unfused():
         assert rel(a, b) < 2e-2
 
 
+def test_expert_ffn_vendor_gemms_match_grouped():
+    """_ExpertFFNFn with host-known counts (one hipBLASLt GEMM per expert,
+    ``ST_MOE_VENDOR_GEMM``) equals the one-launch grouped-kernel path on outputs, input
+    gradient and fp32 weight gradients (empty expert, ragged groups, R_max padding rows)."""
+    from scaletorch_amd.models.moe import _ExpertFFNFn
+
+    G, K, I = 4, 512, 384
+    counts = [100, 0, 257, 60]
+    offs = torch.cumsum(torch.tensor(counts, device="cuda", dtype=torch.int32), 0, dtype=torch.int32)
+    T = sum(counts) + 31
+    res = {}
+    for host in (True, False):
+        torch.manual_seed(12)
+        x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+        w_gu = torch.nn.Parameter(torch.randn(G, 2 * I, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5)
+        w_dn = torch.nn.Parameter(torch.randn(G, K, I, device="cuda", dtype=torch.bfloat16) / I ** 0.5)
+        for w in (w_gu, w_dn):
+            w.main_grad = torch.zeros(w.shape, device="cuda")
+            w._st_fresh = True
+        xin = x * 1
+        xin._st_padded = True
+        y = _ExpertFFNFn.apply(xin, offs, w_gu, w_dn, counts if host else None)
+        y.backward(torch.randn(y.shape, device="cuda", generator=torch.Generator("cuda").manual_seed(3)).to(y.dtype))
+        v = sum(counts)
+        res[host] = (y[:v].float(), x.grad[:v].float(), w_gu.main_grad.clone(), w_dn.main_grad.clone())
+    for a, b in zip(res[True], res[False]):
+        assert rel(a, b) < 2e-2
+
+
 @pytest.mark.parametrize("cp,rank", [(4, 1), (8, 3)])
 def test_cp_two_phase_backward_at_zigzag_offsets(cp, rank):
     """The CP all-gather backward's two phases (parallel/context_parallel.py ``_CPAttnFn``):
