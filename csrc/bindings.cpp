@@ -67,6 +67,8 @@ int st_wgrad_grouped(const void* A, int64_t lda, const void* B, int64_t ldb, flo
 int64_t st_grouped_gemm_slots(int T, int G);
 int st_gemm4w(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t strideW, void* Y, int64_t ldy,
               const int* offs, const int* tile_end, int T, int G, int N, int K, hipStream_t st);
+int st_gemm4w_swiglu(const void* X, int64_t ldx, const void* W, int64_t ldw, void* GU, int64_t ldgu, void* H,
+                     int64_t ldh, int T, int I, int K, hipStream_t st);
 int st_grouped_gemm_bm();
 int st_grouped_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t strideW, void* Y, int64_t ldy,
                     const int* offs, const int* tile_end, int T, int G, int N, int K, int wn, hipStream_t st);
@@ -509,6 +511,27 @@ at::Tensor gemm4w(const at::Tensor& x, const at::Tensor& w, const at::Tensor& of
   if (rc == -2) return at::Tensor();
   ST_CHECK_RC(rc, "gemm4w");
   return y;
+}
+
+// Dense gate|up GEMM with the SwiGLU epilogue (csrc/gemm4w.hip, whole-tile-fragment LDS-DMA
+// kernel): x [T, K] (any row stride), w [2I, K] = gate rows then up rows; returns
+// {gu [T, 2I], h [T, I] = silu(gate) * up}, or {} when the kernel does not take the shape.
+std::vector<at::Tensor> gemm_swiglu(const at::Tensor& x, const at::Tensor& w) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "w");
+  check_same_gpu(w, x, "w");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && w.size(1) == x.size(1) && w.size(0) % 2 == 0,
+              "gemm_swiglu: x [T, K], w [2I, K]");
+  const int64_t T = x.size(0), K = x.size(1), I = w.size(0) / 2;
+  if (x.stride(1) != 1 || w.stride(1) != 1 || T == 0 || T > INT32_MAX || I > INT32_MAX / 2 || K > INT32_MAX) return {};
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  at::Tensor gu = at::empty({T, 2 * I}, x.options());
+  at::Tensor h = at::empty({T, I}, x.options());
+  int rc = st_gemm4w_swiglu(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), gu.data_ptr(), gu.stride(0),
+                            h.data_ptr(), h.stride(0), (int)T, (int)I, (int)K, cur_stream());
+  if (rc == -2) return {};
+  ST_CHECK_RC(rc, "gemm_swiglu");
+  return {gu, h};
 }
 
 // Grouped gate|up GEMM with the SwiGLU epilogue: w [G, 2I, K]; returns {gu [T, 2I], a [T, I]}
@@ -1074,6 +1097,7 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("wgrad_grouped_(Tensor(a!) out, Tensor dy, Tensor x, Tensor offs, int beta) -> bool");
   m.def("grouped_gemm(Tensor x, Tensor w, Tensor offs, bool wn) -> Tensor");
   m.def("grouped_gemm_swiglu(Tensor x, Tensor w, Tensor offs) -> Tensor[]");
+  m.def("gemm_swiglu(Tensor x, Tensor w) -> Tensor[]");
   m.def("gemm4w(Tensor x, Tensor w, Tensor offs) -> Tensor");
   m.def("grouped_gemm_dswiglu(Tensor dy, Tensor w, Tensor offs, Tensor gu) -> Tensor");
   m.def("xgmi_create(int rank, int world, int cap, int epoch_base) -> int", &xgmi_create);
@@ -1118,6 +1142,7 @@ TORCH_LIBRARY_IMPL(st_amd, CUDA, m) {
   m.impl("wgrad_grouped_", &wgrad_grouped_);
   m.impl("grouped_gemm", &grouped_gemm);
   m.impl("grouped_gemm_swiglu", &grouped_gemm_swiglu);
+  m.impl("gemm_swiglu", &gemm_swiglu);
   m.impl("gemm4w", &gemm4w);
   m.impl("grouped_gemm_dswiglu", &grouped_gemm_dswiglu);
   m.impl("qknorm_rope_fwd_", &qknorm_rope_fwd_);

@@ -69,6 +69,17 @@ ST_DEVICE int find_group(const int* __restrict__ tile_end, int G, int s) {
 
 ST_DEVICE void fence() { __builtin_amdgcn_sched_barrier(0); }
 
+// compile-time loop: f(std::integral_constant<int, i>) for i in [B, E) -- every index a constant
+// (a 128-iteration `#pragma unroll` body with several slot tables was left partly rolled by
+// hipcc, with the accumulators indexed dynamically through scratch)
+template <int B, int E, typename F>
+ST_DEVICE void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>());
+    static_for<B + 1, E>(f);
+  }
+}
+
 // work item of this workgroup.  gm == 0: slot-major (N-tile fastest).  gm > 0: XCD-aware --
 // each XCD walks its own contiguous range of ids, in groups of gm slots x (N-tiles) with the
 // slot fastest, so the ~32 workgroups an XCD runs at once start together on gm X tiles and
@@ -453,6 +464,14 @@ ST_DEVICE void dma16(rsrc_t rs, uint32_t lds_base, uint32_t voff) {
                : "s"(lds_base), "v"(voff), "s"(rs)
                : "memory", "m0");
 }
+// the same with the K-tile advance in the instruction's scalar offset: the lane offsets stay
+// loop-invariant VGPRs, no VALU address arithmetic ahead of a piece
+ST_DEVICE void dma16s(rsrc_t rs, uint32_t lds_base, uint32_t voff, uint32_t soff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :
+               : "s"(lds_base), "v"(voff), "s"(rs), "s"(soff)
+               : "memory", "m0");
+}
 #pragma clang diagnostic pop
 
 // ---- "2 x 2, LDS-DMA" variant: the 2 x 2 kernel's per-wave tile and fragment schedule, with
@@ -626,6 +645,249 @@ __global__ __launch_bounds__(NT, 1) void gemm4d_kernel(const bf16_t* __restrict_
     }
 }
 
+// ---- "2 x 2, LDS-DMA, whole-tile fragments" variant.  The K-tile's fragments of BOTH 32-k
+// sub-steps live in registers (fa / fb [ks][8]: 128 VGPRs), so a stage of LDS is dead once its
+// sub-step-1 fragments are read -- 40 % into the tile -- instead of at its end:
+//   phase 0 (MFMAs 0-63, sub-step 0 operands): sub-step 1's fragments read (one per 2 MFMAs);
+//   MFMA 44: s_waitcnt vmcnt(0) lgkmcnt(0) + the tile's ONE barrier -- every wave holds all of
+//   tile kt (its stage is free) and has landed its pieces of tile kt+1 (published);
+//   then tile kt+2's 16 DMA pieces per wave into the freed stage, spread over MFMAs 45-103,
+//   and (phase 1, MFMAs 64-127 on sub-step 1 operands) tile kt+1's sub-step-0 fragments read
+//   into the registers phase 0 released.
+// The DMA of a tile is issued ~1 tile before its barrier (vs ~0.4 in variant 4).
+template <int EPI, int PROBE = 0, int SCHED = 0>
+__global__ __launch_bounds__(NT, 1) void gemm4e_kernel(const bf16_t* __restrict__ X, int64_t ldx,
+                                                       const bf16_t* __restrict__ W, int64_t ldw, int64_t strideW,
+                                                       bf16_t* __restrict__ Y, int64_t ldy,
+                                                       const int* __restrict__ offs, const int* __restrict__ tile_end,
+                                                       int G, int N, int K, int gm, bf16_t* __restrict__ Y2,
+                                                       int64_t ldy2, int I, int Tdense) {
+  static_assert(EPI == 0 || EPI == 1, "EPI 0: plain, 1: gate|up + SwiGLU");
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
+  lds_t* smem = (lds_t*)smem_raw;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int nbn = N / BN;
+  int slot, nt;
+  tile_of(gm, nbn, slot, nt);
+  int g = 0, row0, rows;
+  if (tile_end == nullptr) {  // dense: Tdense rows, one weight
+    if (slot >= (Tdense + BM - 1) / BM) return;  // uniform over the workgroup
+    row0 = slot * BM;
+    rows = min(BM, Tdense - row0);
+  } else {
+    const int total_slots = tile_end[G - 1];
+    if (slot >= total_slots) return;  // uniform over the workgroup: no barrier reached yet
+    g = find_group(tile_end, G, slot);
+    const int first_slot = g ? tile_end[g - 1] : 0;
+    row0 = (g ? offs[g - 1] : 0) + (slot - first_slot) * BM;
+    rows = min(BM, offs[g] - row0);
+  }
+  const int n0 = nt * BN;
+  const rsrc_t rsX = make_rsrc(X + (int64_t)row0 * ldx, (uint32_t)(((int64_t)(rows - 1) * ldx + K) * 2));
+  // EPI 1: the descriptor spans the whole [2I, K] weight (the tile's rows are gathered)
+  const rsrc_t rsW = EPI == 1
+      ? make_rsrc(W + (int64_t)g * strideW, (uint32_t)(((int64_t)(N - 1) * ldw + K) * 2))
+      : make_rsrc(W + (int64_t)g * strideW + (int64_t)n0 * ldw, (uint32_t)(((int64_t)(BN - 1) * ldw + K) * 2));
+  const int KT = K / BK;
+
+  // wave w copies pieces w*8 .. w*8+7 of each image (piece q = image rows 8q .. 8q+7)
+  uint32_t voa[8], vob[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int pr = (wid * 8 + i) * 8 + (lane >> 3), pc = lane & 7;
+    voa[i] = (uint32_t)pr * (uint32_t)(ldx * 2) + (uint32_t)((pc ^ rsw(pr)) * 16);
+    // EPI 1: image row pr of N-tile nt -> wave column wn = pr / 128 holds 64 gate rows then the
+    // 64 matching up rows, so a lane's acc[.][j] and acc[.][j + 4] are gate and up of ONE feature
+    int wrow = pr;
+    if (EPI == 1) {
+      const int loc = pr & 127;
+      wrow = ((loc & 64) ? I : 0) + nt * 128 + (pr >> 7) * 64 + (loc & 63);
+    }
+    vob[i] = (uint32_t)wrow * (uint32_t)(ldw * 2) + (uint32_t)((pc ^ rsw(pr)) * 16);
+  }
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem + (uint32_t)(wid * 8 * 1024));
+  // piece p < 8: X piece p, else W piece p - 8
+  auto dma = [&](int buf, int kt, int p) {
+    if (PROBE == 2 || PROBE == 4) return;
+    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(kt * BK * 2));
+    if (p < 8) dma16s(rsX, lbase + buf * STAGE + p * 1024, voa[p], so);
+    else dma16s(rsW, lbase + buf * STAGE + IMG + (p - 8) * 1024, vob[p - 8], so);
+  };
+
+  const int q = lane >> 4, rl = lane & 15;
+  int foff[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) foff[ks] = rl * 128 + (((4 * ks + q) ^ rsw(rl)) * 16);
+  const int abase = wm * 128 * 128, bbase = IMG + wn * 128 * 128;
+  bfx8 fa[2][8], fb[2][8];
+  // fragment read r < 8: A row-block r, else B column-block r - 8
+  auto read = [&](const lds_t* st, int ks, int r) {
+    if (PROBE == 1 || PROBE == 4) return;
+    if (r < 8) fa[ks][r] = lds_r128(st + abase + r * 16 * 128 + foff[ks]);
+    else fb[ks][r - 8] = lds_r128(st + bbase + (r - 8) * 16 * 128 + foff[ks]);
+  };
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // operands swapped (weight fragment as A): acc[i][j] reg r = C[row 16 i + rl][col 16 j + 4 q + r],
+  // so a lane holds 4 CONSECUTIVE output columns of one row -- 8-byte epilogue stores
+  auto mfma = [&](int ks, int idx) {
+    const int i = idx >> 3, j = idx & 7;
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fb[ks][j]), "v"(fa[ks][i]));
+  };
+
+  // prologue: tiles 0 and 1 requested, tile 0 published, its sub-step-0 fragments read
+#pragma unroll
+  for (int p = 0; p < 16; ++p) dma(0, 0, p);
+  if (KT > 1) {
+#pragma unroll
+    for (int p = 0; p < 16; ++p) dma(1, 1, p);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) read(smem, 0, r);
+
+  // slot tables (MFMA index of each operation).  SCHED bit 1: sub-step 1 reads spread over
+  // MFMAs 0-42 and the next tile's sub-step 0 reads over 64-124 (else packed into 0-30 / 64-94);
+  // bit 0: M0 of a piece written two MFMAs before its DMA (else right before it).
+  constexpr bool SPREAD = SCHED & 2, M0AHEAD = SCHED & 1;
+  constexpr int BAR = SPREAD ? 46 : 44, DMA0 = BAR + 1;
+  constexpr auto rd1_slot = [](int m) constexpr -> int {  // read index of tile kt's sub-step 1 after MFMA m
+    if (SPREAD) {
+      for (int r = 0; r < 16; ++r)
+        if (m == (r * 42) / 15) return r;
+      return -1;
+    }
+    return m < 32 && (m & 1) == 0 ? m >> 1 : -1;
+  };
+  constexpr auto rd0_slot = [](int m) constexpr -> int {  // read index of tile kt+1's sub-step 0
+    if (SPREAD) return m >= 64 && m <= 124 && (m & 3) == 0 ? (m - 64) >> 2 : -1;
+    return m >= 64 && m < 96 && (m & 1) == 0 ? (m - 64) >> 1 : -1;
+  };
+  constexpr auto dma_slot = [](int m) constexpr -> int {
+    return m >= DMA0 && m <= DMA0 + 60 && ((m - DMA0) & 3) == 0 ? (m - DMA0) >> 2 : -1;
+  };
+  auto piece_m0 = [&](int buf, int p) {
+    return lbase + buf * STAGE + (p < 8 ? p * 1024 : IMG + (p - 8) * 1024);
+  };
+  auto set_m0 = [&](uint32_t v) { asm volatile("s_mov_b32 m0, %0" : : "s"(v) : "m0"); };
+  auto dma_nom0 = [&](int kt, int p) {  // M0 already holds the piece's LDS address
+    if (PROBE == 2 || PROBE == 4) return;
+    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(kt * BK * 2));
+    if (p < 8)
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(voa[p]), "s"(rsX), "s"(so) : "memory");
+    else
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(vob[p - 8]), "s"(rsW), "s"(so) : "memory");
+  };
+  auto step = [&](auto more_c, auto more2_c, int kt) {
+    constexpr bool more = decltype(more_c)::value, more2 = decltype(more2_c)::value;
+    const lds_t* cur = smem + (kt & 1) * STAGE;
+    const lds_t* nxt = smem + ((kt + 1) & 1) * STAGE;
+    __builtin_amdgcn_s_setprio(1);
+    static_for<0, 128>([&](auto mc) {
+      constexpr int m = decltype(mc)::value;
+      mfma(m >> 6, m & 63);
+      constexpr int r1 = rd1_slot(m), r0 = rd0_slot(m), pd = dma_slot(m), pn = dma_slot(m + 2);
+      if constexpr (r1 >= 0) {  // sub-step 1 fragments of tile kt
+        fence();
+        read(cur, 1, r1);
+        fence();
+      }
+      if constexpr (m == BAR && more) {
+        fence();
+        __builtin_amdgcn_s_setprio(0);
+        if (PROBE != 3 && PROBE != 4) {
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+        fence();
+      }
+      if constexpr (more2 && M0AHEAD && pn >= 0 && PROBE != 2 && PROBE != 4) {
+        fence();
+        set_m0(piece_m0(kt & 1, pn));
+        fence();
+      }
+      if constexpr (more2 && pd >= 0) {
+        fence();
+        if constexpr (M0AHEAD) dma_nom0(kt + 2, pd);
+        else dma(kt & 1, kt + 2, pd);
+        fence();
+      }
+      if constexpr (more && r0 >= 0) {  // sub-step 0 fragments of tile kt+1
+        fence();
+        read(nxt, 0, r0);
+        fence();
+      }
+    });
+    __builtin_amdgcn_s_setprio(0);
+  };
+  using T1 = std::true_type;
+  using F0 = std::false_type;
+  int kt = 0;
+  for (; kt + 2 < KT; ++kt) step(T1(), T1(), kt);
+  if (kt + 1 < KT) step(T1(), F0(), kt++);
+  step(F0(), F0(), kt);
+
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 3" ::: "memory");
+  auto pk4 = [](float a, float b, float c, float d) {
+    uint2 v;
+    v.x = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+    v.y = (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16);
+    return v;
+  };
+  if constexpr (EPI == 1) {
+    // gu [T, 2I]: gate feature c at column c, up at I + c; h [T, I] = silu(gate) * up of the
+    // bf16-rounded gate / up (what csrc/swiglu.hip computes from the stored gu)
+    const int c0 = nt * 128 + wn * 64 + 4 * q;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = wm * 128 + 16 * i + rl;
+      if (m < rows) {
+        bf16_t* gb = Y + (int64_t)(row0 + m) * ldy + c0;
+        bf16_t* hb = Y2 + (int64_t)(row0 + m) * ldy2 + c0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f32x4 gv = acc[i][j], uv = acc[i][j + 4];
+          const uint2 gp = pk4(gv[0], gv[1], gv[2], gv[3]), up = pk4(uv[0], uv[1], uv[2], uv[3]);
+          *reinterpret_cast<uint2*>(gb + 16 * j) = gp;
+          *reinterpret_cast<uint2*>(gb + I + 16 * j) = up;
+          float hv[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t gw = r < 2 ? gp.x : gp.y, uw = r < 2 ? up.x : up.y;
+            const float gq = __uint_as_float((r & 1) ? (gw & 0xffff0000u) : (gw << 16));
+            const float uq = __uint_as_float((r & 1) ? (uw & 0xffff0000u) : (uw << 16));
+            hv[r] = silu(gq) * uq;
+          }
+          *reinterpret_cast<uint2*>(hb + 16 * j) = pk4(hv[0], hv[1], hv[2], hv[3]);
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = wm * 128 + 16 * i + rl;
+      if (m < rows) {
+        bf16_t* yb = Y + (int64_t)(row0 + m) * ldy + n0 + wn * 128 + 4 * q;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const f32x4 v = acc[i][j];
+          *reinterpret_cast<uint2*>(yb + 16 * j) = pk4(v[0], v[1], v[2], v[3]);
+        }
+      }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -647,7 +909,7 @@ int st_gemm4w(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t st
   if (grid >= (1LL << 31)) return -2;
   const char* pe = std::getenv("ST_GEMM4W_PROBE");  // timing probes (wrong results)
   const int probe = pe ? std::atoi(pe) : 0;
-  const char* ke = std::getenv("ST_GEMM4W_KIND");  // 0: 2 x 2 waves, 1 / 2: 1 x 4 (NS 2 / 3), 4: 2 x 2 LDS-DMA
+  const char* ke = std::getenv("ST_GEMM4W_KIND");  // 0: 2 x 2 waves, 1 / 2: 1 x 4 (NS 2 / 3), 4 / 5: 2 x 2 LDS-DMA (rolling / whole-tile fragments)
   const int kind = ke ? std::atoi(ke) : 0;
   const char* oe = std::getenv("ST_GEMM4W_ORDER");  // slots per XCD group (0: slot-major)
   const int gm = oe ? std::atoi(oe) : 0;
@@ -664,10 +926,42 @@ int st_gemm4w(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t st
   } while (0)
   if (kind == 0) G4LAUNCH(gemm4w_kernel<0);
   else if (kind == 4) G4LAUNCH(gemm4d_kernel<0);
+  else if (kind == 5) {
+#undef G4ARGS
+#define G4ARGS (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, strideW, (bf16_t*)Y, ldy, offs, tile_end, G, N, K, gm, \
+               (bf16_t*)nullptr, (int64_t)0, 0, 0
+    const char* se = std::getenv("ST_GEMM4W_SCHED");
+    const int sched = se ? std::atoi(se) : 0;
+    if (sched == 1) G4LAUNCH(gemm4e_kernel<0, , 1);
+    else if (sched == 2) G4LAUNCH(gemm4e_kernel<0, , 2);
+    else if (sched == 3) G4LAUNCH(gemm4e_kernel<0, , 3);
+    else G4LAUNCH(gemm4e_kernel<0);
+#undef G4ARGS
+#define G4ARGS (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, strideW, (bf16_t*)Y, ldy, offs, tile_end, G, N, K, gm
+  }
   else if (kind == 2) G4LAUNCH(gemm4b_kernel<3);
   else G4LAUNCH(gemm4b_kernel<2);
 #undef G4LAUNCH
 #undef G4ARGS
+  return (int)hipGetLastError();
+}
+
+// gu [T, 2I] = X @ W^T and h [T, I] = silu(gate) * up in ONE launch (dense, W [2I, K] = gate
+// rows then up rows).  0 on success, -2 unsupported shape.
+int st_gemm4w_swiglu(const void* X, int64_t ldx, const void* W, int64_t ldw, void* GU, int64_t ldgu, void* H,
+                     int64_t ldh, int T, int I, int K, hipStream_t st) {
+  if (T <= 0 || I <= 0 || K <= 0 || K % BK || I % 128) return -2;
+  if (ldx % 8 || ldw % 8 || ldgu % 8 || ldh % 8 || ldx < K || ldw < K || ldgu < 2 * I || ldh < I) return -2;
+  if (((uintptr_t)X | (uintptr_t)W | (uintptr_t)GU | (uintptr_t)H) % 16) return -2;
+  if (((int64_t)(BM + 32) * ldx) * 2 >= (int64_t)1 << 32) return -2;
+  if (((int64_t)2 * I * ldw) * 2 >= (int64_t)1 << 32) return -2;
+  const int N = 2 * I;
+  const int64_t grid = (int64_t)((T + BM - 1) / BM) * (N / BN);
+  if (grid >= (1LL << 31)) return -2;
+  const char* oe = std::getenv("ST_GEMM4W_ORDER");
+  const int gm = oe ? std::atoi(oe) : 4;
+  gemm4e_kernel<1, 0><<<(unsigned)grid, NT, 0, st>>>((const bf16_t*)X, ldx, (const bf16_t*)W, ldw, 0, (bf16_t*)GU,
+                                                     ldgu, nullptr, nullptr, 1, N, K, gm, (bf16_t*)H, ldh, I, T);
   return (int)hipGetLastError();
 }
 

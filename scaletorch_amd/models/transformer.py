@@ -124,7 +124,14 @@ class MLP(nn.Module):
         if sp_mlp_applies(self, x):
             # the whole SP MLP in the gathered row layout (tensor_parallel._SPMLPFn)
             return sp_mlp(x, self.gate_up_proj.weight, self.down_proj.weight, self.gate_up_proj.group)
-        return self.down_proj(self.gate_up_proj(x), act="swiglu")
+        gu_lin = self.gate_up_proj
+        if gu_lin.tp == 1 and gu_lin.bias is None and not gu_lin.sequence_parallel:
+            from ..ops.mlp import gate_up_swiglu
+
+            h = gate_up_swiglu(x, gu_lin.weight)  # one kernel: gate|up GEMM + SwiGLU epilogue
+            if h is not None:
+                return self.down_proj(h)
+        return self.down_proj(gu_lin(x), act="swiglu")
 
 
 class DecoderLayer(nn.Module):

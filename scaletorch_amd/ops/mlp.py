@@ -115,3 +115,59 @@ def swiglu_linear(gu: torch.Tensor, weight: torch.Tensor) -> torch.Tensor | None
             and gu.dtype == torch.bfloat16 and gu.shape[-1] % 16 == 0):
         return _SwiGLULinearFn.apply(gu, weight)
     return None
+
+
+class _GateUpSwiGLUFn(torch.autograd.Function):
+    """h = silu(x W_gate^T) * (x W_up^T) as ONE kernel: the gate|up GEMM with the SwiGLU in its
+    epilogue (csrc/gemm4w.hip ``st_gemm4w_swiglu``), which also stores gu = x [W_gate; W_up]^T
+    for the backward -- the separate SwiGLU pass (read gu, write h) is gone.  Backward is the
+    unfused path's: dgu = SwiGLU'(dh, gu), then the gate|up linear's dgrad / fp32 wgrad into
+    ``main_grad``.  Reference: down(silu(gate(x)) * up(x)), scaletorch/models/llama.py:236-249."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        if x.requires_grad:
+            prepare_dgrad_weight(weight)
+        gu, h = _lib.ops().gemm_swiglu(x.reshape(-1, x.shape[-1]), weight)
+        ctx.save_for_backward(x, weight, gu)
+        return h.view(*x.shape[:-1], h.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, weight, gu = ctx.saved_tensors
+        dgu = _lib.ops().swiglu_bwd(dh.reshape(-1, dh.shape[-1]).contiguous(), gu)
+        x2 = x.reshape(-1, x.shape[-1])
+        pre = prefetch_wgrad(weight, dgu, x2) if ctx.needs_input_grad[1] else None  # overlaps the dgrad GEMM
+        dx = dgrad(dgu.view(*x.shape[:-1], dgu.shape[-1]), weight) if ctx.needs_input_grad[0] else None
+        dw = accumulate_linear_wgrad(weight, dgu, x2, pre) if ctx.needs_input_grad[1] else None
+        return dx, dw
+
+
+def _gemm_swiglu_tiles(x2: torch.Tensor, weight: torch.Tensor) -> bool:
+    """The shapes / layouts csrc/gemm4w.hip ``st_gemm4w_swiglu`` takes (it returns -2 otherwise)."""
+    K, I2 = x2.shape[1], weight.shape[0]
+    ldx, ldw = x2.stride(0), weight.stride(0)
+    return (K % 64 == 0 and I2 % 256 == 0 and x2.stride(1) == 1 and weight.stride(1) == 1 and ldx % 8 == 0
+            and ldw % 8 == 0 and ldx >= K and ldw >= K and x2.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0
+            and (256 + 32) * ldx * 2 < 2 ** 32 and I2 * ldw * 2 < 2 ** 32 and 0 < x2.shape[0] < 2 ** 31)
+
+
+def gate_up_swiglu(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor | None:
+    """``swiglu(x @ weight^T)`` for a fused [gate; up] weight in one kernel, or None when it
+    does not apply: opt-in ``ST_MLP_FUSED_SWIGLU=1`` (off by default), CPU, fp32, shapes the
+    kernel does not tile, the activation-recompute mode.  Measured (docs/PERF.md round 5,
+    profiles/r05/gemm4w/): the kernel runs the gate|up GEMM at 1.35-1.41 PF/s against
+    hipBLASLt's 1.37-1.50 there, so the absorbed SwiGLU pass does not pay for it yet --
+    4.29 vs 4.19 ms per layer, 967-972 vs 964-965 ms/step in the headline A/B."""
+    import os
+
+    if (os.environ.get("ST_MLP_FUSED_SWIGLU", "0") != "1" or os.environ.get("ST_MLP_RECOMPUTE_ACT", "0") == "1"
+            or not x.is_cuda or not _lib.use_native(x) or x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16
+            or weight.dim() != 2 or x.numel() == 0):
+        return None
+    if not _gemm_swiglu_tiles(x.reshape(-1, x.shape[-1]), weight):
+        return None
+    if torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad):
+        return _GateUpSwiGLUFn.apply(x, weight)
+    gu, h = _lib.ops().gemm_swiglu(x.reshape(-1, x.shape[-1]), weight)
+    return h.view(*x.shape[:-1], h.shape[-1])

@@ -760,7 +760,56 @@ def test_grouped_gemm_matches_per_expert(N, K, wn):
         off += n
 
 
-@pytest.mark.parametrize("kind", ["0", "1", "2", "4"])
+@pytest.mark.parametrize("T,K,I", [(300, 192, 128), (1000, 1024, 384)])
+def test_gemm_swiglu_matches_fp32(T, K, I):
+    """Dense gate|up GEMM with the SwiGLU epilogue (csrc/gemm4w.hip ``st_gemm4w_swiglu``) vs
+    fp32: gu = x [W_gate; W_up]^T (one bf16 rounding) and h = silu(gate) * up of the stored
+    bf16 gate / up (what csrc/swiglu.hip computes from gu); partial last row tile, strided x."""
+    torch.manual_seed(13)
+    xb = torch.randn(T, K + 64, device="cuda", dtype=torch.bfloat16)
+    x = xb[:, :K]
+    w = torch.randn(2 * I, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
+    gu, h = _lib.ops().gemm_swiglu(x, w)
+    torch.cuda.synchronize()
+    ref = x.float() @ w.float().t()
+    assert rel(gu.float(), ref) < 1e-2
+    g, u = gu[:, :I].float(), gu[:, I:].float()
+    assert rel(h.float(), torch.nn.functional.silu(g) * u) < 1e-2
+    assert torch.equal(h, _lib.ops().swiglu_fwd(gu))
+
+
+def test_mlp_fused_swiglu_matches_unfused():
+    """The Llama MLP with the fused gate|up + SwiGLU kernel (ops.mlp.gate_up_swiglu,
+    ST_MLP_FUSED_SWIGLU=1) equals the unfused path (hipBLASLt GEMM + swiglu kernel) on the
+    output, the input gradient and both fp32 main_grad weight gradients."""
+    import os
+
+    from scaletorch_amd.models.config import get_model_config
+    from scaletorch_amd.models.transformer import MLP
+
+    cfg = get_model_config("tiny-llama", hidden_size=256, intermediate_size=384)
+    res = {}
+    for fused in ("1", "0"):
+        os.environ["ST_MLP_FUSED_SWIGLU"] = fused
+        try:
+            torch.manual_seed(14)
+            mlp = MLP(cfg).cuda().to(torch.bfloat16)
+            for p in mlp.parameters():
+                p.main_grad = torch.zeros(p.shape, device="cuda")
+                p._st_fresh = True
+            x = torch.randn(2, 300, 256, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+            y = mlp(x)
+            y.backward(torch.randn(y.shape, device="cuda", generator=torch.Generator("cuda").manual_seed(5)).to(y.dtype))
+            torch.cuda.synchronize()
+            res[fused] = (y.float(), x.grad.float(), mlp.gate_up_proj.weight.main_grad.clone(),
+                          mlp.down_proj.weight.main_grad.clone())
+        finally:
+            os.environ.pop("ST_MLP_FUSED_SWIGLU", None)
+    for a, b in zip(res["1"], res["0"]):
+        assert rel(a, b) < 2e-2
+
+
+@pytest.mark.parametrize("kind", ["0", "1", "2", "4", "5"])
 def test_gemm4w_variants_match_fp32(kind, monkeypatch):
     """The one-wave-per-SIMD GEMM experiment (csrc/gemm4w.hip; docs/PERF.md round 5) in each
     variant -- 2x2 register-staged, 1x4 direct weight fragments (2- / 3-deep), 2x2 LDS-DMA --

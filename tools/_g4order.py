@@ -3,7 +3,12 @@ import sys, os, torch, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from scaletorch_amd.ops import _lib
 assert _lib.load()
-shapes = {"gate_up": (24576, 4096, 28672), "down": (24576, 14336, 4096), "qkv": (24576, 4096, 6144)}
+shapes = {  # name: (T, K, N) -- forward projections and the TN data gradients on W^T copies
+    "gate_up": (24576, 4096, 28672), "down": (24576, 14336, 4096), "qkv": (24576, 4096, 6144),
+    "o": (24576, 4096, 4096), "down_dgrad": (24576, 4096, 14336), "lm_head_chunk": (4096, 4096, 128256),
+    "gate_up_dgrad": (24576, 28672, 4096), "qkv_dgrad": (24576, 6144, 4096)}
+if len(sys.argv) > 1:
+    shapes = {k: v for k, v in shapes.items() if k in sys.argv[1].split(",")}
 for name, (T, K, N) in shapes.items():
     x = torch.randn(T, K, device='cuda', dtype=torch.bfloat16)
     w = torch.randn(1, N, K, device='cuda', dtype=torch.bfloat16) * 0.02
@@ -11,9 +16,11 @@ for name, (T, K, N) in shapes.items():
     flops = 2.0 * T * K * N
     res = {}
     for rnd in range(3):
-        for kind in ("0", "1", "4"):
-            for order in ("0", "4"):
+        for kind in os.environ.get("G4_KINDS", "5").split(","):
+            for order, sched in [(o, sc) for o in os.environ.get("G4_ORDERS", "0,4,8").split(",")
+                                 for sc in os.environ.get("G4_SCHEDS", "0").split(",")]:
                 os.environ["ST_GEMM4W_KIND"], os.environ["ST_GEMM4W_ORDER"] = kind, order
+                os.environ["ST_GEMM4W_SCHED"] = sched
                 _lib.ops().gemm4w(x, w, offs)
                 torch.cuda.synchronize()
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -21,7 +28,7 @@ for name, (T, K, N) in shapes.items():
                 for _ in range(5):
                     _lib.ops().gemm4w(x, w, offs)
                 e.record(); e.synchronize()
-                key = f"k{kind}o{order}"
+                key = f"k{kind}s{sched}o{order}"
                 res[key] = min(res.get(key, 1e9), s.elapsed_time(e) / 5)
     bl = torch.empty(T, N, device='cuda', dtype=torch.bfloat16)
     w2 = w[0]

@@ -10,7 +10,7 @@ for K, counts in ((128, [37, 0, 300]), (192, [256, 1, 511]), (4096, [700, 300]))
     T, N, G = int(c.sum()), 512, len(counts)
     x = torch.randn(T, K, device='cuda', dtype=torch.bfloat16)
     w = torch.randn(G, N, K, device='cuda', dtype=torch.bfloat16)
-    for kind in ("0", "1", "2", "4"):
+    for kind in ("0", "1", "2", "4", "5"):
         os.environ["ST_GEMM4W_KIND"] = kind
         y = _lib.ops().gemm4w(x, w, offs)
         torch.cuda.synchronize()
