@@ -26,6 +26,7 @@
 // box, and the 8-phase grouped kernel equals variant 0.  PMC (profiles/r05/gemm4w/pmc.md): 0 LDS
 // bank conflicts, L2 hit 64 % (78 % XCD-grouped, hipBLASLt 79 %) at the same ~250-cycle mean
 // L2 latency; hipBLASLt issues 32 LDS instructions per wave and K-tile (DMA fills) vs 48 here.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -93,6 +94,21 @@ ST_DEVICE void tile_of(int gm, int nbn, int& slot, int& nt) {
   }
   const int nslots = (int)gridDim.x / nbn;
   const int id = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+  const int per = gm * nbn, grp = id / per, in = id % per;
+  const int gsz = min(gm, nslots - grp * gm);
+  slot = grp * gm + in % gsz;
+  nt = in / gsz;
+}
+
+// tile_of for a persistent workgroup's virtual tile id vb of nv
+ST_DEVICE void tile_of_v(int gm, int nbn, int vb, int nv, int& slot, int& nt) {
+  if (gm <= 0) {
+    slot = vb / nbn;
+    nt = vb % nbn;
+    return;
+  }
+  const int nslots = nv / nbn;
+  const int id = xcd_remap(vb, nv);
   const int per = gm * nbn, grp = id / per, in = id % per;
   const int gsz = min(gm, nslots - grp * gm);
   slot = grp * gm + in % gsz;
@@ -661,7 +677,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4e_kernel(const bf16_t* __restrict_
                                                        bf16_t* __restrict__ Y, int64_t ldy,
                                                        const int* __restrict__ offs, const int* __restrict__ tile_end,
                                                        int G, int N, int K, int gm, bf16_t* __restrict__ Y2,
-                                                       int64_t ldy2, int I, int Tdense) {
+                                                       int64_t ldy2, int I, int Tdense, int nvirt) {
   static_assert(EPI == 0 || EPI == 1, "EPI 0: plain, 1: gate|up + SwiGLU");
   __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
   lds_t* smem = (lds_t*)smem_raw;
@@ -669,16 +685,22 @@ __global__ __launch_bounds__(NT, 1) void gemm4e_kernel(const bf16_t* __restrict_
   const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   const int nbn = N / BN;
+  // persistent: the workgroup walks virtual tiles vb = blockIdx.x, + gridDim.x, ... (one launch
+  // of #CU workgroups holds the chip for the whole GEMM, so a side-stream kernel cannot wedge
+  // into a CU between two tiles); nvirt == 0: one tile per workgroup
+  const int nv = nvirt ? nvirt : (int)gridDim.x;
+  for (int vb = (int)blockIdx.x; vb < nv; vb += (nvirt ? (int)gridDim.x : nv)) {
+  if (vb != (int)blockIdx.x) __syncthreads();  // every wave is past the previous tile's LDS reads
   int slot, nt;
-  tile_of(gm, nbn, slot, nt);
+  tile_of_v(gm, nbn, vb, nv, slot, nt);
   int g = 0, row0, rows;
   if (tile_end == nullptr) {  // dense: Tdense rows, one weight
-    if (slot >= (Tdense + BM - 1) / BM) return;  // uniform over the workgroup
+    if (slot >= (Tdense + BM - 1) / BM) continue;  // uniform over the workgroup
     row0 = slot * BM;
     rows = min(BM, Tdense - row0);
   } else {
     const int total_slots = tile_end[G - 1];
-    if (slot >= total_slots) return;  // uniform over the workgroup: no barrier reached yet
+    if (slot >= total_slots) continue;  // uniform over the workgroup
     g = find_group(tile_end, G, slot);
     const int first_slot = g ? tile_end[g - 1] : 0;
     row0 = (g ? offs[g - 1] : 0) + (slot - first_slot) * BM;
@@ -757,8 +779,13 @@ __global__ __launch_bounds__(NT, 1) void gemm4e_kernel(const bf16_t* __restrict_
   // slot tables (MFMA index of each operation).  SCHED bit 1: sub-step 1 reads spread over
   // MFMAs 0-42 and the next tile's sub-step 0 reads over 64-124 (else packed into 0-30 / 64-94);
   // bit 0: M0 of a piece written two MFMAs before its DMA (else right before it).
-  constexpr bool SPREAD = SCHED & 2, M0AHEAD = SCHED & 1;
-  constexpr int BAR = SPREAD ? 46 : 44, DMA0 = BAR + 1;
+  // bit 2 (SPLIT): the X region of a stage is released after its sub-step-1 reads (barrier at
+  // MFMA 20, lgkmcnt(3)) and gets tile kt+2's X pieces at MFMAs 21-56; the W region and the
+  // publication of tile kt+1 share one barrier at MFMA 63 (vmcnt(8): all but this step's X
+  // pieces); W pieces at 64-120 -- the pieces spread over the whole tile (hipBLASLt's DTL
+  // kernels release their stage in parts too)
+  constexpr bool SPREAD = SCHED & 2, M0AHEAD = SCHED & 1, SPLIT = SCHED & 4;
+  constexpr int BAR = SPLIT ? 63 : (SPREAD ? 46 : 44), DMA0 = BAR + 1, BARA = 20;
   constexpr auto rd1_slot = [](int m) constexpr -> int {  // read index of tile kt's sub-step 1 after MFMA m
     if (SPREAD) {
       for (int r = 0; r < 16; ++r)
@@ -772,6 +799,11 @@ __global__ __launch_bounds__(NT, 1) void gemm4e_kernel(const bf16_t* __restrict_
     return m >= 64 && m < 96 && (m & 1) == 0 ? (m - 64) >> 1 : -1;
   };
   constexpr auto dma_slot = [](int m) constexpr -> int {
+    if (SPLIT) {
+      if (m >= 21 && m <= 56 && (m - 21) % 5 == 0) return (m - 21) / 5;          // X pieces
+      if (m >= 64 && m <= 120 && ((m - 64) & 7) == 0) return 8 + ((m - 64) >> 3);  // W pieces
+      return -1;
+    }
     return m >= DMA0 && m <= DMA0 + 60 && ((m - DMA0) & 3) == 0 ? (m - DMA0) >> 2 : -1;
   };
   auto piece_m0 = [&](int buf, int p) {
@@ -786,11 +818,23 @@ __global__ __launch_bounds__(NT, 1) void gemm4e_kernel(const bf16_t* __restrict_
     else
       asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(vob[p - 8]), "s"(rsW), "s"(so) : "memory");
   };
+  // PROBE 7 (diagnostic build): shader-cycle stamps per segment of the steady-state step,
+  // summed per wave and written over the output (tools/_g4stamps.py reads them)
+  uint64_t seg[4] = {0, 0, 0, 0};
+  uint64_t ts[5];
+  auto stamp = [&](int k) {
+    if constexpr (PROBE == 7) {
+      fence();
+      ts[k] = __builtin_amdgcn_s_memtime();
+      fence();
+    }
+  };
   auto step = [&](auto more_c, auto more2_c, int kt) {
     constexpr bool more = decltype(more_c)::value, more2 = decltype(more2_c)::value;
     const lds_t* cur = smem + (kt & 1) * STAGE;
     const lds_t* nxt = smem + ((kt + 1) & 1) * STAGE;
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (more2) stamp(0);
     static_for<0, 128>([&](auto mc) {
       constexpr int m = decltype(mc)::value;
       mfma(m >> 6, m & 63);
@@ -800,17 +844,30 @@ __global__ __launch_bounds__(NT, 1) void gemm4e_kernel(const bf16_t* __restrict_
         read(cur, 1, r1);
         fence();
       }
+      if constexpr (SPLIT && m == BARA && more2) {  // X region of cur: every wave's reads done
+        fence();
+        if (PROBE != 3 && PROBE != 4) {
+          asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
+        asm volatile("" ::: "memory");
+        fence();
+      }
       if constexpr (m == BAR && more) {
         fence();
+        if constexpr (more2) stamp(1);
         __builtin_amdgcn_s_setprio(0);
         if (PROBE != 3 && PROBE != 4) {
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          if constexpr (SPLIT && more2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
         }
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_setprio(1);
+        if constexpr (more2) stamp(2);
         fence();
       }
+      if constexpr (m == (SPLIT ? 100 : 63) && more2) stamp(3);
       if constexpr (more2 && M0AHEAD && pn >= 0 && PROBE != 2 && PROBE != 4) {
         fence();
         set_m0(piece_m0(kt & 1, pn));
@@ -828,6 +885,10 @@ __global__ __launch_bounds__(NT, 1) void gemm4e_kernel(const bf16_t* __restrict_
         fence();
       }
     });
+    if constexpr (more2 && PROBE == 7) {
+      stamp(4);
+      for (int k = 0; k < 4; ++k) seg[k] += ts[k + 1] - ts[k];
+    }
     __builtin_amdgcn_s_setprio(0);
   };
   using T1 = std::true_type;
@@ -838,6 +899,14 @@ __global__ __launch_bounds__(NT, 1) void gemm4e_kernel(const bf16_t* __restrict_
   step(F0(), F0(), kt);
 
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 3" ::: "memory");
+  if constexpr (PROBE == 7) {  // lane 0 of each wave: 4 x u64 segment sums + step count at row 4 w + lane
+    if (lane == 0) {
+      uint64_t* d = reinterpret_cast<uint64_t*>(Y + (int64_t)(row0 + wid) * ldy + n0);
+      for (int k = 0; k < 4; ++k) d[k] = seg[k];
+      d[4] = (uint64_t)(KT - 2);
+    }
+    continue;
+  }
   auto pk4 = [](float a, float b, float c, float d) {
     uint2 v;
     v.x = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
@@ -886,9 +955,278 @@ __global__ __launch_bounds__(NT, 1) void gemm4e_kernel(const bf16_t* __restrict_
       }
     }
   }
+  }  // tile loop
+}
+
+
+// ---- gemm4f: the kind-5 tile (whole-tile fragments, split stage release, M0 set ahead) in a
+// PERSISTENT workgroup that treats its tiles as ONE stream of K-tiles: the DMA two steps ahead
+// runs into the next tile's first K-tiles while this tile's last steps and epilogue run, and
+// the next tile's first fragments are read in the last step -- no per-tile prologue, no launch
+// gaps, and (one workgroup per CU for the whole GEMM) no side-stream kernel wedged between
+// tiles.  K must hold >= 2 K-tiles.
+template <int EPI>
+__global__ __launch_bounds__(NT, 1) void gemm4f_kernel(const bf16_t* __restrict__ X, int64_t ldx,
+                                                       const bf16_t* __restrict__ W, int64_t ldw, int64_t strideW,
+                                                       bf16_t* __restrict__ Y, int64_t ldy,
+                                                       const int* __restrict__ offs, const int* __restrict__ tile_end,
+                                                       int G, int N, int K, int gm, bf16_t* __restrict__ Y2,
+                                                       int64_t ldy2, int I, int Tdense, int nvirt) {
+  static_assert(EPI == 0 || EPI == 1, "EPI 0: plain, 1: gate|up + SwiGLU");
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
+  lds_t* smem = (lds_t*)smem_raw;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int nbn = N / BN, KT = K / BK, stride = (int)gridDim.x;
+
+  struct Tile {
+    int vb, g, row0, rows, nt;
+    rsrc_t rsX, rsW;
+  };
+  // the first live virtual tile at or after vb (vb == nvirt: none)
+  auto find = [&](int vb, Tile& tl) -> bool {
+    for (; vb < nvirt; vb += stride) {
+      int slot, nt;
+      tile_of_v(gm, nbn, vb, nvirt, slot, nt);
+      int g = 0, row0, rows;
+      if (tile_end == nullptr) {
+        if (slot >= (Tdense + BM - 1) / BM) continue;
+        row0 = slot * BM;
+        rows = min(BM, Tdense - row0);
+      } else {
+        if (slot >= tile_end[G - 1]) continue;
+        g = find_group(tile_end, G, slot);
+        const int first_slot = g ? tile_end[g - 1] : 0;
+        row0 = (g ? offs[g - 1] : 0) + (slot - first_slot) * BM;
+        rows = min(BM, offs[g] - row0);
+      }
+      tl.vb = vb;
+      tl.g = g;
+      tl.row0 = row0;
+      tl.rows = rows;
+      tl.nt = nt;
+      tl.rsX = make_rsrc(X + (int64_t)row0 * ldx, (uint32_t)(((int64_t)(rows - 1) * ldx + K) * 2));
+      // EPI 1: base at the tile's first gate row, the up rows I further (lane offsets tile-free)
+      tl.rsW = EPI == 1 ? make_rsrc(W + (int64_t)g * strideW + (int64_t)nt * 128 * ldw,
+                                    (uint32_t)(((int64_t)(I + 127) * ldw + K) * 2))
+                        : make_rsrc(W + (int64_t)g * strideW + (int64_t)nt * BN * ldw,
+                                    (uint32_t)(((int64_t)(BN - 1) * ldw + K) * 2));
+      return true;
+    }
+    return false;
+  };
+
+  uint32_t voa[8], vob[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int pr = (wid * 8 + i) * 8 + (lane >> 3), pc = lane & 7;
+    voa[i] = (uint32_t)pr * (uint32_t)(ldx * 2) + (uint32_t)((pc ^ rsw(pr)) * 16);
+    int wrow = pr;
+    if (EPI == 1) {
+      const int loc = pr & 127;
+      wrow = ((loc & 64) ? I : 0) + (pr >> 7) * 64 + (loc & 63);
+    }
+    vob[i] = (uint32_t)wrow * (uint32_t)(ldw * 2) + (uint32_t)((pc ^ rsw(pr)) * 16);
+  }
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem + (uint32_t)(wid * 8 * 1024));
+  auto piece_m0 = [&](int buf, int p) { return lbase + buf * STAGE + (p < 8 ? p * 1024 : IMG + (p - 8) * 1024); };
+  auto set_m0 = [&](uint32_t v) { asm volatile("s_mov_b32 m0, %0" : : "s"(v) : "m0"); };
+  auto dma_nom0 = [&](rsrc_t dX, rsrc_t dW, uint32_t so, int p) {  // M0 holds the piece's LDS address
+    if (p < 8)
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(voa[p]), "s"(dX), "s"(so) : "memory");
+    else
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(vob[p - 8]), "s"(dW), "s"(so) : "memory");
+  };
+  auto dma = [&](int buf, rsrc_t dX, rsrc_t dW, int kt, int p) {
+    set_m0(piece_m0(buf, p));
+    dma_nom0(dX, dW, __builtin_amdgcn_readfirstlane((uint32_t)(kt * BK * 2)), p);
+  };
+
+  const int q = lane >> 4, rl = lane & 15;
+  int foff[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) foff[ks] = rl * 128 + (((4 * ks + q) ^ rsw(rl)) * 16);
+  const int abase = wm * 128 * 128, bbase = IMG + wn * 128 * 128;
+  bfx8 fa[2][8], fb[2][8];
+  auto read = [&](const lds_t* st, int ks, int r) {
+    if (r < 8) fa[ks][r] = lds_r128(st + abase + r * 16 * 128 + foff[ks]);
+    else fb[ks][r - 8] = lds_r128(st + bbase + (r - 8) * 16 * 128 + foff[ks]);
+  };
+
+  Tile cur, nxt;
+  if (!find((int)blockIdx.x, cur)) return;  // uniform: no barrier reached
+  bool has_nxt = find(cur.vb + stride, nxt);
+
+  // prologue: K-tiles 0 and 1 of the first tile requested, 0 published, its sub-step-0 read
+#pragma unroll
+  for (int p = 0; p < 16; ++p) dma(0, cur.rsX, cur.rsW, 0, p);
+#pragma unroll
+  for (int p = 0; p < 16; ++p) dma(1, cur.rsX, cur.rsW, 1, p);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) read(smem, 0, r);
+
+  // slot tables (SCHED 5 of gemm4e): sub-step 1 reads at MFMAs 0-30; X stage region released
+  // at 20 and refilled at 21-56; publication + W region at 63; W pieces at 64-120; the next
+  // step's sub-step 0 reads at 64-94
+  constexpr auto dslot = [](int m) constexpr -> int {
+    if (m >= 21 && m <= 56 && (m - 21) % 5 == 0) return (m - 21) / 5;
+    if (m >= 64 && m <= 120 && ((m - 64) & 7) == 0) return 8 + ((m - 64) >> 3);
+    return -1;
+  };
+  // gs: global step (buffer parity); d / kd: the tile and K-tile two steps ahead
+  auto mfma = [&](f32x4 (&acc)[8][8], int ks, int idx) {
+    const int i = idx >> 3, j = idx & 7;
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fb[ks][j]), "v"(fa[ks][i]));
+  };
+  auto step = [&](f32x4 (&acc)[8][8], auto more_c, auto more2_c, int gs, rsrc_t dX, rsrc_t dW, uint32_t so) {
+    constexpr bool more = decltype(more_c)::value, more2 = decltype(more2_c)::value;
+    const lds_t* cs = smem + (gs & 1) * STAGE;
+    const lds_t* ns = smem + ((gs + 1) & 1) * STAGE;
+    __builtin_amdgcn_s_setprio(1);
+    static_for<0, 128>([&](auto mc) {
+      constexpr int m = decltype(mc)::value;
+      mfma(acc, m >> 6, m & 63);
+      constexpr int pd = dslot(m), pn = dslot(m + 2);
+      if constexpr (m < 32 && (m & 1) == 0) {
+        fence();
+        read(cs, 1, m >> 1);
+        fence();
+      }
+      if constexpr (m == 20 && more2) {  // X region of this stage: every wave's reads done
+        fence();
+        asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        fence();
+      }
+      if constexpr (m == 63 && more) {  // next step's K-tile published, W region free
+        fence();
+        __builtin_amdgcn_s_setprio(0);
+        if constexpr (more2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+        fence();
+      }
+      if constexpr (more2 && pn >= 0) {
+        fence();
+        set_m0(piece_m0(gs & 1, pn));
+        fence();
+      }
+      if constexpr (more2 && pd >= 0) {
+        fence();
+        dma_nom0(dX, dW, so, pd);
+        fence();
+      }
+      if constexpr (more && m >= 64 && m < 96 && (m & 1) == 0) {
+        fence();
+        read(ns, 0, (m - 64) >> 1);
+        fence();
+      }
+    });
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto pk4 = [](float a, float b, float c, float dd) {
+    uint2 v;
+    v.x = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+    v.y = (uint32_t)f2bf(c) | ((uint32_t)f2bf(dd) << 16);
+    return v;
+  };
+  using T1 = std::true_type;
+  using F0 = std::false_type;
+  int gs = 0;
+  for (;;) {
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // steps whose K-tile two ahead exists (this tile's, or the next tile's first two): all of
+    // them when a next tile follows, else all but the last two (the stream's tail)
+    const int kfull = has_nxt ? KT : KT - 2;
+    int kt = 0;
+    for (; kt < kfull; ++kt, ++gs) {
+      const bool in_cur = kt + 2 < KT;
+      const rsrc_t dX = in_cur ? cur.rsX : nxt.rsX, dW = in_cur ? cur.rsW : nxt.rsW;
+      const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)((in_cur ? kt + 2 : kt + 2 - KT) * BK * 2));
+      step(acc, T1(), T1(), gs, dX, dW, so);
+    }
+    if (!has_nxt) {
+      step(acc, T1(), F0(), gs++, cur.rsX, cur.rsW, 0u);
+      step(acc, F0(), F0(), gs++, cur.rsX, cur.rsW, 0u);
+    }
+    asm volatile("s_nop 15\n\ts_nop 3" ::: "memory");
+    // epilogue of `cur` (the next tile's first K-tiles are in flight meanwhile)
+    if constexpr (EPI == 1) {
+      const int c0 = cur.nt * 128 + wn * 64 + 4 * q;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = wm * 128 + 16 * i + rl;
+        if (m < cur.rows) {
+          bf16_t* gb = Y + (int64_t)(cur.row0 + m) * ldy + c0;
+          bf16_t* hb = Y2 + (int64_t)(cur.row0 + m) * ldy2 + c0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f32x4 gv = acc[i][j], uv = acc[i][j + 4];
+            const uint2 gp = pk4(gv[0], gv[1], gv[2], gv[3]), up = pk4(uv[0], uv[1], uv[2], uv[3]);
+            *reinterpret_cast<uint2*>(gb + 16 * j) = gp;
+            *reinterpret_cast<uint2*>(gb + I + 16 * j) = up;
+            float hv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const uint32_t gw = r < 2 ? gp.x : gp.y, uw = r < 2 ? up.x : up.y;
+              const float gq = __uint_as_float((r & 1) ? (gw & 0xffff0000u) : (gw << 16));
+              const float uq = __uint_as_float((r & 1) ? (uw & 0xffff0000u) : (uw << 16));
+              hv[r] = silu(gq) * uq;
+            }
+            *reinterpret_cast<uint2*>(hb + 16 * j) = pk4(hv[0], hv[1], hv[2], hv[3]);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = wm * 128 + 16 * i + rl;
+        if (m < cur.rows) {
+          bf16_t* yb = Y + (int64_t)(cur.row0 + m) * ldy + cur.nt * BN + wn * 128 + 4 * q;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const f32x4 v = acc[i][j];
+            *reinterpret_cast<uint2*>(yb + 16 * j) = pk4(v[0], v[1], v[2], v[3]);
+          }
+        }
+      }
+    }
+    if (!has_nxt) break;
+    cur = nxt;
+    has_nxt = find(cur.vb + stride, nxt);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 }  // namespace
+
+// compute units of the current device (persistent grids)
+static int cu_count() {
+  static int cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
+static bool persist_on() {
+  const char* e = std::getenv("ST_GEMM4W_PERSIST");  // 0: one tile per workgroup (A/B)
+  return !e || std::atoi(e) != 0;
+}
 
 extern "C" {
 
@@ -926,15 +1264,27 @@ int st_gemm4w(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t st
   } while (0)
   if (kind == 0) G4LAUNCH(gemm4w_kernel<0);
   else if (kind == 4) G4LAUNCH(gemm4d_kernel<0);
-  else if (kind == 5) {
+  else if (kind == 6 && K / BK >= 2) {
+    const int64_t lg = std::min<int64_t>(grid, cu_count());
+    gemm4f_kernel<0><<<(unsigned)lg, NT, 0, st>>>((const bf16_t*)X, ldx, (const bf16_t*)W, ldw, strideW,
+                                                  (bf16_t*)Y, ldy, offs, tile_end, G, N, K, gm, nullptr, 0, 0, 0,
+                                                  (int)grid);
+  } else if (kind == 5 || kind == 6) {
+    const int64_t vt = grid;  // virtual tiles
+    const int pv = persist_on() ? (int)vt : 0;
+    const int64_t grid = pv ? std::min<int64_t>(vt, cu_count()) : vt;  // persistent: one workgroup per CU
 #undef G4ARGS
 #define G4ARGS (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, strideW, (bf16_t*)Y, ldy, offs, tile_end, G, N, K, gm, \
-               (bf16_t*)nullptr, (int64_t)0, 0, 0
+               (bf16_t*)nullptr, (int64_t)0, 0, 0, pv
     const char* se = std::getenv("ST_GEMM4W_SCHED");
-    const int sched = se ? std::atoi(se) : 0;
-    if (sched == 1) G4LAUNCH(gemm4e_kernel<0, , 1);
+    const int sched = se ? std::atoi(se) : 5;
+    if (probe == 7 && sched == 4) gemm4e_kernel<0, 7, 4><<<(unsigned)grid, NT, 0, st>>>(G4ARGS);
+    else if (probe == 7) gemm4e_kernel<0, 7><<<(unsigned)grid, NT, 0, st>>>(G4ARGS);
+    else if (sched == 1) G4LAUNCH(gemm4e_kernel<0, , 1);
     else if (sched == 2) G4LAUNCH(gemm4e_kernel<0, , 2);
     else if (sched == 3) G4LAUNCH(gemm4e_kernel<0, , 3);
+    else if (sched == 4) G4LAUNCH(gemm4e_kernel<0, , 4);
+    else if (sched == 5) G4LAUNCH(gemm4e_kernel<0, , 5);
     else G4LAUNCH(gemm4e_kernel<0);
 #undef G4ARGS
 #define G4ARGS (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, strideW, (bf16_t*)Y, ldy, offs, tile_end, G, N, K, gm
@@ -960,8 +1310,17 @@ int st_gemm4w_swiglu(const void* X, int64_t ldx, const void* W, int64_t ldw, voi
   if (grid >= (1LL << 31)) return -2;
   const char* oe = std::getenv("ST_GEMM4W_ORDER");
   const int gm = oe ? std::atoi(oe) : 4;
-  gemm4e_kernel<1, 0><<<(unsigned)grid, NT, 0, st>>>((const bf16_t*)X, ldx, (const bf16_t*)W, ldw, 0, (bf16_t*)GU,
-                                                     ldgu, nullptr, nullptr, 1, N, K, gm, (bf16_t*)H, ldh, I, T);
+  const char* ke = std::getenv("ST_GEMM4W_SWIGLU_KERNEL");  // f (default): stream-persistent, e: kind 5
+  if (K / BK >= 2 && !(ke && ke[0] == 'e')) {
+    const int64_t lg = std::min<int64_t>(grid, cu_count());
+    gemm4f_kernel<1><<<(unsigned)lg, NT, 0, st>>>((const bf16_t*)X, ldx, (const bf16_t*)W, ldw, 0, (bf16_t*)GU, ldgu,
+                                                  nullptr, nullptr, 1, N, K, gm, (bf16_t*)H, ldh, I, T, (int)grid);
+    return (int)hipGetLastError();
+  }
+  const int pv = persist_on() ? (int)grid : 0;
+  const int64_t lg = pv ? std::min<int64_t>(grid, cu_count()) : grid;
+  gemm4e_kernel<1, 0, 5><<<(unsigned)lg, NT, 0, st>>>((const bf16_t*)X, ldx, (const bf16_t*)W, ldw, 0, (bf16_t*)GU,
+                                                      ldgu, nullptr, nullptr, 1, N, K, gm, (bf16_t*)H, ldh, I, T, pv);
   return (int)hipGetLastError();
 }
 

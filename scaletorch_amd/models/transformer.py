@@ -111,8 +111,13 @@ class MLP(nn.Module):
         self.gate_up_proj = FusedColumnParallelLinear(cfg.hidden_size, [I, I], ["gate_proj", "up_proj"],
                                                       sequence_parallel=sequence_parallel, **init)
         self.down_proj = RowParallelLinear(I, cfg.hidden_size, sequence_parallel=sequence_parallel, **init)
-        # the fused SP MLP path reads both weights directly (DataParallel bucket waits)
-        self._st_reads = (self.gate_up_proj, self.down_proj)
+        # the fused SP MLP path reads both weights directly (DataParallel bucket waits); the
+        # other paths call both projections as modules (ST_MLP_WAIT_BOTH=0: each waits for its
+        # own bucket only -- A/B)
+        import os
+
+        if sequence_parallel or os.environ.get("ST_MLP_WAIT_BOTH", "1") == "1":
+            self._st_reads = (self.gate_up_proj, self.down_proj)
 
     def reset_parameters(self) -> None:
         self.gate_up_proj.reset_parameters()
@@ -126,11 +131,10 @@ class MLP(nn.Module):
             return sp_mlp(x, self.gate_up_proj.weight, self.down_proj.weight, self.gate_up_proj.group)
         gu_lin = self.gate_up_proj
         if gu_lin.tp == 1 and gu_lin.bias is None and not gu_lin.sequence_parallel:
-            from ..ops.mlp import gate_up_swiglu
+            from ..ops.mlp import gate_up_swiglu_ok
 
-            h = gate_up_swiglu(x, gu_lin.weight)  # one kernel: gate|up GEMM + SwiGLU epilogue
-            if h is not None:
-                return self.down_proj(h)
+            if gate_up_swiglu_ok(x, gu_lin.weight):  # one kernel: gate|up GEMM + SwiGLU epilogue
+                return self.down_proj(gu_lin(x, act="swiglu"))
         return self.down_proj(gu_lin(x), act="swiglu")
 
 

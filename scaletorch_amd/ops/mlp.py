@@ -152,21 +152,24 @@ def _gemm_swiglu_tiles(x2: torch.Tensor, weight: torch.Tensor) -> bool:
             and (256 + 32) * ldx * 2 < 2 ** 32 and I2 * ldw * 2 < 2 ** 32 and 0 < x2.shape[0] < 2 ** 31)
 
 
-def gate_up_swiglu(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor | None:
-    """``swiglu(x @ weight^T)`` for a fused [gate; up] weight in one kernel, or None when it
-    does not apply: opt-in ``ST_MLP_FUSED_SWIGLU=1`` (off by default), CPU, fp32, shapes the
-    kernel does not tile, the activation-recompute mode.  Measured (docs/PERF.md round 5,
-    profiles/r05/gemm4w/): the kernel runs the gate|up GEMM at 1.35-1.41 PF/s against
-    hipBLASLt's 1.37-1.50 there, so the absorbed SwiGLU pass does not pay for it yet --
-    4.29 vs 4.19 ms per layer, 967-972 vs 964-965 ms/step in the headline A/B."""
+def gate_up_swiglu_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    """Whether ``gate_up_swiglu`` runs the fused kernel for these operands: opt-in
+    ``ST_MLP_FUSED_SWIGLU=1`` (off by default), GPU bf16, shapes the kernel tiles, not the
+    activation-recompute mode.  Measured (docs/PERF.md round 5, profiles/r05/gemm4w/): the
+    kernel runs the gate|up GEMM at hipBLASLt's rate (4.19 vs 4.18 ms with the SwiGLU pass)
+    but the headline step is 8-10 ms slower with it -- the side-stream AdamW overlaps it worse."""
     import os
 
     if (os.environ.get("ST_MLP_FUSED_SWIGLU", "0") != "1" or os.environ.get("ST_MLP_RECOMPUTE_ACT", "0") == "1"
             or not x.is_cuda or not _lib.use_native(x) or x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16
             or weight.dim() != 2 or x.numel() == 0):
-        return None
-    if not _gemm_swiglu_tiles(x.reshape(-1, x.shape[-1]), weight):
-        return None
+        return False
+    return _gemm_swiglu_tiles(x.reshape(-1, x.shape[-1]), weight)
+
+
+def gate_up_swiglu(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """``swiglu(x @ weight^T)`` for a fused [gate; up] weight in ONE kernel (the caller checked
+    ``gate_up_swiglu_ok``); the weight gradient goes to ``weight.main_grad`` when present."""
     if torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad):
         return _GateUpSwiGLUFn.apply(x, weight)
     gu, h = _lib.ops().gemm_swiglu(x.reshape(-1, x.shape[-1]), weight)

@@ -1114,11 +1114,17 @@ class ColumnParallelLinear(nn.Module):
             nn.init.zeros_(self.bias)
 
     def forward(self, x: torch.Tensor, labels: torch.Tensor | None = None, chunk: int | None = None,
-                grad_scale: float | None = None) -> torch.Tensor:
+                grad_scale: float | None = None, act: str | None = None) -> torch.Tensor:
         """Logits shard ``[..., out/tp]``; with ``labels`` (LM head use) the mean
         vocab-parallel cross-entropy instead, fused and chunked so the logits are
-        never materialised (ops/fused_head.py).  Both run as a module call so the
-        forward pre-hook (optimizer-bucket wait) precedes every read of the weight."""
+        never materialised (ops/fused_head.py).  ``act="swiglu"`` (a fused gate|up weight,
+        the caller checked ``ops.mlp.gate_up_swiglu_ok``): silu(gate) * up from ONE kernel.
+        All run as a module call so the forward pre-hook (optimizer-bucket wait) precedes
+        every read of the weight."""
+        if act == "swiglu":
+            from ..ops.mlp import gate_up_swiglu
+
+            return gate_up_swiglu(x, self.weight)
         if labels is not None:
             from ..ops.fused_head import fused_linear_cross_entropy
 

@@ -760,7 +760,7 @@ def test_grouped_gemm_matches_per_expert(N, K, wn):
         off += n
 
 
-@pytest.mark.parametrize("T,K,I", [(300, 192, 128), (1000, 1024, 384)])
+@pytest.mark.parametrize("T,K,I", [(300, 192, 128), (1000, 1024, 384), (5000, 128, 4096)])  # last: 320 tiles, KT 2
 def test_gemm_swiglu_matches_fp32(T, K, I):
     """Dense gate|up GEMM with the SwiGLU epilogue (csrc/gemm4w.hip ``st_gemm4w_swiglu``) vs
     fp32: gu = x [W_gate; W_up]^T (one bf16 rounding) and h = silu(gate) * up of the stored
@@ -809,7 +809,7 @@ def test_mlp_fused_swiglu_matches_unfused():
         assert rel(a, b) < 2e-2
 
 
-@pytest.mark.parametrize("kind", ["0", "1", "2", "4", "5"])
+@pytest.mark.parametrize("kind", ["0", "1", "2", "4", "5", "6"])
 def test_gemm4w_variants_match_fp32(kind, monkeypatch):
     """The one-wave-per-SIMD GEMM experiment (csrc/gemm4w.hip; docs/PERF.md round 5) in each
     variant -- 2x2 register-staged, 1x4 direct weight fragments (2- / 3-deep), 2x2 LDS-DMA --
@@ -817,13 +817,14 @@ def test_gemm4w_variants_match_fp32(kind, monkeypatch):
     K = 192 (three 64-k tiles) and K = 1024."""
     monkeypatch.setenv("ST_GEMM4W_KIND", kind)
     torch.manual_seed(11)
-    for K, counts in ((192, [37, 0, 300, 1, 513]), (1024, [256, 700])):
+    # the last case has 320 tiles: a persistent workgroup (kinds 5, 6) walks several of them
+    for K, counts, N in ((192, [37, 0, 300, 1, 513], 512), (1024, [256, 700], 512), (192, [3000, 0, 1999, 1], 4096)):
         c = torch.tensor(counts, device="cuda", dtype=torch.int32)
         G, T = c.numel(), int(c.sum())
         offs = torch.cumsum(c, 0, dtype=torch.int32)
         xb = torch.randn(T, K + 64, device="cuda", dtype=torch.bfloat16)
         x = xb[:, 32:32 + K]
-        w = torch.randn(G, 512, K, device="cuda", dtype=torch.bfloat16)
+        w = torch.randn(G, N, K, device="cuda", dtype=torch.bfloat16)
         y = _lib.ops().gemm4w(x, w, offs)
         torch.cuda.synchronize()
         off = 0

@@ -16,7 +16,7 @@ for name, (T, K, N) in shapes.items():
     flops = 2.0 * T * K * N
     res = {}
     for rnd in range(3):
-        for kind in os.environ.get("G4_KINDS", "5").split(","):
+        for kind in os.environ.get("G4_KINDS", "5,6").split(","):
             for order, sched in [(o, sc) for o in os.environ.get("G4_ORDERS", "0,4,8").split(",")
                                  for sc in os.environ.get("G4_SCHEDS", "0").split(",")]:
                 os.environ["ST_GEMM4W_KIND"], os.environ["ST_GEMM4W_ORDER"] = kind, order
