@@ -69,6 +69,9 @@ int st_gemm4w(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t st
               const int* offs, const int* tile_end, int T, int G, int N, int K, hipStream_t st);
 int st_gemm4w_swiglu(const void* X, int64_t ldx, const void* W, int64_t ldw, void* GU, int64_t ldgu, void* H,
                      int64_t ldh, int T, int I, int K, hipStream_t st);
+int st_gemm4w_swiglu_grouped(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t strideW, void* GU,
+                             int64_t ldgu, void* H, int64_t ldh, const int* offs, const int* tile_end, int T, int G,
+                             int I, int K, hipStream_t st);
 int st_grouped_gemm_bm();
 int st_grouped_gemm(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t strideW, void* Y, int64_t ldy,
                     const int* offs, const int* tile_end, int T, int G, int N, int K, int wn, hipStream_t st);
@@ -531,6 +534,33 @@ std::vector<at::Tensor> gemm_swiglu(const at::Tensor& x, const at::Tensor& w) {
                             h.data_ptr(), h.stride(0), (int)T, (int)I, (int)K, cur_stream());
   if (rc == -2) return {};
   ST_CHECK_RC(rc, "gemm_swiglu");
+  return {gu, h};
+}
+
+// Grouped gate|up GEMM + SwiGLU epilogue on the one-wave-per-SIMD kernel (csrc/gemm4w.hip):
+// x [T, K], w [G, 2I, K], offs int32 [G] (inclusive); returns {gu [T, 2I], h [T, I]} (rows past
+// offs[G-1] unwritten), or {} when the kernel does not take the shape.
+std::vector<at::Tensor> gemm4w_swiglu_grouped(const at::Tensor& x, const at::Tensor& w, const at::Tensor& offs) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "w");
+  check_same_gpu(w, x, "w");
+  check_same_gpu(offs, x, "offs");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 3 && w.size(2) == x.size(1) && w.size(1) % 2 == 0,
+              "gemm4w_swiglu_grouped: x [T, K], w [G, 2I, K]");
+  TORCH_CHECK(offs.scalar_type() == at::kInt && offs.dim() == 1 && offs.is_contiguous() && offs.size(0) == w.size(0),
+              "gemm4w_swiglu_grouped: offs int32 [G]");
+  const int64_t T = x.size(0), K = x.size(1), G = w.size(0), I = w.size(1) / 2;
+  if (x.stride(1) != 1 || w.stride(2) != 1 || T == 0 || T > INT32_MAX || I > INT32_MAX / 2 || K > INT32_MAX) return {};
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  at::Tensor counts = at::diff(offs, 1, 0, at::zeros({1}, offs.options()));
+  at::Tensor tile_end = at::cumsum(at::floor_divide(counts + 255, 256), 0, at::kInt);
+  at::Tensor gu = at::empty({T, 2 * I}, x.options());
+  at::Tensor h = at::empty({T, I}, x.options());
+  int rc = st_gemm4w_swiglu_grouped(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(1), w.stride(0), gu.data_ptr(),
+                                    gu.stride(0), h.data_ptr(), h.stride(0), offs.data_ptr<int>(),
+                                    tile_end.data_ptr<int>(), (int)T, (int)G, (int)I, (int)K, cur_stream());
+  if (rc == -2) return {};
+  ST_CHECK_RC(rc, "gemm4w_swiglu_grouped");
   return {gu, h};
 }
 
@@ -1098,6 +1128,7 @@ TORCH_LIBRARY(st_amd, m) {
   m.def("grouped_gemm(Tensor x, Tensor w, Tensor offs, bool wn) -> Tensor");
   m.def("grouped_gemm_swiglu(Tensor x, Tensor w, Tensor offs) -> Tensor[]");
   m.def("gemm_swiglu(Tensor x, Tensor w) -> Tensor[]");
+  m.def("gemm4w_swiglu_grouped(Tensor x, Tensor w, Tensor offs) -> Tensor[]");
   m.def("gemm4w(Tensor x, Tensor w, Tensor offs) -> Tensor");
   m.def("grouped_gemm_dswiglu(Tensor dy, Tensor w, Tensor offs, Tensor gu) -> Tensor");
   m.def("xgmi_create(int rank, int world, int cap, int epoch_base) -> int", &xgmi_create);
@@ -1143,6 +1174,7 @@ TORCH_LIBRARY_IMPL(st_amd, CUDA, m) {
   m.impl("grouped_gemm", &grouped_gemm);
   m.impl("grouped_gemm_swiglu", &grouped_gemm_swiglu);
   m.impl("gemm_swiglu", &gemm_swiglu);
+  m.impl("gemm4w_swiglu_grouped", &gemm4w_swiglu_grouped);
   m.impl("gemm4w", &gemm4w);
   m.impl("grouped_gemm_dswiglu", &grouped_gemm_dswiglu);
   m.impl("qknorm_rope_fwd_", &qknorm_rope_fwd_);

@@ -1248,7 +1248,7 @@ int st_gemm4w(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t st
   const char* pe = std::getenv("ST_GEMM4W_PROBE");  // timing probes (wrong results)
   const int probe = pe ? std::atoi(pe) : 0;
   const char* ke = std::getenv("ST_GEMM4W_KIND");  // 0: 2 x 2 waves, 1 / 2: 1 x 4 (NS 2 / 3), 4 / 5: 2 x 2 LDS-DMA (rolling / whole-tile fragments)
-  const int kind = ke ? std::atoi(ke) : 0;
+  const int kind = ke ? std::atoi(ke) : 5;
   const char* oe = std::getenv("ST_GEMM4W_ORDER");  // slots per XCD group (0: slot-major)
   const int gm = oe ? std::atoi(oe) : 0;
 #define G4ARGS (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, strideW, (bf16_t*)Y, ldy, offs, tile_end, G, N, K, gm
@@ -1293,6 +1293,31 @@ int st_gemm4w(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t st
   else G4LAUNCH(gemm4b_kernel<2);
 #undef G4LAUNCH
 #undef G4ARGS
+  return (int)hipGetLastError();
+}
+
+// Grouped form of st_gemm4w_swiglu: rows [offs[g-1], offs[g]) use W[g] ([2I, K], gate rows then
+// up rows, stride strideW); tile_end = inclusive prefix of ceil(n_g / 256) (device).  Rows past
+// offs[G-1] are not written.  0 on success, -2 unsupported shape.
+int st_gemm4w_swiglu_grouped(const void* X, int64_t ldx, const void* W, int64_t ldw, int64_t strideW, void* GU,
+                             int64_t ldgu, void* H, int64_t ldh, const int* offs, const int* tile_end, int T, int G,
+                             int I, int K, hipStream_t st) {
+  if (T <= 0 || G <= 0 || I <= 0 || K <= 0 || K % BK || I % 128) return -2;
+  if (ldx % 8 || ldw % 8 || ldgu % 8 || ldh % 8 || strideW % 8 || ldx < K || ldw < K || ldgu < 2 * I || ldh < I)
+    return -2;
+  if (((uintptr_t)X | (uintptr_t)W | (uintptr_t)GU | (uintptr_t)H) % 16) return -2;
+  if (((int64_t)(BM + 32) * ldx) * 2 >= (int64_t)1 << 32) return -2;
+  if (((int64_t)2 * I * ldw) * 2 >= (int64_t)1 << 32) return -2;
+  const int N = 2 * I;
+  const int64_t grid = st_gemm4w_slots(T, G) * (N / BN);
+  if (grid >= (1LL << 31)) return -2;
+  const char* oe = std::getenv("ST_GEMM4W_ORDER");
+  const int gm = oe ? std::atoi(oe) : 0;
+  const int pv = persist_on() ? (int)grid : 0;
+  const int64_t lg = pv ? std::min<int64_t>(grid, cu_count()) : grid;
+  gemm4e_kernel<1, 0, 5><<<(unsigned)lg, NT, 0, st>>>((const bf16_t*)X, ldx, (const bf16_t*)W, ldw, strideW,
+                                                      (bf16_t*)GU, ldgu, offs, tile_end, G, N, K, gm, (bf16_t*)H, ldh,
+                                                      I, T, pv);
   return (int)hipGetLastError();
 }
 

@@ -555,6 +555,19 @@ def _gmm_fallback(x: torch.Tensor, w: torch.Tensor, offs: torch.Tensor, wn: bool
     return y
 
 
+def _gemm4w_ok(x: torch.Tensor, w: torch.Tensor, N: int) -> bool:
+    """The one-wave-per-SIMD kernel (csrc/gemm4w.hip) takes this [G, N, K] expert GEMM and wins
+    on it: long K (>= 4,096: Mixtral's experts, +8-12 % over the 8-phase grouped kernel; at
+    Qwen3-MoE's K 768 / 2,048 the grouped kernel is ahead -- tools/bench_grouped_gemm.py,
+    profiles/r05/gemm4w/grouped_vs_gemm4w.log).  ``ST_MOE_GEMM4W=0``: off (A/B)."""
+    from ..ops import _lib
+
+    K = x.shape[1]
+    return (os.environ.get("ST_MOE_GEMM4W", "1") == "1" and _lib.use_native(x) and x.dtype == torch.bfloat16
+            and x.stride(1) == 1 and x.stride(0) % 8 == 0 and w.is_contiguous() and K % 64 == 0 and K >= 4096
+            and N % 256 == 0 and x.shape[0] > 0)
+
+
 def _gmm(x: torch.Tensor, w: torch.Tensor, offs: torch.Tensor, wn: bool) -> torch.Tensor:
     """Per-expert ``x[rows of g] @ (w[g] if wn else w[g]^T)`` with device offsets: ONE launch
     of csrc/grouped_gemm.hip.  ``ST_MOE_HIP_GMM=0``, or a shape the kernel does not tile
@@ -565,6 +578,10 @@ def _gmm(x: torch.Tensor, w: torch.Tensor, offs: torch.Tensor, wn: bool) -> torc
 
     K = x.shape[1]
     N = w.shape[2] if wn else w.shape[1]
+    if not wn and _gemm4w_ok(x, w, N):
+        y = _lib.ops().gemm4w(x, w, offs)
+        if y is not None:
+            return y
     if (os.environ.get("ST_MOE_HIP_GMM", "1") == "1" and _lib.use_native(x) and x.dtype == torch.bfloat16
             and x.stride(1) == 1 and x.stride(0) % 8 == 0 and w.is_contiguous() and K % 64 == 0 and N % 128 == 0
             and x.shape[0] > 0):
@@ -581,6 +598,10 @@ def _gmm_swiglu(x: torch.Tensor, w_gu: torch.Tensor, offs: torch.Tensor):
     from ..ops import _lib
 
     K, N = x.shape[1], w_gu.shape[1]
+    if os.environ.get("ST_MOE_FUSED_SWIGLU", "1") == "1" and (N // 2) % 128 == 0 and _gemm4w_ok(x, w_gu, N):
+        out = _lib.ops().gemm4w_swiglu_grouped(x, w_gu, offs)
+        if out:
+            return out[0], out[1]
     if (os.environ.get("ST_MOE_FUSED_SWIGLU", "1") == "1" and _lib.use_native(x) and x.dtype == torch.bfloat16
             and x.stride(1) == 1 and x.stride(0) % 8 == 0 and w_gu.is_contiguous() and K % 64 == 0
             and N % 256 == 0 and x.shape[0] > 0):

@@ -778,6 +778,62 @@ def test_gemm_swiglu_matches_fp32(T, K, I):
     assert torch.equal(h, _lib.ops().swiglu_fwd(gu))
 
 
+def test_gemm4w_swiglu_grouped_matches_fp32():
+    """Grouped gate|up GEMM + SwiGLU epilogue on the one-wave-per-SIMD kernel (the long-K MoE
+    forward, models/moe.py ``_gmm_swiglu``): per-expert fp32 references, an empty expert, a
+    ragged tail, R_max padding rows untouched by the check."""
+    torch.manual_seed(15)
+    counts = [300, 0, 513, 77]
+    G, K, I = len(counts), 4096, 256
+    offs = torch.cumsum(torch.tensor(counts, device="cuda", dtype=torch.int32), 0, dtype=torch.int32)
+    T = sum(counts) + 40
+    x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(G, 2 * I, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
+    gu, h = _lib.ops().gemm4w_swiglu_grouped(x, w, offs)
+    torch.cuda.synchronize()
+    off = 0
+    for e, n in enumerate(counts):
+        if n:
+            ref = x[off:off + n].float() @ w[e].float().t()
+            assert rel(gu[off:off + n].float(), ref) < 1e-2, e
+            assert torch.equal(h[off:off + n], _lib.ops().swiglu_fwd(gu[off:off + n].contiguous())), e
+        off += n
+
+
+def test_expert_ffn_gemm4w_matches_grouped():
+    """_ExpertFFNFn at K 4,096 (Mixtral-like: the forward GEMMs take csrc/gemm4w.hip) equals the
+    8-phase grouped-kernel path (ST_MOE_GEMM4W=0) on outputs, dx and both fp32 weight grads."""
+    import os
+
+    from scaletorch_amd.models.moe import _ExpertFFNFn
+
+    G, K, I = 3, 4096, 256
+    counts = [300, 0, 529]
+    offs = torch.cumsum(torch.tensor(counts, device="cuda", dtype=torch.int32), 0, dtype=torch.int32)
+    T = sum(counts) + 17
+    res = {}
+    for on in ("1", "0"):
+        os.environ["ST_MOE_GEMM4W"] = on
+        try:
+            torch.manual_seed(16)
+            x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+            w_gu = torch.nn.Parameter(torch.randn(G, 2 * I, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5)
+            w_dn = torch.nn.Parameter(torch.randn(G, K, I, device="cuda", dtype=torch.bfloat16) / I ** 0.5)
+            for w in (w_gu, w_dn):
+                w.main_grad = torch.zeros(w.shape, device="cuda")
+                w._st_fresh = True
+            xin = x * 1
+            xin._st_padded = True
+            y = _ExpertFFNFn.apply(xin, offs, w_gu, w_dn)
+            y.backward(torch.randn(y.shape, device="cuda", generator=torch.Generator("cuda").manual_seed(4)).to(y.dtype))
+            v = sum(counts)
+            res[on] = (y[:v].float(), x.grad[:v].float(), w_gu.main_grad.clone(), w_dn.main_grad.clone())
+        finally:
+            os.environ.pop("ST_MOE_GEMM4W", None)
+    for a, b in zip(res["1"], res["0"]):
+        assert rel(a, b) < 2e-2
+
+
 def test_mlp_fused_swiglu_matches_unfused():
     """The Llama MLP with the fused gate|up + SwiGLU kernel (ops.mlp.gate_up_swiglu,
     ST_MLP_FUSED_SWIGLU=1) equals the unfused path (hipBLASLt GEMM + swiglu kernel) on the

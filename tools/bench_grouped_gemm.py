@@ -22,7 +22,10 @@ SHAPES = [  # name, G, rows per expert, K, N, wn
     ("mixtral_down_fwd", 8, 2048, 14336, 4096, False),
     ("mixtral_down_dgrad", 8, 2048, 4096, 14336, True),
     ("mixtral_gate_up_dgrad", 8, 2048, 28672, 4096, True),
+    ("mixtral_1gpu_gate_up_fwd", 8, 1024, 4096, 28672, False),
+    ("mixtral_1gpu_down_fwd", 8, 1024, 14336, 4096, False),
     ("qwen3moe_gate_up_fwd", 128, 512, 2048, 1536, False),
+    ("qwen3moe_down_fwd", 128, 512, 768, 2048, False),
     ("qwen3moe_down_dgrad", 128, 512, 2048, 768, True),
     # dense Llama-3-8B data gradients at micro-batch 6 (G = 1): dX = dY W, W [out, in] = [K][N]
     ("llama_qkv_dgrad", 1, 24576, 6144, 4096, True),
@@ -68,6 +71,18 @@ def main() -> int:
             "torch_grouped_mm": lambda: torch._grouped_mm(x, w if wn else w.transpose(-2, -1), offs=offs),
             "dense_hipblaslt": lambda: torch.matmul(x, w[0] if wn else w[0].t()),
         }
+        if not wn and N % 256 == 0 and K % 64 == 0:  # the one-wave-per-SIMD kernel (csrc/gemm4w.hip)
+            def g4(order):
+                def run():
+                    os.environ["ST_GEMM4W_KIND"], os.environ["ST_GEMM4W_ORDER"] = "5", order
+                    try:
+                        return _lib.ops().gemm4w(x, w, offs)
+                    finally:
+                        os.environ.pop("ST_GEMM4W_KIND", None)
+                        os.environ.pop("ST_GEMM4W_ORDER", None)
+                return run
+            arms["gemm4w_k5_o0"] = g4("0")
+            arms["gemm4w_k5_o4"] = g4("4")
         if not wn and "gate_up" in name:  # SwiGLU epilogue: gu and a = silu(g) * u from the GEMM
             arms["hip_grouped_swiglu_epilogue"] = lambda: _lib.ops().grouped_gemm_swiglu(x, w, offs)
             arms["hip_grouped_swiglu_epilogue_2phase"] = two_phase(lambda: _lib.ops().grouped_gemm_swiglu(x, w, offs))
