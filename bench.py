@@ -378,6 +378,12 @@ def main() -> int:
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
+        if os.environ.get("ST_WGRAD_TUNE_LOG") == "1":  # the per-shape weight-gradient picks (stderr)
+            from scaletorch_amd.ops import grad as G
+
+            for k, v in G._WGRAD_TIMES.items():
+                print("wgrad tune", k[0], k[2], {a: round(b, 3) for a, b in v.items()}, "->", G._WGRAD_CHOICE.get(k),
+                      file=sys.stderr, flush=True)
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()

@@ -644,8 +644,13 @@ int plan(int M, int N, int T, int variant, Launch& L) {
 
 extern "C" {
 
+int st_wgrad4(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int M, int N, int T,
+              int beta, float* ws, hipStream_t st);
+int64_t st_wgrad4_ws_elems(int M, int N, int T);
+
 // fp32 workspace elements the tail split of this launch needs (0: none).
 int64_t st_wgrad_ws_elems(int M, int N, int T, int variant) {
+  if ((variant & 15) == 6) return (variant & 16) ? 0 : st_wgrad4_ws_elems(M, N, T);  // csrc/wgrad4.hip
   Launch L;
   if (plan(M, N, T, variant, L) || L.split <= 1) return 0;
   return (int64_t)(L.split - 1) * L.tail * BM * L.bn;
@@ -653,10 +658,12 @@ int64_t st_wgrad_ws_elems(int M, int N, int T, int variant) {
 
 // 0 on success; -2: shape not supported by this kernel (caller falls back).
 // variant: 0 = default (the 4-stage kernel, or the 8-phase one when ST_WGRAD_P8=1),
-// 1 = the 4-stage kernel, 2 = the 8-phase kernel (ops/grad.py times them per shape);
+// 1 = the 4-stage kernel, 2 = the 8-phase kernel, 6 = csrc/wgrad4.hip (ops/grad.py times them per shape);
 // + 16 = without the tail split.  ws: st_wgrad_ws_elems(...) fp32 elements (may be null when that is 0).
 int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int M,
                   int N, int T, int beta, int variant, float* ws, hipStream_t st) {
+  if ((variant & 15) == 6)  // csrc/wgrad4.hip (+16: tail split off, no workspace)
+    return st_wgrad4(A, lda, B, ldb, C, ldc, M, N, T, beta, (variant & 16) ? nullptr : ws, st);
   Launch L;
   if (plan(M, N, T, variant, L)) return -2;
   if (lda % 8 || ldb % 8 || lda < M || ldb < N || ldc < N) return -2;

@@ -279,7 +279,9 @@ def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> int:
     scratch = torch.zeros(M, N, dtype=torch.float32, device=dy2d.device)
     # +16: the same kernel without the tail split (csrc/wgrad_gemm.hip), where the last
     # partial round of tiles is left partly idle instead of being cut into token ranges
-    arms = {v: (lambda v=v: _lib.ops().wgrad_gemm_(scratch, dy2d, x2d, 1, v)) for v in (1, 2, 17, 18)
+    # 6: the one-wave-per-SIMD kernel (csrc/wgrad4.hip)
+    hip_arms = (1, 2, 6, 17, 18, 22) if os.environ.get("ST_WGRAD4", "1") == "1" else (1, 2, 17, 18)
+    arms = {v: (lambda v=v: _lib.ops().wgrad_gemm_(scratch, dy2d, x2d, 1, v)) for v in hip_arms
             if _lib.ops().wgrad_gemm_(scratch, dy2d, x2d, 0, v)}
     if not arms:
         _WGRAD_CHOICE[key] = 0
@@ -408,8 +410,8 @@ def wgrad_into(out: torch.Tensor, dy2d: torch.Tensor, x2d: torch.Tensor, beta: i
         from . import _lib
 
         if _lib.use_native(dy2d):
-            forced = os.environ.get("ST_WGRAD_VARIANT", "")  # 0-5 / 17 / 18 overrides the pick (A/B)
-            if forced in ("0", "1", "2", "3", "4", "5", "17", "18"):
+            forced = os.environ.get("ST_WGRAD_VARIANT", "")  # 0-6 / 17 / 18 overrides the pick (A/B)
+            if forced in ("0", "1", "2", "3", "4", "5", "6", "17", "18"):
                 variant = int(forced)
             elif variant is None:
                 variant = _wgrad_pick(dy2d, x2d)

@@ -528,6 +528,37 @@ def test_wgrad_gemm_tail_split(T, M, N, beta, split, variant, bn, monkeypatch):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("split", ["1", "auto"])
+@pytest.mark.parametrize("T,M,N", [(512, 4096, 4352), (512, 6144, 4096), (256, 512, 1024), (1024, 256, 256),
+                                   (256, 768, 1280)])
+def test_wgrad4_matches_fp32(T, M, N, split, monkeypatch):
+    """csrc/wgrad4.hip (variant 6): persistent one-wave-per-SIMD tiles, several per workgroup;
+    qkv-like 384 tiles (the last 128 split along K, the partials of ranges 1.. added in order by
+    the tail reduce), sub-round grids; beta 0 over garbage then beta 1 accumulate, on a strided
+    (ldc > N) output as well; bitwise repeatable."""
+    if split != "auto":
+        monkeypatch.setenv("ST_WGRAD4_SPLIT", split)
+    torch.manual_seed(4)
+    dy = torch.randn(T, M, device="cuda", dtype=torch.bfloat16)
+    x = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+    ref = dy.float().t() @ x.float()
+    for ldc in (N, N + 256):
+        big = torch.full((M, ldc), 7.0, device="cuda")
+        out = big[:, :N]
+        assert _lib.ops().wgrad_gemm_(out, dy, x, 0, 6)
+        torch.cuda.synchronize()
+        assert rel(out, ref) < 1e-5
+        assert _lib.ops().wgrad_gemm_(out, dy, x, 1, 6)
+        torch.cuda.synchronize()
+        assert rel(out, 2 * ref) < 1e-5
+        if ldc > N:
+            assert torch.all(big[:, N:] == 7.0)
+        again = torch.zeros(M, N, device="cuda")
+        assert _lib.ops().wgrad_gemm_(again, dy, x, 0, 6)
+        assert _lib.ops().wgrad_gemm_(again, dy, x, 1, 6)
+        assert torch.equal(again, out)
+
+
 @pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("T", [1, 37, 100, 1000, 2047, 2100])
 def test_wgrad_gemm_ragged_tokens(T, variant):

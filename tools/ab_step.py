@@ -96,7 +96,7 @@ def main() -> int:
         print("wgrad tune", k[0], k[2], {a: round(b, 3) for a, b in v.items()}, "->",
               {0: "hipblaslt", 1: "hip 4-stage", 2: "hip 8-phase", 17: "hip 4-stage no split",
                18: "hip 8-phase no split", 3: "hipblaslt one-T", 4: "tuned hipblaslt",
-               5: "tuned hipblaslt one-T"}.get(G._WGRAD_CHOICE.get(k), "?"))
+               5: "tuned hipblaslt one-T", 6: "hip one-wave-per-SIMD"}.get(G._WGRAD_CHOICE.get(k), "?"))
     print(json.dumps({v: round(statistics.median(t), 2) for v, t in times.items()}))
     return 0
 
