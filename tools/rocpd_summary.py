@@ -20,7 +20,8 @@ import sqlite3
 import sys
 
 CLASSES = [  # (class, regex on the kernel name), first match wins
-    ("gemm_wgrad_hip", r"wgrad8_kernel|wgrad_gemm_kernel|wgrad_tail_reduce"),
+    ("gemm_wgrad_hip", r"wgrad8_kernel|wgrad_gemm_kernel|wgrad_tail_reduce|wgrad4_kernel|wgrad4_tail_reduce"),
+    ("gemm_hip(gemm4w)", r"gemm4[a-z_]*kernel|gemm4[bdef]"),
     ("gemm_fp32_out(wgrad_hipblaslt)", r"Cijk_.*_BSS_|Cijk_.*BBS_BS_"),
     ("gemm_bf16(fwd+dgrad)", r"Cijk_"),
     ("grouped_gemm(experts)", r"grouped|Grouped"),
