@@ -533,6 +533,208 @@ __global__ __launch_bounds__(256 * HP, 2 / HP) void flash_fwd_kernel(AttnParams 
   }
 }
 
+// ============================================================== forward, 64 queries per wave
+// Opt-in experiment (ST_FLASH_FWD_W64=1), recorded: each wave owns TWO 32-query blocks (256
+// queries per workgroup, one workgroup per CU), so every K / V^T fragment read feeds two MFMAs
+// -- half the LDS bytes per FLOP of the 4-wave kernel above.  Bitwise equal to it, but 40 %
+// slower at the bench shape (1.18 vs 0.84 ms, profiles/r05/flash/fwd_w64_vs_w32.log): the
+// 4-wave kernel's 1 KiB per 32-cycle MFMA is only half of gfx950's 256 B/clk LDS array, so
+// LDS bandwidth was not its limit, and at one wave per SIMD nothing overlaps the softmax VALU
+// and the barrier waits with the MFMAs (two co-resident 4-wave workgroups do).  The O accumulators (2 x D/32 tiles) are pinned to AGPRs; Q, S and
+// the P fragments stay in VGPRs.  A wave skips the MFMA / softmax work of key blocks wholly
+// past its own last query (it still takes part in the tile DMA and barriers).
+template <int D, bool XCD = true>
+__global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(AttnParams p, bf16_t* __restrict__ o,
+                                                               int64_t sob, int64_t sos, int64_t soh,
+                                                               float* __restrict__ lse) {
+  constexpr int BM = 256, BN = 64, NKK = D / 16, NDT = D / 32;
+  constexpr int TB = BN * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];  // K0 K1 V0 V1
+  lds_t* smem = (lds_t*)smem_raw;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int nqt = (p.Sq + BM - 1) / BM, id = blockIdx.x;
+  int rank, b, hq;
+  const int G = p.H / p.Hkv, BHk = p.B * p.Hkv;
+  if (XCD && BHk % 8 == 0) {  // as flash_fwd_kernel: XCD x takes the kv heads = x mod 8
+    const int j = id >> 3, per_rank = (BHk >> 3) * G, rem = j % per_rank;
+    rank = j / per_rank;
+    const int bhk = (id & 7) + 8 * (rem / G);
+    b = bhk / p.Hkv;
+    hq = (bhk % p.Hkv) * G + rem % G;
+  } else {
+    const int BH = p.B * p.H;
+    rank = id / BH;
+    b = (id % BH) / p.H;
+    hq = id % p.H;
+  }
+  const int qt = p.causal ? nqt - 1 - rank : rank;
+  const int hk = hq / G;
+  const int q0 = qt * BM, wq0 = q0 + wid * 64;
+
+  const rsrc_t rq = make_rsrc(p.q + (int64_t)b * p.sqb + (int64_t)hq * p.sqh, p.Sq, p.sqs, D);
+  const rsrc_t rk = make_rsrc(p.k + (int64_t)b * p.skb + (int64_t)hk * p.skh, p.Sk, p.sks, D);
+  const rsrc_t rv = make_rsrc(p.v + (int64_t)b * p.svb + (int64_t)hk * p.svh, p.Sk, p.svs, D);
+
+  bfx8 qf[2][NKK];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk)
+      qf[qb][kk] = bload_frag(rq, (uint32_t)(wq0 + 32 * qb + r) * (uint32_t)(p.sqs * 2) + (2 * kk + h) * 16);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): see flash_fwd_kernel
+  int nkb, kb_mask, wnkb, wmask;
+  key_blocks<BM, BN>(p, q0, true, nkb, kb_mask);
+  key_blocks<64, BN>(p, wq0, true, wnkb, wmask);  // this wave's own range (wave-uniform)
+
+  LdsAddr<D> la;
+  la.init(lane);
+  DmaStager<D, BN, 4> sk, sv;
+  sk.init(wid, lane, p.sks);
+  sv.init(wid, lane, p.svs);
+
+  f32x16 oacc[2][NDT];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) oacc[qb][dt] = zero16();
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  const float c2 = p.scale * kLog2e;
+  const int64_t qg0 = p.q_offset + wq0 + r;
+
+  if (nkb > 0) {
+    sk.load(rk, smem, 0);
+    sv.load(rv, smem + 2 * TB, 0);
+  }
+  dma_barrier();
+
+  auto step = [&](auto bufc, int kb) {
+    constexpr int BUF = decltype(bufc)::value;
+    if (kb + 1 < nkb) {
+      sk.load(rk, smem + (BUF ^ 1) * TB, (kb + 1) * BN);
+      sv.load(rv, smem + (2 + (BUF ^ 1)) * TB, (kb + 1) * BN);
+    }
+    if (kb < wnkb) {
+      const lds_t* kt = smem + BUF * TB;
+      const lds_t* vt = smem + (2 + BUF) * TB;
+      f32x16 sc[2][2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) sc[qb][0] = sc[qb][1] = zero16();
+      bfx8 fk[NKK][2];
+      fk[0][0] = la.rowf(kt, 0, 0);
+      fk[0][1] = la.rowf(kt, 1, 0);
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        if (kk + 1 < NKK) {
+          fk[kk + 1][0] = la.rowf(kt, 0, kk + 1);
+          fk[kk + 1][1] = la.rowf(kt, 1, kk + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          sc[qb][0] = mfma(fk[kk][0], qf[qb][kk], sc[qb][0]);
+          sc[qb][1] = mfma(fk[kk][1], qf[qb][kk], sc[qb][1]);
+        }
+      }
+      bfx8 pf[2][4];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        f32x16& s0 = sc[qb][0];
+        f32x16& s1 = sc[qb][1];
+        if (kb >= wmask) {
+          const int lim = key_limit(p, kb, BN, qg0 + 32 * qb, h, true);
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            if (acc_row0(i) > lim) s0[i] = -INFINITY;
+            if (acc_row0(i) + 32 > lim) s1[i] = -INFINITY;
+          }
+        }
+        float mx0 = fmaxf(s0[0], s1[0]), mx1 = fmaxf(s0[1], s1[1]);
+#pragma unroll
+        for (int i = 2; i < 16; i += 2) {
+          mx0 = fmaxf(mx0, fmaxf(s0[i], s1[i]));
+          mx1 = fmaxf(mx1, fmaxf(s0[i + 1], s1[i + 1]));
+        }
+        float mx = fmaxf(mx0, mx1);
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mxs = mx * c2;
+        if (__any(mxs > m[qb] + kRescaleThr)) {
+          const float m_new = fmaxf(m[qb], mxs);
+          const float alpha = (m[qb] == m_new) ? 1.f : fast_exp2(m[qb] - m_new);
+          l[qb] *= alpha;
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) oacc[qb][dt][i] *= alpha;
+          m[qb] = m_new;
+        }
+        const float mu = (m[qb] == -INFINITY) ? 0.f : m[qb];
+        float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+          s0[i] = fast_exp2(fmaf(s0[i], c2, -mu));
+          s1[i] = fast_exp2(fmaf(s1[i], c2, -mu));
+          s0[i + 1] = fast_exp2(fmaf(s0[i + 1], c2, -mu));
+          s1[i + 1] = fast_exp2(fmaf(s1[i + 1], c2, -mu));
+          r0 += s0[i];
+          r1 += s1[i];
+          r2 += s0[i + 1];
+          r3 += s1[i + 1];
+        }
+        float rs = (r0 + r1) + (r2 + r3);
+        rs += __shfl_xor(rs, 32, 64);
+        l[qb] += rs;
+        pf[qb][0] = acc_frag(s0, 0);
+        pf[qb][1] = acc_frag(s0, 1);
+        pf[qb][2] = acc_frag(s1, 0);
+        pf[qb][3] = acc_frag(s1, 1);
+      }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const bfx8 v0 = la.trf(vt, 0, 0, dt), v1 = la.trf(vt, 0, 1, dt);
+        const bfx8 v2 = la.trf(vt, 32, 0, dt), v3 = la.trf(vt, 32, 1, dt);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          mfma_acc(oacc[qb][dt], v0, pf[qb][0]);
+          mfma_acc(oacc[qb][dt], v1, pf[qb][1]);
+          mfma_acc(oacc[qb][dt], v2, pf[qb][2]);
+          mfma_acc(oacc[qb][dt], v3, pf[qb][3]);
+        }
+      }
+    }
+    dma_barrier();
+  };
+  int kb = 0;
+  for (; kb + 1 < nkb; kb += 2) {
+    step(Buf<0>(), kb);
+    step(Buf<1>(), kb + 1);
+  }
+  if (kb < nkb) step(Buf<0>(), kb);
+  agpr_fence(oacc[0]);
+  agpr_fence(oacc[1]);
+
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int my_q = wq0 + 32 * qb + r;
+    if (my_q < p.Sq) {
+      const float inv = l[qb] > 0.f ? 1.f / l[qb] : 0.f;
+      bf16_t* orow = o + (int64_t)b * sob + (int64_t)my_q * sos + (int64_t)hq * soh;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = 32 * dt + 8 * g + 4 * h;
+          uint2 w;
+          w.x = pack_bf16x2(oacc[qb][dt][4 * g + 0] * inv, oacc[qb][dt][4 * g + 1] * inv);
+          w.y = pack_bf16x2(oacc[qb][dt][4 * g + 2] * inv, oacc[qb][dt][4 * g + 3] * inv);
+          *reinterpret_cast<uint2*>(orow + d) = w;
+        }
+      }
+      if (h == 0)
+        lse[((int64_t)b * p.H + hq) * p.Sq + my_q] = l[qb] > 0.f ? (m[qb] * kLn2 + __logf(l[qb])) : -INFINITY;
+    }
+  }
+}
+
 // ============================================================== forward, 8-wave ping-pong
 // 256 queries per workgroup in two groups of 4 waves (A = waves 0-3, queries
 // 0-127; B = waves 4-7, queries 128-255); wave w and w+4 share a SIMD.  Every key
@@ -1630,9 +1832,16 @@ int st_flash_fwd(const void* q, const void* k, const void* v, void* o, float* ls
   // 0.852 vs 0.853 ms, profiles/r03/flash_pmc.md), so one head stays the default.
   const char* he = std::getenv("ST_FLASH_FWD_HP");
   const bool hp2 = (H / Hkv) % 2 == 0 && he && std::atoi(he) == 2;
+  // ST_FLASH_FWD_W64=1: 64 queries per wave (half the LDS bytes per MFMA), D = 128
+  const char* we = std::getenv("ST_FLASH_FWD_W64");
+  const bool w64 = D == 128 && we && std::atoi(we) == 1;
   if (D == 128 && pp) {
     const unsigned grid2 = (unsigned)(((Sq + 255) / 256) * B * H);
     flash_fwd_pp_kernel<128><<<grid2, 512, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
+  } else if (w64) {
+    const unsigned grid4 = (unsigned)(((Sq + 255) / 256) * B * H);
+    if (xcd) flash_fwd_w64_kernel<128, true><<<grid4, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
+    else flash_fwd_w64_kernel<128, false><<<grid4, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
   } else if (hp2) {
     const unsigned grid2 = grid / 2;
     if (D == 128 && xcd) flash_fwd_kernel<128, true, 2><<<grid2, 512, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);

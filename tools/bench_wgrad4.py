@@ -24,6 +24,7 @@ assert _lib.ops().wgrad_gemm_(out, dy, x, 1, 6)
 e1 = ((out - 2 * ref).norm() / (2 * ref).norm()).item()
 print("numerics", json.dumps({"rel_err_beta0": e0, "rel_err_beta1": e1}), flush=True)
 
+ORDERS = [o for o in os.environ.get("W4_ORDERS", "").split(",") if o]  # XCD-grouped tile orders to time
 SHAPES = {"qkv": (24576, 6144, 4096), "o": (24576, 4096, 4096), "gate_up": (24576, 28672, 4096),
           "down": (24576, 4096, 14336), "lm_head_chunk": (4096, 128256, 4096)}
 for name, (T, M, N) in SHAPES.items():
@@ -37,6 +38,12 @@ for name, (T, M, N) in SHAPES.items():
         os.environ.pop("ST_WGRAD4_SPLIT")
 
     arms["hip_v6_nosplit"] = v6_nosplit
+    for gm in ORDERS:
+        def v6_order(gm=gm):
+            os.environ["ST_WGRAD4_ORDER"] = gm
+            _lib.ops().wgrad_gemm_(out, dy, x, 1, 6)
+            os.environ.pop("ST_WGRAD4_ORDER")
+        arms[f"hip_v6_order{gm}"] = v6_order
     arms["hipblaslt"] = lambda: torch.ops.aten.addmm.dtype_out(out, dy.t(), x, torch.float32, beta=1, alpha=1, out=out)
     res = {}
     for rnd in range(3):
