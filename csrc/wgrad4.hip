@@ -86,13 +86,17 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
                                                        const bf16_t* __restrict__ B, int64_t ldb,
                                                        float* __restrict__ C, int64_t ldc, int M, int N, int T,
                                                        int beta, int gm, int nfull, int splits,
-                                                       float* __restrict__ ws) {
+                                                       float* __restrict__ ws, const int* __restrict__ offs,
+                                                       int64_t strideC) {
   __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
   lds_t* smem = (lds_t*)smem_raw;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wid >> 1, wn = wid & 1;
-  const int nbm = M / BT, nbn = N / BT, nv = nbm * nbn, KT = (T + BK - 1) / BK;
+  // offs != null: grouped (MoE experts) -- unit u is (expert u / tiles, tile u % tiles), expert g's
+  // tokens are rows [offs[g-1], offs[g]) of A / B and its output C + g strideC
+  const int nbm = M / BT, nbn = N / BT, tiles = nbm * nbn;
+  const int nv = offs ? 0 : tiles;
   const uint32_t sa = (uint32_t)(lda * 2), sb = (uint32_t)(ldb * 2);
 
   // DMA: wave w fills rows 16 w .. 16 w + 15 of every image, 4 pieces (4 rows, 1 KiB) each;
@@ -108,13 +112,23 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
   const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem + (uint32_t)(wid * 4 * 1024));
   auto piece_m0 = [&](int buf, int p) { return lbase + buf * STAGE + (p >> 2) * IMGW + (p & 3) * 1024; };
   auto set_m0 = [&](uint32_t v) { asm volatile("s_mov_b32 m0, %0" : : "s"(v) : "m0"); };
-  // kt-th K-tile: scalar offsets kt * 64 rows of each operand
-  auto dma_nom0 = [&](rsrc_t ra, rsrc_t rb, int kt, int p) {
-    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)kt * (uint32_t)BK * (p < 8 ? sa : sb));
+  // descriptors over K-tile kt onward of an operand slice: base advanced by kt * 64 rows, range
+  // = the rows left, so a ragged last K-tile reads zeros past the token count (the range check
+  // covers the VGPR offset only -- the K offset lives in the base, not in soffset)
+  struct Krs {
+    rsrc_t a, b;
+  };
+  auto krs = [&](const bf16_t* abase, const bf16_t* bbase, int rows, int kt) {
+    const int left = rows - kt * BK;
+    const uint32_t ba = left > 0 ? (uint32_t)(((int64_t)(left - 1) * lda + BT) * 2) : 0u;
+    const uint32_t bb = left > 0 ? (uint32_t)(((int64_t)(left - 1) * ldb + BT) * 2) : 0u;
+    return Krs{make_rsrc(abase + (int64_t)kt * BK * lda, ba), make_rsrc(bbase + (int64_t)kt * BK * ldb, bb)};
+  };
+  auto dma_nom0 = [&](const Krs& k, int p) {
     if (p < 8)
-      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(voff[p]), "s"(ra), "s"(so) : "memory");
+      asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" : : "v"(voff[p]), "s"(k.a) : "memory");
     else
-      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(voff[p]), "s"(rb), "s"(so) : "memory");
+      asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" : : "v"(voff[p]), "s"(k.b) : "memory");
   };
 
   // fragment reads (16 features x 32 tokens, natural k order permuted the same way for both
@@ -149,8 +163,11 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
     if (m >= 64 && m <= 120 && ((m - 64) & 7) == 0) return 8 + ((m - 64) >> 3);
     return -1;
   };
-  auto step = [&](f32x4 (&acc)[8][8], auto more_c, auto more2_c, int kt, rsrc_t ra, rsrc_t rb) {
+  auto step = [&](f32x4 (&acc)[8][8], auto more_c, auto more2_c, int kt, const bf16_t* abase, const bf16_t* bbase,
+                  int rows) {
     constexpr bool more = decltype(more_c)::value, more2 = decltype(more2_c)::value;
+    Krs k2{};
+    if constexpr (decltype(more2_c)::value) k2 = krs(abase, bbase, rows, kt + 2);
     const lds_t* cs = smem + (kt & 1) * STAGE;
     const lds_t* ns = smem + ((kt + 1) & 1) * STAGE;
     __builtin_amdgcn_s_setprio(1);
@@ -187,7 +204,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
       }
       if constexpr (more2 && pd >= 0) {
         fence();
-        dma_nom0(ra, rb, kt + 2, pd);
+        dma_nom0(k2, pd);
         fence();
       }
       if constexpr (more && m >= 64 && m < 96 && (m & 1) == 0) {
@@ -202,10 +219,33 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
   // work units: tiles 0 .. nfull - 1 whole, then the tail tiles as `splits` K ranges each
   // (split-major); range 0 lands in C, range s > 0 in workspace tile (s - 1, tl), added in order
   // by wgrad4_tail_reduce
-  const int nu = nfull + (nv - nfull) * splits, tail = nv - nfull;
+  const int nu = offs ? nfull : nfull + (nv - nfull) * splits, tail = nv - nfull;
   for (int u = (int)blockIdx.x; u < nu; u += (int)gridDim.x) {
     if (u != (int)blockIdx.x) __syncthreads();  // every wave past the previous tile's LDS reads
-    int vb = u, kb = 0, ke = KT, sidx = 0, tl = 0;
+    const bf16_t* Ag = A;
+    const bf16_t* Bg = B;
+    float* Cg = C;
+    int Tg = T, vb = u;
+    if (offs) {
+      const int g = u / tiles, k0 = g ? offs[g - 1] : 0;
+      vb = u % tiles;
+      Tg = offs[g] - k0;
+      Ag += (int64_t)k0 * lda;
+      Bg += (int64_t)k0 * ldb;
+      Cg += (int64_t)g * strideC;
+      if (Tg <= 0) {  // no tokens: C_g unchanged, or zeros for beta 0
+        if (!beta) {
+          int bm, bn;
+          tile_of(gm, nbm, nbn, vb, tiles, bm, bn);
+          float* cz = Cg + (int64_t)(bm * BT) * ldc + bn * BT;
+          for (int e = threadIdx.x * 4; e < BT * BT; e += NT * 4)
+            *reinterpret_cast<f32x4*>(cz + (int64_t)(e / BT) * ldc + e % BT) = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        continue;
+      }
+    }
+    const int KT = (Tg + BK - 1) / BK;
+    int kb = 0, ke = KT, sidx = 0, tl = 0;
     if (u >= nfull) {
       const int t = u - nfull;
       sidx = t / tail;
@@ -215,26 +255,28 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
       ke = (sidx + 1) * KT / splits;
     }
     int bm, bn;
-    tile_of(gm, nbm, nbn, vb, nv, bm, bn);
+    tile_of(gm, nbm, nbn, vb, tiles, bm, bn);
     const int m0 = bm * BT, n0 = bn * BT;
-    const rsrc_t ra = make_rsrc(A + m0, (uint32_t)(((int64_t)(T - 1) * lda + BT) * 2));
-    const rsrc_t rb = make_rsrc(B + n0, (uint32_t)(((int64_t)(T - 1) * ldb + BT) * 2));
+    const bf16_t* abase = Ag + m0;
+    const bf16_t* bbase = Bg + n0;
     f32x4 acc[8][8];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     // prologue: K-tiles kb and kb + 1 requested, kb published, its sub-step-0 fragments read
+    const Krs k0 = krs(abase, bbase, Tg, kb);
 #pragma unroll
     for (int p = 0; p < 16; ++p) {
       set_m0(piece_m0(kb & 1, p));
-      dma_nom0(ra, rb, kb, p);
+      dma_nom0(k0, p);
     }
     if (ke - kb > 1) {
+      const Krs k1 = krs(abase, bbase, Tg, kb + 1);
 #pragma unroll
       for (int p = 0; p < 16; ++p) {
         set_m0(piece_m0((kb + 1) & 1, p));
-        dma_nom0(ra, rb, kb + 1, p);
+        dma_nom0(k1, p);
       }
       asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     } else {
@@ -246,12 +288,12 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
     using T1 = std::true_type;
     using F0 = std::false_type;
     int kt = kb;
-    for (; kt + 2 < ke; ++kt) step(acc, T1(), T1(), kt, ra, rb);
-    if (kt + 1 < ke) step(acc, T1(), F0(), kt++, ra, rb);
-    step(acc, F0(), F0(), kt, ra, rb);
+    for (; kt + 2 < ke; ++kt) step(acc, T1(), T1(), kt, abase, bbase, Tg);
+    if (kt + 1 < ke) step(acc, T1(), F0(), kt++, abase, bbase, Tg);
+    step(acc, F0(), F0(), kt, abase, bbase, Tg);
     asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 3" ::: "memory");
     // epilogue: lane (row 16 i + (lane & 15), cols 16 j + 4 G .. +3) -- 16-B fp32 accesses
-    float* cb = sidx ? ws + ((int64_t)(sidx - 1) * tail + tl) * (BT * BT) : C + (int64_t)m0 * ldc + n0;
+    float* cb = sidx ? ws + ((int64_t)(sidx - 1) * tail + tl) * (BT * BT) : Cg + (int64_t)m0 * ldc + n0;
     const int64_t ld = sidx ? BT : ldc;
     const bool acc_c = beta && !sidx;
 #pragma unroll
@@ -309,7 +351,7 @@ struct Split {
 };
 Split wgrad4_split(int M, int N, int T, int gm) {
   const int64_t nv = (int64_t)(M / BT) * (N / BT);
-  const int cus = cu_count(), KT = T / BK;
+  const int cus = cu_count(), KT = (T + BK - 1) / BK;
   const char* se = std::getenv("ST_WGRAD4_SPLIT");
   const int smax = se ? std::atoi(se) : 4;
   const int tail = (int)(nv % cus);
@@ -325,7 +367,7 @@ extern "C" {
 
 // fp32 workspace elements a launch of this shape needs (0: no tail split).
 int64_t st_wgrad4_ws_elems(int M, int N, int T) {
-  if (M <= 0 || N <= 0 || T <= 0 || M % BT || N % BT || T % BK) return 0;
+  if (M <= 0 || N <= 0 || T <= 0 || M % BT || N % BT) return 0;
   const Split sp = wgrad4_split(M, N, T, wgrad4_order());
   return sp.splits > 1 ? (int64_t)(sp.splits - 1) * sp.tail * BT * BT : 0;
 }
@@ -335,9 +377,8 @@ int64_t st_wgrad4_ws_elems(int M, int N, int T) {
 // 0 on success, -2: shape not supported (caller falls back).
 int st_wgrad4(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int M, int N, int T,
               int beta, float* ws, hipStream_t st) {
-  // T a whole number of K-tiles: every DMA stays inside its operand (the scalar K offset is
-  // not covered by the descriptor's range check)
-  if (M <= 0 || N <= 0 || T <= 0 || M % BT || N % BT || T % BK) return -2;
+  // any T: the K-tile offset is range checked, a ragged last K-tile reads zeros past row T
+  if (M <= 0 || N <= 0 || T <= 0 || M % BT || N % BT) return -2;
   if (lda % 8 || ldb % 8 || ldc % 4 || lda < M || ldb < N || ldc < N) return -2;
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16) return -2;
   // 32-bit buffer offsets: every row a K-tile addresses (up to T + 63) below 2^32 bytes
@@ -353,13 +394,36 @@ int st_wgrad4(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, 
   const int64_t nu = nfull + (int64_t)(nv - nfull) * sp.splits;
   const int64_t grid = std::min<int64_t>(nu, cu_count());
   wgrad4_kernel<<<(unsigned)grid, NT, 0, st>>>((const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, M, N, T,
-                                               beta ? 1 : 0, gm, nfull, sp.splits, ws);
+                                               beta ? 1 : 0, gm, nfull, sp.splits, ws, nullptr, 0);
   if (sp.splits > 1) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     wgrad4_tail_reduce<<<dim3(BT * BT / 1024, (unsigned)sp.tail), 256, 0, st>>>(C, ldc, ws, nbn, sp.nfull, sp.tail,
                                                                                sp.splits);
   }
+  return (int)hipGetLastError();
+}
+
+// Grouped weight gradient on the same kernel (MoE experts): C[g] = beta C[g] + A[rows of g]^T
+// B[rows of g], rows of g = [offs[g-1], offs[g]) (int32 device prefix sums, never read by the
+// host), C[g] at C + g strideC.  Units expert-major, so the ~256 tiles in flight belong to one
+// or two experts (csrc/wgrad_gemm.hip st_wgrad_grouped's order).  T_total bounds every
+// expert's rows.  -2: shape not supported.
+int st_wgrad4_grouped(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc,
+                      int64_t strideC, int M, int N, int G, const int* offs, int T_total, int beta, hipStream_t st) {
+  if (M <= 0 || N <= 0 || G <= 0 || T_total < 0 || M % BT || N % BT) return -2;
+  if (lda % 8 || ldb % 8 || ldc % 4 || strideC % 4 || lda < M || ldb < N || ldc < N) return -2;
+  if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16) return -2;
+  if (((int64_t)(T_total + BK) * lda + M) * 2 >= (int64_t)1 << 32) return -2;
+  if (((int64_t)(T_total + BK) * ldb + N) * 2 >= (int64_t)1 << 32) return -2;
+  const int64_t nu = (int64_t)G * (M / BT) * (N / BT);
+  if (nu >= (1LL << 31)) return -2;
+  // ST_WGRAD4_GROUPED_PERSIST=0: one unit per workgroup (A/B against the persistent grid)
+  const char* pe = std::getenv("ST_WGRAD4_GROUPED_PERSIST");
+  const bool persist = !pe || std::atoi(pe) != 0;
+  const int64_t grid = persist ? std::min<int64_t>(nu, cu_count()) : nu;
+  wgrad4_kernel<<<(unsigned)grid, NT, 0, st>>>((const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, M, N, 0,
+                                               beta ? 1 : 0, wgrad4_order(), (int)nu, 1, nullptr, offs, strideC);
   return (int)hipGetLastError();
 }
 

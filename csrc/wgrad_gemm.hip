@@ -647,6 +647,8 @@ extern "C" {
 int st_wgrad4(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int M, int N, int T,
               int beta, float* ws, hipStream_t st);
 int64_t st_wgrad4_ws_elems(int M, int N, int T);
+int st_wgrad4_grouped(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc,
+                      int64_t strideC, int M, int N, int G, const int* offs, int T_total, int beta, hipStream_t st);
 
 // fp32 workspace elements the tail split of this launch needs (0: none).
 int64_t st_wgrad_ws_elems(int M, int N, int T, int variant) {
@@ -711,6 +713,17 @@ int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float*
 int st_wgrad_grouped(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc,
                      int64_t strideC, int M, int N, int G, const int* offs, int T_total, int beta, hipStream_t st) {
   if (M <= 0 || N <= 0 || G <= 0) return -2;
+  // csrc/wgrad4.hip's one-wave-per-SIMD kernel for experts of at least a chip's worth of 256 x 256
+  // tiles (Mixtral: 1,792 per expert, proxy 136.3 -> 127.3 ms).  Small experts stay here: at
+  // Qwen3-30B-A3B's 24-48 tiles per expert wgrad4 is faster alone but the proxy step 0.7 % slower
+  // (its 128 KiB-LDS workgroups crowd out the concurrent streams; profiles/r05/wgrad4/).
+  // ST_WGRAD_GROUPED4=1 / 0 forces it on / off.
+  const char* g4 = std::getenv("ST_WGRAD_GROUPED4");
+  const bool use4 = g4 ? std::atoi(g4) != 0 : (int64_t)(M / 256) * (N / 256) >= 256;
+  if (use4) {
+    const int rc = st_wgrad4_grouped(A, lda, B, ldb, C, ldc, strideC, M, N, G, offs, T_total, beta, st);
+    if (rc != -2) return rc;
+  }
   if (M % BM || N % 128 || lda % 8 || ldb % 8 || lda < M || ldb < N || ldc < N) return -2;
   if (((uintptr_t)A | (uintptr_t)B) % 16 || (uintptr_t)C % 4) return -2;
   if (((int64_t)(T_total + 63) * lda + M) * 2 >= (int64_t)1 << 32) return -2;

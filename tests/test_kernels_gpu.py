@@ -559,7 +559,7 @@ def test_wgrad4_matches_fp32(T, M, N, split, monkeypatch):
         assert torch.equal(again, out)
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 6])
 @pytest.mark.parametrize("T", [1, 37, 100, 1000, 2047, 2100])
 def test_wgrad_gemm_ragged_tokens(T, variant):
     """Token counts that are not a multiple of the K-tile (MoE experts): the last tile's
@@ -774,12 +774,15 @@ def test_embedding_bwd_long_runs_and_masked_ids():
     assert err < 5e-3 * max(1.0, ref.abs().max().item() / 100), err
 
 
+@pytest.mark.parametrize("impl", ["wgrad4", "4stage"])
 @pytest.mark.parametrize("N", [256, 384])
 @pytest.mark.parametrize("beta", [0, 1])
-def test_wgrad_grouped_matches_per_expert(N, beta):
-    """One-launch grouped weight gradient (csrc/wgrad_gemm.hip st_wgrad_grouped): expert
-    row ranges from device offsets (empty experts, ragged counts, one > 1 K-tile),
-    beta 0 overwrites / 1 accumulates (an empty expert with beta 0 is zeroed)."""
+def test_wgrad_grouped_matches_per_expert(N, beta, impl, monkeypatch):
+    """One-launch grouped weight gradient (csrc/wgrad_gemm.hip st_wgrad_grouped; csrc/wgrad4.hip
+    st_wgrad4_grouped where it tiles the shape, N % 256 == 0): expert row ranges from device
+    offsets (empty experts, ragged counts, one > 1 K-tile), beta 0 overwrites / 1 accumulates
+    (an empty expert with beta 0 is zeroed)."""
+    monkeypatch.setenv("ST_WGRAD_GROUPED4", "1" if impl == "wgrad4" else "0")
     torch.manual_seed(4)
     M = 512
     counts = torch.tensor([37, 0, 300, 1, 64, 0, 1000], device="cuda", dtype=torch.int32)
