@@ -277,12 +277,24 @@ template <typename G>
 __global__ __launch_bounds__(256) void sumsq_kernel(const G* __restrict__ g, int64_t n4,
                                                      float* __restrict__ partial) {
   __shared__ float red[4];
-  float acc = 0.f;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n4;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    float4 v = load_g4<G>(g, t * 4);
-    acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  // four independent 16-byte loads in flight per lane: with one (a load -> wait -> FMA chain)
+  // the 1,024-block grid kept ~16 KiB per CU in flight and read at 2.15 TB/s
+  // (profiles/r05/step_kernels_mbs6_v2.csv)
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  for (; t + 3 * stride < n4; t += 4 * stride) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = load_g4<G>(g, (t + u * stride) * 4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
   }
+  for (; t < n4; t += stride) {
+    const float4 v = load_g4<G>(g, t * 4);
+    a[0] += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  float acc = (a[0] + a[1]) + (a[2] + a[3]);
   acc = block_sum<256>(acc, red);
   if (threadIdx.x == 0) partial[blockIdx.x] = acc;
 }
