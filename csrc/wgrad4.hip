@@ -82,6 +82,11 @@ ST_DEVICE void tile_of(int gm, int nbm, int nbn, int vb, int nv, int& bm, int& b
 
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved: nothing else in this kernel uses it
+// PROBE 7 (diagnostic build, ST_WGRAD4_PROBE=7): shader-cycle stamps per segment of every
+// steady-state K-tile step, summed per wave and written over C (tools/_w4stamps.py reads them)
+// KDESC: the K-tile offset lives in per-K-tile descriptors (ragged token counts, grouped
+// experts); else in soffset over one descriptor per unit (T a multiple of 64, fewer scalar ops)
+template <int PROBE = 0, bool KDESC = true>
 __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                        const bf16_t* __restrict__ B, int64_t ldb,
                                                        float* __restrict__ C, int64_t ldc, int M, int N, int T,
@@ -117,18 +122,26 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
   // covers the VGPR offset only -- the K offset lives in the base, not in soffset)
   struct Krs {
     rsrc_t a, b;
+    uint32_t soa, sob;
   };
+  rsrc_t unit_a = make_rsrc(A, 0u), unit_b = make_rsrc(B, 0u);  // !KDESC: the unit's whole-operand descriptors
   auto krs = [&](const bf16_t* abase, const bf16_t* bbase, int rows, int kt) {
-    const int left = rows - kt * BK;
-    const uint32_t ba = left > 0 ? (uint32_t)(((int64_t)(left - 1) * lda + BT) * 2) : 0u;
-    const uint32_t bb = left > 0 ? (uint32_t)(((int64_t)(left - 1) * ldb + BT) * 2) : 0u;
-    return Krs{make_rsrc(abase + (int64_t)kt * BK * lda, ba), make_rsrc(bbase + (int64_t)kt * BK * ldb, bb)};
+    if constexpr (KDESC) {
+      const int left = rows - kt * BK;
+      const uint32_t ba = left > 0 ? (uint32_t)(((int64_t)(left - 1) * lda + BT) * 2) : 0u;
+      const uint32_t bb = left > 0 ? (uint32_t)(((int64_t)(left - 1) * ldb + BT) * 2) : 0u;
+      return Krs{make_rsrc(abase + (int64_t)kt * BK * lda, ba), make_rsrc(bbase + (int64_t)kt * BK * ldb, bb), 0u,
+                 0u};
+    } else {
+      return Krs{unit_a, unit_b, (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)kt * (uint32_t)BK * sa),
+                 (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)kt * (uint32_t)BK * sb)};
+    }
   };
   auto dma_nom0 = [&](const Krs& k, int p) {
     if (p < 8)
-      asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" : : "v"(voff[p]), "s"(k.a) : "memory");
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(voff[p]), "s"(k.a), "s"(k.soa) : "memory");
     else
-      asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" : : "v"(voff[p]), "s"(k.b) : "memory");
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(voff[p]), "s"(k.b), "s"(k.sob) : "memory");
   };
 
   // fragment reads (16 features x 32 tokens, natural k order permuted the same way for both
@@ -163,6 +176,15 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
     if (m >= 64 && m <= 120 && ((m - 64) & 7) == 0) return 8 + ((m - 64) >> 3);
     return -1;
   };
+  uint64_t seg[5] = {0, 0, 0, 0, 0}, nst = 0;
+  uint64_t ts[6];
+  auto stamp = [&](int k) {
+    if constexpr (PROBE == 7) {
+      fence();
+      ts[k] = __builtin_amdgcn_s_memtime();
+      fence();
+    }
+  };
   auto step = [&](f32x4 (&acc)[8][8], auto more_c, auto more2_c, int kt, const bf16_t* abase, const bf16_t* bbase,
                   int rows) {
     constexpr bool more = decltype(more_c)::value, more2 = decltype(more2_c)::value;
@@ -171,6 +193,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
     const lds_t* cs = smem + (kt & 1) * STAGE;
     const lds_t* ns = smem + ((kt + 1) & 1) * STAGE;
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (more2) stamp(0);
     static_for<0, 128>([&](auto mc) {
       constexpr int m = decltype(mc)::value;
       mfma(acc, m >> 6, m & 63);
@@ -181,13 +204,16 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
         fence();
       }
       if constexpr (m == 20 && more2) {
+        stamp(1);
         fence();
         asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");  // B fragments 8-10 may be in flight
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         fence();
+        stamp(2);
       }
       if constexpr (m == 63 && more) {
+        if constexpr (more2) stamp(3);
         fence();
         __builtin_amdgcn_s_setprio(0);
         if constexpr (more2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
@@ -196,6 +222,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_setprio(1);
         fence();
+        if constexpr (more2) stamp(4);
       }
       if constexpr (more2 && pn >= 0) {
         fence();
@@ -213,6 +240,11 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
         fence();
       }
     });
+    if constexpr (more2 && PROBE == 7) {
+      stamp(5);
+      for (int k = 0; k < 5; ++k) seg[k] += ts[k + 1] - ts[k];
+      ++nst;
+    }
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -259,6 +291,10 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
     const int m0 = bm * BT, n0 = bn * BT;
     const bf16_t* abase = Ag + m0;
     const bf16_t* bbase = Bg + n0;
+    if constexpr (!KDESC) {
+      unit_a = make_rsrc(abase, (uint32_t)(((int64_t)(Tg - 1) * lda + BT) * 2));
+      unit_b = make_rsrc(bbase, (uint32_t)(((int64_t)(Tg - 1) * ldb + BT) * 2));
+    }
     f32x4 acc[8][8];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -292,6 +328,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
     if (kt + 1 < ke) step(acc, T1(), F0(), kt++, abase, bbase, Tg);
     step(acc, F0(), F0(), kt, abase, bbase, Tg);
     asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 3" ::: "memory");
+    if constexpr (PROBE == 7) continue;  // the stamps go over C below: no tile stores
     // epilogue: lane (row 16 i + (lane & 15), cols 16 j + 4 G .. +3) -- 16-B fp32 accesses
     float* cb = sidx ? ws + ((int64_t)(sidx - 1) * tail + tl) * (BT * BT) : Cg + (int64_t)m0 * ldc + n0;
     const int64_t ld = sidx ? BT : ldc;
@@ -306,6 +343,14 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
         if (acc_c) v += *p;
         *p = v;
       }
+    }
+  }
+  if constexpr (PROBE == 7) {  // lane 0 of each wave: 5 x u64 segment sums + step count, row 4 b + w
+    __syncthreads();
+    if (lane == 0) {
+      uint64_t* d = reinterpret_cast<uint64_t*>(C + (int64_t)(blockIdx.x * 4 + wid) * ldc);
+      for (int k = 0; k < 5; ++k) d[k] = seg[k];
+      d[5] = nst;
     }
   }
 }
@@ -393,8 +438,18 @@ int st_wgrad4(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, 
   const int nfull = sp.splits > 1 ? sp.nfull : (int)nv;
   const int64_t nu = nfull + (int64_t)(nv - nfull) * sp.splits;
   const int64_t grid = std::min<int64_t>(nu, cu_count());
-  wgrad4_kernel<<<(unsigned)grid, NT, 0, st>>>((const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, M, N, T,
-                                               beta ? 1 : 0, gm, nfull, sp.splits, ws, nullptr, 0);
+  const char* pe = std::getenv("ST_WGRAD4_PROBE");  // 7: cycle stamps over C (wrong results)
+  const bool probe = pe && std::atoi(pe) == 7 && grid * 4 <= M && ldc >= 12;
+  // whole K-tiles: K offsets in soffset (ST_WGRAD4_KDESC=1 forces the per-K-tile descriptors)
+  const char* ke = std::getenv("ST_WGRAD4_KDESC");
+  const bool kdesc = T % BK != 0 || (ke && std::atoi(ke) == 1);
+#define W4ARGS (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, M, N, T, beta ? 1 : 0, gm, nfull, sp.splits, ws, \
+               nullptr, (int64_t)0
+  if (probe && kdesc) wgrad4_kernel<7, true><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
+  else if (probe) wgrad4_kernel<7, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
+  else if (kdesc) wgrad4_kernel<0, true><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
+  else wgrad4_kernel<0, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
+#undef W4ARGS
   if (sp.splits > 1) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
