@@ -198,12 +198,12 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
       constexpr int m = decltype(mc)::value;
       mfma(acc, m >> 6, m & 63);
       constexpr int pd = dslot(m), pn = dslot(m + 2);
-      if constexpr (m < 32 && (m & 1) == 0) {  // fragment r = m / 2 (A 0-7, then B): 2 tr reads
+      if constexpr (m < 32 && (m & 1) == 0 && PROBE != 2) {  // fragment r = m / 2 (A 0-7, then B): 2 tr reads
         fence();
         read(cs, 1, m >> 1);
         fence();
       }
-      if constexpr (m == 20 && more2) {
+      if constexpr (m == 20 && more2 && PROBE != 3) {
         stamp(1);
         fence();
         asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");  // B fragments 8-10 may be in flight
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
         __builtin_amdgcn_s_setprio(0);
         if constexpr (more2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        if constexpr (PROBE != 3) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_setprio(1);
         fence();
@@ -229,12 +229,12 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
         set_m0(piece_m0(kt & 1, pn));
         fence();
       }
-      if constexpr (more2 && pd >= 0) {
+      if constexpr (more2 && pd >= 0 && PROBE != 1) {
         fence();
         dma_nom0(k2, pd);
         fence();
       }
-      if constexpr (more && m >= 64 && m < 96 && (m & 1) == 0) {
+      if constexpr (more && m >= 64 && m < 96 && (m & 1) == 0 && PROBE != 2) {
         fence();
         read(ns, 0, (m - 64) >> 1);
         fence();
@@ -438,14 +438,20 @@ int st_wgrad4(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, 
   const int nfull = sp.splits > 1 ? sp.nfull : (int)nv;
   const int64_t nu = nfull + (int64_t)(nv - nfull) * sp.splits;
   const int64_t grid = std::min<int64_t>(nu, cu_count());
-  const char* pe = std::getenv("ST_WGRAD4_PROBE");  // 7: cycle stamps over C (wrong results)
-  const bool probe = pe && std::atoi(pe) == 7 && grid * 4 <= M && ldc >= 12;
+  // 7: cycle stamps over C; 1 / 2 / 3: no K-loop DMA / no fragment reads / no barriers (timing
+  // probes; all wrong results)
+  const char* pe = std::getenv("ST_WGRAD4_PROBE");
+  const int pv = pe ? std::atoi(pe) : 0;
+  const bool probe = pv == 7 && grid * 4 <= M && ldc >= 12;
   // whole K-tiles: K offsets in soffset (ST_WGRAD4_KDESC=1 forces the per-K-tile descriptors)
   const char* ke = std::getenv("ST_WGRAD4_KDESC");
   const bool kdesc = T % BK != 0 || (ke && std::atoi(ke) == 1);
 #define W4ARGS (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, M, N, T, beta ? 1 : 0, gm, nfull, sp.splits, ws, \
                nullptr, (int64_t)0
-  if (probe && kdesc) wgrad4_kernel<7, true><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
+  if (pv == 1 && !kdesc) wgrad4_kernel<1, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
+  else if (pv == 2 && !kdesc) wgrad4_kernel<2, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
+  else if (pv == 3 && !kdesc) wgrad4_kernel<3, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
+  else if (probe && kdesc) wgrad4_kernel<7, true><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
   else if (probe) wgrad4_kernel<7, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
   else if (kdesc) wgrad4_kernel<0, true><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
   else wgrad4_kernel<0, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
