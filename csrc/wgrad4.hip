@@ -86,7 +86,9 @@ ST_DEVICE void tile_of(int gm, int nbm, int nbn, int vb, int nv, int& bm, int& b
 // steady-state K-tile step, summed per wave and written over C (tools/_w4stamps.py reads them)
 // KDESC: the K-tile offset lives in per-K-tile descriptors (ragged token counts, grouped
 // experts); else in soffset over one descriptor per unit (T a multiple of 64, fewer scalar ops)
-template <int PROBE = 0, bool KDESC = true>
+// RS 1: fragment halves read one transposed read at a time, spread thinner (sub-step 1: A at
+// MFMAs 0-15, B at even 16-46; next tile's sub-step 0: B then A at even 64-126)
+template <int PROBE = 0, bool KDESC = true, int RS = 0>
 __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                        const bf16_t* __restrict__ B, int64_t ldb,
                                                        float* __restrict__ C, int64_t ldc, int M, int N, int T,
@@ -163,6 +165,21 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
     if (r < 8) fa[ks][r] = lds_tr(st + aoff[r][0] + ks * 32 * RB, st + aoff[r][1] + ks * 32 * RB);
     else fb[ks][r - 8] = lds_tr(st + boff[r - 8][0] + ks * 32 * RB, st + boff[r - 8][1] + ks * 32 * RB);
   };
+  // one transposed read: half hf of A fragment r (r < 8) or B fragment r - 8, of sub-step ks
+  auto read_half = [&](const lds_t* st, int ks, int r, int hf) {
+    typedef __bf16 bfx4l __attribute__((ext_vector_type(4)));
+    if (r < 8) {
+      const bfx4l v = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (bfx4l __attribute__((address_space(3)))*)(st + aoff[r][hf] + ks * 32 * RB));
+      if (hf) fa[ks][r].hi = v;
+      else fa[ks][r].lo = v;
+    } else {
+      const bfx4l v = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (bfx4l __attribute__((address_space(3)))*)(st + boff[r - 8][hf] + ks * 32 * RB));
+      if (hf) fb[ks][r - 8].hi = v;
+      else fb[ks][r - 8].lo = v;
+    }
+  };
   // operands swapped: acc[i][j] reg r = C[row 16 i + (lane & 15)][col 16 j + 4 G + r]
   auto mfma = [&](f32x4 (&acc)[8][8], int ks, int idx) {
     const int i = idx >> 3, j = idx & 7;
@@ -198,15 +215,26 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
       constexpr int m = decltype(mc)::value;
       mfma(acc, m >> 6, m & 63);
       constexpr int pd = dslot(m), pn = dslot(m + 2);
-      if constexpr (m < 32 && (m & 1) == 0 && PROBE != 2) {  // fragment r = m / 2 (A 0-7, then B): 2 tr reads
+      if constexpr (RS == 0 && m < 32 && (m & 1) == 0 && PROBE != 2) {  // fragment r = m / 2 (A 0-7, then B)
         fence();
         read(cs, 1, m >> 1);
+        fence();
+      }
+      if constexpr (RS == 1 && m < 16) {  // sub-step 1: A halves, one per MFMA
+        fence();
+        read_half(cs, 1, m >> 1, m & 1);
+        fence();
+      }
+      if constexpr (RS == 1 && m >= 16 && m < 48 && (m & 1) == 0) {  // then B halves, every other MFMA
+        fence();
+        read_half(cs, 1, 8 + ((m - 16) >> 2), ((m - 16) >> 1) & 1);
         fence();
       }
       if constexpr (m == 20 && more2 && PROBE != 3) {
         stamp(1);
         fence();
-        asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");  // B fragments 8-10 may be in flight
+        if constexpr (RS == 1) asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");  // B reads 16-20 in flight
+        else asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");  // B fragments 8-10 may be in flight
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         fence();
@@ -234,7 +262,13 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
         dma_nom0(k2, pd);
         fence();
       }
-      if constexpr (more && m >= 64 && m < 96 && (m & 1) == 0 && PROBE != 2) {
+      if constexpr (RS == 1 && more && m >= 64 && (m & 1) == 0) {  // next tile's sub-step 0: B halves, then A
+        constexpr int x = (m - 64) >> 1;
+        fence();
+        read_half(ns, 0, x < 16 ? 8 + (x >> 1) : ((x - 16) >> 1), x & 1);
+        fence();
+      }
+      if constexpr (RS == 0 && more && m >= 64 && m < 96 && (m & 1) == 0 && PROBE != 2) {
         fence();
         read(ns, 0, (m - 64) >> 1);
         fence();
@@ -446,6 +480,8 @@ int st_wgrad4(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, 
   // whole K-tiles: K offsets in soffset (ST_WGRAD4_KDESC=1 forces the per-K-tile descriptors)
   const char* ke = std::getenv("ST_WGRAD4_KDESC");
   const bool kdesc = T % BK != 0 || (ke && std::atoi(ke) == 1);
+  const char* re = std::getenv("ST_WGRAD4_RS");  // 1: fragment reads spread half by half (A/B)
+  const int rs = re ? std::atoi(re) : 0;
 #define W4ARGS (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, M, N, T, beta ? 1 : 0, gm, nfull, sp.splits, ws, \
                nullptr, (int64_t)0
   if (pv == 1 && !kdesc) wgrad4_kernel<1, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
@@ -454,6 +490,7 @@ int st_wgrad4(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, 
   else if (probe && kdesc) wgrad4_kernel<7, true><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
   else if (probe) wgrad4_kernel<7, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
   else if (kdesc) wgrad4_kernel<0, true><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
+  else if (rs == 1) wgrad4_kernel<0, false, 1><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
   else wgrad4_kernel<0, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
 #undef W4ARGS
   if (sp.splits > 1) {

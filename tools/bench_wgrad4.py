@@ -23,6 +23,16 @@ e0 = ((out - ref).norm() / ref.norm()).item()
 assert _lib.ops().wgrad_gemm_(out, dy, x, 1, 6)
 e1 = ((out - 2 * ref).norm() / (2 * ref).norm()).item()
 print("numerics", json.dumps({"rel_err_beta0": e0, "rel_err_beta1": e1}), flush=True)
+for rs in ("1",):  # spread-read schedule (ST_WGRAD4_RS)
+    os.environ["ST_WGRAD4_RS"] = rs
+    out.fill_(7.0)
+    assert _lib.ops().wgrad_gemm_(out, dy, x, 0, 6)
+    r0 = ((out - ref).norm() / ref.norm()).item()
+    assert _lib.ops().wgrad_gemm_(out, dy, x, 1, 6)
+    r1 = ((out - 2 * ref).norm() / (2 * ref).norm()).item()
+    os.environ.pop("ST_WGRAD4_RS")
+    print(f"numerics rs={rs}", json.dumps({"rel_err_beta0": r0, "rel_err_beta1": r1}), flush=True)
+    assert r0 < 1e-5 and r1 < 1e-5
 
 ORDERS = [o for o in os.environ.get("W4_ORDERS", "").split(",") if o]  # XCD-grouped tile orders to time
 SHAPES = {"qkv": (24576, 6144, 4096), "o": (24576, 4096, 4096), "gate_up": (24576, 28672, 4096),
@@ -38,6 +48,13 @@ for name, (T, M, N) in SHAPES.items():
         os.environ.pop("ST_WGRAD4_SPLIT")
 
     arms["hip_v6_nosplit"] = v6_nosplit
+
+    def v6_rs1():
+        os.environ["ST_WGRAD4_RS"] = "1"
+        _lib.ops().wgrad_gemm_(out, dy, x, 1, 6)
+        os.environ.pop("ST_WGRAD4_RS")
+
+    arms["hip_v6_rs1"] = v6_rs1
     for gm in ORDERS:
         def v6_order(gm=gm):
             os.environ["ST_WGRAD4_ORDER"] = gm
