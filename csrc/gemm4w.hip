@@ -1335,8 +1335,10 @@ int st_gemm4w_swiglu(const void* X, int64_t ldx, const void* W, int64_t ldw, voi
   if (grid >= (1LL << 31)) return -2;
   const char* oe = std::getenv("ST_GEMM4W_ORDER");
   const int gm = oe ? std::atoi(oe) : 4;
-  const char* ke = std::getenv("ST_GEMM4W_SWIGLU_KERNEL");  // f (default): stream-persistent, e: kind 5
-  if (K / BK >= 2 && !(ke && ke[0] == 'e')) {
+  // e (default): kind 5 (1.39-1.42 PF/s at gate|up), f: the stream-persistent kind 6 (1.08-1.16;
+  // profiles/r05/gemm4w/kind5_persistent_vs_kind6_stream.log)
+  const char* ke = std::getenv("ST_GEMM4W_SWIGLU_KERNEL");
+  if (K / BK >= 2 && ke && ke[0] == 'f') {
     const int64_t lg = std::min<int64_t>(grid, cu_count());
     gemm4f_kernel<1><<<(unsigned)lg, NT, 0, st>>>((const bf16_t*)X, ldx, (const bf16_t*)W, ldw, 0, (bf16_t*)GU, ldgu,
                                                   nullptr, nullptr, 1, N, K, gm, (bf16_t*)H, ldh, I, T, (int)grid);
