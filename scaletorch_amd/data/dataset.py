@@ -68,7 +68,8 @@ class TokenChunkDataset(Dataset):
         return int(self.chunks.shape[0])
 
     def __getitem__(self, i: int) -> dict:
-        return {"input_ids": torch.from_numpy(np.asarray(self.chunks[i], dtype=np.int64))}
+        # a copy: rows of a read-only memmap must not become (non-writable) tensor views
+        return {"input_ids": torch.from_numpy(np.array(self.chunks[i], dtype=np.int64))}
 
 
 def load_tokenizer(path: str):

@@ -48,6 +48,10 @@ class ModelArguments:
     num_key_value_heads: int | None = field(default=None)
     use_flash_attention: bool = field(default=True)
     dtype: str = field(default="bfloat16")
+    hf_weights: str = field(default="auto",
+                            metadata={"help": "auto: load *.safetensors when model_name_or_path is a dir holding "
+                                              "them (reference model_builder.py:82-84) | required: fail without "
+                                              "them | off: random init"})
 
 
 @dataclass
@@ -244,6 +248,8 @@ class ScaleTorchArguments(DataArguments, ModelArguments, ParallelArguments, LrSc
         CheckpointArguments.__post_init__(self)
         if self.micro_batch_size is None:
             self.micro_batch_size = self.batch_size
+        if self.hf_weights not in ("auto", "required", "off"):
+            raise ValueError(f"hf_weights must be auto, required or off, got {self.hf_weights!r}")
         cp = self.context_parallel_size
         if self.sequence_length and cp > 1:
             div = 2 * cp if self.cp_zigzag else cp

@@ -136,6 +136,12 @@ class Trainer:
             finally:
                 torch.set_default_dtype(prev)
         model.cos, model.sin = model.cos.float(), model.sin.float()
+        # HF safetensors (single file or sharded index) when model_name_or_path holds them:
+        # loaded before the DP arena / optimizer exist, so the arena and the fp32 masters
+        # are built from the loaded weights (reference model_builder.py:82-84)
+        from ..utils.checkpoint import maybe_load_hf_weights
+
+        self.hf_tensors_loaded = maybe_load_hf_weights(model, a.model_name_or_path, getattr(a, "hf_weights", "auto"))
         mark_tp_sharded(model)
         self.raw_model = model
         bucket = max(1, int(a.bucket_size_mb * 1024 * 1024) // 4)

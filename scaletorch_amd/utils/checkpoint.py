@@ -226,26 +226,68 @@ def hf_to_internal_name(name: str) -> str | None:
     return None
 
 
-def _tp_slice(name: str, t: torch.Tensor, tp: int, rank: int) -> torch.Tensor:
-    if tp == 1:
-        return t
-    if any(s in name for s in ("q_proj", "k_proj", "v_proj", "gate_proj", "up_proj", "final_proj", "embedding")):
-        if "experts.experts" in name and "down_proj" not in name:
-            return t.chunk(tp, 0)[rank]
-        return t.chunk(tp, 0)[rank]
+def _tp_split_dim(name: str) -> int | None:
+    """Dimension a reference-named weight is split along under TP (None = replicated):
+    column-parallel (q/k/v, gate/up incl. experts, LM head, vocab embedding) on the
+    output rows, row-parallel (o, down incl. experts) on the input columns
+    (reference InitializationManager, scaletorch/utils/checkpoint.py:339-423)."""
     if any(s in name for s in ("out_proj", "down_proj")):
-        return t.chunk(tp, 1)[rank]
-    return t
+        return 1
+    if any(s in name for s in ("q_proj", "k_proj", "v_proj", "gate_proj", "up_proj", "final_proj", "embedding")):
+        return 0
+    return None
+
+
+def _tp_slice(name: str, t: torch.Tensor, tp: int, rank: int) -> torch.Tensor:
+    d = _tp_split_dim(name) if tp > 1 else None
+    return t if d is None else t.chunk(tp, d)[rank]
+
+
+def _read_tp_shard(fh, name: str, iname: str, tp: int, rank: int) -> torch.Tensor:
+    """Read only this TP rank's slice of tensor ``name`` (safetensors slices the
+    memory-mapped file, so an 8B shard never materialises the full matrix)."""
+    d = _tp_split_dim(iname) if tp > 1 else None
+    if d is None:
+        return fh.get_tensor(name)
+    sl = fh.get_slice(name)
+    n = sl.get_shape()[d]
+    if n % tp:
+        raise ValueError(f"{name}: dim {d} of size {n} does not split over tp={tp}")
+    lo, hi = rank * (n // tp), (rank + 1) * (n // tp)
+    return sl[lo:hi] if d == 0 else sl[:, lo:hi]
+
+
+def hf_weight_files(path: str) -> list[str]:
+    """The safetensors files of an HF checkpoint directory: the shards named by
+    ``model.safetensors.index.json`` when present (reference _load_sharded_checkpoint,
+    scaletorch/utils/checkpoint.py:145-187), else every ``*.safetensors``."""
+    if not path or not os.path.isdir(path):
+        return []
+    idx = os.path.join(path, "model.safetensors.index.json")
+    if os.path.exists(idx):
+        with open(idx) as f:
+            shards = sorted(set(json.load(f)["weight_map"].values()))
+        missing = [s for s in shards if not os.path.exists(os.path.join(path, s))]
+        if missing:
+            raise FileNotFoundError(f"{idx} names shards that are not present: {missing}")
+        return [os.path.join(path, s) for s in shards]
+    return sorted(glob.glob(os.path.join(path, "*.safetensors")))
 
 
 def load_hf_safetensors(model, path: str, strict: bool = False, optimizer=None) -> list[str]:
     """Load this rank's shard of an HF checkpoint dir (single file or sharded index) into ``model``.
 
-    Only the tensors of this PP stage / EP shard are read (safetensors memory-maps the files).
-    The bf16 parameters are views into the arena, so the copy lands there; when an
-    arena optimizer already exists pass it as ``optimizer`` so its fp32 master copy
-    is refreshed (otherwise its first step would write the stale masters back).
-    Returns the list of internal names loaded.
+    Only the tensors of this PP stage / EP shard are read, and of those only this TP
+    rank's slice (safetensors memory-maps the files).  HF names map to the internal ones
+    through ``_HF_MAP`` (Llama / Qwen3 / Qwen3-MoE / Mixtral ``w1/w2/w3``); tied
+    embeddings fill the LM head from ``embed_tokens``.  The bf16 parameters may be
+    views into the DP arena, so the copy lands there; when an arena optimizer already
+    exists pass it as ``optimizer`` so its fp32 master copy is refreshed (otherwise
+    its first step would write the stale masters back).
+
+    Raises when the files hold none of this rank's tensors (a wrong directory must
+    not silently train from random weights) and, with ``strict``, when any of them is
+    missing.  Returns the sorted internal names loaded.
     """
     from safetensors import safe_open
 
@@ -253,7 +295,7 @@ def load_hf_safetensors(model, path: str, strict: bool = False, optimizer=None) 
     tp = mesh.tp_size()
     tpr = mesh.tp_rank()
     ep, epr = mesh.ep_size(), mesh.ep_rank()
-    files = sorted(glob.glob(os.path.join(path, "*.safetensors")))
+    files = hf_weight_files(path)
     if not files:
         raise FileNotFoundError(f"no *.safetensors under {path}")
     wanted = set(raw.reference_state_dict().keys())
@@ -273,12 +315,41 @@ def load_hf_safetensors(model, path: str, strict: bool = False, optimizer=None) 
                     iname = f"{m.group(1)}{e % per}{m.group(3)}"
                 if iname not in wanted and not (iname == "embedding.weight" and "final_proj.weight" in wanted):
                     continue
-                sd[iname] = _tp_slice(iname, fh.get_tensor(name), tp, tpr)
+                sd[iname] = _read_tp_shard(fh, name, iname, tp, tpr)
     if raw.config.tie_word_embeddings and "final_proj.weight" in wanted and "final_proj.weight" not in sd \
             and "embedding.weight" in sd:
         sd["final_proj.weight"] = sd["embedding.weight"]
+    if not sd:
+        raise ValueError(f"{path}: {len(files)} safetensors file(s) but none of their tensors maps onto this "
+                         f"rank's {len(wanted)} parameters (wrong architecture or naming?)")
+    missing = sorted(wanted - set(sd))
+    if missing:
+        msg = f"{path}: {len(missing)} of {len(wanted)} parameters not in the checkpoint, e.g. {missing[:4]}"
+        if strict:
+            raise KeyError(msg)
+        logger.warning("%s: they keep their random init", msg)
+    dtype = next(raw.parameters()).dtype
     with torch.no_grad():
-        raw.load_reference_state_dict({k: v.to(next(raw.parameters()).dtype) for k, v in sd.items()}, strict=strict)
+        raw.load_reference_state_dict({k: v.to(dtype) for k, v in sd.items()}, strict=False)
     if optimizer is not None and hasattr(optimizer, "reload_masters"):
         optimizer.reload_masters()
     return sorted(sd)
+
+
+def maybe_load_hf_weights(model, name_or_path: str, mode: str = "auto", optimizer=None) -> int:
+    """Model-build hook (reference model_builder.py:82-84 -> init_model_with_materialized_weights):
+    ``auto`` loads when ``name_or_path`` is a directory holding safetensors, ``required``
+    fails without them, ``off`` keeps the random init.  Returns the tensor count loaded
+    on this rank (0 = random init) and logs it."""
+    if mode == "off":
+        return 0
+    files = hf_weight_files(name_or_path)
+    if not files:
+        if mode == "required":
+            raise FileNotFoundError(f"--hf_weights required but {name_or_path!r} holds no *.safetensors")
+        return 0
+    names = load_hf_safetensors(model, name_or_path, strict=(mode == "required"), optimizer=optimizer)
+    logger.info("loaded %d tensors from %d safetensors file(s) under %s (tp %d/%d, pp stage %d, ep %d/%d)",
+                len(names), len(files), name_or_path, mesh.tp_rank(), mesh.tp_size(),
+                mesh.pgm.pp_rank if mesh.pgm else 0, mesh.ep_rank(), mesh.ep_size())
+    return len(names)
