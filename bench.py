@@ -142,6 +142,38 @@ def _self_launch(n: int, argv: list[str], backend: str) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def _slice_record(out: dict, args, est, tr, dp: int, world: int, elapsed: float) -> dict:
+    """The JSON of a per-rank compute slice: its own kind, never a throughput result."""
+    import torch
+
+    from scaletorch_amd.parallel import mesh
+
+    pg = mesh.pgm
+    coords = {k: getattr(pg, f"{k}_rank") for k in ("dp", "pp", "cp", "ep", "tp")} if pg else {}
+    peak_gb = torch.cuda.max_memory_allocated() / 1e9 if torch.cuda.is_available() else 0.0
+    est_gb = est.total_gb() if hasattr(est, "total_gb") else None
+    rec = {
+        "kind": "per-rank compute slice",
+        "valid": False,
+        "why_not_a_result": "one rank of an 8-GPU layout on one GPU; collectives are same-shape local copies "
+                            "(dist/loopback.py), no communication, no pipeline bubble",
+        "layout": args.layout, "slice_world": world, "rank": int(os.environ.get("ST_LOOPBACK_RANK", "0")),
+        "rank_coords": coords, "model": args.model, "layers_total": tr.model_config.num_hidden_layers,
+        "layers_on_rank": len(tr.raw_model.decoder_layers),
+        "ms_per_step": round(elapsed / args.steps * 1000, 2), "steps": args.steps, "warmup": args.warmup,
+        "tokens_per_step_global": tr.tokens_per_step,
+        "tokens_per_s_per_gpu_upper_bound": out["tokens_per_s_per_gpu"],
+        "mfu_pct_per_rank_upper_bound": out["mfu_pct"], "mfu_pct_strict_per_rank_upper_bound": out["mfu_pct_strict"],
+        "peak_hbm_gb": round(peak_gb, 2), "hbm_estimate_gb": round(est_gb, 2) if est_gb else None,
+        "hbm_estimate_err_pct": round(100 * (peak_gb - est_gb) / est_gb, 1) if est_gb else None,
+        "hbm_estimate": est.summary(),
+        "comm_mb_per_step_rank": out["comm_mb_per_step_rank0"],
+        "moe_dispatch": out["moe_dispatch"], "config": out["config"], "final_loss": out["final_loss"],
+        "dtype": "bf16", "data": out["data"],
+    }
+    return rec
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -183,16 +215,27 @@ def main() -> int:
                          "(torch AdamW on its bf16 model keeps bf16 exp_avg / exp_avg_sq and NO master "
                          "weights); ours keeps fp32 master weights either way")
     ap.add_argument("--moe_ep_chunks", type=int, default=None, help="EP dispatch chunks (capacity mode)")
+    ap.add_argument("--slice", action="store_true",
+                    help="per-rank compute slice: run ONE rank of the --layout on this GPU at full depth, with every "
+                         "collective replaced by a same-shape local copy (dist/loopback.py); prints its own JSON "
+                         "kind, valid: false -- per-rank kernels and HBM of a layout no 8-GPU box is here to run")
+    ap.add_argument("--slice_world", type=int, default=8, help="world size of the sliced layout")
     args = ap.parse_args()
     launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.slice:
+        if launched and world > 1:
+            raise SystemExit("--slice runs ONE rank in one process; do not start it under a launcher")
+        world = args.slice_world
+        args.gpus = world
+        args.backend = "loopback"
     if args.gpus is None:
         args.gpus = world
-    if not launched and args.gpus > 1:
+    if not launched and args.gpus > 1 and not args.slice:
         return _self_launch(args.gpus, sys.argv[1:], args.backend)
     if args.gpus < 1:
         raise SystemExit(f"--gpus must be >= 1 (got {args.gpus})")
-    if world != args.gpus:
+    if world != args.gpus and not args.slice:
         # a mismatch would report a different job size than the one asked for
         raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     preset = dict(model="llama3-8b", micro_batch_size=6, seq_len=4096, grad_acc=1, tp=1, pp=1, cp=1, ep=1, sp=False,
@@ -215,6 +258,11 @@ def main() -> int:
         raise SystemExit(f"world {world} not divisible by tp*pp*cp*ep={mp}")
     dp = world // mp
     ga = args.grad_acc
+    if args.slice:
+        # the rank to impersonate: the LAST pipeline stage (embedding-free, final norm + LM head:
+        # the heavier stage), first of every other axis.  Mesh order [dp, pp, cp, ep, tp], TP fastest.
+        rep = (args.pp - 1) * args.cp * args.ep * args.tp
+        os.environ["ST_LOOPBACK_WORLD"], os.environ["ST_LOOPBACK_RANK"] = str(world), str(rep)
     if args.pp > 1:
         # the (interleaved) 1F1B schedule needs >= pp micro-batches in flight -- a multiple of
         # pp with virtual stages; fewer is an error, never silently raised
@@ -269,7 +317,9 @@ def main() -> int:
     if dist.is_initialized():
         dist.all_reduce(ranks_seen)
     ranks_seen = int(ranks_seen.item())
-    if ranks_seen != world:
+    if args.slice:
+        ranks_seen = 1  # loopback: this process is the only rank that exists
+    elif ranks_seen != world:
         raise SystemExit(f"all-reduce saw {ranks_seen} ranks, WORLD_SIZE={world}")
 
     def sync():
@@ -376,7 +426,9 @@ def main() -> int:
         "launcher": "bench.py self-launch" if os.environ.get("ST_BENCH_SELF_LAUNCHED") else
                     ("torchrun" if launched else "single process"),
     }
-    if rank == 0:
+    if args.slice:
+        out = _slice_record(out, args, est, tr, dp, world, elapsed)
+    if rank == 0 or args.slice:
         print(json.dumps(out), flush=True)
         if os.environ.get("ST_WGRAD_TUNE_LOG") == "1":  # the per-shape weight-gradient picks (stderr)
             from scaletorch_amd.ops import grad as G

@@ -980,7 +980,7 @@ __global__ __launch_bounds__(256) void flash_bwd_pre_kernel(const bf16_t* __rest
 // per lane; dQ^T += K^T dS^T feeds dS^T back as the B operand.  Keys past Sk
 // read as zero (K = V = 0 => dS^T K^T contributes nothing), so only the causal
 // diagonal is masked.
-template <int D, int PROBE = 0>  // PROBE 1: softmax / dS VALU skipped (timing probe, wrong results)
+template <int D, int PROBE = 0>  // PROBE 1 (diagnostic library only): softmax / dS VALU skipped, wrong results
 __global__ __launch_bounds__(256, 1) void flash_bwd_dq_kernel(AttnParams p,
                                                               const bf16_t* __restrict__ dout,
                                                               int64_t sdb, int64_t sds, int64_t sdh,
@@ -1332,7 +1332,7 @@ ST_DEVICE void dkdv_mask(f32x16& s, f32x16& dp, int thr) {
 }
 
 // PROBE 1: softmax / dS VALU skipped; PROBE 2 (with WDS): dS stores skipped (timing
-// probes, wrong results).
+// probes of the diagnostic library, -DST_PROBES; wrong results).
 // WDS: also store dS^T tiles into the dS workspace `dsw` (see ds_prefix) for
 // flash_bwd_dq_ds_kernel.
 template <int D, int PROBE = 0, bool WDS = false>
@@ -1973,12 +1973,18 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
     // query heads per dQ workgroup (sharing each staged K tile): 4, 2 or 1
     const int G = H / Hkv, GH = G % 4 == 0 ? 4 : (G % 2 == 0 ? 2 : 1);
     const unsigned gds = (unsigned)(((Sq + 127) / 128) * B * Hkv * (G / GH) * qsplit);
-    const char* pe = std::getenv("ST_FLASH_PROBE");  // diagnostics only (tools/bench_flash_bwd_ds.py)
+#ifdef ST_PROBES
+    const char* pe = std::getenv("ST_FLASH_PROBE");  // diagnostic library only: 2 = dS stores skipped (wrong dQ)
+    const bool probe2 = D == 128 && pe && std::atoi(pe) == 2;
+#endif
     if (phases & 1) {
-      if (D == 128 && pe && std::atoi(pe) == 2)
+#ifdef ST_PROBES
+      if (probe2)
         flash_bwd_dkdv_kernel<128, 2, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, nlse2, delta, (bf16_t*)dk,
                                                                (bf16_t*)dv, nsplit, part, ds);
-      else if (D == 128)
+      else
+#endif
+      if (D == 128)
         flash_bwd_dkdv_kernel<128, 0, true><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, nlse2, delta, (bf16_t*)dk,
                                                                (bf16_t*)dv, nsplit, part, ds);
       else
@@ -2038,16 +2044,18 @@ int st_flash_bwd(const void* q, const void* k, const void* v, const void* dout, 
     }
   }
   if (D == 128) {
-    const char* pe = std::getenv("ST_FLASH_PROBE");  // diagnostics only (tools/probe_flash.py)
+#ifdef ST_PROBES
+    const char* pe = std::getenv("ST_FLASH_PROBE");  // diagnostic library only: 1 = softmax VALU skipped
     if (pe && std::atoi(pe) == 1) {
       flash_bwd_dq_kernel<128, 1><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq, qsplit, qpart);
       flash_bwd_dkdv_kernel<128, 1><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, nlse2, delta, (bf16_t*)dk,
                                                    (bf16_t*)dv, nsplit, part, nullptr);
-    } else {
-      flash_bwd_dq_kernel<128><<<gq, 256, 0, sq>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq, qsplit, qpart);
-      flash_bwd_dkdv_kernel<128><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, nlse2, delta, (bf16_t*)dk,
-                                                   (bf16_t*)dv, nsplit, part, nullptr);
+      return (int)hipGetLastError();
     }
+#endif
+    flash_bwd_dq_kernel<128><<<gq, 256, 0, sq>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq, qsplit, qpart);
+    flash_bwd_dkdv_kernel<128><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, nlse2, delta, (bf16_t*)dk,
+                                                 (bf16_t*)dv, nsplit, part, nullptr);
   } else if (D == 64) {
     flash_bwd_dq_kernel<64><<<gq, 256, 0, st>>>(pq, dop, sdb, sds, sdh, lse, delta, (bf16_t*)dq, qsplit, qpart);
     flash_bwd_dkdv_kernel<64><<<gk, 256, 0, st>>>(pk, dop, sdb, sds, sdh, nlse2, delta, (bf16_t*)dk,

@@ -30,7 +30,7 @@ namespace {
 typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bfx4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) char lds_t;
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef uint32_t srd_t __attribute__((ext_vector_type(4)));  // buffer descriptor words (SGPR quad)
 
 constexpr int BT = 256, BK = 64, NT = 256;  // output tile BT x BT, K-tile of 64 tokens
 constexpr int RB = 256;                     // bytes per image row: 128 bf16 features
@@ -47,12 +47,18 @@ ST_DEVICE bfx8 lds_tr(const lds_t* p0, const lds_t* p1) {
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-ST_DEVICE rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+// Buffer descriptor as four explicitly wave-uniform words (what __builtin_amdgcn_make_buffer_rsrc
+// emits: base lo, base hi[15:0] with stride 0, num_records, flags 0x20000).  The DMA asm takes
+// them through an "s" constraint, so every word is a readfirstlane result: uniform to the compiler
+// at any optimisation level, not only where -O3's uniformity analysis proves it.
+ST_DEVICE srd_t make_srd(const void* base, uint32_t bytes) {
   const uint64_t a = (uint64_t)base;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
-                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+  srd_t w;
+  w[0] = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  w[1] = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) & 0xffffu;
+  w[2] = __builtin_amdgcn_readfirstlane(bytes);
+  w[3] = 0x00020000u;
+  return w;
 }
 
 ST_DEVICE void fence() { __builtin_amdgcn_sched_barrier(0); }
@@ -86,9 +92,9 @@ ST_DEVICE void tile_of(int gm, int nbm, int nbn, int vb, int nv, int& bm, int& b
 // steady-state K-tile step, summed per wave and written over C (tools/_w4stamps.py reads them)
 // KDESC: the K-tile offset lives in per-K-tile descriptors (ragged token counts, grouped
 // experts); else in soffset over one descriptor per unit (T a multiple of 64, fewer scalar ops)
-// RS 1: fragment halves read one transposed read at a time, spread thinner (sub-step 1: A at
-// MFMAs 0-15, B at even 16-46; next tile's sub-step 0: B then A at even 64-126)
-template <int PROBE = 0, bool KDESC = true, int RS = 0>
+// (A variant reading the fragment halves one transposed read at a time lost its A/B and was
+// removed; profiles/r05/wgrad4/.)  PROBE != 0 exists only in the diagnostic library (-DST_PROBES).
+template <int PROBE = 0, bool KDESC = true>
 __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                        const bf16_t* __restrict__ B, int64_t ldb,
                                                        float* __restrict__ C, int64_t ldc, int M, int N, int T,
@@ -118,21 +124,23 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
   }
   const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)smem + (uint32_t)(wid * 4 * 1024));
   auto piece_m0 = [&](int buf, int p) { return lbase + buf * STAGE + (p >> 2) * IMGW + (p & 3) * 1024; };
-  auto set_m0 = [&](uint32_t v) { asm volatile("s_mov_b32 m0, %0" : : "s"(v) : "m0"); };
+  auto set_m0 = [&](uint32_t v) {
+    asm volatile("s_mov_b32 m0, %0" : : "s"(__builtin_amdgcn_readfirstlane(v)) : "m0");
+  };
   // descriptors over K-tile kt onward of an operand slice: base advanced by kt * 64 rows, range
   // = the rows left, so a ragged last K-tile reads zeros past the token count (the range check
   // covers the VGPR offset only -- the K offset lives in the base, not in soffset)
   struct Krs {
-    rsrc_t a, b;
+    srd_t a, b;
     uint32_t soa, sob;
   };
-  rsrc_t unit_a = make_rsrc(A, 0u), unit_b = make_rsrc(B, 0u);  // !KDESC: the unit's whole-operand descriptors
+  srd_t unit_a = make_srd(A, 0u), unit_b = make_srd(B, 0u);  // !KDESC: the unit's whole-operand descriptors
   auto krs = [&](const bf16_t* abase, const bf16_t* bbase, int rows, int kt) {
     if constexpr (KDESC) {
       const int left = rows - kt * BK;
       const uint32_t ba = left > 0 ? (uint32_t)(((int64_t)(left - 1) * lda + BT) * 2) : 0u;
       const uint32_t bb = left > 0 ? (uint32_t)(((int64_t)(left - 1) * ldb + BT) * 2) : 0u;
-      return Krs{make_rsrc(abase + (int64_t)kt * BK * lda, ba), make_rsrc(bbase + (int64_t)kt * BK * ldb, bb), 0u,
+      return Krs{make_srd(abase + (int64_t)kt * BK * lda, ba), make_srd(bbase + (int64_t)kt * BK * ldb, bb), 0u,
                  0u};
     } else {
       return Krs{unit_a, unit_b, (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)kt * (uint32_t)BK * sa),
@@ -141,9 +149,11 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
   };
   auto dma_nom0 = [&](const Krs& k, int p) {
     if (p < 8)
-      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(voff[p]), "s"(k.a), "s"(k.soa) : "memory");
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds"
+                   : : "v"(voff[p]), "s"(k.a), "s"(__builtin_amdgcn_readfirstlane(k.soa)) : "memory");
     else
-      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" : : "v"(voff[p]), "s"(k.b), "s"(k.sob) : "memory");
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds"
+                   : : "v"(voff[p]), "s"(k.b), "s"(__builtin_amdgcn_readfirstlane(k.sob)) : "memory");
   };
 
   // fragment reads (16 features x 32 tokens, natural k order permuted the same way for both
@@ -164,21 +174,6 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
   auto read = [&](const lds_t* st, int ks, int r) {
     if (r < 8) fa[ks][r] = lds_tr(st + aoff[r][0] + ks * 32 * RB, st + aoff[r][1] + ks * 32 * RB);
     else fb[ks][r - 8] = lds_tr(st + boff[r - 8][0] + ks * 32 * RB, st + boff[r - 8][1] + ks * 32 * RB);
-  };
-  // one transposed read: half hf of A fragment r (r < 8) or B fragment r - 8, of sub-step ks
-  auto read_half = [&](const lds_t* st, int ks, int r, int hf) {
-    typedef __bf16 bfx4l __attribute__((ext_vector_type(4)));
-    if (r < 8) {
-      const bfx4l v = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-          (bfx4l __attribute__((address_space(3)))*)(st + aoff[r][hf] + ks * 32 * RB));
-      if (hf) fa[ks][r].hi = v;
-      else fa[ks][r].lo = v;
-    } else {
-      const bfx4l v = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-          (bfx4l __attribute__((address_space(3)))*)(st + boff[r - 8][hf] + ks * 32 * RB));
-      if (hf) fb[ks][r - 8].hi = v;
-      else fb[ks][r - 8].lo = v;
-    }
   };
   // operands swapped: acc[i][j] reg r = C[row 16 i + (lane & 15)][col 16 j + 4 G + r]
   auto mfma = [&](f32x4 (&acc)[8][8], int ks, int idx) {
@@ -215,26 +210,15 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
       constexpr int m = decltype(mc)::value;
       mfma(acc, m >> 6, m & 63);
       constexpr int pd = dslot(m), pn = dslot(m + 2);
-      if constexpr (RS == 0 && m < 32 && (m & 1) == 0 && PROBE != 2) {  // fragment r = m / 2 (A 0-7, then B)
+      if constexpr (m < 32 && (m & 1) == 0 && PROBE != 2) {  // fragment r = m / 2 (A 0-7, then B)
         fence();
         read(cs, 1, m >> 1);
-        fence();
-      }
-      if constexpr (RS == 1 && m < 16) {  // sub-step 1: A halves, one per MFMA
-        fence();
-        read_half(cs, 1, m >> 1, m & 1);
-        fence();
-      }
-      if constexpr (RS == 1 && m >= 16 && m < 48 && (m & 1) == 0) {  // then B halves, every other MFMA
-        fence();
-        read_half(cs, 1, 8 + ((m - 16) >> 2), ((m - 16) >> 1) & 1);
         fence();
       }
       if constexpr (m == 20 && more2 && PROBE != 3) {
         stamp(1);
         fence();
-        if constexpr (RS == 1) asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");  // B reads 16-20 in flight
-        else asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");  // B fragments 8-10 may be in flight
+        asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");  // B fragments 8-10 may be in flight
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         fence();
@@ -262,13 +246,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
         dma_nom0(k2, pd);
         fence();
       }
-      if constexpr (RS == 1 && more && m >= 64 && (m & 1) == 0) {  // next tile's sub-step 0: B halves, then A
-        constexpr int x = (m - 64) >> 1;
-        fence();
-        read_half(ns, 0, x < 16 ? 8 + (x >> 1) : ((x - 16) >> 1), x & 1);
-        fence();
-      }
-      if constexpr (RS == 0 && more && m >= 64 && m < 96 && (m & 1) == 0 && PROBE != 2) {
+      if constexpr (more && m >= 64 && m < 96 && (m & 1) == 0 && PROBE != 2) {
         fence();
         read(ns, 0, (m - 64) >> 1);
         fence();
@@ -326,8 +304,8 @@ __global__ __launch_bounds__(NT, 1) void wgrad4_kernel(const bf16_t* __restrict_
     const bf16_t* abase = Ag + m0;
     const bf16_t* bbase = Bg + n0;
     if constexpr (!KDESC) {
-      unit_a = make_rsrc(abase, (uint32_t)(((int64_t)(Tg - 1) * lda + BT) * 2));
-      unit_b = make_rsrc(bbase, (uint32_t)(((int64_t)(Tg - 1) * ldb + BT) * 2));
+      unit_a = make_srd(abase, (uint32_t)(((int64_t)(Tg - 1) * lda + BT) * 2));
+      unit_b = make_srd(bbase, (uint32_t)(((int64_t)(Tg - 1) * ldb + BT) * 2));
     }
     f32x4 acc[8][8];
 #pragma unroll
@@ -472,25 +450,27 @@ int st_wgrad4(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, 
   const int nfull = sp.splits > 1 ? sp.nfull : (int)nv;
   const int64_t nu = nfull + (int64_t)(nv - nfull) * sp.splits;
   const int64_t grid = std::min<int64_t>(nu, cu_count());
-  // 7: cycle stamps over C; 1 / 2 / 3: no K-loop DMA / no fragment reads / no barriers (timing
-  // probes; all wrong results)
-  const char* pe = std::getenv("ST_WGRAD4_PROBE");
-  const int pv = pe ? std::atoi(pe) : 0;
-  const bool probe = pv == 7 && grid * 4 <= M && ldc >= 12;
   // whole K-tiles: K offsets in soffset (ST_WGRAD4_KDESC=1 forces the per-K-tile descriptors)
   const char* ke = std::getenv("ST_WGRAD4_KDESC");
   const bool kdesc = T % BK != 0 || (ke && std::atoi(ke) == 1);
-  const char* re = std::getenv("ST_WGRAD4_RS");  // 1: fragment reads spread half by half (A/B)
-  const int rs = re ? std::atoi(re) : 0;
 #define W4ARGS (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, M, N, T, beta ? 1 : 0, gm, nfull, sp.splits, ws, \
                nullptr, (int64_t)0
-  if (pv == 1 && !kdesc) wgrad4_kernel<1, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
-  else if (pv == 2 && !kdesc) wgrad4_kernel<2, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
-  else if (pv == 3 && !kdesc) wgrad4_kernel<3, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
-  else if (probe && kdesc) wgrad4_kernel<7, true><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
-  else if (probe) wgrad4_kernel<7, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
-  else if (kdesc) wgrad4_kernel<0, true><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
-  else if (rs == 1) wgrad4_kernel<0, false, 1><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
+#ifdef ST_PROBES
+  // diagnostic library only (wrong results): 7 = cycle stamps over C; 1 / 2 / 3 = no K-loop DMA /
+  // no fragment reads / no barriers
+  const char* pe = std::getenv("ST_WGRAD4_PROBE");
+  const int pv = pe ? std::atoi(pe) : 0;
+  if (pv) {
+    if (pv == 1 && !kdesc) wgrad4_kernel<1, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
+    else if (pv == 2 && !kdesc) wgrad4_kernel<2, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
+    else if (pv == 3 && !kdesc) wgrad4_kernel<3, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
+    else if (pv == 7 && grid * 4 <= M && ldc >= 12 && kdesc) wgrad4_kernel<7, true><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
+    else if (pv == 7 && grid * 4 <= M && ldc >= 12) wgrad4_kernel<7, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
+    else return -2;
+    return (int)hipGetLastError();
+  }
+#endif
+  if (kdesc) wgrad4_kernel<0, true><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
   else wgrad4_kernel<0, false><<<(unsigned)grid, NT, 0, st>>>(W4ARGS);
 #undef W4ARGS
   if (sp.splits > 1) {

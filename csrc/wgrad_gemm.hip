@@ -679,23 +679,28 @@ int st_wgrad_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, float*
   const SplitPlan sp{ws, L.nfull, L.tail, L.split};
   const int nbm = M / BM, nbn = N / L.bn;
   const int grid = L.split > 1 ? L.nfull + L.tail * L.split : nbm * nbn;
-  const char* pe = std::getenv("ST_WGRAD_PROBE");  // 1: no K-loop DMA, 2: no LDS reads (timing probes, wrong results)
-  const int probe = pe ? std::atoi(pe) : 0;
   const bf16_t *a = (const bf16_t*)A, *b = (const bf16_t*)B;
   const int bt = beta ? 1 : 0;
-  if (L.variant == 2) {
+#ifdef ST_PROBES
+  // diagnostic library only (wrong results): 1 = no K-loop DMA, 2 = no LDS reads, 3 / 4 (8-phase)
+  const char* pe = std::getenv("ST_WGRAD_PROBE");
+  const int probe = pe ? std::atoi(pe) : 0;
+  if (probe && L.variant == 2) {
     if (probe == 1) wgrad8_kernel<1><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
     else if (probe == 2) wgrad8_kernel<2><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
     else if (probe == 3) wgrad8_kernel<3><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
-    else if (probe == 4) wgrad8_kernel<4><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
-    else wgrad8_kernel<0><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
-  } else if (L.bn == 256) {
-    if (probe == 1) wgrad_gemm_kernel<1, 256><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp, GroupPlan{});
-    else wgrad_gemm_kernel<0, 256><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp, GroupPlan{});
-  } else {
-    if (probe == 1) wgrad_gemm_kernel<1, 128><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp, GroupPlan{});
-    else wgrad_gemm_kernel<0, 128><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp, GroupPlan{});
+    else wgrad8_kernel<4><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
+    return (int)hipGetLastError();
   }
+  if (probe == 1) {
+    if (L.bn == 256) wgrad_gemm_kernel<1, 256><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp, GroupPlan{});
+    else wgrad_gemm_kernel<1, 128><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp, GroupPlan{});
+    return (int)hipGetLastError();
+  }
+#endif
+  if (L.variant == 2) wgrad8_kernel<0><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp);
+  else if (L.bn == 256) wgrad_gemm_kernel<0, 256><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp, GroupPlan{});
+  else wgrad_gemm_kernel<0, 128><<<grid, NT, 0, st>>>(a, lda, b, ldb, C, ldc, M, N, T, bt, sp, GroupPlan{});
   ST_HIP_CHECK(hipGetLastError());
   if (L.split > 1) {
     const dim3 rg(BM * L.bn / 1024, L.tail);

@@ -132,8 +132,24 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False, v
     return LIB
 
 
+PROBES = "probes"  # the diagnostic library: build/variants/probes.so
+
+
+def build_probes(verbose: bool = False, force: bool = False) -> Path:
+    """The diagnostic library: every kernel file compiled with ``-DST_PROBES``, which adds the
+    timing-probe kernels (wrong results by design: DMA / LDS reads / stores / softmax skipped,
+    cycle stamps over the output) and their ``ST_*_PROBE`` switches.  The production
+    ``_st_kernels.so`` contains none of them; the Python-side probes refuse to run unless this
+    library is the loaded one (``ST_KERNEL_LIB=build/variants/probes.so``, ``ops/_lib.py``)."""
+    flags = {src.name: ["-DST_PROBES"] for src in CSRC.glob("*.hip")}
+    return build(verbose=verbose, force=force, variant=PROBES, variant_flags=flags)
+
+
 if __name__ == "__main__":
-    # python -m scaletorch_amd._build [--force] [-v] [--variant NAME file.hip="-flag -flag" ...]
+    # python -m scaletorch_amd._build [--force] [-v] [--probes] [--variant NAME file.hip="-flag -flag" ...]
+    if "--probes" in sys.argv:
+        print(build_probes(verbose="-v" in sys.argv, force="--force" in sys.argv))
+        sys.exit(0)
     var, vflags = None, {}
     for a in sys.argv[1:]:
         if a.startswith("--variant="):

@@ -99,6 +99,17 @@ def init_dist(launcher: str | None = None, backend: str | None = None, use_cpu: 
     A single process with no launcher env runs with world size 1 and NO
     process group (like the reference, parallel modules then see ``pgm`` unset).
     """
+    if backend == "loopback":
+        # one rank of a layout on one device (bench.py --slice): world / rank of the rank to
+        # impersonate come from ST_LOOPBACK_WORLD / ST_LOOPBACK_RANK, collectives are local copies
+        from .loopback import init_loopback
+
+        world = int(os.environ.get("ST_LOOPBACK_WORLD", "1"))
+        rank = int(os.environ.get("ST_LOOPBACK_RANK", "0"))
+        if torch.cuda.is_available() and not use_cpu:
+            torch.cuda.set_device(0)
+        init_loopback(world, rank)
+        return rank, 0, world
     launcher = launcher or infer_launcher()
     if launcher == "slurm":
         _slurm_env(port)

@@ -246,16 +246,19 @@ def set_ep_token_bound(n: int | None) -> None:
     _TOKEN_BOUND["n"] = None if n is None else int(n)
 
 
-def ep_rows_range(T: int, group) -> tuple[int, int]:
+def ep_rows_range(T: int, group, agree: bool = False) -> tuple[int, int]:
     """(smallest, largest) local token count over the EP group.
 
     Every rank takes the same branch on every call, so the collectives on the EP group stay
     in step even when the token counts change between calls: with a declared bound
     (``set_ep_token_bound``) no collective runs and the range is (T, bound) -- a local T above
     the bound raises; otherwise ONE all-reduce per call (no cache keyed on the local T: a rank
-    whose T repeats would skip the collective its peers enter -- ADVICE r04)."""
+    whose T repeats would skip the collective its peers enter -- ADVICE r04).  ``agree``
+    forces the all-reduce even with a declared bound: the capacity dispatch needs the TRUE
+    range, so a rank below the bound makes every rank raise together instead of leaving its
+    peers in the all-to-all."""
     n = _TOKEN_BOUND["n"]
-    if n is not None:
+    if n is not None and not agree:
         if int(T) > n:
             raise ValueError(f"MoE call with {T} tokens exceeds the declared EP token bound {n}")
         return int(T), n
@@ -941,7 +944,7 @@ class MoELayer(nn.Module):
         group = mesh.pgm.ep_group
         ep, k = self.ep, self.top_k
         T = x2.shape[0]
-        lo, hi = ep_rows_range(T, group)
+        lo, hi = ep_rows_range(T, group, agree=True)  # one [2] all-reduce: every rank sees the same range
         if lo != hi:  # the static buffers assume one token count on every EP rank (raised on every rank)
             raise ValueError(f"capacity EP dispatch needs the same token count on every EP rank (got {lo}..{hi}); "
                              "use the dropless dispatch (--moe_capacity_factor 0)")

@@ -71,3 +71,22 @@ def ops():
 
 def load_error() -> str | None:
     return _load_error
+
+
+def is_probe_build() -> bool:
+    """True when the loaded kernel library is the diagnostic build (``_build.py --probes``)."""
+    return _LIB_PATH.stem == "probes" and _LIB_PATH.parent.name == "variants"
+
+
+def probe_env(name: str) -> str | None:
+    """Value of a timing-probe switch (``ST_*_PROBE*``: skips or fakes work, so the results are
+    WRONG), or None when unset / "0".  Honoured only with the diagnostic library loaded; set on a
+    production build it raises, so a stray variable can never corrupt a training run."""
+    v = os.environ.get(name)
+    if not v or v == "0":
+        return None
+    if not is_probe_build():
+        raise RuntimeError(f"{name}={v} selects a timing probe with WRONG results; it runs only with the "
+                           "diagnostic kernel library (python -m scaletorch_amd._build --probes; "
+                           "ST_KERNEL_LIB=build/variants/probes.so)")
+    return v

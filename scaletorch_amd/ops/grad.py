@@ -74,8 +74,9 @@ def prepare_dgrad_weight(w: torch.Tensor) -> None:
         w._st_wt_done = pending
         w._st_wt_epoch = _WT_EPOCH[0]
         return
-    if os.environ.get("ST_DGRAD_WT_PROBE_STALE") == "1" and getattr(w, "_st_wt", None) is not None:
-        # timing probe only (WRONG gradients): reuse the previous step's W^T, no transpose
+    if getattr(w, "_st_wt", None) is not None and _lib.probe_env("ST_DGRAD_WT_PROBE_STALE"):
+        # timing probe of the diagnostic library only (WRONG gradients): reuse the previous
+        # step's W^T, no transpose
         w._st_wt_epoch = _WT_EPOCH[0]
         return
     buf = getattr(w, "_st_wt", None)
@@ -322,7 +323,6 @@ def _wgrad_pick(dy2d: torch.Tensor, x2d: torch.Tensor) -> int:
 
 
 _WGRAD_SIDE: dict = {}
-_TN_PROBE_BUFS: dict = {}  # ST_WGRAD_TN_PROBE=1 timing probe: stale token-contiguous operands per shape
 
 
 def wgrad_side_stream(device: torch.device):
@@ -360,19 +360,6 @@ def accumulate_linear_wgrad(param: torch.Tensor, dy2d: torch.Tensor, x2d: torch.
     if pre is None and mg.dtype == torch.float32:
         pre = prefetch_wgrad(param, dy2d, x2d)
     beta = 0 if take_fresh(param) else 1
-    if os.environ.get("ST_WGRAD_TN_PROBE") == "1" and mg.dtype == torch.float32 and dy2d.is_cuda:
-        # TIMING PROBE ONLY (wrong gradients): the weight gradient as a TN GEMM on token-
-        # contiguous dY^T / X^T that cost nothing to produce (stale per-shape buffers) -- the
-        # in-step upper bound of "producers store transposed copies" 
-        from . import _lib
-
-        key = (tuple(dy2d.shape), tuple(x2d.shape), dy2d.device.index)
-        bufs = _TN_PROBE_BUFS.get(key)
-        if bufs is None:
-            bufs = _TN_PROBE_BUFS[key] = (dy2d.t().contiguous(), x2d.t().contiguous())
-        _lib.ops().gemm_(mg.view(mg.shape[0], -1), bufs[0], bufs[1], False, True, 1.0, float(beta))
-        _grad_ready(param)
-        return None
     if pre is not None:
         torch.cuda.current_stream().wait_event(pre.done)
         m2 = mg.view(mg.shape[0], -1)

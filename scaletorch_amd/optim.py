@@ -156,8 +156,8 @@ class _ArenaOptimizer(torch.optim.Optimizer):
     def grad_norm(self, mp_group=None) -> torch.Tensor:
         """Global L2 norm of the gradients (device scalar, fp32)."""
         self._zero_unwritten()
-        if os.environ.get("ST_NORM_PROBE_SKIP") == "1":
-            # timing probe only (no clipping, norm reported as 0): what the norm passes cost
+        if _lib.probe_env("ST_NORM_PROBE_SKIP"):
+            # timing probe of the diagnostic library only (no clipping, norm reported as 0)
             for a in self.arenas:
                 a.sq_count = 0
             return torch.zeros(1, dtype=torch.float32, device=self.arenas[0].grad_flat.device)
@@ -258,9 +258,9 @@ class ArenaAdamW(_ArenaOptimizer):
         st = self.side_stream
         if self.clip_coef is not None:
             self.clip_coef.record_stream(st)
-        # timing probe only (WRONG training: the weights never change): ST_OPT_PROBE_SKIP=1
-        # skips every update kernel, so an A/B prices what the side-stream AdamW costs the step
-        skip = os.environ.get("ST_OPT_PROBE_SKIP") == "1"
+        # timing probe of the diagnostic library only (WRONG training: the weights never change):
+        # ST_OPT_PROBE_SKIP=1 skips every update kernel, so an A/B prices the side-stream AdamW
+        skip = _lib.probe_env("ST_OPT_PROBE_SKIP") is not None
         fuse_wt = os.environ.get("ST_ADAMW_WT", "1") == "1"
         with torch.cuda.stream(st):
             st.wait_event(ev)

@@ -272,9 +272,10 @@ class GradArena:
         st = self.side_stream
         if st is None or os.environ.get("ST_BUCKET_NORM", "1") != "1":  # 0: one pass after backward (A/B)
             return
-        if os.environ.get("ST_NORM_PROBE_SKIP") == "1":  # timing probe (optim.grad_norm)
-            return
         from ..ops import _lib
+
+        if _lib.probe_env("ST_NORM_PROBE_SKIP"):  # timing probe (optim.grad_norm), diagnostic library only
+            return
 
         g = self.grad_flat[b.start: b.end]
         if not _lib.use_native(g) or g.numel() % 4:

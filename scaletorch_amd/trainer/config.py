@@ -65,7 +65,8 @@ class ParallelArguments:
     virtual_pipeline_size: int = field(default=1, metadata={"help": "model chunks per pipeline rank: > 1 runs the "
                                                                       "interleaved 1F1B schedule (needs 1f1b and "
                                                                       "gradient_accumulation_steps % pp == 0)"})
-    backend: str = field(default="nccl", metadata={"help": "nccl (=RCCL) | gloo | hccl (maps to nccl)"})
+    backend: str = field(default="nccl", metadata={"help": "nccl (=RCCL) | gloo | hccl (maps to nccl) | loopback "
+                                                           "(one rank of a layout on one GPU, dist/loopback.py)"})
     sequence_parallel: bool = field(default=False, metadata={"help": "Megatron-SP over the TP group"})
     cp_zigzag: bool = field(default=True, metadata={"help": "zig-zag load-balanced CP chunks"})
     tp_comm: str = field(default="auto", metadata={"help": "TP transport: auto (one node: tp = 2 self-tests the 7-link xGMI pair path, tp 4 / 8 the TP-group communicator's all-reduce / all-gather / reduce-scatter at the run's real message size, each against RCCL at start-up, keeping every collective that is correct and faster) | rccl | xgmi (custom one-/two-shot all-reduce + all-gather / reduce-scatter over IPC peer memory, dist/xgmi.py)"})
@@ -104,8 +105,8 @@ class ParallelArguments:
             raise ValueError(f"ep_comm must be auto, rccl or xgmi, got {self.ep_comm}")
         if self.moe_capacity_factor < 0 or self.moe_ep_chunks < 1:
             raise ValueError("moe_capacity_factor must be >= 0 and moe_ep_chunks >= 1")
-        if self.backend not in {"nccl", "gloo", "hccl"}:
-            raise ValueError(f"backend must be one of {{nccl, gloo, hccl}}, got {self.backend}")
+        if self.backend not in {"nccl", "gloo", "hccl", "loopback"}:
+            raise ValueError(f"backend must be one of {{nccl, gloo, hccl, loopback}}, got {self.backend}")
 
 
 @dataclass

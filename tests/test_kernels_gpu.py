@@ -930,13 +930,13 @@ def test_mlp_fused_swiglu_matches_unfused():
         assert rel(a, b) < 2e-2
 
 
-@pytest.mark.parametrize("kind", ["0", "1", "2", "4", "5", "6"])
-def test_gemm4w_variants_match_fp32(kind, monkeypatch):
-    """The one-wave-per-SIMD GEMM experiment (csrc/gemm4w.hip; docs/PERF.md round 5) in each
-    variant -- 2x2 register-staged, 1x4 direct weight fragments (2- / 3-deep), 2x2 LDS-DMA --
-    vs an fp32 per-group reference: empty / 1-row / partial / multi-tile groups, strided x,
-    K = 192 (three 64-k tiles) and K = 1024."""
-    monkeypatch.setenv("ST_GEMM4W_KIND", kind)
+@pytest.mark.parametrize("persist", ["1", "0"])
+def test_gemm4w_matches_fp32(persist, monkeypatch):
+    """The one-wave-per-SIMD grouped GEMM (csrc/gemm4w.hip: MoE long-K experts), persistent
+    grid and one tile per workgroup, vs an fp32 per-group reference: empty / 1-row / partial /
+    multi-tile groups, strided x, K = 192 (three 64-k tiles) and K = 1024."""
+    monkeypatch.setenv("ST_GEMM4W_PERSIST", persist)
+    kind = "5"
     torch.manual_seed(11)
     # the last case has 320 tiles: a persistent workgroup (kinds 5, 6) walks several of them
     for K, counts, N in ((192, [37, 0, 300, 1, 513], 512), (1024, [256, 700], 512), (192, [3000, 0, 1999, 1], 4096)):

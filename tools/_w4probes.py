@@ -1,5 +1,6 @@
 """wgrad4 timing probes (ST_WGRAD4_PROBE 1 / 2 / 3: the K-loop without its DMA / fragment reads /
 barriers -- wrong results, timing only) vs the real kernel, Llama-3-8B wgrad shapes, no tail split."""
+import os as _os; _os.environ.setdefault("ST_KERNEL_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))), "build", "variants", "probes.so"))  # noqa: E401,E702 -- timing probes exist only in the diagnostic library (python -m scaletorch_amd._build --probes)
 import json
 import os
 import sys

@@ -2,6 +2,7 @@
 K-tile step (64 tokens, 128 16x16x32 MFMAs per wave: floor 2,048 cycles), averaged over every wave.
 Segments: MFMA 0-20 (sub-step-1 reads + A-image release wait), the m=20 barrier, 20-63 (A DMAs),
 the m=63 publish barrier (vmcnt + barrier), 63-127 (B DMAs + next tile's sub-step-0 reads)."""
+import os as _os; _os.environ.setdefault("ST_KERNEL_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))), "build", "variants", "probes.so"))  # noqa: E401,E702 -- timing probes exist only in the diagnostic library (python -m scaletorch_amd._build --probes)
 import json
 import os
 import sys

@@ -49,8 +49,8 @@ def main():
         for name, fn, env in (("hipblaslt_gemm", gemm_only, {}), ("hipblaslt_gemm+swiglu", unfused, {}),
                               ("fused_o0", fused, {"ST_GEMM4W_ORDER": "0"}),
                               ("fused_o4", fused, {"ST_GEMM4W_ORDER": "4"}),
-                              ("gemm4w_k5_o0", plain5, {"ST_GEMM4W_KIND": "5", "ST_GEMM4W_ORDER": "0"}),
-                              ("gemm4w_k5_o4", plain5, {"ST_GEMM4W_KIND": "5", "ST_GEMM4W_ORDER": "4"})):
+                              ("gemm4w_k5_o0", plain5, {"ST_GEMM4W_ORDER": "0"}),
+                              ("gemm4w_k5_o4", plain5, {"ST_GEMM4W_ORDER": "4"})):
             os.environ.update(env)
             ms = timeit(fn)
             for k in env:

@@ -74,11 +74,10 @@ def main() -> int:
         if not wn and N % 256 == 0 and K % 64 == 0:  # the one-wave-per-SIMD kernel (csrc/gemm4w.hip)
             def g4(order):
                 def run():
-                    os.environ["ST_GEMM4W_KIND"], os.environ["ST_GEMM4W_ORDER"] = "5", order
+                    os.environ["ST_GEMM4W_ORDER"] = order
                     try:
                         return _lib.ops().gemm4w(x, w, offs)
                     finally:
-                        os.environ.pop("ST_GEMM4W_KIND", None)
                         os.environ.pop("ST_GEMM4W_ORDER", None)
                 return run
             arms["gemm4w_k5_o0"] = g4("0")

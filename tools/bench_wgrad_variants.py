@@ -5,6 +5,7 @@ tail split), against hipBLASLt.  Checks each against an fp32 product of the same
 operands, then times them interleaved in one process (csrc/wgrad_gemm.hip).  With
 ST_WGRAD_PROBE=1/3/4 the 8-phase arms run the timing probes (no DMA / DMA never waited
 for / DMA from an L2-hot tile; wrong results): profiles/r03/wgrad_ring.md."""
+import os as _os; _os.environ.setdefault("ST_KERNEL_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))), "build", "variants", "probes.so"))  # noqa: E401,E702 -- timing probes exist only in the diagnostic library (python -m scaletorch_amd._build --probes)
 from __future__ import annotations
 
 import argparse

@@ -3,6 +3,7 @@
 full forward + backward vs the VALU-skipped bwd probe (ST_FLASH_PROBE=1, wrong
 results), interleaved in one process.  Run under rocprofv3 --kernel-trace --stats
 for the per-kernel split."""
+import os as _os; _os.environ.setdefault("ST_KERNEL_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))), "build", "variants", "probes.so"))  # noqa: E401,E702 -- timing probes exist only in the diagnostic library (python -m scaletorch_amd._build --probes)
 import os
 import sys
 

@@ -1,3 +1,4 @@
+import os as _os; _os.environ.setdefault("ST_KERNEL_LIB", _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))), "build", "variants", "probes.so"))  # noqa: E401,E702 -- timing probes exist only in the diagnostic library (python -m scaletorch_amd._build --probes)
 import os, sys, torch, json
 sys.path.insert(0, os.getcwd())
 from scaletorch_amd.ops import _lib
