@@ -199,9 +199,16 @@ def _tp_selftest(comm, group, msg_bytes: int):
     ag_r, t_ag_r = timed(lambda: C.all_gather(part, group=group))
     rs_x, t_rs_x = timed(lambda: comm.reduce_scatter(x))
     rs_r, t_rs_r = timed(lambda: C.reduce_scatter(x, group=group))
+    # the one-shot kernel (messages <= 512 KiB: vocab-parallel CE and norm all-reduces) is a
+    # different code path from the two-shot one the run-size probe exercises: check it too
+    ns = min(n, (256 << 10) // 2 // (8 * ws) * (8 * ws))
+    xs = x[:ns].contiguous()
+    ar_s = comm.all_reduce(xs, out=torch.empty_like(xs))
+    ref_s = everyone[:, :ns].sum(0)
     comm.check()
     tol = ref.abs() * 2.0 ** -8 + 1e-6  # one bf16 rounding of the exact (fp32) sum
     ar_ok = bool(((ar_x.float() - ref).abs() <= tol).all())
+    ar_ok = ar_ok and bool(((ar_s.float() - ref_s).abs() <= ref_s.abs() * 2.0 ** -8 + 1e-6).all())
     chunk = n // ws
     rs_ok = bool(((rs_x.float() - ref[r * chunk:(r + 1) * chunk]).abs() <= tol[r * chunk:(r + 1) * chunk]).all())
     ag_ok = bool(torch.equal(ag_x, ag_r))
@@ -216,6 +223,7 @@ def _tp_selftest(comm, group, msg_bytes: int):
     info = {"msg_mb": round(2 * n / (1 << 20), 2), "world": ws,
             "ar_ms": [round(t_ar_x, 3), round(t_ar_r, 3)], "ag_ms": [round(t_ag_x, 3), round(t_ag_r, 3)],
             "rs_ms": [round(t_rs_x, 3), round(t_rs_r, 3)],
+            "small_ar_kib": round(2 * ns / 1024, 1),
             "correct": {"all_reduce": ar_ok, "all_gather": ag_ok, "reduce_scatter": rs_ok}, "local": per_op,
             "timing": "ignored (ranks share one GPU)" if shared else "xgmi kept only where faster"}
     return per_op, info

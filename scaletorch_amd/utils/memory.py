@@ -132,7 +132,11 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
             cp_ds_budget_bytes = _ds_budget_bytes()
         s_loc = seq_len / cp
         widest = micro_batch * (H / tp) * (s_loc / 2) * seq_len * 2  # last zig-zag chunk x its full prefix
-        act += min(cp_ds_budget_bytes, widest) + widest
+        from ..parallel.context_parallel import _CP_ONE_SHOT_REST
+
+        # default (ST_CP_ONE_SHOT_REST=1): only the widest-prefix chunk keeps a dS workspace, the
+        # others run the one-shot backward; all-dS mode: the budgeted workspaces + the widest
+        act += widest if _CP_ONE_SHOT_REST[0] else min(cp_ds_budget_bytes, widest) + widest
     # bf16 W^T copies of the dense projection weights (TN data-gradient GEMMs, ops/grad.py)
     wt = 2 * (dense - 2 * h * layers - (h * cfg.num_experts if cfg.is_moe else 0) * layers)
     g = 1e9
