@@ -533,21 +533,33 @@ __global__ __launch_bounds__(256 * HP, 2 / HP) void flash_fwd_kernel(AttnParams 
   }
 }
 
-// ============================================================== forward, 64 queries per wave
-// Opt-in experiment (ST_FLASH_FWD_W64=1), recorded: each wave owns TWO 32-query blocks (256
-// queries per workgroup, one workgroup per CU), so every K / V^T fragment read feeds two MFMAs
-// -- half the LDS bytes per FLOP of the 4-wave kernel above.  Bitwise equal to it, but 40 %
-// slower at the bench shape (1.18 vs 0.84 ms, profiles/r05/flash/fwd_w64_vs_w32.log): the
-// 4-wave kernel's 1 KiB per 32-cycle MFMA is only half of gfx950's 256 B/clk LDS array, so
-// LDS bandwidth was not its limit, and at one wave per SIMD nothing overlaps the softmax VALU
-// and the barrier waits with the MFMAs (two co-resident 4-wave workgroups do).  The O accumulators (2 x D/32 tiles) are pinned to AGPRs; Q, S and
-// the P fragments stay in VGPRs.  A wave skips the MFMA / softmax work of key blocks wholly
-// past its own last query (it still takes part in the tile DMA and barriers).
-template <int D, bool XCD = true>
-__global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(AttnParams p, bf16_t* __restrict__ o,
-                                                               int64_t sob, int64_t sos, int64_t soh,
-                                                               float* __restrict__ lse) {
-  constexpr int BM = 256, BN = 64, NKK = D / 16, NDT = D / 32;
+// ============================================================== forward, 64 queries per wave, software-pipelined
+// One workgroup per CU (4 waves, one per SIMD), 256 queries of one (b, q-head); each wave owns
+// 64 queries as two 32-row blocks qb, so every K / V^T fragment read from LDS feeds two MFMAs.
+// At one wave per SIMD nothing else hides the softmax, so the kernel pipelines it under the
+// MFMAs of the NEXT product itself -- per key tile j of 64 keys, two phases of 32 MFMAs:
+//   X(j): O += V(j-1) P(j-1)   beside   softmax of S(j): mask, row max, rescale decision,
+//                                        exp2 / row sums (VALU); P(j) fragments written
+//                                        over P(j-1) after the last MFMA that reads it
+//   Y(j): S(j+1) = K(j+1) Q^T  beside   K fragment reads (and the rare O rescale)
+// The O rescale decided in X(j) is applied at the top of Y(j), when PV(j-1) has completed and
+// no P at the new scale has entered O (cdna_hip_programming.md T13 ordering).  Q fragments and
+// O live in AGPRs (asm MFMAs: Q as the B operand read from the AGPR file), S and P in VGPRs.  LDS: K[2] V[2] images as the 4-wave kernel's; iteration j DMAs K(j+2) and
+// V(j) (8 x 1 KiB pieces per wave) right after its barrier -- one barrier per tile.
+// Waves whose queries see fewer key tiles than the workgroup still run every tile (masked to
+// P = 0), so no accumulator crosses a branch.
+ST_DEVICE void mfma_qa(f32x16& s, bfx8 k, const bfx8& q) {  // S += K Q^T, Q from the AGPR file
+  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(s) : "v"(k), "a"(q));
+}
+ST_DEVICE void mfma_qa0(f32x16& s, bfx8 k, const bfx8& q) {  // first k-step: C = 0
+  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=v"(s) : "v"(k), "a"(q));
+}
+
+template <bool XCD = true>
+__global__ __launch_bounds__(256, 1) void flash_fwd_pw_kernel(AttnParams p, bf16_t* __restrict__ o,
+                                                              int64_t sob, int64_t sos, int64_t soh,
+                                                              float* __restrict__ lse) {
+  constexpr int D = 128, BM = 256, BN = 64, NKK = D / 16, NDT = D / 32;
   constexpr int TB = BN * D * 2;
   __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];  // K0 K1 V0 V1
   lds_t* smem = (lds_t*)smem_raw;
@@ -582,9 +594,11 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(AttnParams p, bf1
     for (int kk = 0; kk < NKK; ++kk)
       qf[qb][kk] = bload_frag(rq, (uint32_t)(wq0 + 32 * qb + r) * (uint32_t)(p.sqs * 2) + (2 * kk + h) * 16);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): see flash_fwd_kernel
-  int nkb, kb_mask, wnkb, wmask;
-  key_blocks<BM, BN>(p, q0, true, nkb, kb_mask);
-  key_blocks<64, BN>(p, wq0, true, wnkb, wmask);  // this wave's own range (wave-uniform)
+  int nkb, kbm_wg, wnkb, wmask;
+  key_blocks<BM, BN>(p, q0, true, nkb, kbm_wg);       // tiles any query of the workgroup sees
+  key_blocks<64, BN>(p, wq0, true, wnkb, wmask);      // this wave's own (masking from wmask on)
+  (void)kbm_wg;
+  (void)wnkb;
 
   LdsAddr<D> la;
   la.init(lane);
@@ -597,118 +611,182 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(AttnParams p, bf1
   for (int qb = 0; qb < 2; ++qb)
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) oacc[qb][dt] = zero16();
-  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  f32x16 s[2][2];
+  bfx8 pbuf[2][4];  // [qb][k-step]: P(j), written after the last MFMA that reads P(j-1)
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f}, alpha[2] = {1.f, 1.f};
+  bool resc = false;  // wave-uniform: an O rescale is pending (decided in X, applied in Y)
   const float c2 = p.scale * kLog2e;
   const int64_t qg0 = p.q_offset + wq0 + r;
 
-  if (nkb > 0) {
-    sk.load(rk, smem, 0);
-    sv.load(rv, smem + 2 * TB, 0);
+  // The pieces below are macros, not lambdas: a lambda that captures another lambda keeps the
+  // accumulator arrays addressable and hipcc parks them in scratch (see flash_fwd_pp_kernel).
+  // S(t) = K(t) Q^T from the K image kt (both 32-key halves, both query blocks); K row
+  // fragments one k-step ahead
+#define PW_S_TILE(KT)                                                               \
+  do {                                                                              \
+    const lds_t* kt_ = (KT);                                                        \
+    bfx8 fk[2][2];                                                                  \
+    fk[0][0] = la.rowf(kt_, 0, 0);                                                  \
+    fk[0][1] = la.rowf(kt_, 1, 0);                                                  \
+    _Pragma("unroll") for (int kk = 0; kk < NKK; ++kk) {                            \
+      if (kk + 1 < NKK) {                                                           \
+        fk[(kk + 1) & 1][0] = la.rowf(kt_, 0, kk + 1);                              \
+        fk[(kk + 1) & 1][1] = la.rowf(kt_, 1, kk + 1);                              \
+      }                                                                             \
+      __builtin_amdgcn_sched_barrier(0);                                            \
+      _Pragma("unroll") for (int h2 = 0; h2 < 2; ++h2)                              \
+      _Pragma("unroll") for (int qb = 0; qb < 2; ++qb) {                            \
+        if (kk == 0) mfma_qa0(s[qb][h2], fk[0][h2], qf[qb][0]);                     \
+        else mfma_qa(s[qb][h2], fk[kk & 1][h2], qf[qb][kk]);                        \
+      }                                                                             \
+    }                                                                               \
+  } while (0)
+  // mask (diagonal / tail tiles), row max, rescale decision (l scaled now, O at the next Y)
+#define PW_MASK_MAX(KB)                                                                   \
+  do {                                                                                    \
+    if ((KB) >= wmask) {                                                                  \
+      _Pragma("unroll") for (int qb = 0; qb < 2; ++qb) {                                  \
+        const int lim = key_limit(p, (KB), BN, qg0 + 32 * qb, h, true);                   \
+        _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                  \
+          if (acc_row0(i) > lim) s[qb][0][i] = -INFINITY;                                 \
+          if (acc_row0(i) + 32 > lim) s[qb][1][i] = -INFINITY;                            \
+        }                                                                                 \
+      }                                                                                   \
+    }                                                                                     \
+    float mxs[2];                                                                         \
+    _Pragma("unroll") for (int qb = 0; qb < 2; ++qb) {                                    \
+      float mx0 = fmaxf(s[qb][0][0], s[qb][1][0]), mx1 = fmaxf(s[qb][0][1], s[qb][1][1]); \
+      _Pragma("unroll") for (int i = 2; i < 16; i += 2) {                                 \
+        mx0 = fmaxf(mx0, fmaxf(s[qb][0][i], s[qb][1][i]));                               \
+        mx1 = fmaxf(mx1, fmaxf(s[qb][0][i + 1], s[qb][1][i + 1]));                        \
+      }                                                                                   \
+      float mx = fmaxf(mx0, mx1);                                                         \
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));                                             \
+      mxs[qb] = mx * c2;                                                                  \
+    }                                                                                     \
+    if (__any(mxs[0] > m[0] + kRescaleThr || mxs[1] > m[1] + kRescaleThr)) {              \
+      _Pragma("unroll") for (int qb = 0; qb < 2; ++qb) {                                  \
+        const float m_new = fmaxf(m[qb], mxs[qb]);                                        \
+        alpha[qb] = (m[qb] == m_new) ? 1.f : fast_exp2(m[qb] - m_new);                    \
+        l[qb] *= alpha[qb];                                                               \
+        m[qb] = m_new;                                                                    \
+      }                                                                                   \
+      resc = true;                                                                        \
+    }                                                                                     \
+  } while (0)
+#define PW_EXP_SUM(QB)                                                  \
+  do {                                                                  \
+    const float mu = (m[QB] == -INFINITY) ? 0.f : m[QB];                \
+    float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f;                       \
+    _Pragma("unroll") for (int i = 0; i < 16; i += 2) {                 \
+      s[QB][0][i] = fast_exp2(fmaf(s[QB][0][i], c2, -mu));              \
+      s[QB][1][i] = fast_exp2(fmaf(s[QB][1][i], c2, -mu));              \
+      s[QB][0][i + 1] = fast_exp2(fmaf(s[QB][0][i + 1], c2, -mu));      \
+      s[QB][1][i + 1] = fast_exp2(fmaf(s[QB][1][i + 1], c2, -mu));      \
+      r0 += s[QB][0][i];                                                \
+      r1 += s[QB][1][i];                                                \
+      r2 += s[QB][0][i + 1];                                            \
+      r3 += s[QB][1][i + 1];                                            \
+    }                                                                   \
+    float rs = (r0 + r1) + (r2 + r3);                                   \
+    rs += __shfl_xor(rs, 32, 64);                                       \
+    l[QB] += rs;                                                        \
+  } while (0)
+#define PW_TO_P()                                            \
+  _Pragma("unroll") for (int qb = 0; qb < 2; ++qb) {         \
+    pbuf[qb][0] = acc_frag(s[qb][0], 0);                     \
+    pbuf[qb][1] = acc_frag(s[qb][0], 1);                     \
+    pbuf[qb][2] = acc_frag(s[qb][1], 0);                     \
+    pbuf[qb][3] = acc_frag(s[qb][1], 1);                     \
   }
-  dma_barrier();
+  // O += V(t) P(t) from the V image VT, four d-tile groups of 8 MFMAs; BETWEEN(dt) runs
+  // after group dt (sched_barrier keeps it there)
+#define PW_PV(VT, BETWEEN)                                                        \
+  do {                                                                                \
+    const lds_t* vt_ = (VT);                                                          \
+    bfx8 vf[2][4];                                                                    \
+    _Pragma("unroll") for (int dt = 0; dt < NDT; ++dt) {                              \
+      if (dt == 0) {                                                                  \
+        vf[0][0] = la.trf(vt_, 0, 0, 0);                                              \
+        vf[0][1] = la.trf(vt_, 0, 1, 0);                                              \
+        vf[0][2] = la.trf(vt_, 32, 0, 0);                                             \
+        vf[0][3] = la.trf(vt_, 32, 1, 0);                                             \
+      }                                                                               \
+      if (dt + 1 < NDT) {                                                             \
+        vf[(dt + 1) & 1][0] = la.trf(vt_, 0, 0, dt + 1);                              \
+        vf[(dt + 1) & 1][1] = la.trf(vt_, 0, 1, dt + 1);                              \
+        vf[(dt + 1) & 1][2] = la.trf(vt_, 32, 0, dt + 1);                             \
+        vf[(dt + 1) & 1][3] = la.trf(vt_, 32, 1, dt + 1);                             \
+      }                                                                               \
+      __builtin_amdgcn_sched_barrier(0);                                              \
+      _Pragma("unroll") for (int qb = 0; qb < 2; ++qb)                                \
+      _Pragma("unroll") for (int u = 0; u < 4; ++u)                                   \
+        mfma_acc(oacc[qb][dt], vf[dt & 1][u], pbuf[qb][u]);                           \
+      __builtin_amdgcn_sched_barrier(0);                                              \
+      BETWEEN;                                                                        \
+    }                                                                                 \
+  } while (0)
+#define PW_RESCALE()                                                   \
+  do {                                                                 \
+    if (resc) {                                                        \
+      agpr_fence(oacc[0]);                                             \
+      agpr_fence(oacc[1]);                                             \
+      _Pragma("unroll") for (int qb = 0; qb < 2; ++qb)                 \
+      _Pragma("unroll") for (int dt = 0; dt < NDT; ++dt)               \
+      _Pragma("unroll") for (int i = 0; i < 16; ++i)                   \
+        oacc[qb][dt][i] *= alpha[qb];                                  \
+      resc = false;                                                    \
+    }                                                                  \
+  } while (0)
+  // iteration j's DMA: K(j+2) into K image j & 1, V(j) into V image j & 1
+#define PW_DMA(J)                                                                \
+  do {                                                                           \
+    if ((J) + 2 < nkb) sk.load(rk, smem + ((J) & 1) * TB, ((J) + 2) * BN);       \
+    sv.load(rv, smem + (2 + ((J) & 1)) * TB, (J) * BN);                          \
+  } while (0)
 
-  auto step = [&](auto bufc, int kb) {
-    constexpr int BUF = decltype(bufc)::value;
-    if (kb + 1 < nkb) {
-      sk.load(rk, smem + (BUF ^ 1) * TB, (kb + 1) * BN);
-      sv.load(rv, smem + (2 + (BUF ^ 1)) * TB, (kb + 1) * BN);
-    }
-    if (kb < wnkb) {
-      const lds_t* kt = smem + BUF * TB;
-      const lds_t* vt = smem + (2 + BUF) * TB;
-      f32x16 sc[2][2];
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb) sc[qb][0] = sc[qb][1] = zero16();
-      bfx8 fk[NKK][2];
-      fk[0][0] = la.rowf(kt, 0, 0);
-      fk[0][1] = la.rowf(kt, 1, 0);
-#pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) {
-        if (kk + 1 < NKK) {
-          fk[kk + 1][0] = la.rowf(kt, 0, kk + 1);
-          fk[kk + 1][1] = la.rowf(kt, 1, kk + 1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb) {
-          sc[qb][0] = mfma(fk[kk][0], qf[qb][kk], sc[qb][0]);
-          sc[qb][1] = mfma(fk[kk][1], qf[qb][kk], sc[qb][1]);
-        }
-      }
-      bfx8 pf[2][4];
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
-        f32x16& s0 = sc[qb][0];
-        f32x16& s1 = sc[qb][1];
-        if (kb >= wmask) {
-          const int lim = key_limit(p, kb, BN, qg0 + 32 * qb, h, true);
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            if (acc_row0(i) > lim) s0[i] = -INFINITY;
-            if (acc_row0(i) + 32 > lim) s1[i] = -INFINITY;
-          }
-        }
-        float mx0 = fmaxf(s0[0], s1[0]), mx1 = fmaxf(s0[1], s1[1]);
-#pragma unroll
-        for (int i = 2; i < 16; i += 2) {
-          mx0 = fmaxf(mx0, fmaxf(s0[i], s1[i]));
-          mx1 = fmaxf(mx1, fmaxf(s0[i + 1], s1[i + 1]));
-        }
-        float mx = fmaxf(mx0, mx1);
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mxs = mx * c2;
-        if (__any(mxs > m[qb] + kRescaleThr)) {
-          const float m_new = fmaxf(m[qb], mxs);
-          const float alpha = (m[qb] == m_new) ? 1.f : fast_exp2(m[qb] - m_new);
-          l[qb] *= alpha;
-#pragma unroll
-          for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) oacc[qb][dt][i] *= alpha;
-          m[qb] = m_new;
-        }
-        const float mu = (m[qb] == -INFINITY) ? 0.f : m[qb];
-        float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; i += 2) {
-          s0[i] = fast_exp2(fmaf(s0[i], c2, -mu));
-          s1[i] = fast_exp2(fmaf(s1[i], c2, -mu));
-          s0[i + 1] = fast_exp2(fmaf(s0[i + 1], c2, -mu));
-          s1[i + 1] = fast_exp2(fmaf(s1[i + 1], c2, -mu));
-          r0 += s0[i];
-          r1 += s1[i];
-          r2 += s0[i + 1];
-          r3 += s1[i + 1];
-        }
-        float rs = (r0 + r1) + (r2 + r3);
-        rs += __shfl_xor(rs, 32, 64);
-        l[qb] += rs;
-        pf[qb][0] = acc_frag(s0, 0);
-        pf[qb][1] = acc_frag(s0, 1);
-        pf[qb][2] = acc_frag(s1, 0);
-        pf[qb][3] = acc_frag(s1, 1);
-      }
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        const bfx8 v0 = la.trf(vt, 0, 0, dt), v1 = la.trf(vt, 0, 1, dt);
-        const bfx8 v2 = la.trf(vt, 32, 0, dt), v3 = la.trf(vt, 32, 1, dt);
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb) {
-          mfma_acc(oacc[qb][dt], v0, pf[qb][0]);
-          mfma_acc(oacc[qb][dt], v1, pf[qb][1]);
-          mfma_acc(oacc[qb][dt], v2, pf[qb][2]);
-          mfma_acc(oacc[qb][dt], v3, pf[qb][3]);
-        }
-      }
-    }
+  if (nkb > 0) {
+    // prologue: K(0), K(1) resident, S(0); iteration 0: softmax(0) only (no PV yet)
+    sk.load(rk, smem, 0);
+    if (nkb > 1) sk.load(rk, smem + TB, BN);
     dma_barrier();
-  };
-  int kb = 0;
-  for (; kb + 1 < nkb; kb += 2) {
-    step(Buf<0>(), kb);
-    step(Buf<1>(), kb + 1);
+    PW_S_TILE(smem);
+    __syncthreads();  // every wave is done reading K image 0 before K(2) lands there
+    PW_DMA(0);
+    PW_MASK_MAX(0);
+    PW_EXP_SUM(0);
+    PW_EXP_SUM(1);
+    PW_TO_P();
+    PW_RESCALE();
+    if (nkb > 1) PW_S_TILE(smem + TB);
+    dma_barrier();
+    // steady state: iteration j (parity j & 1): DMA, X(j) = PV(j-1) + softmax(j), Y(j) = S(j+1)
+    auto iter = [&](auto parc, int j) {
+      constexpr int PJ = decltype(parc)::value;
+      PW_DMA(j);
+      PW_PV(smem + (2 + (PJ ^ 1)) * TB,
+            if (dt == 0) PW_MASK_MAX(j); else if (dt == 1) PW_EXP_SUM(0); else if (dt == 2) PW_EXP_SUM(1);
+            else { PW_TO_P(); });
+      PW_RESCALE();
+      if (j + 1 < nkb) PW_S_TILE(smem + (PJ ^ 1) * TB);
+      dma_barrier();
+    };
+    int j = 1;
+    for (; j + 1 < nkb; j += 2) {
+      iter(Buf<1>(), j);
+      iter(Buf<0>(), j + 1);
+    }
+    if (j < nkb) iter(Buf<1>(), j++);
+    // the last tile's PV: tile nkb - 1 (P buffer / V image of its parity)
+    PW_PV(smem + (2 + ((nkb - 1) & 1)) * TB, (void)0);
   }
-  if (kb < nkb) step(Buf<0>(), kb);
+#undef PW_S_TILE
+#undef PW_MASK_MAX
+#undef PW_EXP_SUM
+#undef PW_TO_P
+#undef PW_PV
+#undef PW_RESCALE
+#undef PW_DMA
   agpr_fence(oacc[0]);
   agpr_fence(oacc[1]);
 
@@ -1832,16 +1910,16 @@ int st_flash_fwd(const void* q, const void* k, const void* v, void* o, float* ls
   // 0.852 vs 0.853 ms, profiles/r03/flash_pmc.md), so one head stays the default.
   const char* he = std::getenv("ST_FLASH_FWD_HP");
   const bool hp2 = (H / Hkv) % 2 == 0 && he && std::atoi(he) == 2;
-  // ST_FLASH_FWD_W64=1: 64 queries per wave (half the LDS bytes per MFMA), D = 128
-  const char* we = std::getenv("ST_FLASH_FWD_W64");
-  const bool w64 = D == 128 && we && std::atoi(we) == 1;
+  // ST_FLASH_FWD=pw: the software-pipelined 64-queries-per-wave kernel (D = 128)
+  const char* fe = std::getenv("ST_FLASH_FWD");
+  const bool pw = D == 128 && fe && fe[0] == 'p' && fe[1] == 'w';
   if (D == 128 && pp) {
     const unsigned grid2 = (unsigned)(((Sq + 255) / 256) * B * H);
     flash_fwd_pp_kernel<128><<<grid2, 512, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
-  } else if (w64) {
+  } else if (pw) {
     const unsigned grid4 = (unsigned)(((Sq + 255) / 256) * B * H);
-    if (xcd) flash_fwd_w64_kernel<128, true><<<grid4, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
-    else flash_fwd_w64_kernel<128, false><<<grid4, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
+    if (xcd) flash_fwd_pw_kernel<true><<<grid4, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
+    else flash_fwd_pw_kernel<false><<<grid4, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
   } else if (hp2) {
     const unsigned grid2 = grid / 2;
     if (D == 128 && xcd) flash_fwd_kernel<128, true, 2><<<grid2, 512, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);

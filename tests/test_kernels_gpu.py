@@ -646,15 +646,15 @@ def _attn_rows_ref(q, k, v, rows, scale, q_offset=0):
 
 
 @pytest.mark.parametrize("S", [4096, 8192, 32768])
-@pytest.mark.parametrize("pp", ["1", "0", "w64"])
+@pytest.mark.parametrize("pp", ["1", "0", "pw"])
 def test_flash_long_sequence_sampled_rows(S, pp, monkeypatch):
     """Long causal sequences (the bench's 4K, 8K and the CP8@32K global length):
     the kernel's output and lse on sampled query rows (start, middle, end) against
-    an fp32 reference over every visible key; both forward kernels (8-wave
-    ping-pong, opt-in via ST_FLASH_PP=1, the 64-queries-per-wave one via ST_FLASH_FWD_W64=1,
-    and the default 4-wave one)."""
-    if pp == "w64":
-        monkeypatch.setenv("ST_FLASH_FWD_W64", "1")
+    an fp32 reference over every visible key; every forward kernel (8-wave ping-pong,
+    ST_FLASH_PP=1; the software-pipelined 64-queries-per-wave one, ST_FLASH_FWD=pw; the
+    4-wave one)."""
+    if pp == "pw":
+        monkeypatch.setenv("ST_FLASH_FWD", "pw")
         pp = "0"
     monkeypatch.setenv("ST_FLASH_PP", pp)
     torch.manual_seed(0)
@@ -675,11 +675,11 @@ def test_flash_long_sequence_sampled_rows(S, pp, monkeypatch):
 @pytest.mark.parametrize("B,Sq,Sk,H,Hkv,causal,q_off,k_off", [
     (2, 1024, 1024, 8, 2, True, 0, 0), (1, 777, 777, 4, 4, True, 0, 0), (2, 640, 1000, 4, 1, False, 0, 0),
     (1, 300, 1500, 4, 2, True, 1200, 0), (1, 512, 512, 8, 8, True, 512, 256), (8, 256, 256, 4, 2, True, 0, 0)])
-def test_flash_fwd_w64_matches_ref(B, Sq, Sk, H, Hkv, causal, q_off, k_off, xcd, monkeypatch):
-    """csrc/flash_attn.hip flash_fwd_w64_kernel (ST_FLASH_FWD_W64=1: 64 queries per wave, 256
-    per workgroup): causal / full, GQA, ragged Sq / Sk, CP offsets (a wave whose rows see no key
-    block is skipped), both workgroup orders; output and lse vs the fp32 reference and vs the
-    default kernel."""
+def test_flash_fwd_pw_matches_ref(B, Sq, Sk, H, Hkv, causal, q_off, k_off, xcd, monkeypatch):
+    """csrc/flash_attn.hip flash_fwd_pw_kernel (ST_FLASH_FWD=pw: software-pipelined, 64 queries
+    per wave, 256 per workgroup): causal / full, GQA, ragged Sq / Sk, CP offsets (a wave whose
+    rows see no key of a tile computes it masked), both workgroup orders; output and lse vs the
+    fp32 reference and vs the default kernel."""
     monkeypatch.setenv("ST_FLASH_XCD", xcd)
     torch.manual_seed(5)
     D = 128
@@ -688,7 +688,7 @@ def test_flash_fwd_w64_matches_ref(B, Sq, Sk, H, Hkv, causal, q_off, k_off, xcd,
     v = torch.randn(B, Sk, Hkv, D, device="cuda", dtype=torch.bfloat16)
     scale = 1 / math.sqrt(D)
     o0, l0 = ops.flash_attn_fwd(q, k, v, scale, causal, q_off, k_off)
-    monkeypatch.setenv("ST_FLASH_FWD_W64", "1")
+    monkeypatch.setenv("ST_FLASH_FWD", "pw")
     o1, l1 = ops.flash_attn_fwd(q, k, v, scale, causal, q_off, k_off)
     ref_o, ref_l = ops.sdpa_ref(q, k, v, causal, scale, q_off, k_off)
     assert rel(o1, ref_o) < 1e-2
@@ -696,6 +696,27 @@ def test_flash_fwd_w64_matches_ref(B, Sq, Sk, H, Hkv, causal, q_off, k_off, xcd,
     assert torch.equal(fin, torch.isfinite(l1))
     assert (l1[fin] - ref_l[fin]).abs().max().item() < 1e-2
     assert rel(o1, o0) < 1e-2
+
+
+@pytest.mark.parametrize("kernel", ["default", "pw"])
+def test_flash_fwd_rescale_spikes(kernel, monkeypatch):
+    """The deferred O rescale (running max grown by > 2^8 after P of earlier tiles is already
+    in O) fires only on data that spikes late: key rows with 6x the norm at several positions
+    deep into the sequence (cdna_hip_programming.md T13 / rule 26), vs the fp32 reference."""
+    if kernel == "pw":
+        monkeypatch.setenv("ST_FLASH_FWD", "pw")
+    torch.manual_seed(21)
+    B, S, H, Hkv, D = 2, 2048, 4, 2, 128
+    q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, S, Hkv, D, device="cuda", dtype=torch.bfloat16)
+    for t in (300, 301, 700, 1333, 1900):
+        k[:, t] = (k[:, t].float() * 6).to(torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    out, lse = ops.flash_attn_fwd(q, k, v, scale, True, 0, 0)
+    ref_o, ref_l = ops.sdpa_ref(q, k, v, True, scale, 0, 0)
+    assert rel(out, ref_o) < 1e-2
+    assert (lse - ref_l).abs().max().item() < 2e-2
 
 
 @pytest.mark.parametrize("q_off", [0, 12288, 28672])
