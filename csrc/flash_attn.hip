@@ -555,7 +555,9 @@ ST_DEVICE void mfma_qa0(f32x16& s, bfx8 k, const bfx8& q) {  // first k-step: C 
   asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=v"(s) : "v"(k), "a"(q));
 }
 
-template <bool XCD = true>
+// FINE: the softmax of X(j) cut into 32 slices, one after each PV MFMA (else four blocks, one
+// after each 8-MFMA d-tile group)
+template <bool XCD = true, bool FINE = false>
 __global__ __launch_bounds__(256, 1) void flash_fwd_pw_kernel(AttnParams p, bf16_t* __restrict__ o,
                                                               int64_t sob, int64_t sos, int64_t soh,
                                                               float* __restrict__ lse) {
@@ -726,6 +728,86 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_pw_kernel(AttnParams p, bf16
       BETWEEN;                                                                        \
     }                                                                                 \
   } while (0)
+  // FINE form of X(j): after PV MFMA m (= 8 dt + 4 qb + u) one slice of tile KB's softmax:
+  // dt 0: mask qb 0 / 1, row max in four halves, the rescale decision; dt 1 / 2: exp2 and row
+  // sums of query block 0 / 1, two register pairs per slice; dt 3: P fragment m & 7, written
+  // right after the last MFMA that reads its P(j-1) predecessor
+#define PW_PV_FINE(VT, KB)                                                                      \
+  do {                                                                                          \
+    const lds_t* vt_ = (VT);                                                                    \
+    bfx8 vf[2][4];                                                                              \
+    float mxa[2] = {0.f, 0.f}, mxs[2] = {0.f, 0.f}, mu = 0.f;                                   \
+    float ra = 0.f, rb = 0.f, rc = 0.f, rd = 0.f;                                               \
+    _Pragma("unroll") for (int dt = 0; dt < NDT; ++dt) {                                        \
+      if (dt == 0) {                                                                            \
+        vf[0][0] = la.trf(vt_, 0, 0, 0);                                                        \
+        vf[0][1] = la.trf(vt_, 0, 1, 0);                                                        \
+        vf[0][2] = la.trf(vt_, 32, 0, 0);                                                       \
+        vf[0][3] = la.trf(vt_, 32, 1, 0);                                                       \
+      }                                                                                         \
+      if (dt + 1 < NDT) {                                                                       \
+        vf[(dt + 1) & 1][0] = la.trf(vt_, 0, 0, dt + 1);                                        \
+        vf[(dt + 1) & 1][1] = la.trf(vt_, 0, 1, dt + 1);                                        \
+        vf[(dt + 1) & 1][2] = la.trf(vt_, 32, 0, dt + 1);                                       \
+        vf[(dt + 1) & 1][3] = la.trf(vt_, 32, 1, dt + 1);                                       \
+      }                                                                                         \
+      _Pragma("unroll") for (int mq = 0; mq < 8; ++mq) {                                        \
+        const int qb = mq >> 2, u = mq & 3;                                                     \
+        __builtin_amdgcn_sched_barrier(0);                                                      \
+        mfma_acc(oacc[qb][dt], vf[dt & 1][u], pbuf[qb][u]);                                     \
+        if (dt == 0) {                                                                          \
+          if (mq < 2) {                                                                         \
+            if ((KB) >= wmask) {                                                                \
+              const int lim = key_limit(p, (KB), BN, qg0 + 32 * mq, h, true);                   \
+              _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                  \
+                if (acc_row0(i) > lim) s[mq][0][i] = -INFINITY;                                 \
+                if (acc_row0(i) + 32 > lim) s[mq][1][i] = -INFINITY;                            \
+              }                                                                                 \
+            }                                                                                   \
+          } else if (mq < 6) {                                                                  \
+            const int q2 = (mq - 2) >> 1, i0 = ((mq - 2) & 1) * 8;                              \
+            float x = i0 ? mxa[q2] : fmaxf(s[q2][0][0], s[q2][1][0]);                           \
+            _Pragma("unroll") for (int i = 0; i < 8; ++i)                                       \
+              x = fmaxf(x, fmaxf(s[q2][0][i0 + i], s[q2][1][i0 + i]));                          \
+            mxa[q2] = x;                                                                        \
+            if (i0) mxs[q2] = fmaxf(x, __shfl_xor(x, 32, 64)) * c2;                             \
+          } else if (mq == 6) {                                                                 \
+            if (__any(mxs[0] > m[0] + kRescaleThr || mxs[1] > m[1] + kRescaleThr)) {            \
+              _Pragma("unroll") for (int q2 = 0; q2 < 2; ++q2) {                                \
+                const float m_new = fmaxf(m[q2], mxs[q2]);                                      \
+                alpha[q2] = (m[q2] == m_new) ? 1.f : fast_exp2(m[q2] - m_new);                  \
+                l[q2] *= alpha[q2];                                                             \
+                m[q2] = m_new;                                                                  \
+              }                                                                                 \
+              resc = true;                                                                      \
+            }                                                                                   \
+          }                                                                                     \
+        } else if (dt <= 2) {                                                                   \
+          const int q2 = dt - 1, i = 2 * mq;                                                    \
+          if (mq == 0) {                                                                        \
+            mu = (m[q2] == -INFINITY) ? 0.f : m[q2];                                            \
+            ra = rb = rc = rd = 0.f;                                                            \
+          }                                                                                     \
+          s[q2][0][i] = fast_exp2(fmaf(s[q2][0][i], c2, -mu));                                  \
+          s[q2][1][i] = fast_exp2(fmaf(s[q2][1][i], c2, -mu));                                  \
+          s[q2][0][i + 1] = fast_exp2(fmaf(s[q2][0][i + 1], c2, -mu));                          \
+          s[q2][1][i + 1] = fast_exp2(fmaf(s[q2][1][i + 1], c2, -mu));                          \
+          ra += s[q2][0][i];                                                                    \
+          rb += s[q2][1][i];                                                                    \
+          rc += s[q2][0][i + 1];                                                                \
+          rd += s[q2][1][i + 1];                                                                \
+          if (mq == 7) {                                                                        \
+            float rs = (ra + rb) + (rc + rd);                                                   \
+            rs += __shfl_xor(rs, 32, 64);                                                       \
+            l[q2] += rs;                                                                        \
+          }                                                                                     \
+        } else {                                                                                \
+          pbuf[qb][u] = acc_frag(s[qb][u >> 1], u & 1);                                         \
+        }                                                                                       \
+      }                                                                                         \
+    }                                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                                          \
+  } while (0)
 #define PW_RESCALE()                                                   \
   do {                                                                 \
     if (resc) {                                                        \
@@ -764,9 +846,13 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_pw_kernel(AttnParams p, bf16
     auto iter = [&](auto parc, int j) {
       constexpr int PJ = decltype(parc)::value;
       PW_DMA(j);
-      PW_PV(smem + (2 + (PJ ^ 1)) * TB,
-            if (dt == 0) PW_MASK_MAX(j); else if (dt == 1) PW_EXP_SUM(0); else if (dt == 2) PW_EXP_SUM(1);
-            else { PW_TO_P(); });
+      if constexpr (FINE) {
+        PW_PV_FINE(smem + (2 + (PJ ^ 1)) * TB, j);
+      } else {
+        PW_PV(smem + (2 + (PJ ^ 1)) * TB,
+              if (dt == 0) PW_MASK_MAX(j); else if (dt == 1) PW_EXP_SUM(0); else if (dt == 2) PW_EXP_SUM(1);
+              else { PW_TO_P(); });
+      }
       PW_RESCALE();
       if (j + 1 < nkb) PW_S_TILE(smem + (PJ ^ 1) * TB);
       dma_barrier();
@@ -785,6 +871,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_pw_kernel(AttnParams p, bf16
 #undef PW_EXP_SUM
 #undef PW_TO_P
 #undef PW_PV
+#undef PW_PV_FINE
 #undef PW_RESCALE
 #undef PW_DMA
   agpr_fence(oacc[0]);
@@ -1910,15 +1997,19 @@ int st_flash_fwd(const void* q, const void* k, const void* v, void* o, float* ls
   // 0.852 vs 0.853 ms, profiles/r03/flash_pmc.md), so one head stays the default.
   const char* he = std::getenv("ST_FLASH_FWD_HP");
   const bool hp2 = (H / Hkv) % 2 == 0 && he && std::atoi(he) == 2;
-  // ST_FLASH_FWD=pw: the software-pipelined 64-queries-per-wave kernel (D = 128)
+  // ST_FLASH_FWD=pw / pwf: the software-pipelined 64-queries-per-wave kernel (D = 128), softmax
+  // in four blocks / in 32 slices between the PV MFMAs
   const char* fe = std::getenv("ST_FLASH_FWD");
   const bool pw = D == 128 && fe && fe[0] == 'p' && fe[1] == 'w';
+  const bool pwf = pw && fe[2] == 'f';
   if (D == 128 && pp) {
     const unsigned grid2 = (unsigned)(((Sq + 255) / 256) * B * H);
     flash_fwd_pp_kernel<128><<<grid2, 512, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
   } else if (pw) {
     const unsigned grid4 = (unsigned)(((Sq + 255) / 256) * B * H);
-    if (xcd) flash_fwd_pw_kernel<true><<<grid4, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
+    if (pwf && xcd) flash_fwd_pw_kernel<true, true><<<grid4, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
+    else if (pwf) flash_fwd_pw_kernel<false, true><<<grid4, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
+    else if (xcd) flash_fwd_pw_kernel<true><<<grid4, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
     else flash_fwd_pw_kernel<false><<<grid4, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
   } else if (hp2) {
     const unsigned grid2 = grid / 2;

@@ -8,3 +8,5 @@ tail -3 $O/tests.log
 timeout -k 10 200 python tools/bench_flash_shapes.py --no-bwd > $O/base.jsonl
 ST_FLASH_FWD=pw timeout -k 10 200 python tools/bench_flash_shapes.py --no-bwd > $O/pw.jsonl
 cat $O/base.jsonl $O/pw.jsonl
+ST_FLASH_FWD=pwf timeout -k 10 200 python tools/bench_flash_shapes.py --no-bwd > $O/pwf.jsonl
+cat $O/pwf.jsonl
