@@ -151,7 +151,7 @@ def _slice_record(out: dict, args, est, tr, dp: int, world: int, elapsed: float)
     pg = mesh.pgm
     coords = {k: getattr(pg, f"{k}_rank") for k in ("dp", "pp", "cp", "ep", "tp")} if pg else {}
     peak_gb = torch.cuda.max_memory_allocated() / 1e9 if torch.cuda.is_available() else 0.0
-    est_gb = est.total_gb() if hasattr(est, "total_gb") else None
+    est_gb = float(est.total_gb)
     rec = {
         "kind": "per-rank compute slice",
         "valid": False,

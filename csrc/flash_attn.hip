@@ -261,6 +261,9 @@ struct DmaStager {
 #pragma unroll
     for (int i = 0; i < NI; ++i) lds_dma16(rs, tile + wave_base + i * 1024, voff[i] + o);
   }
+  ST_DEVICE void load_piece(rsrc_t rs, lds_t* tile, int row0, int i) const {  // piece i of load()
+    lds_dma16(rs, tile + wave_base + i * 1024, voff[i] + (uint32_t)row0 * stride_bytes);
+  }
 };
 
 struct AttnParams {
@@ -627,19 +630,21 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_pw_kernel(AttnParams p, bf16
 #define PW_S_TILE(KT)                                                               \
   do {                                                                              \
     const lds_t* kt_ = (KT);                                                        \
-    bfx8 fk[2][2];                                                                  \
+    bfx8 fk[3][2];                                                                  \
     fk[0][0] = la.rowf(kt_, 0, 0);                                                  \
     fk[0][1] = la.rowf(kt_, 1, 0);                                                  \
+    fk[1][0] = la.rowf(kt_, 0, 1);                                                  \
+    fk[1][1] = la.rowf(kt_, 1, 1);                                                  \
     _Pragma("unroll") for (int kk = 0; kk < NKK; ++kk) {                            \
-      if (kk + 1 < NKK) {                                                           \
-        fk[(kk + 1) & 1][0] = la.rowf(kt_, 0, kk + 1);                              \
-        fk[(kk + 1) & 1][1] = la.rowf(kt_, 1, kk + 1);                              \
+      if (kk + 2 < NKK) {                                                           \
+        fk[(kk + 2) % 3][0] = la.rowf(kt_, 0, kk + 2);                              \
+        fk[(kk + 2) % 3][1] = la.rowf(kt_, 1, kk + 2);                              \
       }                                                                             \
       __builtin_amdgcn_sched_barrier(0);                                            \
       _Pragma("unroll") for (int h2 = 0; h2 < 2; ++h2)                              \
       _Pragma("unroll") for (int qb = 0; qb < 2; ++qb) {                            \
         if (kk == 0) mfma_qa0(s[qb][h2], fk[0][h2], qf[qb][0]);                     \
-        else mfma_qa(s[qb][h2], fk[kk & 1][h2], qf[qb][kk]);                        \
+        else mfma_qa(s[qb][h2], fk[kk % 3][h2], qf[qb][kk]);                        \
       }                                                                             \
     }                                                                               \
   } while (0)
@@ -732,7 +737,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_pw_kernel(AttnParams p, bf16
   // dt 0: mask qb 0 / 1, row max in four halves, the rescale decision; dt 1 / 2: exp2 and row
   // sums of query block 0 / 1, two register pairs per slice; dt 3: P fragment m & 7, written
   // right after the last MFMA that reads its P(j-1) predecessor
-#define PW_PV_FINE(VT, KB)                                                                      \
+#define PW_PV_FINE(VT, KB)    /* also issues iteration KB's 8 DMA pieces, one per dt-0 MFMA */  \
   do {                                                                                          \
     const lds_t* vt_ = (VT);                                                                    \
     bfx8 vf[2][4];                                                                              \
@@ -756,6 +761,11 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_pw_kernel(AttnParams p, bf16
         __builtin_amdgcn_sched_barrier(0);                                                      \
         mfma_acc(oacc[qb][dt], vf[dt & 1][u], pbuf[qb][u]);                                     \
         if (dt == 0) {                                                                          \
+          if (mq < 4) {                                                                         \
+            if ((KB) + 2 < nkb) sk.load_piece(rk, smem + ((KB) & 1) * TB, ((KB) + 2) * BN, mq);  \
+          } else {                                                                              \
+            sv.load_piece(rv, smem + (2 + ((KB) & 1)) * TB, (KB) * BN, mq - 4);                  \
+          }                                                                                     \
           if (mq < 2) {                                                                         \
             if ((KB) >= wmask) {                                                                \
               const int lim = key_limit(p, (KB), BN, qg0 + 32 * mq, h, true);                   \
@@ -845,7 +855,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_pw_kernel(AttnParams p, bf16
     // steady state: iteration j (parity j & 1): DMA, X(j) = PV(j-1) + softmax(j), Y(j) = S(j+1)
     auto iter = [&](auto parc, int j) {
       constexpr int PJ = decltype(parc)::value;
-      PW_DMA(j);
+      if constexpr (!FINE) PW_DMA(j);
       if constexpr (FINE) {
         PW_PV_FINE(smem + (2 + (PJ ^ 1)) * TB, j);
       } else {

@@ -78,3 +78,27 @@ def test_loopback_collectives_are_same_shape_local_copies():
     assert r["ag"].tolist() == [0.0, 1.0] * 8
     assert r["a2a"].tolist() == [0.0, 1.0, 2.0, 3.0, 0.0, 1.0, 2.0, 3.0, 0.0, 1.0]
     assert r["p2p"].tolist() == [7.0, 7.0, 7.0]  # the batch's own send, looped back
+
+
+@pytest.mark.parametrize("layout,model", [("tp2pp2dp2", "tiny-llama"), ("mixtral_ep8", "tiny-mixtral")])
+def test_bench_slice_prints_its_own_kind(layout, model):
+    """``bench.py --layout L --slice`` (CPU here): one JSON line of kind "per-rank compute slice",
+    valid false, the impersonated rank's coordinates and its HBM estimate."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--layout", layout, "--slice", "--model", model,
+                        "--steps", "1", "--warmup", "1", "--seq_len", "128", "--layers", "4"],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["kind"] == "per-rank compute slice" and rec["valid"] is False
+    assert rec["slice_world"] == 8 and rec["layers_total"] == 4
+    if layout == "tp2pp2dp2":
+        assert rec["rank_coords"]["pp"] == 1 and rec["layers_on_rank"] == 2
+    assert rec["hbm_estimate_gb"] is not None and rec["ms_per_step"] > 0
