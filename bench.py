@@ -142,7 +142,7 @@ def _self_launch(n: int, argv: list[str], backend: str) -> int:
     return subprocess.call(cmd, env=env)
 
 
-def _slice_record(out: dict, args, est, tr, dp: int, world: int, elapsed: float) -> dict:
+def _slice_record(out: dict, args, est, est_run, tr, dp: int, world: int, elapsed: float) -> dict:
     """The JSON of a per-rank compute slice: its own kind, never a throughput result."""
     import torch
 
@@ -167,6 +167,7 @@ def _slice_record(out: dict, args, est, tr, dp: int, world: int, elapsed: float)
         "peak_hbm_gb": round(peak_gb, 2), "hbm_estimate_gb": round(est_gb, 2) if est_gb else None,
         "hbm_estimate_err_pct": round(100 * (peak_gb - est_gb) / est_gb, 1) if est_gb else None,
         "hbm_estimate": est.summary(),
+        "hbm_estimate_8gpu_worst_rank_gb": round(float(est_run.total_gb), 2),
         "comm_mb_per_step_rank": out["comm_mb_per_step_rank0"],
         "moe_dispatch": out["moe_dispatch"], "config": out["config"], "final_loss": out["final_loss"],
         "dtype": "bf16", "data": out["data"],
@@ -220,6 +221,12 @@ def main() -> int:
                          "collective replaced by a same-shape local copy (dist/loopback.py); prints its own JSON "
                          "kind, valid: false -- per-rank kernels and HBM of a layout no 8-GPU box is here to run")
     ap.add_argument("--slice_world", type=int, default=8, help="world size of the sliced layout")
+    ap.add_argument("--slice_stage", default="last", choices=["first", "last"],
+                    help="pipeline stage the slice impersonates: last (final norm + LM head + loss, the "
+                         "heavier compute) or first (embedding, the most micro-batches in flight: peak HBM)")
+    ap.add_argument("--ep_comm", default="auto", choices=["auto", "rccl", "xgmi"],
+                    help="EP exchange transport: rccl (host counts, exact-row expert buffers), xgmi (push "
+                         "exchange, device counts, R_max-row buffers), auto (xgmi when its self-test passes)")
     args = ap.parse_args()
     launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -261,7 +268,8 @@ def main() -> int:
     if args.slice:
         # the rank to impersonate: the LAST pipeline stage (embedding-free, final norm + LM head:
         # the heavier stage), first of every other axis.  Mesh order [dp, pp, cp, ep, tp], TP fastest.
-        rep = (args.pp - 1) * args.cp * args.ep * args.tp
+        stage = args.pp - 1 if args.slice_stage == "last" else 0
+        rep = stage * args.cp * args.ep * args.tp
         os.environ["ST_LOOPBACK_WORLD"], os.environ["ST_LOOPBACK_RANK"] = str(world), str(rep)
     if args.pp > 1:
         # the (interleaved) 1F1B schedule needs >= pp micro-batches in flight -- a multiple of
@@ -276,21 +284,28 @@ def main() -> int:
     from scaletorch_amd.utils.memory import estimate_rank_memory
 
     mcfg = get_model_config(args.model, num_hidden_layers=args.layers)
-    est = estimate_rank_memory(mcfg, tp=args.tp, pp=args.pp, cp=args.cp, ep=args.ep, dp=dp,
-                               micro_batch=args.micro_batch_size, seq_len=args.seq_len, grad_acc=ga,
-                               zero1=args.zero >= 1 and dp * args.cp * args.ep > 1, sequence_parallel=args.sp,
-                               gradient_checkpointing=(args.recompute if args.gc else False),
-                               grad_reduce_dtype=args.grad_reduce_dtype,
-                               fused_head_chunk=args.head_chunk if args.fused_head else 0,
-                               moe_dropless=args.moe_capacity_factor == 0 and args.ep > 1,
-                               optimizer_state_dtype=args.opt_state_dtype,
-                               xgmi_ipc_bytes=_planned_ipc(args, mcfg))
+    def estimate(slice_rank: bool):
+        """HBM of the 8-GPU run's worst rank (first stage, planned IPC areas, the transport's
+        expert buffers) or, ``slice_rank``, of the rank this slice runs (no IPC areas, RCCL EP)."""
+        return estimate_rank_memory(
+            mcfg, tp=args.tp, pp=args.pp, cp=args.cp, ep=args.ep, dp=dp, micro_batch=args.micro_batch_size,
+            seq_len=args.seq_len, grad_acc=ga, zero1=args.zero >= 1 and dp * args.cp * args.ep > 1,
+            sequence_parallel=args.sp, gradient_checkpointing=(args.recompute if args.gc else False),
+            grad_reduce_dtype=args.grad_reduce_dtype, fused_head_chunk=args.head_chunk if args.fused_head else 0,
+            moe_dropless=args.moe_capacity_factor == 0 and args.ep > 1, optimizer_state_dtype=args.opt_state_dtype,
+            xgmi_ipc_bytes=0 if slice_rank else _planned_ipc(args, mcfg),
+            pp_rank=(args.pp - 1 if slice_rank and args.slice_stage == "last" else 0),
+            virtual_pipeline=args.vpp if args.pp > 1 else 1,
+            moe_exact_rows=args.ep_comm == "rccl" or slice_rank)
+
+    est_run = estimate(False)
+    est = estimate(True) if args.slice else est_run
     if int(os.environ.get("RANK", "0")) == 0:
         print(f"[bench] layout {args.layout}: {args.model} tp{args.tp} pp{args.pp} cp{args.cp} ep{args.ep} dp{dp} "
               f"mbs{args.micro_batch_size} ga{ga} seq{args.seq_len}; HBM estimate {est.summary()}",
               file=sys.stderr, flush=True)
-    if not est.fits():
-        raise SystemExit(f"layout {args.layout} would not fit: {est.summary()}")
+    if not est.fits() or not est_run.fits():
+        raise SystemExit(f"layout {args.layout} would not fit: {est_run.summary()}")
     a = ScaleTorchArguments(
         model_name_or_path=args.model, synthetic_data=True, micro_batch_size=args.micro_batch_size,
         sequence_length=args.seq_len, gradient_accumulation_steps=ga, total_train_steps=args.warmup + args.steps,
@@ -303,13 +318,14 @@ def main() -> int:
         num_hidden_layers=args.layers, dtype="bfloat16", weight_decay=0.1, betas=(0.9, 0.95),
         zero_stage=args.zero, fused_lm_head=bool(args.fused_head), lm_head_chunk_tokens=args.head_chunk,
         moe_capacity_factor=args.moe_capacity_factor, moe_ep_chunks=args.moe_ep_chunks,
-        optimizer_state_dtype=args.opt_state_dtype, gemm_tuning=args.gemm_tuning,
+        optimizer_state_dtype=args.opt_state_dtype, gemm_tuning=args.gemm_tuning, ep_comm=args.ep_comm,
     )
     if args.backend == "gloo" and torch.cuda.is_available():  # 1-GPU multi-rank rehearsal
         from scaletorch_amd.dist.gloo_staging import stage_gloo_cuda_p2p
 
         stage_gloo_cuda_p2p()
     tr = Trainer(a)
+    mem_built = torch.cuda.memory_allocated() / 1e9 if torch.cuda.is_available() else 0.0
     rank = tr.rank
     dev = tr.device
     # ranks that really take part in the backend's collectives: an 8-byte all-reduce of ones
@@ -427,7 +443,14 @@ def main() -> int:
                     ("torchrun" if launched else "single process"),
     }
     if args.slice:
-        out = _slice_record(out, args, est, tr, dp, world, elapsed)
+        out = _slice_record(out, args, est, est_run, tr, dp, world, elapsed)
+        # where the bytes sit: after the build (weights, grads, buffers) and between steps
+        # (+ optimizer state), against the estimate's resident terms -- the rest of the peak is
+        # the step's activations and workspaces
+        out["hbm_after_build_gb"] = round(mem_built, 2)
+        out["hbm_resident_between_steps_gb"] = round(
+            torch.cuda.memory_allocated() / 1e9 if torch.cuda.is_available() else 0.0, 2)
+        out["hbm_estimate_resident_gb"] = round(est.params_gb + est.grads_gb + est.optimizer_gb + est.comm_gb, 2)
     if rank == 0 or args.slice:
         print(json.dumps(out), flush=True)
         if os.environ.get("ST_WGRAD_TUNE_LOG") == "1":  # the per-shape weight-gradient picks (stderr)

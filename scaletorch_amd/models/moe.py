@@ -634,13 +634,17 @@ def _gmm_dswiglu(dy: torch.Tensor, w_dn: torch.Tensor, offs: torch.Tensor, gu: t
 
 
 def _vendor_expert_gemms() -> str:
-    """``ST_MOE_VENDOR_GEMM``: ``auto`` (default) -- per-expert hipBLASLt GEMMs when the
-    routing counts are already on the host (the RCCL EP exchange reads them) and the rank
-    holds few experts with many rows each, the one-launch HIP grouped kernel otherwise;
-    ``1`` -- always (one host read of the counts per layer when they are not); ``0`` --
-    never.  Measured (``tools/bench_expert_ffn.py``): the grouped kernel wins on the 1-GPU
-    proxies by 16 % (Mixtral, 8 x 1,024 rows) and 4.4x (Qwen3-30B-A3B, 128 x 512 rows)."""
-    return os.environ.get("ST_MOE_VENDOR_GEMM", "auto")
+    """``ST_MOE_VENDOR_GEMM``: ``0`` (default) -- the HIP grouped kernels (gate|up with the
+    SwiGLU in its epilogue, the down dgrad with the SwiGLU backward in its epilogue) on
+    every transport; ``1`` -- one hipBLASLt GEMM per local expert (one host read of the
+    counts per layer when the transport has not already made one); ``auto`` -- hipBLASLt
+    when the RCCL exchange already holds the counts on the host and the rank has few
+    experts with many rows each.  In the step the grouped kernels win even there: the
+    Mixtral EP8 slice (one expert x ~8,192 rows per micro-batch) runs 760.7 ms/step on them
+    against 806.9 ms with per-expert hipBLASLt + separate SwiGLU passes
+    (profiles/r06/slices/mixtral_variants.md), although the isolated FFN microbench had
+    hipBLASLt 7 % ahead (tools/bench_expert_ffn.py, profiles/r05/expert_ffn_ab.log)."""
+    return os.environ.get("ST_MOE_VENDOR_GEMM", "0")
 
 
 def _gemm_per_expert(x: torch.Tensor, w: torch.Tensor, counts: list, wn: bool, rows: int) -> torch.Tensor:
@@ -655,6 +659,29 @@ def _gemm_per_expert(x: torch.Tensor, w: torch.Tensor, counts: list, wn: bool, r
             torch.matmul(x[s:s + n], w[e] if wn else w[e].t(), out=y[s:s + n])
         s += n
     return y
+
+
+def _expert_wgrad(w: torch.Tensor, dout: torch.Tensor, inp: torch.Tensor, offs: torch.Tensor, counts):
+    """``w.main_grad[e] (+)= dout[rows of e]^T inp[rows of e]`` for every local expert: ONE
+    grouped launch (csrc/wgrad_gemm.hip ``st_wgrad_grouped``), else per-expert GEMMs after one
+    host read of the counts (returned, so the second weight reuses it)."""
+    from ..ops import _lib
+    from ..ops.grad import take_fresh, wgrad_into
+
+    fresh = take_fresh(w)
+    grouped = os.environ.get("ST_MOE_GROUPED_WGRAD", "1") == "1"  # 0: per-expert launches (A/B)
+    if grouped and _lib.ops().wgrad_grouped_(w.main_grad, dout, inp, offs, 0 if fresh else 1):
+        return counts
+    if counts is None:
+        counts = torch.diff(offs, prepend=offs.new_zeros(1)).tolist()
+    off = 0
+    for e, n in enumerate(counts):
+        if n:
+            wgrad_into(w.main_grad[e], dout[off:off + n], inp[off:off + n], 0 if fresh else 1, variant=1)
+        elif fresh:
+            w.main_grad[e].zero_()
+        off += n
+    return counts
 
 
 class _ExpertFFNFn(torch.autograd.Function):
@@ -698,7 +725,7 @@ class _ExpertFFNFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         from ..ops import _lib
-        from ..ops.grad import _grad_ready, take_fresh, wgrad_into
+        from ..ops.grad import _grad_ready
 
         x, gu, a, offs = ctx.saved_tensors
         w_gu, w_dn = ctx.w_gu, ctx.w_dn
@@ -715,19 +742,7 @@ class _ExpertFFNFn(torch.autograd.Function):
             dx = _gmm(dgu, w_gu, offs, wn=True)
         counts = ch
         for w, dout, inp in ((w_dn, dy, a), (w_gu, dgu, x)):
-            fresh = take_fresh(w)
-            grouped = os.environ.get("ST_MOE_GROUPED_WGRAD", "1") == "1"  # 0: per-expert launches (A/B)
-            if not (grouped and _lib.ops().wgrad_grouped_(w.main_grad, dout, inp, offs, 0 if fresh else 1)):
-                if counts is None:  # fallback: per-expert GEMMs (one host read of the counts)
-                    counts = torch.diff(offs, prepend=offs.new_zeros(1)).tolist()
-                off = 0
-                for e, n in enumerate(counts):
-                    if n:
-                        wgrad_into(w.main_grad[e], dout[off:off + n], inp[off:off + n], 0 if fresh else 1,
-                                   variant=1)
-                    elif fresh:
-                        w.main_grad[e].zero_()
-                    off += n
+            counts = _expert_wgrad(w, dout, inp, offs, counts)
             _grad_ready(w)
         return dx, None, None, None, None
 
@@ -908,14 +923,20 @@ class MoELayer(nn.Module):
         Mh = M.detach().to("cpu", torch.int64) if comm is None else None
         mine = M[:, self.ep_rank * El:(self.ep_rank + 1) * El]
         offs = torch.cumsum(mine.sum(0), 0, dtype=torch.int32)  # grouped-GEMM offsets (device)
-        xe = _EPExchange.apply(xs, M, El, 0, R_max, (R_max, Tk_max), group, comm, Mh)
-        xe._st_padded = True  # R_max rows, the first offs[-1] real: the FFN recomputes a over those
-        # the RCCL exchange already holds the counts on the host: per-expert library GEMMs where
-        # they beat the grouped kernel -- few local experts with many rows each (Mixtral EP 8:
-        # one expert x 8,192 rows, 6.9 vs 7.4 ms fwd+bwd; at 16 x 4,096 or 8 x 1,024 rows the
-        # grouped kernel wins, tools/bench_expert_ffn.py, profiles/r05/expert_ffn_ab.log)
+        # RCCL transport: the host counts size the expert buffers EXACTLY (the rows this rank
+        # receives); the xGMI push exchange writes into R_max-row buffers (device counts), of
+        # which the first offs[-1] rows are real -- the FFN then recomputes a over those
+        # instead of keeping an R_max x I activation.  At Mixtral EP 8, R_max = 32,768 rows
+        # against ~8,192 received: the exact buffers hold ~4x less per MoE layer.
+        rows = int(Mh[:, self.ep_rank * El:(self.ep_rank + 1) * El].sum()) if Mh is not None else R_max
+        xe = _EPExchange.apply(xs, M, El, 0, rows, (R_max, Tk_max), group, comm, Mh)
+        xe._st_padded = Mh is None
+        # host counts (RCCL exchange) hand the per-expert hipBLASLt path its row counts when
+        # ST_MOE_VENDOR_GEMM asks for it (``_vendor_expert_gemms``: the grouped kernels win in
+        # the step by default)
+        mode = _vendor_expert_gemms()
         ch = Mh[:, self.ep_rank * El:(self.ep_rank + 1) * El].sum(0).tolist() if Mh is not None else None
-        if ch is not None and _vendor_expert_gemms() == "auto" and not (El <= 4 and sum(ch) >= 4096 * El):
+        if ch is not None and (mode == "0" or (mode == "auto" and not (El <= 4 and sum(ch) >= 4096 * El))):
             ch = None
         ye = self.experts(xe, offs=offs, counts_host=ch)
         self.dropped_rows = xs.new_zeros((), dtype=torch.int64)  # dropless by construction

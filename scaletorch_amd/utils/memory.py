@@ -54,14 +54,22 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
                          pp_engine: str = "1f1b", grad_reduce_dtype: str = "bf16",
                          fused_head_chunk: int = 0, recompute_swiglu: bool | None = None,
                          moe_dropless: bool = False, optimizer_state_dtype: str = "fp32",
-                         xgmi_ipc_bytes: float = 0.0, cp_ds_budget_bytes: float | None = None) -> MemoryEstimate:
-    """Worst-rank estimate (first pipeline stage for activations, largest stage for weights).
+                         xgmi_ipc_bytes: float = 0.0, cp_ds_budget_bytes: float | None = None,
+                         pp_rank: int = 0, virtual_pipeline: int = 1, moe_exact_rows: bool = False) -> MemoryEstimate:
+    """Per-rank estimate: weights of the largest stage, activations of pipeline stage
+    ``pp_rank`` (default 0, the first stage: it holds the most micro-batches in flight, so
+    the default is the worst rank).  In-flight work per stage: plain 1F1B holds
+    min(pp - pp_rank, grad_acc) micro-batches of the whole stage; interleaved 1F1B
+    (``virtual_pipeline`` V > 1) holds warm-up + 1 chunk-micro-batches of layers/V each
+    (parallel/interleaved.num_warmup); AFAB holds all of them.
 
     ``fused_head_chunk`` > 0: the fused chunked LM head (ops/fused_head.py) -- one
     chunk of logits and dX instead of the logits and their gradient.
     ``moe_dropless`` (EP > 1, models/moe.py dropless exchange): each MoE layer keeps its
     expert input and gate|up output at the host bound R_max = ep * T * min(k, E/ep) rows
-    (the SwiGLU output is recomputed in backward), plus the sorted rows of the combine."""
+    (the SwiGLU output is recomputed in backward), plus the sorted rows of the combine;
+    ``moe_exact_rows`` (the RCCL transport, host counts): the buffers hold the rows the rank
+    receives, T * k at uniform routing, and the SwiGLU output is kept."""
     h, d = cfg.hidden_size, cfg.head_dim
     H, Hkv = cfg.num_attention_heads, cfg.num_key_value_heads
     L = cfg.num_hidden_layers
@@ -85,7 +93,14 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
     # activations of the micro-batches a rank holds at once
     tokens = micro_batch * seq_len / cp
     if pp > 1:
-        tokens *= grad_acc if pp_engine == "afab" else min(pp, grad_acc)
+        if pp_engine == "afab":
+            tokens *= grad_acc
+        elif virtual_pipeline > 1:
+            from ..parallel.interleaved import num_warmup
+
+            tokens *= (num_warmup(pp, virtual_pipeline, grad_acc, pp_rank) + 1) / virtual_pipeline
+        else:
+            tokens *= min(pp - pp_rank, grad_acc)
     if cfg.is_moe:
         k_eff = cfg.num_experts_per_tok * cfg.moe_intermediate_size / max(1, cfg.intermediate_size)
     else:
@@ -101,9 +116,11 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
         k = cfg.num_experts_per_tok
         per_layer = _ACT_ATTN * h
         t_micro = micro_batch * seq_len / cp
-        r_max = ep * t_micro * min(k, cfg.num_experts // ep)
-        moe_extra = (r_max * (2 * h + 4 * cfg.moe_intermediate_size / tp) + t_micro * k * 4 * h) * (
-            tokens / t_micro)
+        if moe_exact_rows:
+            rows, per_row = t_micro * k, 2 * h + 6 * cfg.moe_intermediate_size / tp  # x, gu, a
+        else:
+            rows, per_row = ep * t_micro * min(k, cfg.num_experts // ep), 2 * h + 4 * cfg.moe_intermediate_size / tp
+        moe_extra = (rows * per_row + t_micro * k * 4 * h) * (tokens / t_micro)
     if tp > 1:
         per_layer = per_layer / tp if sequence_parallel else 8 * h + (per_layer - 8 * h) / tp
     if gradient_checkpointing == "selective":  # attention activations kept, norm + MLP recomputed

@@ -5,7 +5,7 @@ cd /tmp && export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/slices
 mkdir -p $O
-for L in ${SLICES:-dp tp2pp2dp2 cp8_32k mixtral_ep8}; do
+for L in $([ "${SKIP_RUN:-0}" = "1" ] || echo ${SLICES:-dp tp2pp2dp2 cp8_32k mixtral_ep8}); do
   echo "== slice $L $(date +%T)"
   timeout -k 10 420 python bench.py --layout $L --slice --steps ${STEPS:-3} --warmup ${WARMUP:-2} > $O/$L.json 2> $O/$L.err || { tail -30 $O/$L.err; exit 1; }
   tail -1 $O/$L.json
