@@ -17,6 +17,10 @@ from dataclasses import dataclass
 HBM_GB = 288.0
 _ACT_ATTN = 14  # bytes per (token, layer, hidden element): norms, QKV, attention out, residual
 _ACT_MLP = 20   # gate|up output, SwiGLU output, down input (dense MLP with I = 3.5 h)
+# resident outside every term above: library GEMM workspaces, RoPE tables, the side streams'
+# buffers -- measured between steps of the per-rank slices (bench.py --slice,
+# profiles/r06/slices): +1.5 GB over the resident terms at DP 8, +2.0-2.5 GB at TP 2 x PP 2
+_WORKSPACE_GB = 2.0
 _ACT_SWIGLU = 7  # the SwiGLU output alone (I = 3.5 h bf16): not kept when it is recomputed
                  # in backward (ops/mlp.swiglu_linear: one rank, opt-in ST_MLP_RECOMPUTE_ACT=1)
 
@@ -29,11 +33,12 @@ class MemoryEstimate:
     activations_gb: float
     logits_gb: float
     comm_gb: float
+    workspace_gb: float = 0.0
 
     @property
     def total_gb(self) -> float:
         return (self.params_gb + self.grads_gb + self.optimizer_gb + self.activations_gb + self.logits_gb
-                + self.comm_gb)
+                + self.comm_gb + self.workspace_gb)
 
     def fits(self, capacity_gb: float = HBM_GB, headroom_gb: float | None = None) -> bool:
         import os
@@ -45,7 +50,8 @@ class MemoryEstimate:
     def summary(self) -> str:
         return (f"{self.total_gb:.1f} GB/rank (params {self.params_gb:.1f}, grads {self.grads_gb:.1f}, "
                 f"optimizer {self.optimizer_gb:.1f}, activations {self.activations_gb:.1f}, "
-                f"logits {self.logits_gb:.1f}, comm buffers {self.comm_gb:.1f}) of {HBM_GB:.0f} GB")
+                f"logits {self.logits_gb:.1f}, comm buffers {self.comm_gb:.1f}, workspaces {self.workspace_gb:.1f}) "
+                f"of {HBM_GB:.0f} GB")
 
 
 def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1, dp: int = 1,
@@ -158,4 +164,4 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
     wt = 2 * (dense - 2 * h * layers - (h * cfg.num_experts if cfg.is_moe else 0) * layers)
     g = 1e9
     return MemoryEstimate(params_gb=(2 * n + wt) / g, grads_gb=4 * n / g, optimizer_gb=opt / g, activations_gb=act / g,
-                          logits_gb=logits / g, comm_gb=comm / g)
+                          logits_gb=logits / g, comm_gb=comm / g, workspace_gb=_WORKSPACE_GB)
