@@ -594,6 +594,36 @@ def _gmm(x: torch.Tensor, w: torch.Tensor, offs: torch.Tensor, wn: bool) -> torc
     return _gmm_fallback(x, w, offs, wn)
 
 
+def _gmm_tail_split(x: torch.Tensor, w: torch.Tensor, offs: torch.Tensor, wn: bool, padded: bool) -> torch.Tensor:
+    """One local expert (G = 1) whose rows are exactly ``x``'s (the RCCL exchange sizes the
+    buffer): a narrow GEMM (N = 4,096: 16 column tiles of 256) fills the 256 CUs only in
+    whole bands of 4,096 rows, so a few hundred rows past a band cost a third, mostly idle,
+    wave (tools/bench_ep8_expert.py: gate|up dgrad 1.46 ms at 8,192 rows, 1.98 ms at 8,544).
+    The whole bands run on the grouped kernel and a tail of at most half a band as ONE
+    batched hipBLASLt product over K slices (fp32 partials summed once): as one plain GEMM
+    the tail's 16-32 tiles took 0.33 ms of a 1.75 ms call.  ``ST_MOE_TAIL_SPLIT=0``: off (A/B)."""
+    N = w.shape[2] if wn else w.shape[1]
+    M = x.shape[0]
+    band = (256 * 256 * 256) // N if N else 0  # rows per full wave of 256 x 256 tiles on 256 CUs
+    tail = M % band if band else 0
+    if (padded or w.shape[0] != 1 or not x.is_cuda or band == 0 or M < band or tail == 0 or tail > band // 2
+            or os.environ.get("ST_MOE_TAIL_SPLIT", "1") != "1"):
+        return _gmm(x, w, offs, wn)
+    M1 = M - tail
+    head = _gmm(x[:M1], w, offs.new_full((1,), M1), wn)
+    # the tail's few row tiles alone would leave most CUs idle: split its K over ks batched
+    # products (fp32 partials, summed once) so ~a wave of tiles covers the chip
+    K = x.shape[1]
+    tiles = -(-tail // 256) * (N // 256)
+    ks = 1
+    while ks < 8 and tiles * ks * 2 <= 256 and K % (ks * 2 * 64) == 0:
+        ks *= 2
+    wk = (w[0] if wn else w[0].t()).unflatten(0, (ks, K // ks))          # [ks, K/ks, N]
+    xk = x[M1:].unflatten(1, (ks, K // ks)).transpose(0, 1)               # [ks, tail, K/ks]
+    rest = torch.ops.aten.bmm.dtype(xk, wk, torch.float32).sum(0).to(x.dtype)
+    return torch.cat([head, rest], 0)
+
+
 def _gmm_swiglu(x: torch.Tensor, w_gu: torch.Tensor, offs: torch.Tensor):
     """(gu, a = silu(gate) * up) of the grouped gate|up GEMM: ONE launch with the SwiGLU
     in the epilogue (csrc/grouped_gemm.hip EPI 1) when the kernel takes the shape
@@ -713,11 +743,12 @@ class _ExpertFFNFn(torch.autograd.Function):
             y = _gemm_per_expert(a, w_dn, counts_host, False, R)
         else:
             gu, a = _gmm_swiglu(x, w_gu, offs)
-            y = _gmm(a, w_dn, offs, wn=False)
+            y = _gmm_tail_split(a, w_dn, offs, False, getattr(x, "_st_padded", False))
         # padded buffers (dropless EP: R_max rows, the real ones counted on the device):
         # keep only gu and recompute a over the valid rows in backward
         ctx.keep_a = os.environ.get("ST_MOE_SAVE_ACT", "auto") == "1" or (
             os.environ.get("ST_MOE_SAVE_ACT", "auto") == "auto" and not getattr(x, "_st_padded", False))
+        ctx.padded = getattr(x, "_st_padded", False)
         ctx.save_for_backward(x, gu, a if ctx.keep_a else None, offs)
         ctx.w_gu, ctx.w_dn = w_gu, w_dn
         return y
@@ -739,7 +770,7 @@ class _ExpertFFNFn(torch.autograd.Function):
             dx = _gemm_per_expert(dgu, w_gu, ch, True, dy.shape[0])
         else:
             dgu = _gmm_dswiglu(dy, w_dn, offs, gu)
-            dx = _gmm(dgu, w_gu, offs, wn=True)
+            dx = _gmm_tail_split(dgu, w_gu, offs, True, ctx.padded)
         counts = ch
         for w, dout, inp in ((w_dn, dy, a), (w_gu, dgu, x)):
             counts = _expert_wgrad(w, dout, inp, offs, counts)

@@ -1080,6 +1080,25 @@ def test_expert_ffn_vendor_gemms_match_grouped():
         assert rel(a, b) < 2e-2
 
 
+@pytest.mark.parametrize("wn", [False, True])
+@pytest.mark.parametrize("M", [4096 + 352, 8192 + 1536, 8192 - 300])
+def test_gmm_tail_split_matches_fp32(M, wn):
+    """The narrow (N = 4,096) one-expert GEMM split into whole 4,096-row waves on the grouped /
+    gemm4w kernel plus a hipBLASLt tail (models/moe.py ``_gmm_tail_split``) equals the fp32
+    product, for a tail it splits (352, 1,536 rows) and one it leaves whole (3,796)."""
+    from scaletorch_amd.models.moe import _gmm_tail_split
+
+    torch.manual_seed(5)
+    K, N = 4096, 4096  # K >= 4096: the wn=False bands run on gemm4w
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn((1, K, N) if wn else (1, N, K), device="cuda", dtype=torch.bfloat16) / K ** 0.5)
+    offs = torch.tensor([M], device="cuda", dtype=torch.int32)
+    y = _gmm_tail_split(x, w, offs, wn, False)
+    ref = x.float() @ (w[0].float() if wn else w[0].float().t())
+    assert y.shape == (M, N)
+    assert rel(y.float(), ref) < 1e-2
+
+
 @pytest.mark.parametrize("cp,rank", [(4, 1), (8, 3)])
 def test_cp_two_phase_backward_at_zigzag_offsets(cp, rank):
     """The CP all-gather backward's two phases (parallel/context_parallel.py ``_CPAttnFn``):

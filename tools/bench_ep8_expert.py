@@ -18,6 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
+from scaletorch_amd.models.moe import _gmm_tail_split  # noqa: E402
 from scaletorch_amd.ops import _lib  # noqa: E402
 
 
@@ -36,6 +37,7 @@ def timeit(fn, iters=10):
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", default="8192,8544,16384")
+    ap.add_argument("--ops", default="", help="comma list of ops to time (default all)")
     ap.add_argument("--h", type=int, default=4096)
     ap.add_argument("--inter", type=int, default=14336)
     a = ap.parse_args()
@@ -69,6 +71,7 @@ def main() -> int:
                 "gemm4w": lambda: ops.gemm4w(act, w_dn, offs),
                 "grouped": lambda: ops.grouped_gemm(act, w_dn, offs, False),
                 "hipblaslt": lambda: torch.matmul(act, w_dn[0].t()),
+                "bands+hipblaslt_tail": lambda: _gmm_tail_split(act, w_dn, offs, False, False),
             }),
             "down_dgrad_dswiglu": (f_dn, {
                 "grouped_dswiglu": lambda: ops.grouped_gemm_dswiglu(dy, w_dn, offs, gu),
@@ -81,6 +84,7 @@ def main() -> int:
                 "grouped": lambda: ops.grouped_gemm(dgu, w_gu, offs, True),
                 "hipblaslt_NN": lambda: torch.matmul(dgu, w_gu[0]),
                 "hipblaslt_TN_on_WT": lambda: torch.nn.functional.linear(dgu, w_gu_t),
+                "bands+hipblaslt_tail": lambda: _gmm_tail_split(dgu, w_gu, offs, True, False),
             }),
             "gate_up_wgrad_acc": (f_gu, {
                 "wgrad4_grouped": lambda: ops.wgrad_grouped_(mg_gu, dgu, x, offs, 1),
@@ -95,6 +99,8 @@ def main() -> int:
         }
         res = {}
         for op, (flops, fns) in arms.items():
+            if a.ops and op not in a.ops.split(","):
+                continue
             r = {}
             for arm, fn in fns.items():
                 try:
