@@ -261,9 +261,6 @@ struct DmaStager {
 #pragma unroll
     for (int i = 0; i < NI; ++i) lds_dma16(rs, tile + wave_base + i * 1024, voff[i] + o);
   }
-  ST_DEVICE void load_piece(rsrc_t rs, lds_t* tile, int row0, int i) const {  // piece i of load()
-    lds_dma16(rs, tile + wave_base + i * 1024, voff[i] + (uint32_t)row0 * stride_bytes);
-  }
 };
 
 struct AttnParams {
@@ -533,380 +530,6 @@ __global__ __launch_bounds__(256 * HP, 2 / HP) void flash_fwd_kernel(AttnParams 
     }
     if (h == 0)
       lse[((int64_t)b * p.H + hq) * p.Sq + my_q] = l > 0.f ? (m * kLn2 + __logf(l)) : -INFINITY;
-  }
-}
-
-// ============================================================== forward, 64 queries per wave, software-pipelined
-// One workgroup per CU (4 waves, one per SIMD), 256 queries of one (b, q-head); each wave owns
-// 64 queries as two 32-row blocks qb, so every K / V^T fragment read from LDS feeds two MFMAs.
-// At one wave per SIMD nothing else hides the softmax, so the kernel pipelines it under the
-// MFMAs of the NEXT product itself -- per key tile j of 64 keys, two phases of 32 MFMAs:
-//   X(j): O += V(j-1) P(j-1)   beside   softmax of S(j): mask, row max, rescale decision,
-//                                        exp2 / row sums (VALU); P(j) fragments written
-//                                        over P(j-1) after the last MFMA that reads it
-//   Y(j): S(j+1) = K(j+1) Q^T  beside   K fragment reads (and the rare O rescale)
-// The O rescale decided in X(j) is applied at the top of Y(j), when PV(j-1) has completed and
-// no P at the new scale has entered O (cdna_hip_programming.md T13 ordering).  Q fragments and
-// O live in AGPRs (asm MFMAs: Q as the B operand read from the AGPR file), S and P in VGPRs.  LDS: K[2] V[2] images as the 4-wave kernel's; iteration j DMAs K(j+2) and
-// V(j) (8 x 1 KiB pieces per wave) right after its barrier -- one barrier per tile.
-// Waves whose queries see fewer key tiles than the workgroup still run every tile (masked to
-// P = 0), so no accumulator crosses a branch.
-ST_DEVICE void mfma_qa(f32x16& s, bfx8 k, const bfx8& q) {  // S += K Q^T, Q from the AGPR file
-  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(s) : "v"(k), "a"(q));
-}
-ST_DEVICE void mfma_qa0(f32x16& s, bfx8 k, const bfx8& q) {  // first k-step: C = 0
-  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=v"(s) : "v"(k), "a"(q));
-}
-
-// FINE: the softmax of X(j) cut into 32 slices, one after each PV MFMA (else four blocks, one
-// after each 8-MFMA d-tile group)
-template <bool XCD = true, bool FINE = false>
-__global__ __launch_bounds__(256, 1) void flash_fwd_pw_kernel(AttnParams p, bf16_t* __restrict__ o,
-                                                              int64_t sob, int64_t sos, int64_t soh,
-                                                              float* __restrict__ lse) {
-  constexpr int D = 128, BM = 256, BN = 64, NKK = D / 16, NDT = D / 32;
-  constexpr int TB = BN * D * 2;
-  __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];  // K0 K1 V0 V1
-  lds_t* smem = (lds_t*)smem_raw;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 31, h = lane >> 5;
-  const int nqt = (p.Sq + BM - 1) / BM, id = blockIdx.x;
-  int rank, b, hq;
-  const int G = p.H / p.Hkv, BHk = p.B * p.Hkv;
-  if (XCD && BHk % 8 == 0) {  // as flash_fwd_kernel: XCD x takes the kv heads = x mod 8
-    const int j = id >> 3, per_rank = (BHk >> 3) * G, rem = j % per_rank;
-    rank = j / per_rank;
-    const int bhk = (id & 7) + 8 * (rem / G);
-    b = bhk / p.Hkv;
-    hq = (bhk % p.Hkv) * G + rem % G;
-  } else {
-    const int BH = p.B * p.H;
-    rank = id / BH;
-    b = (id % BH) / p.H;
-    hq = id % p.H;
-  }
-  const int qt = p.causal ? nqt - 1 - rank : rank;
-  const int hk = hq / G;
-  const int q0 = qt * BM, wq0 = q0 + wid * 64;
-
-  const rsrc_t rq = make_rsrc(p.q + (int64_t)b * p.sqb + (int64_t)hq * p.sqh, p.Sq, p.sqs, D);
-  const rsrc_t rk = make_rsrc(p.k + (int64_t)b * p.skb + (int64_t)hk * p.skh, p.Sk, p.sks, D);
-  const rsrc_t rv = make_rsrc(p.v + (int64_t)b * p.svb + (int64_t)hk * p.svh, p.Sk, p.svs, D);
-
-  bfx8 qf[2][NKK];
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-    for (int kk = 0; kk < NKK; ++kk)
-      qf[qb][kk] = bload_frag(rq, (uint32_t)(wq0 + 32 * qb + r) * (uint32_t)(p.sqs * 2) + (2 * kk + h) * 16);
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): see flash_fwd_kernel
-  int nkb, kbm_wg, wnkb, wmask;
-  key_blocks<BM, BN>(p, q0, true, nkb, kbm_wg);       // tiles any query of the workgroup sees
-  key_blocks<64, BN>(p, wq0, true, wnkb, wmask);      // this wave's own (masking from wmask on)
-  (void)kbm_wg;
-  (void)wnkb;
-
-  LdsAddr<D> la;
-  la.init(lane);
-  DmaStager<D, BN, 4> sk, sv;
-  sk.init(wid, lane, p.sks);
-  sv.init(wid, lane, p.svs);
-
-  f32x16 oacc[2][NDT];
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) oacc[qb][dt] = zero16();
-  f32x16 s[2][2];
-  bfx8 pbuf[2][4];  // [qb][k-step]: P(j), written after the last MFMA that reads P(j-1)
-  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f}, alpha[2] = {1.f, 1.f};
-  bool resc = false;  // wave-uniform: an O rescale is pending (decided in X, applied in Y)
-  const float c2 = p.scale * kLog2e;
-  const int64_t qg0 = p.q_offset + wq0 + r;
-
-  // The pieces below are macros, not lambdas: a lambda that captures another lambda keeps the
-  // accumulator arrays addressable and hipcc parks them in scratch (see flash_fwd_pp_kernel).
-  // S(t) = K(t) Q^T from the K image kt (both 32-key halves, both query blocks); K row
-  // fragments one k-step ahead
-#define PW_S_TILE(KT)                                                               \
-  do {                                                                              \
-    const lds_t* kt_ = (KT);                                                        \
-    bfx8 fk[3][2];                                                                  \
-    fk[0][0] = la.rowf(kt_, 0, 0);                                                  \
-    fk[0][1] = la.rowf(kt_, 1, 0);                                                  \
-    fk[1][0] = la.rowf(kt_, 0, 1);                                                  \
-    fk[1][1] = la.rowf(kt_, 1, 1);                                                  \
-    _Pragma("unroll") for (int kk = 0; kk < NKK; ++kk) {                            \
-      if (kk + 2 < NKK) {                                                           \
-        fk[(kk + 2) % 3][0] = la.rowf(kt_, 0, kk + 2);                              \
-        fk[(kk + 2) % 3][1] = la.rowf(kt_, 1, kk + 2);                              \
-      }                                                                             \
-      __builtin_amdgcn_sched_barrier(0);                                            \
-      _Pragma("unroll") for (int h2 = 0; h2 < 2; ++h2)                              \
-      _Pragma("unroll") for (int qb = 0; qb < 2; ++qb) {                            \
-        if (kk == 0) mfma_qa0(s[qb][h2], fk[0][h2], qf[qb][0]);                     \
-        else mfma_qa(s[qb][h2], fk[kk % 3][h2], qf[qb][kk]);                        \
-      }                                                                             \
-    }                                                                               \
-  } while (0)
-  // mask (diagonal / tail tiles), row max, rescale decision (l scaled now, O at the next Y)
-#define PW_MASK_MAX(KB)                                                                   \
-  do {                                                                                    \
-    if ((KB) >= wmask) {                                                                  \
-      _Pragma("unroll") for (int qb = 0; qb < 2; ++qb) {                                  \
-        const int lim = key_limit(p, (KB), BN, qg0 + 32 * qb, h, true);                   \
-        _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                  \
-          if (acc_row0(i) > lim) s[qb][0][i] = -INFINITY;                                 \
-          if (acc_row0(i) + 32 > lim) s[qb][1][i] = -INFINITY;                            \
-        }                                                                                 \
-      }                                                                                   \
-    }                                                                                     \
-    float mxs[2];                                                                         \
-    _Pragma("unroll") for (int qb = 0; qb < 2; ++qb) {                                    \
-      float mx0 = fmaxf(s[qb][0][0], s[qb][1][0]), mx1 = fmaxf(s[qb][0][1], s[qb][1][1]); \
-      _Pragma("unroll") for (int i = 2; i < 16; i += 2) {                                 \
-        mx0 = fmaxf(mx0, fmaxf(s[qb][0][i], s[qb][1][i]));                               \
-        mx1 = fmaxf(mx1, fmaxf(s[qb][0][i + 1], s[qb][1][i + 1]));                        \
-      }                                                                                   \
-      float mx = fmaxf(mx0, mx1);                                                         \
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));                                             \
-      mxs[qb] = mx * c2;                                                                  \
-    }                                                                                     \
-    if (__any(mxs[0] > m[0] + kRescaleThr || mxs[1] > m[1] + kRescaleThr)) {              \
-      _Pragma("unroll") for (int qb = 0; qb < 2; ++qb) {                                  \
-        const float m_new = fmaxf(m[qb], mxs[qb]);                                        \
-        alpha[qb] = (m[qb] == m_new) ? 1.f : fast_exp2(m[qb] - m_new);                    \
-        l[qb] *= alpha[qb];                                                               \
-        m[qb] = m_new;                                                                    \
-      }                                                                                   \
-      resc = true;                                                                        \
-    }                                                                                     \
-  } while (0)
-#define PW_EXP_SUM(QB)                                                  \
-  do {                                                                  \
-    const float mu = (m[QB] == -INFINITY) ? 0.f : m[QB];                \
-    float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f;                       \
-    _Pragma("unroll") for (int i = 0; i < 16; i += 2) {                 \
-      s[QB][0][i] = fast_exp2(fmaf(s[QB][0][i], c2, -mu));              \
-      s[QB][1][i] = fast_exp2(fmaf(s[QB][1][i], c2, -mu));              \
-      s[QB][0][i + 1] = fast_exp2(fmaf(s[QB][0][i + 1], c2, -mu));      \
-      s[QB][1][i + 1] = fast_exp2(fmaf(s[QB][1][i + 1], c2, -mu));      \
-      r0 += s[QB][0][i];                                                \
-      r1 += s[QB][1][i];                                                \
-      r2 += s[QB][0][i + 1];                                            \
-      r3 += s[QB][1][i + 1];                                            \
-    }                                                                   \
-    float rs = (r0 + r1) + (r2 + r3);                                   \
-    rs += __shfl_xor(rs, 32, 64);                                       \
-    l[QB] += rs;                                                        \
-  } while (0)
-#define PW_TO_P()                                            \
-  _Pragma("unroll") for (int qb = 0; qb < 2; ++qb) {         \
-    pbuf[qb][0] = acc_frag(s[qb][0], 0);                     \
-    pbuf[qb][1] = acc_frag(s[qb][0], 1);                     \
-    pbuf[qb][2] = acc_frag(s[qb][1], 0);                     \
-    pbuf[qb][3] = acc_frag(s[qb][1], 1);                     \
-  }
-  // O += V(t) P(t) from the V image VT, four d-tile groups of 8 MFMAs; BETWEEN(dt) runs
-  // after group dt (sched_barrier keeps it there)
-#define PW_PV(VT, BETWEEN)                                                        \
-  do {                                                                                \
-    const lds_t* vt_ = (VT);                                                          \
-    bfx8 vf[2][4];                                                                    \
-    _Pragma("unroll") for (int dt = 0; dt < NDT; ++dt) {                              \
-      if (dt == 0) {                                                                  \
-        vf[0][0] = la.trf(vt_, 0, 0, 0);                                              \
-        vf[0][1] = la.trf(vt_, 0, 1, 0);                                              \
-        vf[0][2] = la.trf(vt_, 32, 0, 0);                                             \
-        vf[0][3] = la.trf(vt_, 32, 1, 0);                                             \
-      }                                                                               \
-      if (dt + 1 < NDT) {                                                             \
-        vf[(dt + 1) & 1][0] = la.trf(vt_, 0, 0, dt + 1);                              \
-        vf[(dt + 1) & 1][1] = la.trf(vt_, 0, 1, dt + 1);                              \
-        vf[(dt + 1) & 1][2] = la.trf(vt_, 32, 0, dt + 1);                             \
-        vf[(dt + 1) & 1][3] = la.trf(vt_, 32, 1, dt + 1);                             \
-      }                                                                               \
-      __builtin_amdgcn_sched_barrier(0);                                              \
-      _Pragma("unroll") for (int qb = 0; qb < 2; ++qb)                                \
-      _Pragma("unroll") for (int u = 0; u < 4; ++u)                                   \
-        mfma_acc(oacc[qb][dt], vf[dt & 1][u], pbuf[qb][u]);                           \
-      __builtin_amdgcn_sched_barrier(0);                                              \
-      BETWEEN;                                                                        \
-    }                                                                                 \
-  } while (0)
-  // FINE form of X(j): after PV MFMA m (= 8 dt + 4 qb + u) one slice of tile KB's softmax:
-  // dt 0: mask qb 0 / 1, row max in four halves, the rescale decision; dt 1 / 2: exp2 and row
-  // sums of query block 0 / 1, two register pairs per slice; dt 3: P fragment m & 7, written
-  // right after the last MFMA that reads its P(j-1) predecessor
-#define PW_PV_FINE(VT, KB)    /* also issues iteration KB's 8 DMA pieces, one per dt-0 MFMA */  \
-  do {                                                                                          \
-    const lds_t* vt_ = (VT);                                                                    \
-    bfx8 vf[2][4];                                                                              \
-    float mxa[2] = {0.f, 0.f}, mxs[2] = {0.f, 0.f}, mu = 0.f;                                   \
-    float ra = 0.f, rb = 0.f, rc = 0.f, rd = 0.f;                                               \
-    _Pragma("unroll") for (int dt = 0; dt < NDT; ++dt) {                                        \
-      if (dt == 0) {                                                                            \
-        vf[0][0] = la.trf(vt_, 0, 0, 0);                                                        \
-        vf[0][1] = la.trf(vt_, 0, 1, 0);                                                        \
-        vf[0][2] = la.trf(vt_, 32, 0, 0);                                                       \
-        vf[0][3] = la.trf(vt_, 32, 1, 0);                                                       \
-      }                                                                                         \
-      if (dt + 1 < NDT) {                                                                       \
-        vf[(dt + 1) & 1][0] = la.trf(vt_, 0, 0, dt + 1);                                        \
-        vf[(dt + 1) & 1][1] = la.trf(vt_, 0, 1, dt + 1);                                        \
-        vf[(dt + 1) & 1][2] = la.trf(vt_, 32, 0, dt + 1);                                       \
-        vf[(dt + 1) & 1][3] = la.trf(vt_, 32, 1, dt + 1);                                       \
-      }                                                                                         \
-      _Pragma("unroll") for (int mq = 0; mq < 8; ++mq) {                                        \
-        const int qb = mq >> 2, u = mq & 3;                                                     \
-        __builtin_amdgcn_sched_barrier(0);                                                      \
-        mfma_acc(oacc[qb][dt], vf[dt & 1][u], pbuf[qb][u]);                                     \
-        if (dt == 0) {                                                                          \
-          if (mq < 4) {                                                                         \
-            if ((KB) + 2 < nkb) sk.load_piece(rk, smem + ((KB) & 1) * TB, ((KB) + 2) * BN, mq);  \
-          } else {                                                                              \
-            sv.load_piece(rv, smem + (2 + ((KB) & 1)) * TB, (KB) * BN, mq - 4);                  \
-          }                                                                                     \
-          if (mq < 2) {                                                                         \
-            if ((KB) >= wmask) {                                                                \
-              const int lim = key_limit(p, (KB), BN, qg0 + 32 * mq, h, true);                   \
-              _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                  \
-                if (acc_row0(i) > lim) s[mq][0][i] = -INFINITY;                                 \
-                if (acc_row0(i) + 32 > lim) s[mq][1][i] = -INFINITY;                            \
-              }                                                                                 \
-            }                                                                                   \
-          } else if (mq < 6) {                                                                  \
-            const int q2 = (mq - 2) >> 1, i0 = ((mq - 2) & 1) * 8;                              \
-            float x = i0 ? mxa[q2] : fmaxf(s[q2][0][0], s[q2][1][0]);                           \
-            _Pragma("unroll") for (int i = 0; i < 8; ++i)                                       \
-              x = fmaxf(x, fmaxf(s[q2][0][i0 + i], s[q2][1][i0 + i]));                          \
-            mxa[q2] = x;                                                                        \
-            if (i0) mxs[q2] = fmaxf(x, __shfl_xor(x, 32, 64)) * c2;                             \
-          } else if (mq == 6) {                                                                 \
-            if (__any(mxs[0] > m[0] + kRescaleThr || mxs[1] > m[1] + kRescaleThr)) {            \
-              _Pragma("unroll") for (int q2 = 0; q2 < 2; ++q2) {                                \
-                const float m_new = fmaxf(m[q2], mxs[q2]);                                      \
-                alpha[q2] = (m[q2] == m_new) ? 1.f : fast_exp2(m[q2] - m_new);                  \
-                l[q2] *= alpha[q2];                                                             \
-                m[q2] = m_new;                                                                  \
-              }                                                                                 \
-              resc = true;                                                                      \
-            }                                                                                   \
-          }                                                                                     \
-        } else if (dt <= 2) {                                                                   \
-          const int q2 = dt - 1, i = 2 * mq;                                                    \
-          if (mq == 0) {                                                                        \
-            mu = (m[q2] == -INFINITY) ? 0.f : m[q2];                                            \
-            ra = rb = rc = rd = 0.f;                                                            \
-          }                                                                                     \
-          s[q2][0][i] = fast_exp2(fmaf(s[q2][0][i], c2, -mu));                                  \
-          s[q2][1][i] = fast_exp2(fmaf(s[q2][1][i], c2, -mu));                                  \
-          s[q2][0][i + 1] = fast_exp2(fmaf(s[q2][0][i + 1], c2, -mu));                          \
-          s[q2][1][i + 1] = fast_exp2(fmaf(s[q2][1][i + 1], c2, -mu));                          \
-          ra += s[q2][0][i];                                                                    \
-          rb += s[q2][1][i];                                                                    \
-          rc += s[q2][0][i + 1];                                                                \
-          rd += s[q2][1][i + 1];                                                                \
-          if (mq == 7) {                                                                        \
-            float rs = (ra + rb) + (rc + rd);                                                   \
-            rs += __shfl_xor(rs, 32, 64);                                                       \
-            l[q2] += rs;                                                                        \
-          }                                                                                     \
-        } else {                                                                                \
-          pbuf[qb][u] = acc_frag(s[qb][u >> 1], u & 1);                                         \
-        }                                                                                       \
-      }                                                                                         \
-    }                                                                                           \
-    __builtin_amdgcn_sched_barrier(0);                                                          \
-  } while (0)
-#define PW_RESCALE()                                                   \
-  do {                                                                 \
-    if (resc) {                                                        \
-      agpr_fence(oacc[0]);                                             \
-      agpr_fence(oacc[1]);                                             \
-      _Pragma("unroll") for (int qb = 0; qb < 2; ++qb)                 \
-      _Pragma("unroll") for (int dt = 0; dt < NDT; ++dt)               \
-      _Pragma("unroll") for (int i = 0; i < 16; ++i)                   \
-        oacc[qb][dt][i] *= alpha[qb];                                  \
-      resc = false;                                                    \
-    }                                                                  \
-  } while (0)
-  // iteration j's DMA: K(j+2) into K image j & 1, V(j) into V image j & 1
-#define PW_DMA(J)                                                                \
-  do {                                                                           \
-    if ((J) + 2 < nkb) sk.load(rk, smem + ((J) & 1) * TB, ((J) + 2) * BN);       \
-    sv.load(rv, smem + (2 + ((J) & 1)) * TB, (J) * BN);                          \
-  } while (0)
-
-  if (nkb > 0) {
-    // prologue: K(0), K(1) resident, S(0); iteration 0: softmax(0) only (no PV yet)
-    sk.load(rk, smem, 0);
-    if (nkb > 1) sk.load(rk, smem + TB, BN);
-    dma_barrier();
-    PW_S_TILE(smem);
-    __syncthreads();  // every wave is done reading K image 0 before K(2) lands there
-    PW_DMA(0);
-    PW_MASK_MAX(0);
-    PW_EXP_SUM(0);
-    PW_EXP_SUM(1);
-    PW_TO_P();
-    PW_RESCALE();
-    if (nkb > 1) PW_S_TILE(smem + TB);
-    dma_barrier();
-    // steady state: iteration j (parity j & 1): DMA, X(j) = PV(j-1) + softmax(j), Y(j) = S(j+1)
-    auto iter = [&](auto parc, int j) {
-      constexpr int PJ = decltype(parc)::value;
-      if constexpr (!FINE) PW_DMA(j);
-      if constexpr (FINE) {
-        PW_PV_FINE(smem + (2 + (PJ ^ 1)) * TB, j);
-      } else {
-        PW_PV(smem + (2 + (PJ ^ 1)) * TB,
-              if (dt == 0) PW_MASK_MAX(j); else if (dt == 1) PW_EXP_SUM(0); else if (dt == 2) PW_EXP_SUM(1);
-              else { PW_TO_P(); });
-      }
-      PW_RESCALE();
-      if (j + 1 < nkb) PW_S_TILE(smem + (PJ ^ 1) * TB);
-      dma_barrier();
-    };
-    int j = 1;
-    for (; j + 1 < nkb; j += 2) {
-      iter(Buf<1>(), j);
-      iter(Buf<0>(), j + 1);
-    }
-    if (j < nkb) iter(Buf<1>(), j++);
-    // the last tile's PV: tile nkb - 1 (P buffer / V image of its parity)
-    PW_PV(smem + (2 + ((nkb - 1) & 1)) * TB, (void)0);
-  }
-#undef PW_S_TILE
-#undef PW_MASK_MAX
-#undef PW_EXP_SUM
-#undef PW_TO_P
-#undef PW_PV
-#undef PW_PV_FINE
-#undef PW_RESCALE
-#undef PW_DMA
-  agpr_fence(oacc[0]);
-  agpr_fence(oacc[1]);
-
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int my_q = wq0 + 32 * qb + r;
-    if (my_q < p.Sq) {
-      const float inv = l[qb] > 0.f ? 1.f / l[qb] : 0.f;
-      bf16_t* orow = o + (int64_t)b * sob + (int64_t)my_q * sos + (int64_t)hq * soh;
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int d = 32 * dt + 8 * g + 4 * h;
-          uint2 w;
-          w.x = pack_bf16x2(oacc[qb][dt][4 * g + 0] * inv, oacc[qb][dt][4 * g + 1] * inv);
-          w.y = pack_bf16x2(oacc[qb][dt][4 * g + 2] * inv, oacc[qb][dt][4 * g + 3] * inv);
-          *reinterpret_cast<uint2*>(orow + d) = w;
-        }
-      }
-      if (h == 0)
-        lse[((int64_t)b * p.H + hq) * p.Sq + my_q] = l[qb] > 0.f ? (m[qb] * kLn2 + __logf(l[qb])) : -INFINITY;
-    }
   }
 }
 
@@ -2007,20 +1630,9 @@ int st_flash_fwd(const void* q, const void* k, const void* v, void* o, float* ls
   // 0.852 vs 0.853 ms, profiles/r03/flash_pmc.md), so one head stays the default.
   const char* he = std::getenv("ST_FLASH_FWD_HP");
   const bool hp2 = (H / Hkv) % 2 == 0 && he && std::atoi(he) == 2;
-  // ST_FLASH_FWD=pw / pwf: the software-pipelined 64-queries-per-wave kernel (D = 128), softmax
-  // in four blocks / in 32 slices between the PV MFMAs
-  const char* fe = std::getenv("ST_FLASH_FWD");
-  const bool pw = D == 128 && fe && fe[0] == 'p' && fe[1] == 'w';
-  const bool pwf = pw && fe[2] == 'f';
   if (D == 128 && pp) {
     const unsigned grid2 = (unsigned)(((Sq + 255) / 256) * B * H);
     flash_fwd_pp_kernel<128><<<grid2, 512, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
-  } else if (pw) {
-    const unsigned grid4 = (unsigned)(((Sq + 255) / 256) * B * H);
-    if (pwf && xcd) flash_fwd_pw_kernel<true, true><<<grid4, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
-    else if (pwf) flash_fwd_pw_kernel<false, true><<<grid4, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
-    else if (xcd) flash_fwd_pw_kernel<true><<<grid4, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
-    else flash_fwd_pw_kernel<false><<<grid4, 256, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);
   } else if (hp2) {
     const unsigned grid2 = grid / 2;
     if (D == 128 && xcd) flash_fwd_kernel<128, true, 2><<<grid2, 512, 0, st>>>(p, (bf16_t*)o, sob, sos, soh, lse);

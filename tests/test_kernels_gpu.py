@@ -646,16 +646,12 @@ def _attn_rows_ref(q, k, v, rows, scale, q_offset=0):
 
 
 @pytest.mark.parametrize("S", [4096, 8192, 32768])
-@pytest.mark.parametrize("pp", ["1", "0", "pw", "pwf"])
+@pytest.mark.parametrize("pp", ["1", "0"])
 def test_flash_long_sequence_sampled_rows(S, pp, monkeypatch):
     """Long causal sequences (the bench's 4K, 8K and the CP8@32K global length):
     the kernel's output and lse on sampled query rows (start, middle, end) against
-    an fp32 reference over every visible key; every forward kernel (8-wave ping-pong,
-    ST_FLASH_PP=1; the software-pipelined 64-queries-per-wave one, ST_FLASH_FWD=pw; the
-    4-wave one)."""
-    if pp in ("pw", "pwf"):
-        monkeypatch.setenv("ST_FLASH_FWD", pp)
-        pp = "0"
+    an fp32 reference over every visible key; both forward kernels (8-wave ping-pong,
+    ST_FLASH_PP=1, and the 4-wave one)."""
     monkeypatch.setenv("ST_FLASH_PP", pp)
     torch.manual_seed(0)
     B, H, Hkv, D = 1, 4, 2, 128
@@ -671,41 +667,12 @@ def test_flash_long_sequence_sampled_rows(S, pp, monkeypatch):
         assert (lse[:, :, rows] - rl).abs().max().item() < 1e-2, start
 
 
-@pytest.mark.parametrize("variant", ["pw", "pwf"])
-@pytest.mark.parametrize("xcd", ["1", "0"])
-@pytest.mark.parametrize("B,Sq,Sk,H,Hkv,causal,q_off,k_off", [
-    (2, 1024, 1024, 8, 2, True, 0, 0), (1, 777, 777, 4, 4, True, 0, 0), (2, 640, 1000, 4, 1, False, 0, 0),
-    (1, 300, 1500, 4, 2, True, 1200, 0), (1, 512, 512, 8, 8, True, 512, 256), (8, 256, 256, 4, 2, True, 0, 0)])
-def test_flash_fwd_pw_matches_ref(B, Sq, Sk, H, Hkv, causal, q_off, k_off, xcd, variant, monkeypatch):
-    """csrc/flash_attn.hip flash_fwd_pw_kernel (ST_FLASH_FWD=pw: software-pipelined, 64 queries
-    per wave, 256 per workgroup): causal / full, GQA, ragged Sq / Sk, CP offsets (a wave whose
-    rows see no key of a tile computes it masked), both workgroup orders; output and lse vs the
-    fp32 reference and vs the default kernel."""
-    monkeypatch.setenv("ST_FLASH_XCD", xcd)
-    torch.manual_seed(5)
-    D = 128
-    q = torch.randn(B, Sq, H, D, device="cuda", dtype=torch.bfloat16)
-    k = torch.randn(B, Sk, Hkv, D, device="cuda", dtype=torch.bfloat16)
-    v = torch.randn(B, Sk, Hkv, D, device="cuda", dtype=torch.bfloat16)
-    scale = 1 / math.sqrt(D)
-    o0, l0 = ops.flash_attn_fwd(q, k, v, scale, causal, q_off, k_off)
-    monkeypatch.setenv("ST_FLASH_FWD", variant)
-    o1, l1 = ops.flash_attn_fwd(q, k, v, scale, causal, q_off, k_off)
-    ref_o, ref_l = ops.sdpa_ref(q, k, v, causal, scale, q_off, k_off)
-    assert rel(o1, ref_o) < 1e-2
-    fin = torch.isfinite(ref_l)
-    assert torch.equal(fin, torch.isfinite(l1))
-    assert (l1[fin] - ref_l[fin]).abs().max().item() < 1e-2
-    assert rel(o1, o0) < 1e-2
-
-
-@pytest.mark.parametrize("kernel", ["default", "pw", "pwf"])
+@pytest.mark.parametrize("kernel", ["default", "pp"])
 def test_flash_fwd_rescale_spikes(kernel, monkeypatch):
     """The deferred O rescale (running max grown by > 2^8 after P of earlier tiles is already
     in O) fires only on data that spikes late: key rows with 6x the norm at several positions
     deep into the sequence (cdna_hip_programming.md T13 / rule 26), vs the fp32 reference."""
-    if kernel != "default":
-        monkeypatch.setenv("ST_FLASH_FWD", kernel)
+    monkeypatch.setenv("ST_FLASH_PP", "1" if kernel == "pp" else "0")
     torch.manual_seed(21)
     B, S, H, Hkv, D = 2, 2048, 4, 2, 128
     q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
