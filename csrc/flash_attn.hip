@@ -207,6 +207,19 @@ ST_DEVICE void lds_dma16(rsrc_t rs, lds_t* dst, uint32_t voff) {
 #pragma clang diagnostic pop
 }
 
+// The same 16-byte DMA with the non-temporal hint: for data read exactly once (the dS
+// workspace in the dQ pass), so it streams past L2 instead of evicting re-read tiles.
+ST_DEVICE void lds_dma16_nt(rsrc_t rs, lds_t* dst, uint32_t voff) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds"
+               :
+               : "s"(m0), "v"(voff), "s"(rs)
+               : "memory", "m0");
+#pragma clang diagnostic pop
+}
+
 // 4 bytes per lane (64 floats per wave-instruction): the per-query softmax
 // statistics (lse, delta) of a 64-query block go through the same DMA path, so
 // the loop carries no ordinary global load (hipcc would drain every DMA with
@@ -1007,7 +1020,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dq_ds_kernel(AttnParams p, c
     for (int j = 0; j < GH; ++j)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        lds_dma16(rs, dst + j * TS + wid * (TS / 4) + i * 1024, o + (uint32_t)j * head_stride + sv[i]);
+        lds_dma16_nt(rs, dst + j * TS + wid * (TS / 4) + i * 1024, o + (uint32_t)j * head_stride + sv[i]);
   };
 
   f32x16 dqacc[GH][NDT];
@@ -1199,7 +1212,11 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkdv_kernel(
     ds_voff[s2] = (uint32_t)ds_off(ds_row, 0, 0, s2, h) - 1024 * s2;  // + 2048 u + 1024 s2 as immediates
   auto ds_store = [&](rsrc_t rs, uint32_t soff, int u, int s2, u32x4 w) {
     if constexpr (PROBE != 2)
-      __builtin_amdgcn_raw_buffer_store_b128(w, rs, (int)(ds_voff[s2] + 2048 * u + 1024 * s2), (int)soff, 0);
+      // non-temporal (aux 2): each dS tile is read once, by the dQ pass, long after this
+      // kernel -- kept out of L2, whose hit rate on the re-read Q / dO tiles then rises
+      // (bench shape: backward 2.87 -> 2.75 ms, cp8 rank-3 chunk 3.85 -> 3.69 ms;
+      // profiles/r06/flash/nt_ds/)
+      __builtin_amdgcn_raw_buffer_store_b128(w, rs, (int)(ds_voff[s2] + 2048 * u + 1024 * s2), (int)soff, 2);
   };
   const int nq = nqb > qb0 ? nqb - qb0 : 0;
   const int total = G * nq;
