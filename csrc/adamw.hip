@@ -26,17 +26,32 @@ using namespace st;
 
 namespace {
 
+// Every byte these passes touch is touched once per step (gradients read by the norm and the
+// update, parameters and W^T written for a forward that reads them long after), and the passes
+// run on a side stream beside the forward / backward GEMMs: all their accesses carry the
+// non-temporal hint, so the stream does not evict the GEMMs' re-read tiles from L2.
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 template <typename G>
 ST_DEVICE float4 load_g4(const G* g, int64_t i);
 template <>
 ST_DEVICE float4 load_g4<float>(const float* g, int64_t i) {
-  return ld4f(g + i);
+  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g + i));
+  return make_float4(v[0], v[1], v[2], v[3]);
 }
 template <>
 ST_DEVICE float4 load_g4<bf16_t>(const bf16_t* g, int64_t i) {
-  uint2 v = *reinterpret_cast<const uint2*>(g + i);
-  return make_float4(__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
-                     __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u));
+  const u32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(g + i));
+  return make_float4(__uint_as_float(v[0] << 16), __uint_as_float(v[0] & 0xffff0000u),
+                     __uint_as_float(v[1] << 16), __uint_as_float(v[1] & 0xffff0000u));
+}
+ST_DEVICE void store_p4(bf16_t* p, uint32_t lo, uint32_t hi) {  // 4 bf16 parameters
+  const u32x2_t v = {lo, hi};
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x2_t*>(p));
+}
+ST_DEVICE void store_wt8(bf16_t* p, const BF8& o) {  // 8 bf16 of W^T
+  const u32x4_t v = {o.w[0], o.w[1], o.w[2], o.w[3]};
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(p));
 }
 
 // Optimizer moments: fp32 (default) or bf16 (ST optimizer_state_dtype="bf16": the
@@ -166,12 +181,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, 
       sr_words<S>(ii[u] + sr_base, key, rm, rv);
       store_s4<S>(m, ii[u], mm[u], rm);
       store_s4<S>(v, ii[u], vv[u], rv);
-      if (p) {
-        uint2 o;
-        o.x = pack_bf16x2(w[u][0], w[u][1]);
-        o.y = pack_bf16x2(w[u][2], w[u][3]);
-        *reinterpret_cast<uint2*>(p + ii[u]) = o;
-      }
+      if (p) store_p4(p + ii[u], pack_bf16x2(w[u][0], w[u][1]), pack_bf16x2(w[u][2], w[u][3]));
     }
   }
 }
@@ -232,7 +242,7 @@ __global__ __launch_bounds__(256) void adamw_wt_kernel(float* __restrict__ maste
     store_s4<S>(m, i, mm[u], rm);
     store_s4<S>(v, i, vv[u], rv);
     const uint32_t lo = pack_bf16x2(w[u][0], w[u][1]), hi = pack_bf16x2(w[u][2], w[u][3]);
-    *reinterpret_cast<uint2*>(p + i) = make_uint2(lo, hi);
+    store_p4(p + i, lo, hi);
     // padded LDS row (132 B): 4-B aligned only
     uint32_t* d = reinterpret_cast<uint32_t*>(tile + (lr0 + 16 * u) * kWLd + lc);
     d[0] = lo;
@@ -250,7 +260,7 @@ __global__ __launch_bounds__(256) void adamw_wt_kernel(float* __restrict__ maste
       const uint32_t c = tile[(chunk * 8 + 2 * j + 1) * kWLd + oc];
       o.w[j] = a | (c << 16);
     }
-    st8(wt + (int64_t)(c0 + oc) * R + r0 + chunk * 8, o);
+    store_wt8(wt + (int64_t)(c0 + oc) * R + r0 + chunk * 8, o);
   }
 }
 
