@@ -53,8 +53,11 @@ LAYOUTS = {
     "dp": dict(),
     # 3-D: TP inside an xGMI pair, 2 pipeline stages, DP over the rest; 8 micro-batches through
     # the interleaved 1F1B schedule with 2 chunks per stage keep the bubble at
-    # (pp-1)/(V*M+pp-1) = 6 % (11 % plain 1F1B); sequence parallel shards norm/residual activations
-    "tp2pp2dp2": dict(tp=2, pp=2, sp=True, micro_batch_size=4, grad_acc=8, vpp=2),
+    # (pp-1)/(V*M+pp-1) = 6 % (11 % plain 1F1B); sequence parallel shards norm/residual activations.
+    # Layers per chunk 9,8,8,7 (stage 0: 17, last stage: 15 + final norm, LM head and loss): the
+    # per-rank slices ran the even split at 1333 / 1487 ms per stage and this one at 1417 / 1401,
+    # so the pipeline's pace (its slowest stage) drops 4.7 % (profiles/r06/pp_balance/)
+    "tp2pp2dp2": dict(tp=2, pp=2, sp=True, micro_batch_size=4, grad_acc=8, vpp=2, layer_distribution="9,8,8,7"),
     # long context: 32K tokens over 8 CP ranks (4K local), zig-zag chunks, GQA-sized K/V
     "cp8_32k": dict(cp=-1, seq_len=32768, micro_batch_size=1),
     # Mixtral 8x7B: one expert per GPU (EP carved out of DP), dense weights ZeRO-1 over DP x EP;
@@ -193,6 +196,8 @@ def main() -> int:
     ap.add_argument("--ep", type=int, default=None)
     ap.add_argument("--sp", action="store_true", default=None)
     ap.add_argument("--vpp", type=int, default=None, help="model chunks per pipeline stage (interleaved 1F1B)")
+    ap.add_argument("--layer_distribution", default=None,
+                    help="comma list of layers per pipeline chunk (global chunk order with --vpp > 1)")
     ap.add_argument("--cp_comm", default="auto", help="auto | allgather | ring | ulysses")
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) | gloo (debug rehearsals only)")
     ap.add_argument("--gc", action="store_true", help="activation checkpointing")
@@ -246,8 +251,9 @@ def main() -> int:
         # a mismatch would report a different job size than the one asked for
         raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     preset = dict(model="llama3-8b", micro_batch_size=6, seq_len=4096, grad_acc=1, tp=1, pp=1, cp=1, ep=1, sp=False,
-                  vpp=1, moe_capacity_factor=0.0, moe_ep_chunks=1)
+                  vpp=1, moe_capacity_factor=0.0, moe_ep_chunks=1, layer_distribution=None)
     preset.update({k: (world if v == -1 else v) for k, v in LAYOUTS[args.layout].items()})
+    user_dist = args.layer_distribution
     for k, v in preset.items():
         if getattr(args, k) is None:
             setattr(args, k, v)
@@ -284,6 +290,14 @@ def main() -> int:
     from scaletorch_amd.utils.memory import estimate_rank_memory
 
     mcfg = get_model_config(args.model, num_hidden_layers=args.layers)
+    if args.layer_distribution:
+        d = [int(x) for x in args.layer_distribution.split(",")]
+        nchunks = args.pp * (args.vpp if args.pp > 1 else 1)
+        if args.pp == 1 or len(d) != nchunks or sum(d) != mcfg.num_hidden_layers:
+            if user_dist:
+                raise SystemExit(f"--layer_distribution {user_dist}: need {nchunks} entries summing to "
+                                 f"{mcfg.num_hidden_layers} layers")
+            args.layer_distribution = None  # the preset's split is for its own model / layout
     def estimate(slice_rank: bool):
         """HBM of the 8-GPU run's worst rank (first stage, planned IPC areas, the transport's
         expert buffers) or, ``slice_rank``, of the rank this slice runs (no IPC areas, RCCL EP)."""
@@ -296,7 +310,8 @@ def main() -> int:
             xgmi_ipc_bytes=0 if slice_rank else _planned_ipc(args, mcfg),
             pp_rank=(args.pp - 1 if slice_rank and args.slice_stage == "last" else 0),
             virtual_pipeline=args.vpp if args.pp > 1 else 1,
-            moe_exact_rows=args.ep_comm == "rccl" or slice_rank)
+            moe_exact_rows=args.ep_comm == "rccl" or slice_rank,
+            layer_distribution=[int(x) for x in args.layer_distribution.split(",")] if args.layer_distribution else None)
 
     est_run = estimate(False)
     est = estimate(True) if args.slice else est_run
@@ -310,7 +325,7 @@ def main() -> int:
         model_name_or_path=args.model, synthetic_data=True, micro_batch_size=args.micro_batch_size,
         sequence_length=args.seq_len, gradient_accumulation_steps=ga, total_train_steps=args.warmup + args.steps,
         tensor_parallel_size=args.tp, pipeline_parallel_size=args.pp, context_parallel_size=args.cp,
-        virtual_pipeline_size=args.vpp if args.pp > 1 else 1,
+        virtual_pipeline_size=args.vpp if args.pp > 1 else 1, layer_distribution=args.layer_distribution,
         expert_parallel_size=args.ep, data_parallel_size=dp, sequence_parallel=args.sp,
         cp_comm=args.cp_comm, backend=args.backend,
         gradient_checkpointing=args.gc, recompute_granularity=args.recompute, learning_rate=3e-4, lr_scheduler_type="cosine", warmup_steps=0,
@@ -415,7 +430,7 @@ def main() -> int:
         "config": {"model": args.model, "global_batch": dp * args.ep * args.micro_batch_size * ga,
                    "micro_batch": args.micro_batch_size, "grad_accum": ga, "seq_len": args.seq_len,
                    "parallelism": par, "layout": args.layout, "sequence_parallel": args.sp, "activation_checkpointing": args.gc,
-                   "virtual_pipeline": args.vpp if args.pp > 1 else 1,
+                   "virtual_pipeline": args.vpp if args.pp > 1 else 1, "layer_distribution": args.layer_distribution,
                    "lm_head": f"fused, {args.head_chunk}-token chunks" if args.fused_head else "logits + CE",
                    "grad_reduce_dtype": args.grad_reduce_dtype, "zero_stage": args.zero if dp * args.cp * args.ep > 1 else 0,
                    "optimizer": f"AdamW, fp32 master, {args.opt_state_dtype} moments",

@@ -214,11 +214,16 @@ class TransformerLM(nn.Module):
         # evenly into pp*V chunks; this rank holds global chunks v*pp + pr, v = 0..V-1
         self.virtual_stages = max(1, int(virtual_stages))
         if self.virtual_stages > 1:
-            if layer_distribution:
-                raise ValueError("layer_distribution is not supported with virtual pipeline stages")
-            if cfg.num_hidden_layers < pp * self.virtual_stages:
+            nchunks = pp * self.virtual_stages
+            if cfg.num_hidden_layers < nchunks:
                 raise ValueError(f"{cfg.num_hidden_layers} layers cannot fill {pp} x {self.virtual_stages} chunks")
-            self.chunk_ranges = [stage_layer_range(cfg.num_hidden_layers, pp * self.virtual_stages, v * pp + pr)
+            # layer_distribution with virtual stages: one entry per GLOBAL chunk (chunk v * pp + stage,
+            # in model order), e.g. "9,8,8,7" at pp 2 x V 2 gives stage 0 chunks 0 + 2 (17 layers) and
+            # the last stage, which also runs the LM head and the loss, chunks 1 + 3 (15 layers)
+            if layer_distribution and (len(layer_distribution) != nchunks or min(layer_distribution) < 1):
+                raise ValueError(f"layer distribution {layer_distribution}: need {nchunks} entries (pp x virtual "
+                                 f"stages, global chunk order), each >= 1")
+            self.chunk_ranges = [stage_layer_range(cfg.num_hidden_layers, nchunks, v * pp + pr, layer_distribution)
                                  for v in range(self.virtual_stages)]
         else:
             self.chunk_ranges = [stage_layer_range(cfg.num_hidden_layers, pp, pr, layer_distribution)]

@@ -21,6 +21,7 @@ _ACT_MLP = 20   # gate|up output, SwiGLU output, down input (dense MLP with I = 
 # buffers -- measured between steps of the per-rank slices (bench.py --slice,
 # profiles/r06/slices): +1.5 GB over the resident terms at DP 8, +2.0-2.5 GB at TP 2 x PP 2
 _WORKSPACE_GB = 2.0
+_TP_ACT_UPLIFT = 1.08
 _ACT_SWIGLU = 7  # the SwiGLU output alone (I = 3.5 h bf16): not kept when it is recomputed
                  # in backward (ops/mlp.swiglu_linear: one rank, opt-in ST_MLP_RECOMPUTE_ACT=1)
 
@@ -61,13 +62,15 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
                          fused_head_chunk: int = 0, recompute_swiglu: bool | None = None,
                          moe_dropless: bool = False, optimizer_state_dtype: str = "fp32",
                          xgmi_ipc_bytes: float = 0.0, cp_ds_budget_bytes: float | None = None,
-                         pp_rank: int = 0, virtual_pipeline: int = 1, moe_exact_rows: bool = False) -> MemoryEstimate:
+                         pp_rank: int = 0, virtual_pipeline: int = 1, moe_exact_rows: bool = False,
+                         layer_distribution: list[int] | None = None) -> MemoryEstimate:
     """Per-rank estimate: weights of the largest stage, activations of pipeline stage
     ``pp_rank`` (default 0, the first stage: it holds the most micro-batches in flight, so
     the default is the worst rank).  In-flight work per stage: plain 1F1B holds
     min(pp - pp_rank, grad_acc) micro-batches of the whole stage; interleaved 1F1B
     (``virtual_pipeline`` V > 1) holds warm-up + 1 chunk-micro-batches of layers/V each
-    (parallel/interleaved.num_warmup); AFAB holds all of them.
+    (parallel/interleaved.num_warmup); AFAB holds all of them.  ``layer_distribution``: layers
+    per pipeline chunk (``--layer_distribution``), this stage's sum replaces the even split.
 
     ``fused_head_chunk`` > 0: the fused chunked LM head (ops/fused_head.py) -- one
     chunk of logits and dX instead of the logits and their gradient.
@@ -80,6 +83,9 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
     H, Hkv = cfg.num_attention_heads, cfg.num_key_value_heads
     L = cfg.num_hidden_layers
     layers = -(-L // pp)
+    if layer_distribution and pp > 1:
+        # per-chunk layer counts (global chunk order v * pp + stage): this stage's chunks
+        layers = sum(layer_distribution[v * pp + pp_rank] for v in range(len(layer_distribution) // pp))
     attn = (h * d * (H + 2 * Hkv) + H * d * h) / tp + 2 * h
     dense, expert = 0.0, 0.0
     for i in range(layers):
@@ -129,6 +135,11 @@ def estimate_rank_memory(cfg, tp: int = 1, pp: int = 1, cp: int = 1, ep: int = 1
         moe_extra = (rows * per_row + t_micro * k * 4 * h) * (tokens / t_micro)
     if tp > 1:
         per_layer = per_layer / tp if sequence_parallel else 8 * h + (per_layer - 8 * h) / tp
+        # measured: the tp 2 + SP pipeline stages hold 6-16 % more per (layer, micro-batch) than
+        # the dense calibration divided by tp (bench.py --slice, profiles/r06/slices: 1.21-1.32
+        # vs 1.14 GB) -- buffers that do not shard with the heads (full-sequence gathers in
+        # flight, the fused head's chunk on the last stage)
+        per_layer *= _TP_ACT_UPLIFT
     if gradient_checkpointing == "selective":  # attention activations kept, norm + MLP recomputed
         mlp = _ACT_MLP * h * k_eff * cfg.intermediate_size / (3.5 * h) / tp
         kept = max(per_layer - mlp, 2 * h)

@@ -14,6 +14,12 @@ MEASURED = {
                                    sequence_parallel=True, virtual_pipeline=2, pp_rank=0), 78.51),
     "tp2pp2dp2_last_stage": (dict(model="llama3-8b", tp=2, pp=2, dp=2, micro_batch=4, grad_acc=8, zero1=True,
                                   sequence_parallel=True, virtual_pipeline=2, pp_rank=1), 60.69),
+    "tp2pp2dp2_9_8_8_7_first": (dict(model="llama3-8b", tp=2, pp=2, dp=2, micro_batch=4, grad_acc=8, zero1=True,
+                                     sequence_parallel=True, virtual_pipeline=2, pp_rank=0,
+                                     layer_distribution=[9, 8, 8, 7]), 84.71),
+    "tp2pp2dp2_9_8_8_7_last": (dict(model="llama3-8b", tp=2, pp=2, dp=2, micro_batch=4, grad_acc=8, zero1=True,
+                                    sequence_parallel=True, virtual_pipeline=2, pp_rank=1,
+                                    layer_distribution=[9, 8, 8, 7]), 59.06),
     "cp8_32k": (dict(model="llama3-8b", cp=8, micro_batch=1, seq_len=32768, zero1=True), 115.89),
     "mixtral_ep8_rccl": (dict(model="mixtral-8x7b", ep=8, micro_batch=1, grad_acc=2, zero1=True, moe_dropless=True,
                               moe_exact_rows=True), 140.18),

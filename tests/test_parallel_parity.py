@@ -162,6 +162,17 @@ def test_interleaved_1f1b_parity(pp, v, ga, extra):
     _compare(ref, res)
 
 
+def test_interleaved_uneven_layer_distribution_parity():
+    """Interleaved 1F1B with an uneven per-chunk layer distribution (global chunk order:
+    chunk v * pp + stage) -- "2,1,2,1": stage 0 holds 4 layers, the last stage (LM head) 2 --
+    equals the single-process step on loss and every weight."""
+    ref = _reference("tiny-llama", 2, num_hidden_layers=6)
+    res = run_workers(_worker, 2, "tiny-llama", dict(pipeline_parallel_size=2, micro_batch_size=GLOBAL_B // 2,
+                                                     gradient_accumulation_steps=2, virtual_pipeline_size=2,
+                                                     num_hidden_layers=6, layer_distribution="2,1,2,1"))
+    _compare(ref, res)
+
+
 @pytest.mark.parametrize("engine", ["1f1b", "afab"])
 def test_pp3_parity(engine):
     """Three pipeline stages (a middle stage that both receives and sends in each
