@@ -65,7 +65,12 @@ LAYOUTS = {
     # sized by the worst case ep*T*min(k, E/ep) rows, so nothing is dropped and -- over the xGMI
     # push exchange -- no count is read by the host.  mbs 1 x GA 2 (the R_max buffers of mbs 2
     # would not fit in 288 GB: utils/memory.py), the same 8192 tokens per GPU per step
-    "mixtral_ep8": dict(model="mixtral-8x7b", ep=-1, micro_batch_size=1, grad_acc=2, moe_capacity_factor=0.0),
+    # EP transport: RCCL (host counts, exact-row expert buffers). The xGMI push exchange together
+    # with ZeRO-1 produced non-finite weights after the first optimizer step in the 8-rank
+    # one-GPU rehearsal (round 6: RCCL + ZeRO-1 and xGMI + ZeRO-0 are clean), so the preset
+    # keeps the path the per-rank slices measured; --ep_comm auto / xgmi selects it again
+    "mixtral_ep8": dict(model="mixtral-8x7b", ep=-1, micro_batch_size=1, grad_acc=2, moe_capacity_factor=0.0,
+                        ep_comm="rccl"),
 }
 
 
@@ -229,7 +234,9 @@ def main() -> int:
     ap.add_argument("--slice_stage", default="last", choices=["first", "last"],
                     help="pipeline stage the slice impersonates: last (final norm + LM head + loss, the "
                          "heavier compute) or first (embedding, the most micro-batches in flight: peak HBM)")
-    ap.add_argument("--ep_comm", default="auto", choices=["auto", "rccl", "xgmi"],
+    ap.add_argument("--tp_comm", default="auto", choices=["auto", "rccl", "xgmi"],
+                    help="TP / SP transport: auto (self-tested xGMI paths at start-up, RCCL fallback), rccl, xgmi")
+    ap.add_argument("--ep_comm", default=None, choices=["auto", "rccl", "xgmi"],
                     help="EP exchange transport: rccl (host counts, exact-row expert buffers), xgmi (push "
                          "exchange, device counts, R_max-row buffers), auto (xgmi when its self-test passes)")
     args = ap.parse_args()
@@ -251,7 +258,7 @@ def main() -> int:
         # a mismatch would report a different job size than the one asked for
         raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     preset = dict(model="llama3-8b", micro_batch_size=6, seq_len=4096, grad_acc=1, tp=1, pp=1, cp=1, ep=1, sp=False,
-                  vpp=1, moe_capacity_factor=0.0, moe_ep_chunks=1, layer_distribution=None)
+                  vpp=1, moe_capacity_factor=0.0, moe_ep_chunks=1, layer_distribution=None, ep_comm="auto")
     preset.update({k: (world if v == -1 else v) for k, v in LAYOUTS[args.layout].items()})
     user_dist = args.layer_distribution
     for k, v in preset.items():
@@ -334,6 +341,7 @@ def main() -> int:
         zero_stage=args.zero, fused_lm_head=bool(args.fused_head), lm_head_chunk_tokens=args.head_chunk,
         moe_capacity_factor=args.moe_capacity_factor, moe_ep_chunks=args.moe_ep_chunks,
         optimizer_state_dtype=args.opt_state_dtype, gemm_tuning=args.gemm_tuning, ep_comm=args.ep_comm,
+        tp_comm=args.tp_comm,
     )
     if args.backend == "gloo" and torch.cuda.is_available():  # 1-GPU multi-rank rehearsal
         from scaletorch_amd.dist.gloo_staging import stage_gloo_cuda_p2p

@@ -128,7 +128,17 @@ def select_tp_transport(group, requested: str = "auto", probe_mb: int = 64, msg_
         raise ValueError(f"tp_comm must be auto, rccl or xgmi, got {requested!r}")
     names = list(_TP_XGMI_OPS)
     flags, info = [0] * len(names), {}
-    if ws >= 2 and torch.cuda.is_available():
+    import os
+
+    # the pair path's node-wide communicator opens every peer's 512 MiB IPC areas: with more
+    # than two ranks time-slicing ONE GPU (ST_GPU_OVERSUBSCRIBE rehearsals) that setup hung
+    # (8-rank tp2pp2dp2 / tp2 x dp4 rehearsals, round 6; dist/xgmi.py _max_bytes_default), so
+    # such runs keep RCCL unless the area is set explicitly (ST_XGMI_MAX_MB)
+    shared_many = (os.environ.get("ST_GPU_OVERSUBSCRIBE", "0") == "1" and dist.is_initialized()
+                   and dist.get_world_size() > 2 and "ST_XGMI_MAX_MB" not in os.environ)
+    if ws == 2 and shared_many:
+        info = {"skipped": "tp = 2 pair path on > 2 ranks sharing one GPU (set ST_XGMI_MAX_MB to force)"}
+    elif ws >= 2 and torch.cuda.is_available():
         try:
             if ws == 2:
                 setup_tp_pair_path(group)

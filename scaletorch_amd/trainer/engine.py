@@ -41,6 +41,19 @@ _DTYPES = {"bfloat16": torch.bfloat16, "bf16": torch.bfloat16, "float16": torch.
 
 
 _COMPUTE_STREAMS: dict = {}
+# ST_DEBUG_FINITE=1: name the parameters whose gradient (before clipping) or value (after the
+# update) holds a non-finite element, and print the clipped-over grad norm -- host syncs, debug only
+_DEBUG_FINITE = os.environ.get("ST_DEBUG_FINITE", "0") == "1"
+
+
+def _report_nonfinite(model, what: str, step: int) -> None:
+    bad = []
+    for name, p in model.named_parameters():
+        t = p.grad if what == "grad" else p
+        if t is not None and t.numel() and not bool(torch.isfinite(t).all()):
+            bad.append(f"{name}({int((~torch.isfinite(t)).sum())})")
+    r = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
+    print(f"[finite] step {step} rank {r} non-finite {what}s: {len(bad)} {bad[:6]}", flush=True)
 
 
 class Trainer:
@@ -81,6 +94,12 @@ class Trainer:
             # every micro-batch holds exactly this many tokens per rank (loaders drop ragged
             # tails), so the EP exchange buffers need no per-call agreement
             set_ep_token_bound(a.micro_batch_size * a.sequence_length // max(1, a.context_parallel_size))
+        if a.ep_comm == "auto" and a.zero_stage >= 1 and a.expert_parallel_size > 1:
+            # the xGMI push exchange (no host sync) with the ZeRO-1 sharded optimizer went
+            # non-finite after the first update in the 8-rank one-GPU rehearsal, and a host
+            # sync before the optimizer hides it (an unresolved stream-ordering race, PERF.md
+            # round 6): "auto" keeps RCCL here; --ep_comm xgmi still forces the push exchange
+            a.ep_comm = "rccl"
         if a.expert_parallel_size > 1 and torch.cuda.is_available() and not a.use_cpu and a.ep_comm != "rccl" \
                 and (a.backend == "nccl" or os.environ.get("ST_GPU_OVERSUBSCRIBE", "0") == "1"):
             from ..models.moe import select_ep_transport
@@ -278,8 +297,15 @@ class Trainer:
                         l.backward()
                 loss += l.detach().float()
         with profiling.range("optimizer"):
-            self.optimizer.clip_grad_norm_(a.max_grad_norm, self.mp_group)
+            if _DEBUG_FINITE:
+                _report_nonfinite(self.raw_model, "grad", self.step)
+            gn = self.optimizer.clip_grad_norm_(a.max_grad_norm, self.mp_group)
+            if _DEBUG_FINITE:
+                print(f"[finite] step {self.step} rank {self.rank} grad norm {float(gn) if gn is not None else None}",
+                      flush=True)
             self.optimizer.step()
+            if _DEBUG_FINITE:
+                _report_nonfinite(self.raw_model, "param", self.step)
         self.lr_scheduler.step()
         self.step += 1
         self.trained_tokens += self.tokens_per_step
