@@ -65,10 +65,8 @@ LAYOUTS = {
     # sized by the worst case ep*T*min(k, E/ep) rows, so nothing is dropped and -- over the xGMI
     # push exchange -- no count is read by the host.  mbs 1 x GA 2 (the R_max buffers of mbs 2
     # would not fit in 288 GB: utils/memory.py), the same 8192 tokens per GPU per step
-    # EP transport: RCCL (host counts, exact-row expert buffers). The xGMI push exchange together
-    # with ZeRO-1 produced non-finite weights after the first optimizer step in the 8-rank
-    # one-GPU rehearsal (round 6: RCCL + ZeRO-1 and xGMI + ZeRO-0 are clean), so the preset
-    # keeps the path the per-rank slices measured; --ep_comm auto / xgmi selects it again
+    # EP transport: RCCL (host counts -> exact-row expert buffers: 140 vs 179 GB peak per rank),
+    # the path the per-rank slices measured; --ep_comm auto / xgmi select the push exchange
     "mixtral_ep8": dict(model="mixtral-8x7b", ep=-1, micro_batch_size=1, grad_acc=2, moe_capacity_factor=0.0,
                         ep_comm="rccl"),
 }

@@ -28,7 +28,7 @@ each of the others, so a TP group can all-reduce by READING its peers' buffers:
   the memory of every other GPU of the node (the relay GPU runs nothing), so all 7
   links of each partner carry a share.  The communicator spans the node; only the
   pair calls it (``XgmiComm(node_group)``, any disjoint pairs at once);
-* every wait is bounded (``ST_XGMI_TIMEOUT_S``, default 2 s): a peer that never
+* every wait is bounded (``ST_XGMI_TIMEOUT_S``, default 60 s): a peer that never
   arrives sets an error word instead of hanging the GPU; ``check()`` (polled by the
   trainer at every logging step, tensor_parallel.check_xgmi) turns it into an
   exception so the job exits non-zero and a torchrun restart can resume.
@@ -66,6 +66,18 @@ def _ep_blocks(area_rows: int, x: torch.Tensor, world: int) -> int:
     return _blocks_for(area_rows * x.shape[1] * x.element_size() // max(1, world))
 
 
+def _default_timeout() -> str:
+    """Peer-arrival bound of every spin wait.  It guards against a dead peer, not a slow one:
+    ranks legitimately drift apart by seconds (first-call GEMM tuning, a checkpoint write on
+    one rank, gloo's host staging), and a kernel that gives up leaves its output unwritten.
+    Round 6's 8-rank one-GPU Mixtral rehearsal hit the old 2-s bound in the EP exchange,
+    and the unwritten rows turned the weights non-finite by step 2.  60 s, or 300 s when
+    ranks time-share one GPU (ST_GPU_OVERSUBSCRIBE=1)."""
+    import os
+
+    return "300" if os.environ.get("ST_GPU_OVERSUBSCRIBE", "0") == "1" else "60"
+
+
 _MODES = {"oneshot": 0, "twoshot": 1, "all_gather": 2, "reduce_scatter": 3, "all_to_all": 4,
           "pair_all_gather": 5, "pair_reduce_scatter": 6}
 
@@ -89,7 +101,7 @@ class XgmiAllReduce:
         self.group = group
         self.oneshot_max = oneshot_max
         self.cap = (max_bytes + 255) // 256 * 256
-        self.timeout_s = float(timeout_s if timeout_s is not None else os.environ.get("ST_XGMI_TIMEOUT_S", "2.0"))
+        self.timeout_s = float(timeout_s if timeout_s is not None else os.environ.get("ST_XGMI_TIMEOUT_S", _default_timeout()))
         if _sim is not None:  # in-process simulation (tests): (rank, world, epoch base)
             self.rank, self.world, base = _sim
             self.id = int(_ops().xgmi_create(self.rank, self.world, self.cap, base))

@@ -100,6 +100,13 @@ def setup_ep_xgmi(group, area_bytes: int | None = None) -> None:
         _EP_XGMI[id(group)] = XgmiAllReduce(group, max_bytes=size)
 
 
+def check_ep_xgmi() -> None:
+    """Raise if an EP exchange of this process timed out: a kernel that gave up waiting for
+    a peer leaves its output rows unwritten (one host sync per communicator)."""
+    for comm in list(_EP_XGMI.values()):
+        comm.check()
+
+
 def _ep_a2a(x: torch.Tensor, group, async_op: bool):
     """Equal-split all-to-all: the xGMI push kernel when set up and the message fits
     (on a side stream when ``async_op``), else RCCL.  Returns out or (out, work)."""

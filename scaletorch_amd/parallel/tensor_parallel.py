@@ -322,6 +322,8 @@ def check_xgmi() -> None:
     communicator; the trainer polls it at logging steps -- ADVICE r1)."""
     for comm in list(_XGMI.values()):
         comm.check()
+    if _PAIR[0] is not None:
+        _PAIR[0].comm.check()
 
 
 class CopyToTensorParallelRegion(torch.autograd.Function):

@@ -94,12 +94,6 @@ class Trainer:
             # every micro-batch holds exactly this many tokens per rank (loaders drop ragged
             # tails), so the EP exchange buffers need no per-call agreement
             set_ep_token_bound(a.micro_batch_size * a.sequence_length // max(1, a.context_parallel_size))
-        if a.ep_comm == "auto" and a.zero_stage >= 1 and a.expert_parallel_size > 1:
-            # the xGMI push exchange (no host sync) with the ZeRO-1 sharded optimizer went
-            # non-finite after the first update in the 8-rank one-GPU rehearsal, and a host
-            # sync before the optimizer hides it (an unresolved stream-ordering race, PERF.md
-            # round 6): "auto" keeps RCCL here; --ep_comm xgmi still forces the push exchange
-            a.ep_comm = "rccl"
         if a.expert_parallel_size > 1 and torch.cuda.is_available() and not a.use_cpu and a.ep_comm != "rccl" \
                 and (a.backend == "nccl" or os.environ.get("ST_GPU_OVERSUBSCRIBE", "0") == "1"):
             from ..models.moe import select_ep_transport
@@ -388,6 +382,9 @@ class Trainer:
             from ..parallel.tensor_parallel import check_xgmi
 
             check_xgmi()
+        from ..models.moe import check_ep_xgmi
+
+        check_ep_xgmi()
         if getattr(self.args, "fused_lm_head", False):
             from ..ops.fused_head import check_grad_scale
 

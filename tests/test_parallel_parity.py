@@ -322,20 +322,16 @@ def test_zero1_moe_ep2_dense_sharded():
         _compare(b, [r], atol=1e-5, rtol=1e-4)
 
 
-def _ep_comm_worker(rank, world, zero_stage):
-    from scaletorch_amd.trainer.engine import Trainer
+def test_xgmi_default_timeout(monkeypatch):
+    """The spin-wait bound guards against a dead peer, not a slow one: 60 s by default and
+    300 s when ranks time-share one GPU (the old 2 s fired in the 8-rank one-GPU Mixtral
+    rehearsal and left EP exchange rows unwritten)."""
+    from scaletorch_amd.dist.xgmi import _default_timeout
 
-    tr = Trainer(_make_args("tiny-moe", expert_parallel_size=2, micro_batch_size=2, zero_stage=zero_stage),
-                 build_data=False)
-    return tr.args.ep_comm
-
-
-def test_ep_comm_auto_keeps_rccl_under_zero1():
-    """--ep_comm auto with ZeRO-1 resolves to the RCCL exchange (the xGMI push exchange plus
-    ZeRO-1 raced in the 8-rank rehearsal, docs/PERF.md round 6); ZeRO-0 leaves "auto" to the
-    start-up self-test."""
-    assert run_workers(_ep_comm_worker, 2, 1) == ["rccl", "rccl"]
-    assert run_workers(_ep_comm_worker, 2, 0) == ["auto", "auto"]
+    monkeypatch.delenv("ST_GPU_OVERSUBSCRIBE", raising=False)
+    assert float(_default_timeout()) == 60
+    monkeypatch.setenv("ST_GPU_OVERSUBSCRIBE", "1")
+    assert float(_default_timeout()) == 300
 
 
 def _ckpt_worker(rank, world, tmpdir):
