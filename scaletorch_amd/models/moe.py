@@ -360,6 +360,7 @@ def _ep_exchange_rccl(x: torch.Tensor, M: torch.Tensor, El: int, direction: int,
 
 _ZERO_PAD = [os.environ.get("ST_MOE_ZERO_PAD", "0") == "1"]  # zero the unused tail of R_max buffers (debug)
 _DEBUG_ROUTING = [os.environ.get("ST_MOE_DEBUG", "0") == "1"]  # router input / index checks (debug runs)
+_DEBUG_CALLS = [0]  # router calls checked so far
 
 
 def _ep_exchange(x, M, El, direction, out_rows, area_rows, group, comm, Mh=None):
@@ -543,11 +544,11 @@ class MoERouter(nn.Module):
         # Switch aux loss: coef * E * sum_e f_e * P_e
         T = x2d.shape[0]
         if _DEBUG_ROUTING[0]:  # ST_MOE_DEBUG=1: host checks (one sync per router call) before the scatter
-            _DEBUG_ROUTING.append(0)  # call counter: len - 1 router calls so far
+            _DEBUG_CALLS[0] += 1
             bad_in = int((~torch.isfinite(x2d)).sum())
             lo, hi = int(topi.min()), int(topi.max())
             if bad_in or lo < 0 or hi >= self.num_experts:
-                raise RuntimeError(f"router call {len(_DEBUG_ROUTING) - 1}: {bad_in} non-finite inputs, top-k "
+                raise RuntimeError(f"router call {_DEBUG_CALLS[0]}: {bad_in} non-finite inputs, top-k "
                                    f"indices in [{lo}, {hi}] of {self.num_experts} experts (T {T})")
         counts = torch.zeros(self.num_experts, device=x2d.device, dtype=torch.float32)
         counts.scatter_add_(0, topi.reshape(-1).long(), torch.ones(topi.numel(), device=x2d.device))
