@@ -211,6 +211,26 @@ def test_xgmi_absent_peer_times_out_and_check_raises():
             c.close()
 
 
+def test_xgmi_ep_exchange_absent_peer_health_check_raises(monkeypatch):
+    """The round-6 rehearsal failure mode: an EP dispatch whose peer does not arrive within
+    the bound gives up (no GPU hang) and the trainer's EP poll raises instead of training on
+    the unwritten rows."""
+    from scaletorch_amd.models import moe
+
+    comms = XgmiAllReduce.simulate(2, max_bytes=1 << 20, timeout_s=0.05)
+    try:
+        M = torch.tensor([[3, 2], [1, 4]], dtype=torch.int32, device="cuda")  # [world, E], El = 1
+        x = torch.randn(5, 64, device="cuda", dtype=torch.bfloat16)  # rank 0's rows, sorted by expert
+        comms[0].ep_exchange(x, M, 1, 0, 4, 8)  # rank 1 never calls
+        torch.cuda.synchronize()
+        monkeypatch.setattr(moe, "_EP_XGMI", {0: comms[0]})
+        with pytest.raises(RuntimeError, match="did not arrive"):
+            moe.check_ep_xgmi()
+    finally:
+        for c in comms:
+            c.close()
+
+
 @pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("n", [8, 4096 + 8, 200_000])
